@@ -1,0 +1,188 @@
+/* newsrec_hip.h — C ABI of libnewsrec_hip.so, the MI355X (gfx950) kernels of the two-tower
+ * news-recommendation train/score path of tyh666/News-Recommendation-MIND.
+ *
+ * The reference is 100 % Python/PyTorch: it has no FFI of its own.  Each entry point below
+ * replaces the aten ops that one reference function launches (cited per entry); the Python
+ * shim (news-recommendation-mind_amd/newsrec_amd/_lib.py) binds them with ctypes and keeps
+ * the reference's nn.Module contracts.
+ *
+ * Conventions (all entries):
+ *   - every pointer is a DEVICE pointer; the caller owns all memory (inputs, outputs and
+ *     workspace).  The library never allocates, frees or synchronises.
+ *   - calls are stream-ordered on `stream` and may be captured into a hipGraph.
+ *   - return 0 on success, a negative hipError_t on a launch failure, or
+ *     -1000 - k for an invalid argument k.
+ *   - fp32 storage and fp32 arithmetic (the reference has no autocast anywhere).
+ */
+#ifndef NEWSREC_HIP_H
+#define NEWSREC_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* hipStream_t;
+
+/* ------------------------------------------------------------------ GEMM operands */
+
+/* How the stored row index of an operand is found. */
+enum nr_rows_map {
+  NR_ROWS_PLAIN = 0,  /* row r  -> data + r * ld                                          */
+  NR_ROWS_GATHER = 1, /* row r  -> data + rows[r] * ld   (word-embedding gather, BERT.py:39) */
+  NR_ROWS_CONV3 = 2   /* row r = (news n, pos t), tap j in {0,1,2} of a k=3, pad=1 Conv1d:
+                         data + rows[n*seq_len + t+j-1] * ld, zeros when t+j-1 is outside
+                         [0, seq_len) (CNN.py:12-17).  Column c of tap j is c - j*seg.    */
+};
+
+enum nr_layout {
+  NR_KCONTIG = 0, /* stored rows are the M (or N) index, k contiguous: A[M][K], B[N][K]   */
+  NR_MNCONTIG = 1 /* stored rows are the k index, M (or N) contiguous: A[K][M], B[K][N]   */
+};
+
+typedef struct nr_operand {
+  const float* data;
+  int64_t ld;          /* elements between stored rows (GATHER/CONV3 tables: multiple of 4,
+                          16-B aligned; plain operands take float4 loads when aligned)   */
+  const int64_t* rows; /* row table for GATHER / CONV3 (token ids), else NULL             */
+  int32_t map;         /* enum nr_rows_map                                                 */
+  int32_t seq_len;     /* CONV3: tokens per news (L)                                       */
+  int32_t seg;         /* CONV3: columns per tap (E)                                       */
+  int32_t layout;      /* enum nr_layout                                                   */
+} nr_operand;
+
+enum nr_epilogue {
+  NR_EPI_STORE = 0,      /* C[m][n] = acc + bias[n]                                          */
+  NR_EPI_STORE_RELU = 1, /* C[m][n] = max(acc + bias[n], 0)                 (CNN.py:41-42)   */
+  NR_EPI_ATOMIC = 2,     /* C[m][n] += acc  (split-K weight gradients; C pre-zeroed)          */
+  NR_EPI_SCATTER = 3,    /* C[c_rows(m)][n'] += acc, rows equal to pad_row skipped: the
+                            embedding backward (nn.Embedding padding_idx) fused into dgrad  */
+  NR_EPI_STORE_TANH = 4, /* C[m][n] = tanh(acc + bias[n])                   (CNN.py:46)      */
+  NR_EPI_ACCUM_GATE = 5, /* C[m][n] = aux[m][n] > 0 ? C[m][n] + acc : 0, aux = c_rows->data
+                            (ld c_rows->ld): adds a second gradient path, then ReLU's mask   */
+  NR_EPI_ACCUM = 6       /* C[m][n] += acc + bias[n]  (row tiles are block-exclusive)         */
+};
+
+/* C (op)= A(m,k) * B(k,n) over k in [0,K), fp32 on the f32-input MFMA.
+ * Replaces: nn.Linear / F.linear of models/Modules/Attention.py:107-108 (keyProject,
+ * valueProject), CNN.py:23 (wordQueryProject is done in nr_attn_pool), the Conv1d of
+ * CNN.py:12-17 (as a K = 3E GEMM over CONV3 rows) and their autograd backward.
+ * split_k > 1 requires NR_EPI_ATOMIC or NR_EPI_SCATTER. */
+int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B,
+                float* C, int64_t ldc, const float* bias, int32_t epilogue,
+                const nr_operand* c_rows, int64_t pad_row, int32_t split_k,
+                hipStream_t stream);
+
+/* ------------------------------------------------------------------ attention */
+
+/* Tied-QK multi-head self attention core, one sequence of L <= 64 tokens per (seq, head):
+ * out[s*L+i][h*dv:(h+1)*dv] = Σ_j XSoftmax(qk_i·qk_j * scale, m_i m_j) v_j.
+ * Replaces MultiheadAttention.forward after the projections (models/Modules/Attention.py:
+ * 125-147), get_attn_mask (:33-53) and XSoftmax.forward (:66-74).  (dk, dv) in
+ * {(64,32),(32,32),(64,64),(64,16),(16,16)} for L <= 32, {(32,32),(64,64),(16,16),(64,32)}
+ * for L <= 64.  mask: [nseq, L] of enum nr_mask_dtype (0=u8, 1=i64, 2=f64, 3=f32). */
+int nr_mha_attn_fwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v,
+                    const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L,
+                    int32_t heads, int32_t dk, int32_t dv, float scale, float* out,
+                    int64_t ld_out, hipStream_t stream);
+
+/* Backward of nr_mha_attn_fwd (XSoftmax.backward, Attention.py:77-80, and the two matmuls);
+ * recomputes P.  dqk receives the gradient of the shared key projection (both roles). */
+int nr_mha_attn_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v,
+                    const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L,
+                    int32_t heads, int32_t dk, int32_t dv, float scale, const float* dout,
+                    int64_t ld_dout, float* dqk, int64_t ld_dqk, float* dv_out, int64_t ld_dv,
+                    hipStream_t stream);
+
+/* ------------------------------------------------------------------ pooling */
+
+/* Learned-query attention pooling of nseq sequences of L <= 64 rows of D features:
+ *   Z = Dropout_p(LayerNorm(X))  (gamma == NULL: no LN; p_drop == 0: no dropout)
+ *   out[s] = Σ_l XSoftmax(scale * q·K_l, mask)_l Z_l,   K = key rows, or Z when key == NULL
+ * Replaces MHA_Encoder.forward :37-38 (LN eps, dropout with a stateless (seed, offset)
+ * counter RNG), MHA_User_Encoder :72, Attention_Pooling.forward (Pooling.py:22-24) and the
+ * pooling of CNN_Encoder (CNN.py:46, key = tanh(W c + b) from nr_gemm_f32).
+ * Saves stats [nseq*L][2] (mean, rstd; LN only) and probs [nseq*L] for the backward;
+ * zout (optional) receives Z, the encoder's per-token output. */
+int nr_attn_pool_fwd(const float* x, int64_t ldx, const float* key, int64_t ldk, const float* q,
+                     const void* mask, int32_t mask_dtype, const float* gamma, const float* beta,
+                     float eps, float p_drop, uint64_t seed, uint64_t offset, int64_t nseq,
+                     int32_t L, int32_t D, float scale, float* out, int64_t ldo, float* zout,
+                     int64_t ldz, float* stats, float* probs, hipStream_t stream);
+
+/* Backward of nr_attn_pool_fwd (dz: optional upstream grad of Z, added to the pooling's):
+ * writes dx (through dropout and LN) and dk (key != NULL;
+ * multiplied by 1 - K² when key_tanh), and ATOMICALLY ACCUMULATES dq[D], dgamma[D],
+ * dbeta[D] (caller zeroes them). */
+int nr_attn_pool_bwd(const float* x, int64_t ldx, const float* key, int64_t ldk, const float* q,
+                     const void* mask, int32_t mask_dtype, const float* gamma, const float* beta,
+                     float p_drop, uint64_t seed, uint64_t offset, int64_t nseq, int32_t L,
+                     int32_t D, float scale, const float* stats, const float* probs,
+                     const float* dout, int64_t lddo, const float* dz, int64_t lddz, float* dx,
+                     int64_t lddx, float* dk, int64_t lddk, int32_t key_tanh, float* dq,
+                     float* dgamma, float* dbeta, hipStream_t stream);
+
+/* ------------------------------------------------------------------ recurrent user encoders */
+
+enum nr_cell { NR_CELL_LSTM = 0, NR_CELL_GRU = 1 };
+
+/* Sequential part of a one-layer LSTM/GRU over B sequences of N steps (RNN.py:50-73 with
+ * pack_padded_sequence semantics: len = count of nonzero mask[b, :], output h at step
+ * len-1; mask == NULL: len = N, as LSTUR, RNN.py:100-104).  gx = x W_ihᵀ + b_ih for all
+ * steps [B*N][G*H] (G = 4 LSTM, 3 GRU), whh_t = W_hhᵀ [H][G*H].  reverse: step t reads row
+ * N-1-t (flip(dims=[1])).  h0 rows: h0[h0_idx[b]] (or h0[b]; NULL = zeros), c0 = 0.
+ * Saves gates [B*N][4H] (LSTM i,f,g,o / GRU r,z,n,W_hn h+b_hn), hprev, cprev (LSTM). */
+int nr_rnn_fwd(int32_t cell, const float* gx, int64_t ldgx, const float* whh_t, const float* bhh,
+               const float* h0, int64_t ldh0, const int64_t* h0_idx, const void* mask,
+               int32_t mask_dtype, int32_t reverse, int64_t B, int32_t N, int32_t H,
+               float* gates, float* hprev, float* cprev, float* hout, int64_t ldho,
+               hipStream_t stream);
+
+/* BPTT of nr_rnn_fwd.  Writes the pre-activation gate gradients of the input path dgi and
+ * of the recurrent path dgh ([B*N][G*H]; equal for LSTM, dgh may be NULL then) and dh0. */
+int nr_rnn_bwd(int32_t cell, const float* whh, const float* gates, const float* hprev,
+               const float* cprev, const void* mask, int32_t mask_dtype, int32_t reverse,
+               int64_t B, int32_t N, int32_t H, const float* dhout, int64_t lddho, float* dgi,
+               float* dgh, int64_t lddg, float* dh0, int64_t lddh0, hipStream_t stream);
+
+/* ------------------------------------------------------------------ scorer, optimizer, misc */
+
+enum nr_score_mode { NR_SCORE_RAW = 0, NR_SCORE_LOG_SOFTMAX = 1, NR_SCORE_SIGMOID = 2 };
+
+/* logits[b][c] = head(cdd_row(b,c) · user[b] / sqrt(H)); cdd_row = cdd[cdd_idx[b*C+c]]
+ * (predict_fast's news-table gather, TwoTowerBaseModel.py:80) or cdd[b*C+c].
+ * Replaces compute_score + log_softmax / sigmoid (TwoTowerBaseModel.py:51-75). */
+int nr_score_fwd(const float* cdd, int64_t ldc, const int64_t* cdd_idx, const float* user,
+                 int64_t ldu, int64_t B, int32_t C, int32_t H, int32_t mode, float* logits,
+                 hipStream_t stream);
+
+/* Backward of nr_score_fwd (cdd_idx == NULL form) given dlogits [B][C]. */
+int nr_score_bwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
+                 const float* logits, const float* dlogits, int64_t B, int32_t C, int32_t H,
+                 int32_t mode, float* dcdd, int64_t lddc, float* duser, int64_t lddu,
+                 hipStream_t stream);
+
+/* One torch.optim.Adam step (amsgrad=False) on n contiguous fp32 elements; `step` is the
+ * 1-based step count after increment (bias corrections as torch).  Manager.py:404-413,647. */
+int nr_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+            float lr, float beta1, float beta2, float eps, float weight_decay, int64_t step,
+            hipStream_t stream);
+
+/* out[i] = table[idx[i]] rows of E floats (E % 4 == 0).  BERT_Embedding.forward, BERT.py:39. */
+int nr_embedding_fwd(const float* table, int64_t V, int64_t E, const int64_t* idx, int64_t n,
+                     float* out, hipStream_t stream);
+
+/* dtable[idx[i]] += dout[i] for idx[i] != padding_idx (atomic; dtable pre-zeroed):
+ * embedding_dense_backward with nn.Embedding(padding_idx=0). */
+int nr_embedding_bwd(const float* dout, int64_t V, int64_t E, const int64_t* idx, int64_t n,
+                     int64_t padding_idx, float* dtable, hipStream_t stream);
+
+/* out[c] += Σ_r x[r][c]  (bias gradients; out pre-zeroed or accumulated). */
+int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out,
+              hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEWSREC_HIP_H */

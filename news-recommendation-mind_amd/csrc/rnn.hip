@@ -1,0 +1,239 @@
+// Recurrent user encoders over the click history (one layer, batch_first):
+//   RNN_User_Encoder  (models/Encoders/RNN.py:50-73): LSTM or GRU, h0 = 0, run over
+//                     pack_padded_sequence(lens = Σ his_mask), output h at step len-1
+//   LSTUR_User_Encoder (models/Encoders/RNN.py:88-104): LSTM over the FLIPPED history, all N
+//                     steps, h0 = userEmbedding[u] (gathered here), c0 = 0
+// PyTorch gate layout: LSTM rows (i, f, g, o), GRU rows (r, z, n) of weight_ih / weight_hh.
+//
+// The input projections x_t W_ihᵀ + b_ih of all steps are one MFMA GEMM (nr_gemm_f32) before
+// this kernel; here only the sequential part runs: one workgroup per sequence keeps h (and c)
+// in LDS and, per step, computes h W_hhᵀ + b_hh with W_hh streamed from L2 in a transposed,
+// coalesced layout.  The forward saves the activated gates and h_{t-1} (and c_{t-1}) of every
+// step, so the backward is exact BPTT without recomputation, and the weight gradients become
+// two more GEMMs: dW_ih = dGIᵀ X, dW_hh = dGHᵀ H_prev.
+#include "common.h"
+#include "../../include/newsrec_hip.h"
+
+namespace {
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+struct RnnArgs {
+  int cell;  // NR_CELL_LSTM / NR_CELL_GRU
+  const float* gx; int64_t ldgx;
+  const float* whh;           // fwd: W_hhᵀ [H][G*H];  bwd: W_hh [G*H][H]
+  const float* bhh;
+  const float* h0; int64_t ldh0; const int64_t* h0_idx;
+  const void* mask; int mask_dt;
+  int reverse;
+  int64_t B; int N; int H;
+  float* gates;               // [B*N][4H]
+  float* hprev;               // [B*N][H]
+  float* cprev;               // [B*N][H] (LSTM)
+  float* hout; int64_t ldho;
+  // bwd
+  const float* dhout; int64_t lddho;
+  float* dgi; float* dgh; int64_t lddg;
+  float* dh0; int64_t lddh0;
+};
+
+__device__ int seq_len(const RnnArgs& g, int64_t b, int* red) {
+  if (!g.mask) return g.N;
+  int cnt = 0;
+  for (int j = threadIdx.x; j < g.N; j += blockDim.x) cnt += nr_mask_at(g.mask, g.mask_dt, b * g.N + j) ? 1 : 0;
+  atomicAdd(red, cnt);
+  __syncthreads();
+  const int len = *red;
+  return len;
+}
+
+__global__ __launch_bounds__(256) void rnn_fwd_kernel(RnnArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int H = g.H, G = g.cell == NR_CELL_LSTM ? 4 : 3, GH = G * H;
+  float* h = sm;            // [H]
+  float* c = h + H;         // [H]
+  float* gh = c + H;        // [GH]
+  int* red = reinterpret_cast<int*>(gh + GH);
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (tid == 0) *red = 0;
+  for (int u = tid; u < H; u += blockDim.x) {
+    float h0 = 0.f;
+    if (g.h0) {
+      const int64_t r = g.h0_idx ? g.h0_idx[b] : b;
+      h0 = g.h0[r * g.ldh0 + u];
+    }
+    h[u] = h0;
+    c[u] = 0.f;
+  }
+  __syncthreads();
+  const int len = seq_len(g, b, red);
+  for (int t = 0; t < g.N; ++t) {
+    const int tt = g.reverse ? g.N - 1 - t : t;
+    const int64_t row = b * g.N + tt;
+    if (t >= len) {   // padded steps: zero what the backward GEMMs read
+      for (int r = tid; r < 4 * H; r += blockDim.x) g.gates[row * 4 * H + r] = 0.f;
+      for (int u = tid; u < H; u += blockDim.x) {
+        g.hprev[row * H + u] = 0.f;
+        if (g.cprev) g.cprev[row * H + u] = 0.f;
+      }
+      continue;
+    }
+    for (int r = tid; r < GH; r += blockDim.x) {
+      float acc = g.bhh ? g.bhh[r] : 0.f;
+      const float* wc = g.whh + r;
+      for (int k = 0; k < H; ++k) acc = fmaf(wc[(int64_t)k * GH], h[k], acc);
+      gh[r] = acc;
+    }
+    __syncthreads();
+    const float* xs = g.gx + row * g.ldgx;
+    float hn[2], cn[2];
+    int nu = 0;
+    for (int u = tid; u < H; u += blockDim.x, ++nu) {
+      float* gs = g.gates + row * 4 * H;
+      g.hprev[row * H + u] = h[u];
+      if (g.cell == NR_CELL_LSTM) {
+        const float ig = sigm(xs[u] + gh[u]);
+        const float fg = sigm(xs[H + u] + gh[H + u]);
+        const float gg = tanhf(xs[2 * H + u] + gh[2 * H + u]);
+        const float og = sigm(xs[3 * H + u] + gh[3 * H + u]);
+        const float cc = fmaf(fg, c[u], ig * gg);
+        g.cprev[row * H + u] = c[u];
+        gs[u] = ig; gs[H + u] = fg; gs[2 * H + u] = gg; gs[3 * H + u] = og;
+        cn[nu] = cc;
+        hn[nu] = og * tanhf(cc);
+      } else {
+        const float rg = sigm(xs[u] + gh[u]);
+        const float zg = sigm(xs[H + u] + gh[H + u]);
+        const float ng = tanhf(fmaf(rg, gh[2 * H + u], xs[2 * H + u]));
+        gs[u] = rg; gs[H + u] = zg; gs[2 * H + u] = ng; gs[3 * H + u] = gh[2 * H + u];
+        cn[nu] = 0.f;
+        hn[nu] = fmaf(zg, h[u] - ng, ng);     // (1 - z) n + z h
+      }
+    }
+    __syncthreads();
+    nu = 0;
+    for (int u = tid; u < H; u += blockDim.x, ++nu) {
+      h[u] = hn[nu];
+      c[u] = cn[nu];
+      if (t == len - 1) g.hout[b * g.ldho + u] = hn[nu];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void rnn_bwd_kernel(RnnArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int H = g.H, G = g.cell == NR_CELL_LSTM ? 4 : 3, GH = G * H;
+  float* dh = sm;           // [H]
+  float* dc = dh + H;       // [H]  (LSTM: dc carried to t-1 ; GRU: dh direct path)
+  float* dg = dc + H;       // [GH] recurrent-path gate grads
+  int* red = reinterpret_cast<int*>(dg + GH);
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (tid == 0) *red = 0;
+  for (int u = tid; u < H; u += blockDim.x) {
+    dh[u] = g.dhout[b * g.lddho + u];
+    dc[u] = 0.f;
+  }
+  __syncthreads();
+  const int len = seq_len(g, b, red);
+  for (int t = len; t < g.N; ++t) {
+    const int tt = g.reverse ? g.N - 1 - t : t;
+    const int64_t row = b * g.N + tt;
+    for (int r = tid; r < GH; r += blockDim.x) {
+      g.dgi[row * g.lddg + r] = 0.f;
+      if (g.dgh) g.dgh[row * g.lddg + r] = 0.f;
+    }
+  }
+  for (int t = len - 1; t >= 0; --t) {
+    const int tt = g.reverse ? g.N - 1 - t : t;
+    const int64_t row = b * g.N + tt;
+    const float* gs = g.gates + row * 4 * H;
+    float* dgi = g.dgi + row * g.lddg;
+    float* dgh = g.dgh ? g.dgh + row * g.lddg : nullptr;
+    for (int u = tid; u < H; u += blockDim.x) {
+      if (g.cell == NR_CELL_LSTM) {
+        const float ig = gs[u], fg = gs[H + u], gg = gs[2 * H + u], og = gs[3 * H + u];
+        const float cp = g.cprev[row * H + u];
+        const float cc = fmaf(fg, cp, ig * gg);
+        const float tc = tanhf(cc);
+        const float dcc = dc[u] + dh[u] * og * (1.f - tc * tc);
+        const float di = dcc * gg * ig * (1.f - ig);
+        const float df = dcc * cp * fg * (1.f - fg);
+        const float dgg = dcc * ig * (1.f - gg * gg);
+        const float dog = dh[u] * tc * og * (1.f - og);
+        dgi[u] = di; dgi[H + u] = df; dgi[2 * H + u] = dgg; dgi[3 * H + u] = dog;
+        if (dgh) { dgh[u] = di; dgh[H + u] = df; dgh[2 * H + u] = dgg; dgh[3 * H + u] = dog; }
+        dg[u] = di; dg[H + u] = df; dg[2 * H + u] = dgg; dg[3 * H + u] = dog;
+        dc[u] = dcc * fg;                           // -> c_{t-1}
+      } else {
+        const float rg = gs[u], zg = gs[H + u], ng = gs[2 * H + u], ghn = gs[3 * H + u];
+        const float hp = g.hprev[row * H + u];
+        const float dn = dh[u] * (1.f - zg) * (1.f - ng * ng);
+        const float dz = dh[u] * (hp - ng) * zg * (1.f - zg);
+        const float dr = dn * ghn * rg * (1.f - rg);
+        dgi[u] = dr; dgi[H + u] = dz; dgi[2 * H + u] = dn;
+        dgh[u] = dr; dgh[H + u] = dz; dgh[2 * H + u] = dn * rg;
+        dg[u] = dr; dg[H + u] = dz; dg[2 * H + u] = dn * rg;
+        dc[u] = dh[u] * zg;                         // direct path to h_{t-1}
+      }
+    }
+    __syncthreads();
+    float nd[2];
+    int nu = 0;
+    for (int k = tid; k < H; k += blockDim.x, ++nu) {
+      float acc = g.cell == NR_CELL_GRU ? dc[k] : 0.f;
+      for (int r = 0; r < GH; ++r) acc = fmaf(dg[r], g.whh[(int64_t)r * H + k], acc);
+      nd[nu] = acc;
+    }
+    __syncthreads();
+    nu = 0;
+    for (int k = tid; k < H; k += blockDim.x, ++nu) {
+      dh[k] = nd[nu];
+      if (g.cell == NR_CELL_GRU) dc[k] = 0.f;
+    }
+    __syncthreads();
+  }
+  if (g.dh0)
+    for (int u = tid; u < H; u += blockDim.x) g.dh0[b * g.lddh0 + u] = dh[u];
+}
+
+size_t rnn_smem(int cell, int H) { return (size_t)(2 * H + (cell == NR_CELL_LSTM ? 4 : 3) * H + 4) * sizeof(float); }
+
+}  // namespace
+
+extern "C" int nr_rnn_fwd(int32_t cell, const float* gx, int64_t ldgx, const float* whh_t, const float* bhh,
+                          const float* h0, int64_t ldh0, const int64_t* h0_idx, const void* mask,
+                          int32_t mask_dtype, int32_t reverse, int64_t B, int32_t N, int32_t H, float* gates,
+                          float* hprev, float* cprev, float* hout, int64_t ldho, hipStream_t stream) {
+  if ((cell != NR_CELL_LSTM && cell != NR_CELL_GRU) || B < 0 || N < 1 || H < 1 || H > 512) return NR_EINVAL(0);
+  if (!gx || !whh_t || !gates || !hprev || !hout || (cell == NR_CELL_LSTM && !cprev)) return NR_EINVAL(1);
+  if (B == 0) return NR_OK;
+  RnnArgs g{};
+  g.cell = cell; g.gx = gx; g.ldgx = ldgx; g.whh = whh_t; g.bhh = bhh; g.h0 = h0; g.ldh0 = ldh0;
+  g.h0_idx = h0_idx; g.mask = mask; g.mask_dt = mask_dtype; g.reverse = reverse; g.B = B; g.N = N; g.H = H;
+  g.gates = gates; g.hprev = hprev; g.cprev = cprev; g.hout = hout; g.ldho = ldho;
+  hipLaunchKernelGGL(rnn_fwd_kernel, dim3((unsigned)B), dim3(256), rnn_smem(cell, H), stream, g);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_rnn_bwd(int32_t cell, const float* whh, const float* gates, const float* hprev,
+                          const float* cprev, const void* mask, int32_t mask_dtype, int32_t reverse, int64_t B,
+                          int32_t N, int32_t H, const float* dhout, int64_t lddho, float* dgi, float* dgh,
+                          int64_t lddg, float* dh0, int64_t lddh0, hipStream_t stream) {
+  if ((cell != NR_CELL_LSTM && cell != NR_CELL_GRU) || B < 0 || N < 1 || H < 1 || H > 512) return NR_EINVAL(0);
+  if (!whh || !gates || !hprev || !dhout || !dgi || (cell == NR_CELL_LSTM && !cprev) ||
+      (cell == NR_CELL_GRU && !dgh))
+    return NR_EINVAL(1);
+  if (B == 0) return NR_OK;
+  RnnArgs g{};
+  g.cell = cell; g.whh = whh; g.gates = const_cast<float*>(gates); g.hprev = const_cast<float*>(hprev);
+  g.cprev = const_cast<float*>(cprev); g.mask = mask; g.mask_dt = mask_dtype; g.reverse = reverse; g.B = B;
+  g.N = N; g.H = H; g.dhout = dhout; g.lddho = lddho; g.dgi = dgi; g.dgh = dgh; g.lddg = lddg; g.dh0 = dh0;
+  g.lddh0 = lddh0;
+  hipLaunchKernelGGL(rnn_bwd_kernel, dim3((unsigned)B), dim3(256), rnn_smem(cell, H), stream, g);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}

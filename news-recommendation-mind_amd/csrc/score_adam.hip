@@ -1,0 +1,243 @@
+// Small HBM-bound kernels of the path:
+//   nr_score_fwd/bwd      batched user x candidate scorer + log_softmax / sigmoid head
+//                         (models/TwoTowerBaseModel.py:51-75, predict_fast :78-83 with a
+//                         gathered news table)
+//   nr_adam               Adam update, torch.optim.Adam semantics (utils/Manager.py:404-413,647)
+//   nr_embedding_fwd/bwd  standalone word-embedding lookup and its padding_idx-aware
+//                         scatter-add backward (models/Embeddings/BERT.py:39)
+//   nr_colsum             column sums (bias gradients of the projections)
+#include "common.h"
+#include "../../include/newsrec_hip.h"
+
+namespace {
+
+// one workgroup (256 threads) per impression b; one wave per candidate dot product
+__global__ __launch_bounds__(256) void score_fwd_kernel(const float* cdd, int64_t ldc, const int64_t* cdd_idx,
+                                                        const float* user, int64_t ldu, int C, int H,
+                                                        float scale, int mode, float* logits) {
+  extern __shared__ float sc[];
+  const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const float* u = user + (int64_t)b * ldu;
+  for (int c = w; c < C; c += 4) {
+    const int64_t row = cdd_idx ? cdd_idx[(int64_t)b * C + c] : (int64_t)b * C + c;
+    const float* x = cdd + row * ldc;
+    float s = 0.f;
+    for (int d = lane; d < H; d += 64) s = fmaf(x[d], u[d], s);
+    s = nr_wave_sum(s);
+    if (lane == 0) sc[c] = s * scale;
+  }
+  __syncthreads();
+  if (mode == NR_SCORE_LOG_SOFTMAX) {
+    if (w == 0) {
+      float mx = -INFINITY;
+      for (int c = lane; c < C; c += 64) mx = fmaxf(mx, sc[c]);
+      mx = nr_wave_max(mx);
+      float sum = 0.f;
+      for (int c = lane; c < C; c += 64) sum += __expf(sc[c] - mx);
+      const float lse = mx + __logf(nr_wave_sum(sum));
+      for (int c = lane; c < C; c += 64) logits[(int64_t)b * C + c] = sc[c] - lse;
+    }
+  } else {
+    for (int c = tid; c < C; c += 256) {
+      const float s = sc[c];
+      logits[(int64_t)b * C + c] = mode == NR_SCORE_SIGMOID ? 1.f / (1.f + __expf(-s)) : s;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void score_bwd_kernel(const float* cdd, int64_t ldc, const float* user,
+                                                        int64_t ldu, const float* logits,
+                                                        const float* dlogits, int C, int H, float scale,
+                                                        int mode, float* dcdd, int64_t lddc, float* duser,
+                                                        int64_t lddu) {
+  extern __shared__ float ds[];
+  const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  // d score
+  if (w == 0) {
+    if (mode == NR_SCORE_LOG_SOFTMAX) {
+      float sg = 0.f;
+      for (int c = lane; c < C; c += 64) sg += dlogits[(int64_t)b * C + c];
+      sg = nr_wave_sum(sg);
+      for (int c = lane; c < C; c += 64) {
+        const int64_t o = (int64_t)b * C + c;
+        ds[c] = (dlogits[o] - __expf(logits[o]) * sg) * scale;
+      }
+    } else {
+      for (int c = lane; c < C; c += 64) {
+        const int64_t o = (int64_t)b * C + c;
+        const float y = logits[o];
+        ds[c] = (mode == NR_SCORE_SIGMOID ? dlogits[o] * y * (1.f - y) : dlogits[o]) * scale;
+      }
+    }
+  }
+  __syncthreads();
+  const float* u = user + (int64_t)b * ldu;
+  for (int d = tid; d < H; d += 256) {
+    float acc = 0.f;
+    const float ud = u[d];
+    for (int c = 0; c < C; ++c) {
+      const float* x = cdd + ((int64_t)b * C + c) * ldc;
+      acc = fmaf(ds[c], x[d], acc);
+      dcdd[((int64_t)b * C + c) * lddc + d] = ds[c] * ud;
+    }
+    duser[(int64_t)b * lddu + d] = acc;
+  }
+}
+
+// torch.optim.Adam (foreach=False, maximize=False, amsgrad=False) per element:
+//   g += wd * p;  m = lerp(m, g, 1 - b1);  v = b2 v + (1 - b2) g²
+//   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                   float step, float b1, float b2, float eps,
+                                                   float bc2_sqrt, float wd) {
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+#define NR_ADAM1(c)                                            \
+    {                                                          \
+      float gc = gg.c;                                         \
+      if (wd != 0.f) gc = fmaf(wd, pp.c, gc);                  \
+      mm.c = fmaf(1.f - b1, gc - mm.c, mm.c);                  \
+      vv.c = fmaf(vv.c, b2, (1.f - b2) * gc * gc);             \
+      const float den = sqrtf(vv.c) / bc2_sqrt + eps;          \
+      pp.c = fmaf(-step, mm.c / den, pp.c);                    \
+    }
+    NR_ADAM1(x) NR_ADAM1(y) NR_ADAM1(z) NR_ADAM1(w)
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float gc = g[i];
+    if (wd != 0.f) gc = fmaf(wd, p[i], gc);
+    m[i] = fmaf(1.f - b1, gc - m[i], m[i]);
+    v[i] = fmaf(v[i], b2, (1.f - b2) * gc * gc);
+    const float den = sqrtf(v[i]) / bc2_sqrt + eps;
+    p[i] = fmaf(-step, m[i] / den, p[i]);
+  }
+#undef NR_ADAM1
+}
+
+// one wave per output row, float4 along E
+__global__ __launch_bounds__(256) void embedding_fwd_kernel(const float* table, int64_t E, const int64_t* idx,
+                                                            int64_t n, float* out) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const float4* src = reinterpret_cast<const float4*>(table + idx[row] * E);
+  float4* dst = reinterpret_cast<float4*>(out + row * E);
+  for (int64_t c = lane; c < E / 4; c += 64) dst[c] = src[c];
+}
+
+__global__ __launch_bounds__(256) void embedding_bwd_kernel(const float* dout, int64_t E, const int64_t* idx,
+                                                            int64_t n, int64_t pad, float* dtable) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const int64_t t = idx[row];
+  if (t == pad) return;
+  for (int64_t c = lane; c < E; c += 64) atomicAdd(&dtable[t * E + c], dout[row * E + c]);
+}
+
+__global__ __launch_bounds__(256) void colsum_kernel(const float* x, int64_t ldx, int64_t rows, int64_t cols,
+                                                     int64_t chunk, float* out) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int64_t r0 = (int64_t)blockIdx.y * chunk;
+  const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
+  float acc = 0.f;
+  for (int64_t r = r0; r < r1; ++r) acc += x[r * ldx + c];
+  atomicAdd(&out[c], acc);
+}
+
+}  // namespace
+
+extern "C" int nr_score_fwd(const float* cdd, int64_t ldc, const int64_t* cdd_idx, const float* user,
+                            int64_t ldu, int64_t B, int32_t C, int32_t H, int32_t mode, float* logits,
+                            hipStream_t stream) {
+  if (B < 0 || C < 1 || H < 1 || mode < 0 || mode > 2) return NR_EINVAL(0);
+  if (!cdd || !user || !logits) return NR_EINVAL(1);
+  if (B == 0) return NR_OK;
+  hipLaunchKernelGGL(score_fwd_kernel, dim3((unsigned)B), dim3(256), (size_t)C * sizeof(float), stream, cdd,
+                     ldc, cdd_idx, user, ldu, C, H, 1.0f / sqrtf((float)H), mode, logits);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_score_bwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
+                            const float* logits, const float* dlogits, int64_t B, int32_t C, int32_t H,
+                            int32_t mode, float* dcdd, int64_t lddc, float* duser, int64_t lddu,
+                            hipStream_t stream) {
+  if (B < 0 || C < 1 || H < 1 || mode < 0 || mode > 2) return NR_EINVAL(0);
+  if (!cdd || !user || !logits || !dlogits || !dcdd || !duser) return NR_EINVAL(1);
+  if (B == 0) return NR_OK;
+  hipLaunchKernelGGL(score_bwd_kernel, dim3((unsigned)B), dim3(256), (size_t)C * sizeof(float), stream, cdd,
+                     ldc, user, ldu, logits, dlogits, C, H, 1.0f / sqrtf((float)H), mode, dcdd, lddc,
+                     duser, lddu);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                       float lr, float beta1, float beta2, float eps, float weight_decay, int64_t step,
+                       hipStream_t stream) {
+  if (n < 0 || step < 1) return NR_EINVAL(0);
+  if (!param || !grad || !exp_avg || !exp_avg_sq) return NR_EINVAL(1);
+  if ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
+       reinterpret_cast<uintptr_t>(exp_avg) | reinterpret_cast<uintptr_t>(exp_avg_sq)) & 15)
+    return NR_EINVAL(2);
+  if (n == 0) return NR_OK;
+  // bias corrections in double, as torch computes them in Python floats
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  int64_t blocks = (n / 4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, param, grad, exp_avg,
+                     exp_avg_sq, n, (float)((double)lr / bc1), beta1, beta2, eps, (float)sqrt(bc2), weight_decay);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_embedding_fwd(const float* table, int64_t V, int64_t E, const int64_t* idx, int64_t n,
+                                float* out, hipStream_t stream) {
+  if (V < 1 || E < 4 || (E & 3) || n < 0) return NR_EINVAL(0);
+  if (!table || !idx || !out) return NR_EINVAL(1);
+  if (n == 0) return NR_OK;
+  hipLaunchKernelGGL(embedding_fwd_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, stream, table, E, idx,
+                     n, out);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_embedding_bwd(const float* dout, int64_t V, int64_t E, const int64_t* idx, int64_t n,
+                                int64_t padding_idx, float* dtable, hipStream_t stream) {
+  if (V < 1 || E < 1 || n < 0) return NR_EINVAL(0);
+  if (!dout || !idx || !dtable) return NR_EINVAL(1);
+  if (n == 0) return NR_OK;
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, stream, dout, E, idx,
+                     n, padding_idx, dtable);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out,
+                         hipStream_t stream) {
+  if (rows < 0 || cols < 0) return NR_EINVAL(0);
+  if (!x || !out) return NR_EINVAL(1);
+  if (rows == 0 || cols == 0) return NR_OK;
+  const int64_t cb = (cols + 255) / 256;
+  int64_t chunks = (512 + cb - 1) / cb;
+  if (chunks > rows) chunks = rows;
+  const int64_t chunk = (rows + chunks - 1) / chunks;
+  chunks = (rows + chunk - 1) / chunk;
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)cb, (unsigned)chunks), dim3(256), 0, stream, x, ldx, rows,
+                     cols, chunk, out);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}

@@ -1,0 +1,126 @@
+"""ctypes binding of libnewsrec_hip.so (C ABI: include/newsrec_hip.h).
+
+This is the only place Python touches the native library.  There is NO fallback: if the
+library is missing, or a call fails, the product path raises — a silent eager/CPU
+fallback would void every parity claim.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libnewsrec_hip.so")
+
+c_f32p = ctypes.c_void_p
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_f32 = ctypes.c_float
+c_u64 = ctypes.c_uint64
+c_ptr = ctypes.c_void_p
+
+# enum nr_rows_map / nr_layout / nr_epilogue / nr_mask_dtype
+ROWS_PLAIN, ROWS_GATHER, ROWS_CONV3 = 0, 1, 2
+KCONTIG, MNCONTIG = 0, 1
+EPI_STORE, EPI_STORE_RELU, EPI_ATOMIC, EPI_SCATTER = 0, 1, 2, 3
+MASK_U8, MASK_I64, MASK_F64, MASK_F32 = 0, 1, 2, 3
+EPI_STORE_TANH, EPI_ACCUM_GATE, EPI_ACCUM = 4, 5, 6
+CELL_LSTM, CELL_GRU = 0, 1
+SCORE_RAW, SCORE_LOG_SOFTMAX, SCORE_SIGMOID = 0, 1, 2
+
+
+class nr_operand(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("ld", c_i64), ("rows", ctypes.c_void_p),
+                ("map", c_i32), ("seq_len", c_i32), ("seg", c_i32), ("layout", c_i32)]
+
+
+# name -> argtypes (restype is always int32)
+_SIGS = {
+    "nr_gemm_f32": [c_i64, c_i64, c_i64, ctypes.POINTER(nr_operand), ctypes.POINTER(nr_operand),
+                    c_ptr, c_i64, c_ptr, c_i32, ctypes.POINTER(nr_operand), c_i64, c_i32, c_ptr],
+    "nr_mha_attn_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
+                        c_f32, c_ptr, c_i64, c_ptr],
+    "nr_mha_attn_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
+                        c_f32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr],
+    "nr_attn_pool_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_ptr, c_ptr, c_f32, c_f32, c_u64,
+                         c_u64, c_i64, c_i32, c_i32, c_f32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr],
+    "nr_attn_pool_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_ptr, c_ptr, c_f32, c_u64, c_u64,
+                         c_i64, c_i32, c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64,
+                         c_ptr, c_i64, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
+    "nr_rnn_fwd": [c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i32, c_i64, c_i32,
+                   c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr],
+    "nr_rnn_bwd": [c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_i64, c_i32, c_i32, c_ptr, c_i64,
+                   c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr],
+    "nr_score_fwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i64, c_i32, c_i32, c_i32, c_ptr, c_ptr],
+    "nr_score_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i32, c_i32, c_i32, c_ptr, c_i64, c_ptr,
+                     c_i64, c_ptr],
+    "nr_adam": [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_ptr],
+    "nr_embedding_fwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr],
+    "nr_embedding_bwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_ptr],
+    "nr_colsum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr],
+}
+
+_lib = None
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the ctypes library.  Raises if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HipError("libnewsrec_hip.so not built (%s): run __graft_entry__.build()" % LIB_PATH)
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, argtypes in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = c_i32
+        _lib = lib
+    return _lib
+
+
+def declared_symbols():
+    return list(_SIGS)
+
+
+def register(name, argtypes):
+    _SIGS[name] = argtypes
+    if _lib is not None:
+        fn = getattr(_lib, name)
+        fn.argtypes = argtypes
+        fn.restype = c_i32
+
+
+def check(rc, name):
+    if rc != 0:
+        if rc <= -1000:
+            raise HipError("%s: invalid argument %d" % (name, -1000 - rc))
+        raise HipError("%s failed: hipError %d" % (name, -rc))
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    check(rc, name)
+
+
+def stream_ptr(t=None):
+    dev = t.device if t is not None else torch.device("cuda", torch.cuda.current_device())
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def require_gpu(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise HipError("newsrec_amd kernels run on the GPU only (got a %s tensor)" % t.device)
+
+
+def operand(t, ld=None, rows=None, mapping=ROWS_PLAIN, seq_len=1, seg=1, layout=KCONTIG):
+    return nr_operand(t.data_ptr(), ld if ld is not None else t.stride(-2) if t.dim() >= 2 else t.shape[-1],
+                      rows.data_ptr() if rows is not None else 0, mapping, seq_len, seg, layout)

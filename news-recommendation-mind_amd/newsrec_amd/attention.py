@@ -1,0 +1,91 @@
+"""Attention primitives with the reference's public interface
+(models/Modules/Attention.py): ``scaled_dp_attention``, ``get_attn_mask``, ``XSoftmax`` and
+``MultiheadAttention`` (Q and K both from ``keyProject``, no output projection).
+
+``MultiheadAttention`` keeps the reference's parameter names (``keyProject``,
+``valueProject``) so checkpoints load unchanged; its forward runs the projections on the
+fp32 MFMA GEMM and the attention core in ``nr_mha_attn_fwd``.  The towers do not call it:
+they run the whole encoder as one fused autograd Function (functions.py).
+"""
+import math
+
+import torch
+from torch import nn
+
+from . import _lib as L
+from .functions import MHAFn, AttnPoolFn
+
+
+def get_attn_mask(attn_mask):
+    """Attention.py:33-53: [N, L] -> pairwise [N, 1, L, L] = m_i * m_j."""
+    if attn_mask is None:
+        return None
+    assert attn_mask.dim() == 2
+    return attn_mask[:, None, :, None] * attn_mask[:, None, None, :]
+
+
+class XSoftmax(torch.autograd.Function):
+    """Attention.py:56-80 — masked softmax whose masked (and fully masked) entries are exactly
+    zero.  Interface kept for callers that use it directly; the fused kernels inline it."""
+
+    @staticmethod
+    def forward(ctx, input, mask, dim):
+        keep = mask.bool()
+        out = torch.softmax(input.masked_fill(~keep, float("-inf")), dim).masked_fill(~keep, 0.0)
+        ctx.dim = dim
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        (out,) = ctx.saved_tensors
+        return torch._softmax_backward_data(grad, out, ctx.dim, out.dtype), None, None
+
+
+def scaled_dp_attention(query, key, value, attn_mask=None):
+    """Attention.py:5-30: softmax(q kᵀ / sqrt(d)) v with an optional XSoftmax mask."""
+    assert query.shape[-1] == key.shape[-1]
+    s = torch.matmul(query, key.transpose(-2, -1)) / math.sqrt(query.shape[-1])
+    p = torch.softmax(s, -1) if attn_mask is None else XSoftmax.apply(s, attn_mask, -1)
+    return torch.matmul(p, value)
+
+
+class MultiheadAttention(nn.Module):
+    """Attention.py:83-147 with the same constructor, parameters and init."""
+
+    def __init__(self, hidden_dim, head_num, key_dim=None, value_dim=None):
+        super().__init__()
+        self.head_num = head_num
+        if not (key_dim and value_dim):
+            assert hidden_dim % head_num == 0, "hidden_dim {} must divide head_num {}".format(hidden_dim, head_num)
+            head_dim = hidden_dim // head_num
+        self.hidden_dim = hidden_dim
+        self.key_dim = key_dim if key_dim else head_dim
+        self.value_dim = value_dim if value_dim else head_dim
+        self.keyProject = nn.Linear(hidden_dim, self.key_dim * head_num)
+        self.valueProject = nn.Linear(hidden_dim, self.value_dim * head_num)
+        nn.init.xavier_normal_(self.keyProject.weight)
+        nn.init.xavier_normal_(self.valueProject.weight)
+
+    def fused_weight(self):
+        """[keyProject; valueProject] stacked for the single projection GEMM."""
+        w = torch.cat([self.keyProject.weight, self.valueProject.weight], 0)
+        b = torch.cat([self.keyProject.bias, self.valueProject.bias], 0)
+        return w, b
+
+    def forward(self, hidden_states, attention_mask=None):
+        """hidden_states [N, L, D]; attention_mask: the pairwise [N, 1, L, L] mask built by
+        ``get_attn_mask`` (only pairwise-product masks are supported: the token mask is read
+        off its diagonal, since m_i * m_i = m_i) or None."""
+        n, l, d = hidden_states.shape
+        L.require_gpu(hidden_states)
+        if attention_mask is None:
+            tok_mask = torch.ones(n, l, dtype=torch.uint8, device=hidden_states.device)
+        else:
+            tok_mask = torch.diagonal(attention_mask.reshape(n, l, l), dim1=-2, dim2=-1).contiguous()
+        w, b = self.fused_weight()
+        x = hidden_states.reshape(n * l, d)
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        out = MHAFn.apply(x, tok_mask, w, b, n, l, self.head_num, self.key_dim, self.value_dim)
+        return out.reshape(n, l, -1)

@@ -1,0 +1,342 @@
+"""autograd.Functions over the HIP kernels — the fused hot path of the two towers.
+
+Every forward/backward here launches only libnewsrec_hip.so kernels (plus torch allocations
+and zero-fills); nothing computes on the CPU.  Token ids are int64 [T] (T = news * L), masks
+are passed in their reference dtype (i64 token masks, f64 history masks).
+
+News towers read the word-embedding table directly (the gather is fused into the first GEMM's
+operand loader) and scatter the table gradient straight out of the dgrad GEMM, so the
+[T, 768] embedding activations are never materialised.  A standalone ``encoderN(emb, mask)``
+call uses the same functions with the embeddings as the "table" and identity row ids.
+"""
+import torch
+
+from . import _lib as L
+from . import kernels as K
+
+
+def _pad4(n):
+    return (n + 3) // 4 * 4
+
+
+def _empty(rows, cols, like, ld=None):
+    """[rows, cols] view of a row-major buffer with a float4-friendly leading dimension."""
+    ld = _pad4(cols) if ld is None else ld
+    buf = torch.empty(rows, ld, device=like.device, dtype=torch.float32)
+    return buf[:, :cols]
+
+
+def _split_k(m, n, k, target=640):
+    tiles = max(1, ((m + 127) // 128) * ((n + 127) // 128))
+    return int(max(1, min(64, target // tiles, k // 512)))
+
+
+def _proj_wgrad(dY, X_op, dW, db, M_rows):
+    """dW[n_out, k_in] += dYᵀ X ; db += colsum(dY).  dY: [rows, n_out] view, X_op: operand of
+    the layer input with MN-contiguous layout (rows = token index)."""
+    n_out = dW.shape[0]
+    k_in = dW.shape[1]
+    K.gemm(n_out, k_in, M_rows, K.operand(dY, L.MNCONTIG), X_op, dW, epilogue=L.EPI_ATOMIC,
+           split_k=_split_k(n_out, k_in, M_rows))
+    if db is not None:
+        K.colsum(dY, M_rows, n_out, db)
+
+
+class TableRows:
+    """How a news tower reaches its token rows: a [V, E] table + int64 ids (fused gather)."""
+
+    def __init__(self, table, ids, pad_row):
+        self.table, self.ids, self.pad_row = table, ids, pad_row
+
+
+# ---------------------------------------------------------------------- MHA news encoder
+
+class MHANewsFn(torch.autograd.Function):
+    """MHA_Encoder.forward (models/Encoders/MHA.py:21-39) on gathered token rows:
+    Y = X [Wk; Wv]ᵀ + b  (one GEMM, gather fused)  ->  tied-QK 12-head attention
+    -> LayerNorm -> Dropout -> learned-query pooling.   Returns (news [n, H], tok [T, H] or None)."""
+
+    @staticmethod
+    def forward(ctx, table, ids, mask, w_cat, b_cat, gamma, beta, query, heads, dk, dv, seq_len,
+                pad_row, p_drop, seed, offset, want_tokens):
+        T = ids.numel()
+        n = T // seq_len
+        E = table.shape[1]
+        H = heads * dv
+        NQ = heads * dk
+        NY = NQ + H
+        Y = _empty(T, NY, table)
+        K.gemm(T, NY, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(w_cat, L.KCONTIG),
+               Y, bias=b_cat)
+        O = _empty(T, H, table)
+        K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, O)
+        news = _empty(n, H, table)
+        probs = torch.empty(T, device=table.device)
+        stats = torch.empty(T, 2, device=table.device)
+        tok = _empty(T, H, table) if want_tokens else None
+        K.attn_pool_fwd(O, query, mask, n, seq_len, news, probs, gamma=gamma, beta=beta, stats=stats,
+                        p_drop=p_drop, seed=seed, offset=offset, zout=tok)
+        ctx.save_for_backward(table, ids, mask, w_cat, gamma, beta, query, Y, O, probs, stats)
+        ctx.cfg = (heads, dk, dv, seq_len, pad_row, p_drop, seed, offset)
+        return news, tok
+
+    @staticmethod
+    def backward(ctx, dnews, dtok):
+        table, ids, mask, w_cat, gamma, beta, query, Y, O, probs, stats = ctx.saved_tensors
+        heads, dk, dv, seq_len, pad_row, p_drop, seed, offset = ctx.cfg
+        T = ids.numel()
+        n = T // seq_len
+        V, E = table.shape
+        H = heads * dv
+        NQ = heads * dk
+        NY = NQ + H
+        dnews = dnews.contiguous()
+        dO = _empty(T, H, table)
+        dq = torch.zeros(H, device=table.device)
+        dgamma = torch.zeros(H, device=table.device)
+        dbeta = torch.zeros(H, device=table.device)
+        K.attn_pool_bwd(O, query, mask, n, seq_len, probs, dnews, dO, dq, gamma=gamma, beta=beta, stats=stats,
+                        dgamma=dgamma, dbeta=dbeta, p_drop=p_drop, seed=seed, offset=offset,
+                        dz=dtok.contiguous() if dtok is not None else None)
+        dY = _empty(T, NY, table)
+        K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
+        dtable = None
+        if ctx.needs_input_grad[0]:
+            dtable = torch.zeros(V, E, device=table.device)
+            K.gemm(T, E, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dtable,
+                   epilogue=L.EPI_SCATTER, c_rows=K.rows_map(ids, L.ROWS_GATHER), pad_row=pad_row)
+        dw = torch.zeros(NY, E, device=table.device)
+        db = torch.zeros(NY, device=table.device)
+        _proj_wgrad(dY, K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dw, db, T)
+        return (dtable, None, None, dw, db, dgamma, dbeta, dq.view_as(query), None, None, None, None, None,
+                None, None, None, None)
+
+
+# ---------------------------------------------------------------------- CNN news encoder
+
+class CNNNewsFn(torch.autograd.Function):
+    """CNN_Encoder.forward (models/Encoders/CNN.py:30-50): Conv1d(E->H, k=3, pad=1) as a
+    K = 3E GEMM over CONV3 rows of the table (gather fused) with bias+ReLU epilogue; key =
+    tanh(C Wqᵀ + bq) (GEMM, tanh epilogue); learned-query pooling with the token mask.
+    ``w3`` is the conv weight as [H][tap*E + e].  Returns (news [n, H], C [T, H])."""
+
+    @staticmethod
+    def forward(ctx, table, ids, mask, w3, conv_b, wq, bq, query, seq_len, pad_row):
+        T = ids.numel()
+        n = T // seq_len
+        E = table.shape[1]
+        H = w3.shape[0]
+        C = _empty(T, H, table)
+        K.gemm(T, H, 3 * E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_CONV3, seq_len=seq_len, seg=E),
+               K.operand(w3, L.KCONTIG), C, bias=conv_b, epilogue=L.EPI_STORE_RELU)
+        Kq = _empty(T, H, table)
+        K.gemm(T, H, H, K.operand(C, L.KCONTIG), K.operand(wq, L.KCONTIG), Kq, bias=bq, epilogue=L.EPI_STORE_TANH)
+        news = _empty(n, H, table)
+        probs = torch.empty(T, device=table.device)
+        K.attn_pool_fwd(C, query, mask, n, seq_len, news, probs, key=Kq)
+        ctx.save_for_backward(table, ids, mask, w3, wq, query, C, Kq, probs)
+        ctx.cfg = (seq_len, pad_row)
+        return news, C
+
+    @staticmethod
+    def backward(ctx, dnews, dC_out):
+        table, ids, mask, w3, wq, query, C, Kq, probs = ctx.saved_tensors
+        seq_len, pad_row = ctx.cfg
+        T = ids.numel()
+        n = T // seq_len
+        V, E = table.shape
+        H = w3.shape[0]
+        dev = table.device
+        dnews = dnews.contiguous()
+        dC = _empty(T, H, table)
+        dKq = _empty(T, H, table)
+        dq = torch.zeros(H, device=dev)
+        K.attn_pool_bwd(C, query, mask, n, seq_len, probs, dnews, dC, dq, key=Kq, dk=dKq, key_tanh=True,
+                        dz=dC_out.contiguous() if dC_out is not None else None)
+        # key projection: dWq = dKqᵀ C, dbq = colsum(dKq); dC += dKq Wq, then ReLU'(C)
+        dwq = torch.zeros(H, H, device=dev)
+        dbq = torch.zeros(H, device=dev)
+        _proj_wgrad(dKq, K.operand(C, L.MNCONTIG), dwq, dbq, T)
+        K.gemm(T, H, H, K.operand(dKq, L.KCONTIG), K.operand(wq, L.MNCONTIG), dC, epilogue=L.EPI_ACCUM_GATE,
+               c_rows=K.aux_operand(C))
+        dconv_b = torch.zeros(H, device=dev)
+        dw3 = torch.zeros(H, 3 * E, device=dev)
+        _proj_wgrad(dC, K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_CONV3, seq_len=seq_len, seg=E),
+                    dw3, dconv_b, T)
+        dtable = None
+        if ctx.needs_input_grad[0]:
+            dtable = torch.zeros(V, E, device=dev)
+            K.gemm(T, 3 * E, H, K.operand(dC, L.KCONTIG), K.operand(w3, L.MNCONTIG), dtable,
+                   epilogue=L.EPI_SCATTER, c_rows=K.rows_map(ids, L.ROWS_CONV3, seq_len=seq_len, seg=E),
+                   pad_row=pad_row)
+        return dtable, None, None, dw3, dconv_b, dwq, dbq, dq.view_as(query), None, None
+
+
+# ---------------------------------------------------------------------- pooling user encoder
+
+class AttnPoolFn(torch.autograd.Function):
+    """Attention_Pooling.forward (models/Encoders/Pooling.py:12-25): learned-query pooling of
+    the history with the history mask.  x: [B*N, H] rows view; returns [B, H]."""
+
+    @staticmethod
+    def forward(ctx, x, query, mask, B, N):
+        H = query.numel()
+        out = _empty(B, H, x)
+        probs = torch.empty(B * N, device=x.device)
+        K.attn_pool_fwd(x, query, mask, B, N, out, probs)
+        ctx.save_for_backward(x, query, mask, probs)
+        ctx.cfg = (B, N)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, query, mask, probs = ctx.saved_tensors
+        B, N = ctx.cfg
+        H = query.numel()
+        dx = _empty(B * N, H, x)
+        dq = torch.zeros(H, device=x.device)
+        K.attn_pool_bwd(x, query, mask, B, N, probs, dout.contiguous(), dx, dq)
+        return dx, dq.view_as(query), None, None, None
+
+
+# ---------------------------------------------------------------------- MHA over rows
+
+class MHAFn(torch.autograd.Function):
+    """MultiheadAttention.forward (models/Modules/Attention.py:115-147) on plain rows:
+    Y = x [Wk; Wv]ᵀ + b (GEMM) -> tied-QK attention core (pairwise token mask).
+    x: [nseq*L, D] -> [nseq*L, heads*dv].  Used by MHA_User_Encoder (MHA.py:58-75) and the
+    standalone MultiheadAttention module."""
+
+    @staticmethod
+    def forward(ctx, x, mask, w_cat, b_cat, nseq, seq_len, heads, dk, dv):
+        D = x.shape[1]
+        NQ = heads * dk
+        NY = w_cat.shape[0]
+        rows = nseq * seq_len
+        Y = _empty(rows, NY, x)
+        K.gemm(rows, NY, D, K.operand(x, L.KCONTIG), K.operand(w_cat, L.KCONTIG), Y, bias=b_cat)
+        O = _empty(rows, heads * dv, x)
+        K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:NY], mask, nseq, seq_len, heads, dk, dv, O)
+        ctx.save_for_backward(x, mask, w_cat, Y)
+        ctx.cfg = (nseq, seq_len, heads, dk, dv)
+        return O
+
+    @staticmethod
+    def backward(ctx, dO):
+        x, mask, w_cat, Y = ctx.saved_tensors
+        nseq, seq_len, heads, dk, dv = ctx.cfg
+        D = x.shape[1]
+        NQ = heads * dk
+        NY = w_cat.shape[0]
+        rows = nseq * seq_len
+        dev = x.device
+        if dO.stride(-1) != 1 or dO.stride(0) % 4 or dO.data_ptr() % 16:
+            dO = dO.contiguous()
+        dY = _empty(rows, NY, x)
+        K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, nseq, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
+        dx = _empty(rows, D, x)
+        K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx)
+        dw = torch.zeros(NY, D, device=dev)
+        db = torch.zeros(NY, device=dev)
+        _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows)
+        return dx, None, dw, db, None, None, None, None, None
+
+
+# ---------------------------------------------------------------------- recurrent user encoders
+
+class RNNUserFn(torch.autograd.Function):
+    """RNN_User_Encoder (RNN.py:50-73) and LSTUR_User_Encoder (RNN.py:88-104):
+    gx = x W_ihᵀ + b_ih for all steps (GEMM) -> sequential cell kernel -> h at step len-1.
+    LSTUR: reverse=True, mask=None (all N steps), h0 = user_table[h0_idx]."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, user_table, cell, mask, B, N, reverse, h0_idx):
+        H = x.shape[1]
+        G = 4 if cell == L.CELL_LSTM else 3
+        dev = x.device
+        gx = _empty(B * N, G * H, x)
+        K.gemm(B * N, G * H, H, K.operand(x, L.KCONTIG), K.operand(w_ih, L.KCONTIG), gx, bias=b_ih)
+        gates = torch.empty(B * N, 4 * H, device=dev)
+        hprev = torch.empty(B * N, H, device=dev)
+        cprev = torch.empty(B * N, H, device=dev) if cell == L.CELL_LSTM else None
+        hout = _empty(B, H, x)
+        whh_t = w_hh.detach().t().contiguous()
+        K.rnn_fwd(cell, gx, whh_t, b_hh, B, N, H, gates, hprev, cprev, hout,
+                  h0=user_table if user_table is not None else None, h0_idx=h0_idx, mask=mask, reverse=reverse)
+        ctx.save_for_backward(x, w_ih, w_hh, gates, hprev, cprev, mask, h0_idx, user_table)
+        ctx.cfg = (cell, B, N, reverse)
+        return hout
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, w_ih, w_hh, gates, hprev, cprev, mask, h0_idx, user_table = ctx.saved_tensors
+        cell, B, N, reverse = ctx.cfg
+        H = x.shape[1]
+        G = 4 if cell == L.CELL_LSTM else 3
+        dev = x.device
+        dgi = torch.empty(B * N, G * H, device=dev)
+        dgh = torch.empty(B * N, G * H, device=dev) if cell == L.CELL_GRU else None
+        dh0 = torch.empty(B, H, device=dev) if user_table is not None else None
+        K.rnn_bwd(cell, w_hh.contiguous(), gates, hprev, cprev, B, N, H, dh.contiguous(), dgi, dgh=dgh, dh0=dh0,
+                  mask=mask, reverse=reverse)
+        dgh_ = dgi if dgh is None else dgh
+        dx = _empty(B * N, H, x)
+        K.gemm(B * N, H, G * H, K.operand(dgi, L.KCONTIG), K.operand(w_ih, L.MNCONTIG), dx)
+        dw_ih = torch.zeros(G * H, H, device=dev)
+        db_ih = torch.zeros(G * H, device=dev)
+        _proj_wgrad(dgi, K.operand(x, L.MNCONTIG), dw_ih, db_ih, B * N)
+        dw_hh = torch.zeros(G * H, H, device=dev)
+        db_hh = torch.zeros(G * H, device=dev)
+        _proj_wgrad(dgh_, K.operand(hprev, L.MNCONTIG), dw_hh, db_hh, B * N)
+        dtab = None
+        if user_table is not None and ctx.needs_input_grad[5]:
+            dtab = torch.zeros_like(user_table)
+            K.embedding_bwd(dh0, h0_idx, dtab, padding_idx=None)
+        return dx, dw_ih, dw_hh, db_ih, db_hh, dtab, None, None, None, None, None, None
+
+
+# ---------------------------------------------------------------------- scorer
+
+class ScoreFn(torch.autograd.Function):
+    """compute_score + log_softmax (training) / sigmoid (eval)
+    (models/TwoTowerBaseModel.py:51-75).  cdd [B*C, H] rows view, user [B, H] -> [B, C]."""
+
+    @staticmethod
+    def forward(ctx, cdd, user, B, C, mode):
+        H = user.shape[1]
+        logits = torch.empty(B, C, device=user.device)
+        K.score_fwd(cdd, user, B, C, H, mode, logits)
+        ctx.save_for_backward(cdd, user, logits)
+        ctx.cfg = (B, C, mode)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        cdd, user, logits = ctx.saved_tensors
+        B, C, mode = ctx.cfg
+        H = user.shape[1]
+        dcdd = _empty(B * C, H, user)
+        duser = _empty(B, H, user)
+        K.score_bwd(cdd, user, logits, dlogits.contiguous(), B, C, H, mode, dcdd, duser)
+        return dcdd, duser, None, None, None
+
+
+class EmbeddingFn(torch.autograd.Function):
+    """BERT_Embedding.forward (models/Embeddings/BERT.py:24-40): row gather; the backward is
+    a padding_idx-aware scatter-add into a dense table gradient (embedding_dense_backward)."""
+
+    @staticmethod
+    def forward(ctx, table, ids, padding_idx):
+        out = torch.empty(ids.numel(), table.shape[1], device=table.device)
+        K.embedding_fwd(table, ids, out)
+        ctx.save_for_backward(ids)
+        ctx.cfg = (tuple(table.shape), padding_idx)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (ids,) = ctx.saved_tensors
+        shape, pad = ctx.cfg
+        dtable = torch.zeros(shape, device=dout.device)
+        K.embedding_bwd(dout.contiguous(), ids, dtable, padding_idx=pad)
+        return dtable, None, None

@@ -1,0 +1,258 @@
+"""Thin tensor-level wrappers over the C ABI (one function per entry point).
+
+Each wrapper validates shapes/dtypes on the host BEFORE launching (a wrong shape on the
+device is a memory fault, not an exception), then calls the kernel on the current stream.
+"""
+import torch
+
+from . import _lib as L
+
+
+def _f32(*ts):
+    for t in ts:
+        if t is not None and (t.dtype != torch.float32 or not t.is_cuda):
+            raise L.HipError("expected a float32 CUDA tensor, got %s on %s" % (t.dtype, t.device))
+
+
+def _check_rows(rows, limit, name):
+    if rows is not None:
+        if rows.dtype != torch.int64 or not rows.is_cuda or not rows.is_contiguous():
+            raise L.HipError("%s: row table must be a contiguous int64 CUDA tensor" % name)
+
+
+def gemm(M, N, K, A, B, C, ldc=None, bias=None, epilogue=L.EPI_STORE, c_rows=None,
+         pad_row=-1, split_k=1):
+    """C (op)= A(m,k) B(k,n); A, B, c_rows are nr_operand structs built by ``operand``."""
+    _f32(C, bias)
+    if bias is not None and bias.numel() < N:
+        raise L.HipError("gemm: bias has %d < N=%d entries" % (bias.numel(), N))
+    L.call("nr_gemm_f32", M, N, K, A, B, L.ptr(C), ldc if ldc is not None else C.stride(0),
+           L.ptr(bias), epilogue, c_rows, pad_row, split_k, L.stream_ptr(C))
+
+
+def operand(t, layout, rows=None, mapping=L.ROWS_PLAIN, seq_len=1, seg=1, ld=None):
+    """Describe a stored matrix ``t`` (2-D, row-major, ld % 4 == 0, 16-B aligned)."""
+    _f32(t)
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise L.HipError("operand must be a 2-D row-major tensor")
+    ld = t.stride(0) if ld is None else ld
+    if mapping != L.ROWS_PLAIN and (ld % 4 or t.data_ptr() % 16):
+        raise L.HipError("gathered operand needs ld %% 4 == 0 and 16-B alignment (ld=%d)" % ld)
+    _check_rows(rows, None, "operand")
+    if mapping != L.ROWS_PLAIN and rows is None:
+        raise L.HipError("gather/conv3 operand needs a row table")
+    op = L.nr_operand(t.data_ptr(), ld, rows.data_ptr() if rows is not None else 0,
+                      mapping, seq_len, seg, layout)
+    op._keep = (t, rows)   # the struct holds raw pointers: keep the tensors alive with it
+    return op
+
+
+def rows_map(rows, mapping, seq_len=1, seg=1):
+    """A row map for the SCATTER epilogue (no data)."""
+    _check_rows(rows, None, "rows_map")
+    op = L.nr_operand(0, 0, rows.data_ptr(), mapping, seq_len, seg, 0)
+    op._keep = (rows,)
+    return op
+
+
+_MASK_DT = {torch.uint8: L.MASK_U8, torch.bool: L.MASK_U8, torch.int64: L.MASK_I64,
+            torch.float64: L.MASK_F64, torch.float32: L.MASK_F32}
+
+
+def mask_arg(mask, numel):
+    """(pointer, dtype code) of a contiguous CUDA mask with ``numel`` elements."""
+    if mask.dtype not in _MASK_DT or not mask.is_cuda or not mask.is_contiguous():
+        raise L.HipError("mask must be a contiguous CUDA bool/u8/i64/f32/f64 tensor")
+    if mask.numel() != numel:
+        raise L.HipError("mask has %d elements, expected %d" % (mask.numel(), numel))
+    return L.ptr(mask), _MASK_DT[mask.dtype]
+
+
+def _cols(t, need, name):
+    if t.dim() != 2 or t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
+        raise L.HipError("%s: 2-D row-major, ld %% 4 == 0, 16-B aligned required" % name)
+    if t.shape[1] < need:
+        raise L.HipError("%s: needs %d columns, has %d" % (name, need, t.shape[1]))
+
+
+def mha_attn_fwd(qk, v, mask, nseq, seq_len, heads, dk, dv, out):
+    """Tied-QK multi-head attention core (Attention.py:115-147).  qk: [nseq*L, >=heads*dk]
+    (column views allowed), v: [nseq*L, >=heads*dv], mask: [nseq, L], out: [nseq*L, heads*dv]."""
+    _f32(qk, v, out)
+    for t, need, n in ((qk, heads * dk, "qk"), (v, heads * dv, "v"), (out, heads * dv, "out")):
+        _cols(t, need, n)
+        if t.shape[0] != nseq * seq_len:
+            raise L.HipError("%s has %d rows, expected %d" % (n, t.shape[0], nseq * seq_len))
+    mp, mdt = mask_arg(mask, nseq * seq_len)
+    L.call("nr_mha_attn_fwd", L.ptr(qk), qk.stride(0), L.ptr(v), v.stride(0), mp, mdt, nseq, seq_len,
+           heads, dk, dv, 1.0 / float(dk) ** 0.5, L.ptr(out), out.stride(0), L.stream_ptr(out))
+
+
+def mha_attn_bwd(qk, v, mask, nseq, seq_len, heads, dk, dv, dout, dqk, dvv):
+    _f32(qk, v, dout, dqk, dvv)
+    for t, need, n in ((qk, heads * dk, "qk"), (v, heads * dv, "v"), (dout, heads * dv, "dout"),
+                       (dqk, heads * dk, "dqk"), (dvv, heads * dv, "dv")):
+        _cols(t, need, n)
+        if t.shape[0] != nseq * seq_len:
+            raise L.HipError("%s has %d rows, expected %d" % (n, t.shape[0], nseq * seq_len))
+    mp, mdt = mask_arg(mask, nseq * seq_len)
+    L.call("nr_mha_attn_bwd", L.ptr(qk), qk.stride(0), L.ptr(v), v.stride(0), mp, mdt, nseq, seq_len,
+           heads, dk, dv, 1.0 / float(dk) ** 0.5, L.ptr(dout), dout.stride(0), L.ptr(dqk), dqk.stride(0),
+           L.ptr(dvv), dvv.stride(0), L.stream_ptr(dout))
+
+
+def aux_operand(t):
+    """The gate matrix of NR_EPI_ACCUM_GATE (passed through the c_rows slot)."""
+    _f32(t)
+    op = L.nr_operand(t.data_ptr(), t.stride(0), 0, L.ROWS_PLAIN, 1, 1, 0)
+    op._keep = (t,)
+    return op
+
+
+def _rows_ok(t, rows, ncols, name):
+    if t is None:
+        return
+    if t.dim() != 2 or t.stride(1) != 1 or t.shape[0] < rows or t.shape[1] < ncols:
+        raise L.HipError("%s: expected a row-major [>=%d, >=%d] matrix, got %s stride %s"
+                         % (name, rows, ncols, tuple(t.shape), t.stride()))
+
+
+def attn_pool_fwd(x, q, mask, nseq, seq_len, out, probs, key=None, gamma=None, beta=None, stats=None,
+                  eps=1e-5, p_drop=0.0, seed=0, offset=0, scale=None, zout=None):
+    D = q.numel()
+    _f32(x, q, out, probs, key, gamma, beta, stats, zout)
+    _rows_ok(zout, nseq * seq_len, D, "zout")
+    _rows_ok(x, nseq * seq_len, D, "x")
+    _rows_ok(key, nseq * seq_len, D, "key")
+    _rows_ok(out, nseq, D, "out")
+    if probs.numel() < nseq * seq_len or (gamma is not None and stats.numel() < 2 * nseq * seq_len):
+        raise L.HipError("attn_pool_fwd: probs/stats too small")
+    mp, mdt = mask_arg(mask, nseq * seq_len)
+    scale = 1.0 / float(D) ** 0.5 if scale is None else scale
+    L.call("nr_attn_pool_fwd", L.ptr(x), x.stride(0), L.ptr(key), key.stride(0) if key is not None else 0,
+           L.ptr(q), mp, mdt, L.ptr(gamma), L.ptr(beta), eps, p_drop, seed, offset, nseq, seq_len, D,
+           scale, L.ptr(out), out.stride(0), L.ptr(zout), zout.stride(0) if zout is not None else 0,
+           L.ptr(stats), L.ptr(probs), L.stream_ptr(x))
+
+
+def attn_pool_bwd(x, q, mask, nseq, seq_len, probs, dout, dx, dq, key=None, dk=None, key_tanh=False,
+                  gamma=None, beta=None, stats=None, dgamma=None, dbeta=None, p_drop=0.0, seed=0, offset=0,
+                  scale=None, dz=None):
+    D = q.numel()
+    _f32(x, q, probs, dout, dx, dq, key, dk, gamma, beta, stats, dgamma, dbeta, dz)
+    _rows_ok(dz, nseq * seq_len, D, "dz")
+    _rows_ok(x, nseq * seq_len, D, "x")
+    _rows_ok(dx, nseq * seq_len, D, "dx")
+    _rows_ok(key, nseq * seq_len, D, "key")
+    _rows_ok(dk, nseq * seq_len, D, "dk")
+    _rows_ok(dout, nseq, D, "dout")
+    mp, mdt = mask_arg(mask, nseq * seq_len)
+    scale = 1.0 / float(D) ** 0.5 if scale is None else scale
+    L.call("nr_attn_pool_bwd", L.ptr(x), x.stride(0), L.ptr(key), key.stride(0) if key is not None else 0,
+           L.ptr(q), mp, mdt, L.ptr(gamma), L.ptr(beta), p_drop, seed, offset, nseq, seq_len, D, scale,
+           L.ptr(stats), L.ptr(probs), L.ptr(dout), dout.stride(0), L.ptr(dz),
+           dz.stride(0) if dz is not None else 0, L.ptr(dx), dx.stride(0), L.ptr(dk),
+           dk.stride(0) if dk is not None else 0, int(key_tanh), L.ptr(dq), L.ptr(dgamma), L.ptr(dbeta),
+           L.stream_ptr(x))
+
+
+def rnn_fwd(cell, gx, whh_t, bhh, B, N, H, gates, hprev, cprev, hout, h0=None, h0_idx=None, mask=None,
+            reverse=False):
+    G = 4 if cell == L.CELL_LSTM else 3
+    _f32(gx, whh_t, bhh, gates, hprev, cprev, hout, h0)
+    _rows_ok(gx, B * N, G * H, "gx")
+    if tuple(whh_t.shape) != (H, G * H) or not whh_t.is_contiguous():
+        raise L.HipError("rnn_fwd: whh_t must be contiguous [H, G*H]")
+    _rows_ok(gates, B * N, 4 * H, "gates")
+    _rows_ok(hprev, B * N, H, "hprev")
+    _rows_ok(hout, B, H, "hout")
+    if gates.stride(0) != 4 * H or hprev.stride(0) != H or (cprev is not None and cprev.stride(0) != H):
+        raise L.HipError("rnn_fwd: gates/hprev/cprev must be dense")
+    if h0_idx is not None:
+        _check_rows(h0_idx, None, "h0_idx")
+    mp, mdt = mask_arg(mask, B * N) if mask is not None else (L.ptr(None), 0)
+    L.call("nr_rnn_fwd", cell, L.ptr(gx), gx.stride(0), L.ptr(whh_t), L.ptr(bhh), L.ptr(h0),
+           h0.stride(0) if h0 is not None else 0, L.ptr(h0_idx), mp, mdt, int(reverse), B, N, H,
+           L.ptr(gates), L.ptr(hprev), L.ptr(cprev), L.ptr(hout), hout.stride(0), L.stream_ptr(gx))
+
+
+def rnn_bwd(cell, whh, gates, hprev, cprev, B, N, H, dhout, dgi, dgh=None, dh0=None, mask=None, reverse=False):
+    G = 4 if cell == L.CELL_LSTM else 3
+    _f32(whh, gates, hprev, cprev, dhout, dgi, dgh, dh0)
+    if tuple(whh.shape) != (G * H, H) or not whh.is_contiguous():
+        raise L.HipError("rnn_bwd: whh must be contiguous [G*H, H]")
+    _rows_ok(dgi, B * N, G * H, "dgi")
+    _rows_ok(dgh, B * N, G * H, "dgh")
+    if dgh is not None and dgh.stride(0) != dgi.stride(0):
+        raise L.HipError("rnn_bwd: dgi/dgh must share a leading dimension")
+    _rows_ok(dhout, B, H, "dhout")
+    mp, mdt = mask_arg(mask, B * N) if mask is not None else (L.ptr(None), 0)
+    L.call("nr_rnn_bwd", cell, L.ptr(whh), L.ptr(gates), L.ptr(hprev), L.ptr(cprev), mp, mdt, int(reverse), B,
+           N, H, L.ptr(dhout), dhout.stride(0), L.ptr(dgi), L.ptr(dgh), dgi.stride(0), L.ptr(dh0),
+           dh0.stride(0) if dh0 is not None else 0, L.stream_ptr(dhout))
+
+
+def score_fwd(cdd, user, B, C, H, mode, logits, cdd_idx=None):
+    _f32(cdd, user, logits)
+    _rows_ok(user, B, H, "user")
+    if cdd_idx is None:
+        _rows_ok(cdd, B * C, H, "cdd")
+    else:
+        _check_rows(cdd_idx, None, "cdd_idx")
+        if cdd_idx.numel() != B * C:
+            raise L.HipError("score_fwd: cdd_idx has %d entries, expected %d" % (cdd_idx.numel(), B * C))
+        _rows_ok(cdd, 1, H, "cdd")
+    if logits.numel() < B * C or not logits.is_contiguous():
+        raise L.HipError("score_fwd: logits must be contiguous [B, C]")
+    L.call("nr_score_fwd", L.ptr(cdd), cdd.stride(0), L.ptr(cdd_idx), L.ptr(user), user.stride(0), B, C, H,
+           mode, L.ptr(logits), L.stream_ptr(user))
+
+
+def score_bwd(cdd, user, logits, dlogits, B, C, H, mode, dcdd, duser):
+    _f32(cdd, user, logits, dlogits, dcdd, duser)
+    _rows_ok(cdd, B * C, H, "cdd")
+    _rows_ok(dcdd, B * C, H, "dcdd")
+    _rows_ok(user, B, H, "user")
+    _rows_ok(duser, B, H, "duser")
+    if not (logits.is_contiguous() and dlogits.is_contiguous()):
+        raise L.HipError("score_bwd: logits/dlogits must be contiguous")
+    L.call("nr_score_bwd", L.ptr(cdd), cdd.stride(0), L.ptr(user), user.stride(0), L.ptr(logits),
+           L.ptr(dlogits), B, C, H, mode, L.ptr(dcdd), dcdd.stride(0), L.ptr(duser), duser.stride(0),
+           L.stream_ptr(user))
+
+
+def adam(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step):
+    _f32(param, grad, exp_avg, exp_avg_sq)
+    n = param.numel()
+    for t in (param, grad, exp_avg, exp_avg_sq):
+        if not t.is_contiguous() or t.numel() != n:
+            raise L.HipError("adam: tensors must be contiguous with equal numel")
+    L.call("nr_adam", L.ptr(param), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), n, lr, beta1, beta2, eps,
+           weight_decay, step, L.stream_ptr(param))
+
+
+def embedding_fwd(table, idx, out):
+    _f32(table, out)
+    _check_rows(idx, None, "idx")
+    V, E = table.shape
+    if not table.is_contiguous() or out.numel() != idx.numel() * E or not out.is_contiguous():
+        raise L.HipError("embedding_fwd: shape mismatch")
+    L.call("nr_embedding_fwd", L.ptr(table), V, E, L.ptr(idx), idx.numel(), L.ptr(out), L.stream_ptr(table))
+
+
+def embedding_bwd(dout, idx, dtable, padding_idx=-1):
+    _f32(dout, dtable)
+    _check_rows(idx, None, "idx")
+    V, E = dtable.shape
+    if not dtable.is_contiguous() or not dout.is_contiguous() or dout.numel() != idx.numel() * E:
+        raise L.HipError("embedding_bwd: shape mismatch")
+    L.call("nr_embedding_bwd", L.ptr(dout), V, E, L.ptr(idx), idx.numel(),
+           -1 if padding_idx is None else padding_idx, L.ptr(dtable), L.stream_ptr(dtable))
+
+
+def colsum(x, rows, cols, out):
+    _f32(x, out)
+    _rows_ok(x, rows, cols, "x")
+    if out.numel() < cols:
+        raise L.HipError("colsum: out too small")
+    L.call("nr_colsum", L.ptr(x), x.stride(0), rows, cols, L.ptr(out), L.stream_ptr(x))
