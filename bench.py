@@ -1,0 +1,214 @@
+"""Benchmark of the north-star path: NRMS (MHA news encoder + MHA user encoder, H=384,
+12 heads) two-tower TRAIN step on synthetic MIND-large-shaped impressions.
+
+One step = one batch of B=32 impressions per GPU (1 clicked + 4 negative candidates, a
+50-click history, 30-token titles) through forward (fused embedding gather,
+news tower over 55 titles per impression, user tower, scorer + log-softmax), NLL loss,
+backward, gradient all-reduce (N > 1) and Adam (two groups, lr 1e-4 / 6e-6 for the 23.4 M
+parameter word table), exactly as utils/Manager.py:636-647.  Inputs are resident in HBM
+before the timed region.  fp32 storage and arithmetic (the reference's precision).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+
+Rank 0 prints ONE JSON line.  For N > 1 launch with torch.distributed.run (one rank/GPU).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "news-recommendation-mind_amd"))
+sys.path.insert(0, ROOT)
+
+import torch
+import torch.distributed as dist
+
+B, C, NH, L, V, E, H, HEADS = 32, 5, 50, 30, 30522, 768, 384, 12
+USERS_LARGE, NEWS_LARGE_DEV = 876956, 72023
+FP32_MFMA_PEAK_TF = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = f32 vector peak
+HBM_PEAK_GBS = 8000.0
+
+
+def synth_batch(gen, device, b=B, c=C, nh=NH, l=L, full=True):
+    """MIND-shaped train batch (MIND.py:311-365 keys).  Token ids U[1000, V) with [CLS]=101 at
+    position 0 and [SEP]=102 at the last real position; throughput runs use full titles."""
+    def titles(n):
+        tok = torch.randint(1000, V, (n, l), generator=gen)
+        if full:
+            lens = torch.full((n,), l)
+        else:
+            lens = torch.randint(5, l + 1, (n,), generator=gen)
+        pos = torch.arange(l)[None]
+        mask = (pos < lens[:, None]).long()
+        tok = tok * mask
+        tok[:, 0] = 101
+        tok[torch.arange(n), lens - 1] = 102
+        return tok, mask
+    ct, cm = titles(b * c)
+    ht, hm = titles(b * nh)
+    x = {
+        "cdd_encoded_index": ct.view(b, c, l), "cdd_attn_mask": cm.view(b, c, l),
+        "his_encoded_index": ht.view(b, nh, l), "his_attn_mask": hm.view(b, nh, l),
+        "his_mask": torch.ones(b, nh, 1, dtype=torch.float64),
+        "user_id": torch.randint(1, USERS_LARGE + 1, (b,), generator=gen),
+        "label": torch.zeros(b, dtype=torch.long),
+        "cdd_id": torch.randint(1, NEWS_LARGE_DEV + 1, (b, c), generator=gen),
+    }
+    return {k: v.to(device) for k, v in x.items()}
+
+
+def build(device):
+    from newsrec_amd.manager import build_model
+    torch.manual_seed(42)
+    return build_model("mha", "mha", H, vocab=V, device=device, user_num=USERS_LARGE, dropout_p=0.2)
+
+
+def make_optim(model):
+    from newsrec_amd.manager import get_optim
+    return get_optim(model)
+
+
+def train_step(model, opt, x, world):
+    opt.zero_grad(set_to_none=True)
+    logits, _ = model(x)
+    loss = torch.nn.functional.nll_loss(logits, x["label"])
+    loss.backward()
+    if world > 1:
+        works = [dist.all_reduce(p.grad, async_op=True) for p in model.parameters() if p.grad is not None]
+        for w in works:
+            w.wait()
+        for p in model.parameters():
+            if p.grad is not None:
+                p.grad.mul_(1.0 / world)
+    opt.step()
+    return loss
+
+
+def cpu_baseline(seconds=20.0):
+    """The oracle (oracle/restatement.py, torch fp32 CPU) on the same NRMS step, timed on this
+    host's cores over a bounded sample (steps of B=32 until ~`seconds` elapse)."""
+    from oracle import restatement as R
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    model = build("cpu")
+    P = {n: p.detach().clone().requires_grad_(True) for n, p in model.named_parameters()}
+    gen = torch.Generator().manual_seed(7)
+    x = synth_batch(gen, "cpu")
+    kw = {"p_drop": 0.2}      # the reference's nn.Dropout(0.2) in training (MHA.py:19,37)
+    _, _, opt = R.train_step(P, x, "mha", "mha", None, cdd_kw=kw, his_kw=kw)      # warm-up
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        _, _, opt = R.train_step(P, x, "mha", "mha", opt, cdd_kw=kw, his_kw=kw)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or steps >= 50:
+            break
+    return {"value": round(steps * B / el, 2), "unit": "impressions/s", "cores": threads, "kind": "port",
+            "sample": "%d NRMS train steps of B=32 (fwd+bwd+Adam, fp32) after 1 warm-up, oracle/restatement.py" % steps}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from newsrec_amd import functions as F
+    model = build(dev)
+    model.train()
+    if world > 1:
+        with torch.no_grad():
+            for p in model.parameters():
+                dist.broadcast(p, 0)
+    opt = make_optim(model)
+    gen = torch.Generator().manual_seed(1234 + rank)
+    batches = [synth_batch(gen, dev) for _ in range(4)]
+
+    for i in range(a.warmup):
+        train_step(model, opt, batches[i % len(batches)], world)
+    torch.cuda.synchronize()
+
+    # per-launch timing of the dominant kernel (the fused gather + key/value projection GEMM)
+    F.PROBE.enable()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        train_step(model, opt, batches[i % len(batches)], world)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    probe = F.PROBE.collect()
+    F.PROBE.disable()
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # eval: forward in eval mode (sigmoid) over the same batch shape -> candidates scored/s
+    model.eval()
+    with torch.no_grad():
+        for i in range(3):
+            model(batches[i % len(batches)])
+        torch.cuda.synchronize()
+        ne = max(5, a.steps // 2)
+        t1 = time.perf_counter()
+        for i in range(ne):
+            model(batches[i % len(batches)])
+        torch.cuda.synchronize()
+        el_eval = time.perf_counter() - t1
+
+    if rank == 0:
+        ms = el / a.steps * 1e3
+        value = world * B * a.steps / el
+        gemm_ms = probe.get("proj_fwd_ms")
+        gemm_flops = 2.0 * B * (C + NH) * L * E * (E + H)     # per launch: [T,768] x [768,1152]
+        achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms else None
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_proj_fwd.json")
+        if os.path.exists(pmc):
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        out = {
+            "metric": "impressions/sec (train) + candidates scored/sec (eval), NRMS MIND-large 1/8 GPU",
+            "value": round(value, 1), "unit": "impressions/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (MIND-large-shaped, random-init weights)",
+            "config": {"workload": "NRMS train step: MHA news encoder + MHA user encoder, H=384, 12 heads, "
+                                   "V=30522 word table (trainable), dropout 0.2, Adam",
+                       "global_batch": B * world, "per_gpu_batch": B, "candidates": C, "history": NH,
+                       "seq_len": L, "parallelism": "dp%d" % world},
+            "eval": {"candidates_per_s": round(world * B * C * ne / el_eval, 1),
+                     "impressions_per_s": round(world * B * ne / el_eval, 1), "mode": "forward, eval (sigmoid)"},
+            "roofline": {"kernel": "gemm_f32 gather+key/value projection (fwd)", "bound": "mfma",
+                         "achieved": round(achieved, 2) if achieved else None, "peak": FP32_MFMA_PEAK_TF,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TF, 4) if achieved else None,
+                         "traffic": traffic, "launch_ms": round(gemm_ms, 4) if gemm_ms else None,
+                         "flops_per_launch": gemm_flops},
+        }
+        if not a.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

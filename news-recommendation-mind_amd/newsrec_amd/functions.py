@@ -42,11 +42,40 @@ def _proj_wgrad(dY, X_op, dW, db, M_rows):
         K.colsum(dY, M_rows, n_out, db)
 
 
-class TableRows:
-    """How a news tower reaches its token rows: a [V, E] table + int64 ids (fused gather)."""
+class _Probe:
+    """Per-launch timing of the dominant kernel (the fused gather + projection GEMM of the
+    news tower) with HIP events recorded on the stream the kernel is launched on."""
 
-    def __init__(self, table, ids, pad_row):
-        self.table, self.ids, self.pad_row = table, ids, pad_row
+    def __init__(self):
+        self.on = False
+        self.events = []
+
+    def enable(self):
+        self.on, self.events = True, []
+
+    def disable(self):
+        self.on = False
+
+    def record(self):
+        if not self.on:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def add(self, name, start, end):
+        if start is not None:
+            self.events.append((name, start, end))
+
+    def collect(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, s, e in self.events:
+            out.setdefault(name, []).append(s.elapsed_time(e))
+        return {k + "_ms": sum(v) / len(v) for k, v in out.items()}
+
+
+PROBE = _Probe()
 
 
 # ---------------------------------------------------------------------- MHA news encoder
@@ -66,8 +95,10 @@ class MHANewsFn(torch.autograd.Function):
         NQ = heads * dk
         NY = NQ + H
         Y = _empty(T, NY, table)
+        ev0 = PROBE.record()
         K.gemm(T, NY, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(w_cat, L.KCONTIG),
                Y, bias=b_cat)
+        PROBE.add("proj_fwd", ev0, PROBE.record())
         O = _empty(T, H, table)
         K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, O)
         news = _empty(n, H, table)
