@@ -95,6 +95,27 @@ int nr_mha_attn_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v
                     int64_t ld_dout, float* dqk, int64_t ld_dqk, float* dv_out, int64_t ld_dv,
                     hipStream_t stream);
 
+/* Fused MHA news-encoder tail, one workgroup per title (L <= 32): for each head the tied-QK
+ * attention on the f32 MFMA (S = Kp Kpᵀ / sqrt(dk), XSoftmax with m_i m_j, O = P Vp), then
+ * LayerNorm (eps) -> dropout(p, counter RNG) -> learned-query pooling, all in LDS.
+ * y = [T][heads*dk | heads*dv] projections.  (dk, dv, heads*dv) in {(64,32,384), (64,64,768),
+ * (64,32,256), (32,32,384)}.  Replaces MultiheadAttention.forward :125-147 + MHA.py:37-38.
+ * Saves stats [T][2] and probs [T]; zout (optional) receives Z = the encoder's token output. */
+int nr_mha_pool_fwd(const float* y, int64_t ldy, const void* mask, int32_t mask_dtype, int64_t nseq,
+                    int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
+                    const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset,
+                    const float* q, float* news, int64_t ldn, float* zout, int64_t ldz,
+                    float* stats, float* probs, hipStream_t stream);
+
+/* Backward of nr_mha_pool_fwd (recomputes the attention): writes dy [T][heads*(dk+dv)] and
+ * ATOMICALLY ACCUMULATES dbias (= column sums of dy), dq, dgamma, dbeta (caller zeroes). */
+int nr_mha_pool_bwd(const float* y, int64_t ldy, const void* mask, int32_t mask_dtype, int64_t nseq,
+                    int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
+                    const float* beta, float p_drop, uint64_t seed, uint64_t offset,
+                    const float* q, const float* stats, const float* probs, const float* dnews,
+                    int64_t ldn, const float* dz, int64_t lddz, float* dy, int64_t lddy,
+                    float* dbias, float* dq, float* dgamma, float* dbeta, hipStream_t stream);
+
 /* ------------------------------------------------------------------ pooling */
 
 /* Learned-query attention pooling of nseq sequences of L <= 64 rows of D features:

@@ -1,0 +1,469 @@
+// Fused MHA news encoder tail, one workgroup per title (L <= 32 tokens):
+//
+//   per head h:  S = Kp_h Kp_hᵀ · scale          (Q = K = keyProject(x), Attention.py:125-126)
+//                P = XSoftmax(S, m_i m_j)         (Attention.py:56-80, pairwise mask :33-53)
+//                O_h = P Vp_h                     (heads concatenated, no output projection)
+//   Z = Dropout(LayerNorm(O));  news = Σ_l XSoftmax(q·Z_l / sqrt(H))_l Z_l     (MHA.py:37-38)
+//
+// The attention runs on the f32 matrix cores (v_mfma_f32_32x32x2_f32, exact fp32) with the
+// title padded to a 32x32 tile, one wave per head:
+//   * S needs no LDS: lane (c, half) holds its own key row's half (K[c][half*DK/2 ..]) and
+//     feeds it as BOTH operands (A = K, B = Kᵀ use the same register).
+//   * S is symmetric, so the accumulator (column c on the lane) is also ROW c of S: the row
+//     softmax is 16 in-register values + one cross-half exchange, and P lands in the layout
+//     an A operand needs for the next product — O = P V takes P straight from registers with
+//     the k index permuted to the accumulator's row order (crow below).
+// O is staged in LDS [L x H], then LayerNorm / dropout (stateless counter RNG) / pooling run
+// on it in the same workgroup: the [T, H] attention output never touches HBM.
+//
+// The backward recomputes S, P, O from the projections, runs the pooling / dropout / LN
+// backward in LDS, then per head dPᵀ = V dOᵀ, dS = P∘(dP − rowsum), the symmetric
+// dKp = scale (dS + dSᵀ) Kp and dVp = Pᵀ dO, with the transposes through a per-wave 32x33 LDS
+// tile, and accumulates the projection-bias gradient (column sums of dY) in the epilogue.
+#include "common.h"
+#include "../../include/newsrec_hip.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+// row of accumulator register r in lane half h (32x32 C/D layout)
+__device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct MPArgs {
+  const float* y; int64_t ldy;        // [T][heads*dk + heads*dv] projections
+  const void* mask; int mask_dt;      // [nseq][L]
+  int64_t nseq; int L; int heads;
+  float scale_attn, scale_pool;
+  const float* gamma; const float* beta; float eps;
+  float p_drop; uint64_t seed; uint64_t offset;
+  const float* q;                     // [H] query_words
+  float* news; int64_t ldn;           // fwd out / bwd: dnews in (const)
+  float* zout; int64_t ldz;           // fwd: optional token output Z
+  float* stats; float* probs;         // [T][2], [T]
+  const float* dz; int64_t lddz;      // bwd: optional grad of Z
+  float* dy; int64_t lddy;            // bwd: [T][heads*dk + heads*dv]
+  float* dbias; float* dq; float* dgamma; float* dbeta;
+};
+
+__device__ __forceinline__ float drop_scale(const MPArgs& g, int64_t elem) {
+  if (g.p_drop <= 0.f) return 1.f;
+  return nr_dropout_keep(g.seed, g.offset + (uint64_t)elem, g.p_drop) ? 1.f / (1.f - g.p_drop) : 0.f;
+}
+
+__device__ __forceinline__ uint64_t token_bits(const MPArgs& g, int64_t seq) {
+  const int lane = threadIdx.x & 63;
+  const bool m = lane < g.L && nr_mask_at(g.mask, g.mask_dt, seq * g.L + lane);
+  return __ballot(m);
+}
+
+// S and P of one head for this lane's row c = lane & 31; returns P in p[16] (C layout).
+template <int DK>
+__device__ __forceinline__ void head_probs(const MPArgs& g, int64_t seq, int head, uint64_t bits, float (&p)[16]) {
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  constexpr int HK = DK / 2;
+  float a[HK];
+  if (c < g.L) {
+    const float* kr = g.y + (seq * g.L + c) * g.ldy + head * DK + h * HK;
+#pragma unroll
+    for (int s = 0; s < HK; s += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(kr + s);
+      a[s] = v.x; a[s + 1] = v.y; a[s + 2] = v.z; a[s + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < HK; ++s) a[s] = 0.f;
+  }
+  f32x16 S;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) S[r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < HK; ++s) S = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], a[s], S, 0, 0, 0);
+  const bool mj = (bits >> c) & 1ull;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const bool keep = mj && ((bits >> crow(r, h)) & 1ull);
+    p[r] = keep ? S[r] * g.scale_attn : -INFINITY;
+    mx = fmaxf(mx, p[r]);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float e = p[r] == -INFINITY ? 0.f : __expf(p[r] - mx);
+    p[r] = e;
+    sum += e;
+  }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = sum > 0.f ? 1.f / sum : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) p[r] *= inv;
+}
+
+// O_h = P V_h into the LDS image os[32][so] at columns head*DV ..
+template <int DK, int DV>
+__device__ __forceinline__ void head_out(const MPArgs& g, int64_t seq, int head, const float (&p)[16], float* os,
+                                         int so) {
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  const int nq = g.heads * DK;
+#pragma unroll
+  for (int vb = 0; vb < DV / 32; ++vb) {
+    f32x16 O;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = crow(s, h);
+      const float bv = k < g.L ? g.y[(seq * g.L + k) * g.ldy + nq + head * DV + vb * 32 + c] : 0.f;
+      O = __builtin_amdgcn_mfma_f32_32x32x2f32(p[s], bv, O, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) os[crow(r, h) * so + head * DV + vb * 32 + c] = O[r];
+  }
+}
+
+template <int DK, int DV>
+__device__ void attention_to_lds(const MPArgs& g, int64_t seq, uint64_t bits, float* os, int so) {
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int head = w; head < g.heads; head += nw) {
+    float p[16];
+    head_probs<DK>(g, seq, head, bits, p);
+    head_out<DK, DV>(g, seq, head, p, os, so);
+  }
+}
+
+template <int DK, int DV, int NH64>
+__global__ __launch_bounds__(256) void mha_pool_fwd_kernel(MPArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int H = NH64 * 64;
+  constexpr int SO = H + 1;
+  float* os = sm;                       // [32][SO]  O, then Z
+  float* sc = os + 32 * SO;             // [32] scores -> probs
+  const int64_t seq = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t bits = token_bits(g, seq);
+  attention_to_lds<DK, DV>(g, seq, bits, os, SO);
+  __syncthreads();
+  // LayerNorm + dropout in place, scores; one wave per row
+  for (int l = w; l < g.L; l += 4) {
+    const int64_t row = seq * g.L + l;
+    float x[NH64];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NH64; ++k) { x[k] = os[l * SO + lane + 64 * k]; s += x[k]; }
+    const float mean = nr_wave_sum(s) * (1.f / H);
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < NH64; ++k) { const float d = x[k] - mean; v = fmaf(d, d, v); }
+    const float rstd = rsqrtf(nr_wave_sum(v) * (1.f / H) + g.eps);
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NH64; ++k) {
+      const int d = lane + 64 * k;
+      const float z = ((x[k] - mean) * rstd * g.gamma[d] + g.beta[d]) * drop_scale(g, row * H + d);
+      os[l * SO + d] = z;
+      if (g.zout) g.zout[row * g.ldz + d] = z;
+      dot = fmaf(g.q[d], z, dot);
+    }
+    dot = nr_wave_sum(dot);
+    if (lane == 0) {
+      g.stats[2 * row] = mean;
+      g.stats[2 * row + 1] = rstd;
+      sc[l] = dot * g.scale_pool;
+    }
+  }
+  __syncthreads();
+  if (w == 0) {
+    const bool keep = lane < 32 && ((bits >> lane) & 1ull);
+    const float v = keep ? sc[lane & 31] : -INFINITY;
+    const float mx = nr_wave_max(v);
+    const float e = keep ? __expf(v - mx) : 0.f;
+    const float sum = nr_wave_sum(e);
+    const float pr = sum > 0.f ? e / sum : 0.f;
+    if (lane < g.L) {
+      sc[lane] = pr;
+      g.probs[seq * g.L + lane] = pr;
+    }
+  }
+  __syncthreads();
+  for (int d = tid; d < H; d += 256) {
+    float acc = 0.f;
+    for (int l = 0; l < g.L; ++l) acc = fmaf(sc[l], os[l * SO + d], acc);
+    g.news[seq * g.ldn + d] = acc;
+  }
+}
+
+template <int DK, int DV, int NH64>
+__global__ __launch_bounds__(256) void mha_pool_bwd_kernel(MPArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int H = NH64 * 64;
+  constexpr int SO = H + 1;
+  float* os = sm;                       // [32][SO]  O, then dO
+  float* ts = os + 32 * SO;             // [4][32][33] per-wave transpose tiles
+  float* ps = ts + 4 * 32 * 33;         // [32] pooling probs
+  float* ds = ps + 32;                  // [32] dp -> ds
+  float* st = ds + 32;                  // [32][2] mean, rstd
+  float* red = st + 64;                 // [4][2][H] per-wave dgamma / dbeta partials
+  const int64_t seq = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
+  const uint64_t bits = token_bits(g, seq);
+  attention_to_lds<DK, DV>(g, seq, bits, os, SO);
+  if (tid < 32) {
+    ps[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
+    st[2 * tid] = tid < g.L ? g.stats[2 * (seq * g.L + tid)] : 0.f;
+    st[2 * tid + 1] = tid < g.L ? g.stats[2 * (seq * g.L + tid) + 1] : 0.f;
+  }
+  __syncthreads();
+  const float* dnews = g.news + seq * g.ldn;
+  // (B1) dp_l = dnews · Z_l
+  for (int l = w; l < g.L; l += 4) {
+    const int64_t row = seq * g.L + l;
+    const float mean = st[2 * l], rstd = st[2 * l + 1];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NH64; ++k) {
+      const int d = lane + 64 * k;
+      const float z = ((os[l * SO + d] - mean) * rstd * g.gamma[d] + g.beta[d]) * drop_scale(g, row * H + d);
+      dot = fmaf(dnews[d], z, dot);
+    }
+    dot = nr_wave_sum(dot);
+    if (lane == 0) ds[l] = dot;
+  }
+  __syncthreads();
+  if (w == 0) {
+    const float pl = lane < 32 ? ps[lane & 31] : 0.f;
+    const float dp = lane < g.L ? ds[lane & 31] : 0.f;
+    const float r = nr_wave_sum(pl * dp);
+    if (lane < g.L) ds[lane] = pl * (dp - r) * g.scale_pool;
+  }
+  __syncthreads();
+  // (B3) dq[d] += Σ_l ds_l Z_l[d]
+  for (int d = tid; d < H; d += 256) {
+    float acc = 0.f;
+    for (int l = 0; l < g.L; ++l) {
+      const float z = ((os[l * SO + d] - st[2 * l]) * st[2 * l + 1] * g.gamma[d] + g.beta[d]) *
+                      drop_scale(g, (seq * g.L + l) * H + d);
+      acc = fmaf(ds[l], z, acc);
+    }
+    atomicAdd(&g.dq[d], acc);
+  }
+  __syncthreads();
+  // (B4) dZ -> dropout -> LayerNorm backward; dO overwrites O row by row
+  float dgam[NH64], dbet[NH64];
+#pragma unroll
+  for (int k = 0; k < NH64; ++k) { dgam[k] = 0.f; dbet[k] = 0.f; }
+  for (int l = w; l < g.L; l += 4) {
+    const int64_t row = seq * g.L + l;
+    const float mean = st[2 * l], rstd = st[2 * l + 1], pl = ps[l], dsl = ds[l];
+    float xh[NH64], dyv[NH64];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int k = 0; k < NH64; ++k) {
+      const int d = lane + 64 * k;
+      float dz = fmaf(pl, dnews[d], dsl * g.q[d]);
+      if (g.dz) dz += g.dz[row * g.lddz + d];
+      dyv[k] = dz * drop_scale(g, row * H + d);
+      xh[k] = (os[l * SO + d] - mean) * rstd;
+      const float gg = dyv[k] * g.gamma[d];
+      sg += gg;
+      sgx = fmaf(gg, xh[k], sgx);
+      dgam[k] = fmaf(dyv[k], xh[k], dgam[k]);
+      dbet[k] += dyv[k];
+    }
+    sg = nr_wave_sum(sg) * (1.f / H);
+    sgx = nr_wave_sum(sgx) * (1.f / H);
+#pragma unroll
+    for (int k = 0; k < NH64; ++k) {
+      const int d = lane + 64 * k;
+      os[l * SO + d] = rstd * (dyv[k] * g.gamma[d] - sg - xh[k] * sgx);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NH64; ++k) {
+    red[(w * 2) * H + lane + 64 * k] = dgam[k];
+    red[(w * 2 + 1) * H + lane + 64 * k] = dbet[k];
+  }
+  __syncthreads();
+  for (int d = tid; d < H; d += 256) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) { a += red[(ww * 2) * H + d]; b += red[(ww * 2 + 1) * H + d]; }
+    atomicAdd(&g.dgamma[d], a);
+    atomicAdd(&g.dbeta[d], b);
+  }
+  // (C) attention backward per head
+  const int nq = g.heads * DK;
+  float* tw = ts + w * 32 * 33;
+  for (int head = w; head < g.heads; head += 4) {
+    float p[16];
+    head_probs<DK>(g, seq, head, bits, p);
+    // dPᵀ = V dOᵀ  (lane (c, h): V[c][h*DV/2 + s], dO[c][h*DV/2 + s])
+    f32x16 dpt;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dpt[r] = 0.f;
+    {
+      constexpr int HV = DV / 2;
+      const float* vr = g.y + (seq * g.L + c) * g.ldy + nq + head * DV + h * HV;
+      const bool rv = c < g.L;
+#pragma unroll
+      for (int s = 0; s < HV; s += 4) {
+        float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (rv) v4 = *reinterpret_cast<const float4*>(vr + s);
+        const float* dor = os + c * SO + head * DV + h * HV + s;
+        dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.x, dor[0], dpt, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.y, dor[1], dpt, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.z, dor[2], dpt, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.w, dor[3], dpt, 0, 0, 0);
+      }
+    }
+    float rs = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rs = fmaf(p[r], dpt[r], rs);
+    rs += __shfl_xor(rs, 32, 64);
+    float dsv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dsv[r] = p[r] * (dpt[r] - rs) * g.scale_attn;
+    // W = dS + dSᵀ via the per-wave transpose tile
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tw[c * 33 + crow(r, h)] = dsv[r];
+    wave_lds_fence();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dsv[r] += tw[crow(r, h) * 33 + c];
+    wave_lds_fence();
+    // dKp = W Kp  -> dY[:, head*DK ..]
+#pragma unroll
+    for (int kb = 0; kb < DK / 32; ++kb) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int k = crow(s, h);
+        const float bk = k < g.L ? g.y[(seq * g.L + k) * g.ldy + head * DK + kb * 32 + c] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(dsv[s], bk, acc, 0, 0, 0);
+      }
+      float cs = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = crow(r, h);
+        if (j < g.L) g.dy[(seq * g.L + j) * g.lddy + head * DK + kb * 32 + c] = acc[r];
+        cs += acc[r];
+      }
+      cs += __shfl_xor(cs, 32, 64);
+      if (h == 0) atomicAdd(&g.dbias[head * DK + kb * 32 + c], cs);
+    }
+    // dVp = Pᵀ dO: Pᵀ through the transpose tile, dO from the LDS image
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tw[c * 33 + crow(r, h)] = p[r];
+    wave_lds_fence();
+    float pt[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) pt[s] = tw[crow(s, h) * 33 + c];
+    wave_lds_fence();
+#pragma unroll
+    for (int vb = 0; vb < DV / 32; ++vb) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pt[s], os[crow(s, h) * SO + head * DV + vb * 32 + c], acc, 0, 0, 0);
+      float cs = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = crow(r, h);
+        if (i < g.L) g.dy[(seq * g.L + i) * g.lddy + nq + head * DV + vb * 32 + c] = acc[r];
+        cs += acc[r];
+      }
+      cs += __shfl_xor(cs, 32, 64);
+      if (h == 0) atomicAdd(&g.dbias[nq + head * DV + vb * 32 + c], cs);
+    }
+  }
+}
+
+size_t fwd_smem(int H) { return (size_t)(32 * (H + 1) + 32) * sizeof(float); }
+size_t bwd_smem(int H) { return (size_t)(32 * (H + 1) + 4 * 32 * 33 + 32 + 32 + 64 + 8 * H) * sizeof(float); }
+
+template <int DK, int DV, int NH64>
+int launch(const MPArgs& g, bool bwd, hipStream_t s) {
+  const int H = NH64 * 64;
+  if (bwd) {
+    const size_t sz = bwd_smem(H);
+    if (sz > 64 * 1024)
+      hipFuncSetAttribute((const void*)mha_pool_bwd_kernel<DK, DV, NH64>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)sz);
+    hipLaunchKernelGGL((mha_pool_bwd_kernel<DK, DV, NH64>), dim3((unsigned)g.nseq), dim3(256), sz, s, g);
+  } else {
+    const size_t sz = fwd_smem(H);
+    if (sz > 64 * 1024)
+      hipFuncSetAttribute((const void*)mha_pool_fwd_kernel<DK, DV, NH64>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)sz);
+    hipLaunchKernelGGL((mha_pool_fwd_kernel<DK, DV, NH64>), dim3((unsigned)g.nseq), dim3(256), sz, s, g);
+  }
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+int dispatch(const MPArgs& g, int dk, int dv, bool bwd, hipStream_t s) {
+  const int H = g.heads * dv;
+  if (H % 64) return NR_EINVAL(9);
+  const int nh64 = H / 64;
+#define NR_CASE(K, V, N) \
+  if (dk == K && dv == V && nh64 == N) return launch<K, V, N>(g, bwd, s);
+  NR_CASE(64, 32, 6)    // NRMS news encoder: E=768 -> 12 heads x 64, H = 384
+  NR_CASE(64, 64, 12)   // H = 768
+  NR_CASE(64, 32, 4)    // H = 256 (8 heads)
+  NR_CASE(32, 32, 6)
+#undef NR_CASE
+  return NR_EINVAL(8);
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const void* mask, int32_t mask_dtype, int64_t nseq,
+                               int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
+                               const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset,
+                               const float* q, float* news, int64_t ldn, float* zout, int64_t ldz, float* stats,
+                               float* probs, hipStream_t stream) {
+  if (L < 1 || L > 32 || heads < 1) return NR_EINVAL(0);
+  if (!y || !mask || !gamma || !beta || !q || !news || !stats || !probs) return NR_EINVAL(1);
+  if ((ldy & 3) || !al16(y)) return NR_EINVAL(2);
+  if (nseq == 0) return NR_OK;
+  MPArgs g{};
+  g.y = y; g.ldy = ldy; g.mask = mask; g.mask_dt = mask_dtype; g.nseq = nseq; g.L = L; g.heads = heads;
+  g.scale_attn = 1.0f / sqrtf((float)dk); g.scale_pool = 1.0f / sqrtf((float)(heads * dv));
+  g.gamma = gamma; g.beta = beta; g.eps = eps; g.p_drop = p_drop; g.seed = seed; g.offset = offset; g.q = q;
+  g.news = news; g.ldn = ldn; g.zout = zout; g.ldz = ldz; g.stats = stats; g.probs = probs;
+  return dispatch(g, dk, dv, false, stream);
+}
+
+extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const void* mask, int32_t mask_dtype, int64_t nseq,
+                               int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
+                               const float* beta, float p_drop, uint64_t seed, uint64_t offset, const float* q,
+                               const float* stats, const float* probs, const float* dnews, int64_t ldn,
+                               const float* dz, int64_t lddz, float* dy, int64_t lddy, float* dbias, float* dq,
+                               float* dgamma, float* dbeta, hipStream_t stream) {
+  if (L < 1 || L > 32 || heads < 1) return NR_EINVAL(0);
+  if (!y || !mask || !gamma || !beta || !q || !stats || !probs || !dnews || !dy || !dbias || !dq || !dgamma ||
+      !dbeta)
+    return NR_EINVAL(1);
+  if ((ldy & 3) || !al16(y)) return NR_EINVAL(2);
+  if (nseq == 0) return NR_OK;
+  MPArgs g{};
+  g.y = y; g.ldy = ldy; g.mask = mask; g.mask_dt = mask_dtype; g.nseq = nseq; g.L = L; g.heads = heads;
+  g.scale_attn = 1.0f / sqrtf((float)dk); g.scale_pool = 1.0f / sqrtf((float)(heads * dv));
+  g.gamma = gamma; g.beta = beta; g.p_drop = p_drop; g.seed = seed; g.offset = offset; g.q = q;
+  g.news = const_cast<float*>(dnews); g.ldn = ldn; g.stats = const_cast<float*>(stats);
+  g.probs = const_cast<float*>(probs); g.dz = dz; g.lddz = lddz; g.dy = dy; g.lddy = lddy; g.dbias = dbias;
+  g.dq = dq; g.dgamma = dgamma; g.dbeta = dbeta;
+  return dispatch(g, dk, dv, true, stream);
+}

@@ -26,9 +26,11 @@ def _empty(rows, cols, like, ld=None):
     return buf[:, :cols]
 
 
-def _split_k(m, n, k, target=640):
+def _split_k(m, n, k, slots=512):
+    """Split-K factor for a wgrad GEMM: fill the 256 CUs x 2 resident 128x128 blocks in ONE
+    wave (a 1.16-wave grid runs as two), keeping >= 512 k per split."""
     tiles = max(1, ((m + 127) // 128) * ((n + 127) // 128))
-    return int(max(1, min(64, target // tiles, k // 512)))
+    return int(max(1, min(64, slots // tiles, k // 512)))
 
 
 def _proj_wgrad(dY, X_op, dW, db, M_rows):
@@ -99,22 +101,29 @@ class MHANewsFn(torch.autograd.Function):
         K.gemm(T, NY, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(w_cat, L.KCONTIG),
                Y, bias=b_cat)
         PROBE.add("proj_fwd", ev0, PROBE.record())
-        O = _empty(T, H, table)
-        K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, O)
         news = _empty(n, H, table)
         probs = torch.empty(T, device=table.device)
         stats = torch.empty(T, 2, device=table.device)
         tok = _empty(T, H, table) if want_tokens else None
-        K.attn_pool_fwd(O, query, mask, n, seq_len, news, probs, gamma=gamma, beta=beta, stats=stats,
-                        p_drop=p_drop, seed=seed, offset=offset, zout=tok)
+        fused = K.mha_pool_supported(seq_len, heads, dk, dv)
+        if fused:
+            # attention + LN + dropout + pooling in one kernel per title; O stays in LDS
+            O = None
+            K.mha_pool_fwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, news, stats, probs,
+                           p_drop=p_drop, seed=seed, offset=offset, zout=tok)
+        else:
+            O = _empty(T, H, table)
+            K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, O)
+            K.attn_pool_fwd(O, query, mask, n, seq_len, news, probs, gamma=gamma, beta=beta, stats=stats,
+                            p_drop=p_drop, seed=seed, offset=offset, zout=tok)
         ctx.save_for_backward(table, ids, mask, w_cat, gamma, beta, query, Y, O, probs, stats)
-        ctx.cfg = (heads, dk, dv, seq_len, pad_row, p_drop, seed, offset)
+        ctx.cfg = (heads, dk, dv, seq_len, pad_row, p_drop, seed, offset, fused)
         return news, tok
 
     @staticmethod
     def backward(ctx, dnews, dtok):
         table, ids, mask, w_cat, gamma, beta, query, Y, O, probs, stats = ctx.saved_tensors
-        heads, dk, dv, seq_len, pad_row, p_drop, seed, offset = ctx.cfg
+        heads, dk, dv, seq_len, pad_row, p_drop, seed, offset, fused = ctx.cfg
         T = ids.numel()
         n = T // seq_len
         V, E = table.shape
@@ -122,23 +131,28 @@ class MHANewsFn(torch.autograd.Function):
         NQ = heads * dk
         NY = NQ + H
         dnews = dnews.contiguous()
-        dO = _empty(T, H, table)
         dq = torch.zeros(H, device=table.device)
         dgamma = torch.zeros(H, device=table.device)
         dbeta = torch.zeros(H, device=table.device)
-        K.attn_pool_bwd(O, query, mask, n, seq_len, probs, dnews, dO, dq, gamma=gamma, beta=beta, stats=stats,
-                        dgamma=dgamma, dbeta=dbeta, p_drop=p_drop, seed=seed, offset=offset,
-                        dz=dtok.contiguous() if dtok is not None else None)
         dY = _empty(T, NY, table)
-        K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
+        dz = dtok.contiguous() if dtok is not None else None
+        db = torch.zeros(NY, device=table.device)
+        if fused:
+            K.mha_pool_bwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, stats, probs, dnews, dY, db, dq,
+                           dgamma, dbeta, p_drop=p_drop, seed=seed, offset=offset, dz=dz)
+        else:
+            dO = _empty(T, H, table)
+            K.attn_pool_bwd(O, query, mask, n, seq_len, probs, dnews, dO, dq, gamma=gamma, beta=beta, stats=stats,
+                            dgamma=dgamma, dbeta=dbeta, p_drop=p_drop, seed=seed, offset=offset, dz=dz)
+            K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
+            K.colsum(dY, T, NY, db)
         dtable = None
         if ctx.needs_input_grad[0]:
             dtable = torch.zeros(V, E, device=table.device)
             K.gemm(T, E, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dtable,
                    epilogue=L.EPI_SCATTER, c_rows=K.rows_map(ids, L.ROWS_GATHER), pad_row=pad_row)
         dw = torch.zeros(NY, E, device=table.device)
-        db = torch.zeros(NY, device=table.device)
-        _proj_wgrad(dY, K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dw, db, T)
+        _proj_wgrad(dY, K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dw, None, T)
         return (dtable, None, None, dw, db, dgamma, dbeta, dq.view_as(query), None, None, None, None, None,
                 None, None, None, None)
 

@@ -256,3 +256,45 @@ def colsum(x, rows, cols, out):
     if out.numel() < cols:
         raise L.HipError("colsum: out too small")
     L.call("nr_colsum", L.ptr(x), x.stride(0), rows, cols, L.ptr(out), L.stream_ptr(x))
+
+
+MHA_POOL_SHAPES = {(64, 32, 384), (64, 64, 768), (64, 32, 256), (32, 32, 384)}
+
+
+def mha_pool_supported(seq_len, heads, dk, dv):
+    return seq_len <= 32 and (dk, dv, heads * dv) in MHA_POOL_SHAPES
+
+
+def mha_pool_fwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, news, stats, probs, eps=1e-5,
+                 p_drop=0.0, seed=0, offset=0, zout=None):
+    """Fused tied-QK attention + LayerNorm + dropout + query pooling per title."""
+    H = heads * dv
+    _f32(y, gamma, beta, q, news, stats, probs, zout)
+    _rows_ok(y, nseq * seq_len, heads * (dk + dv), "y")
+    if y.stride(0) % 4 or y.data_ptr() % 16:
+        raise L.HipError("mha_pool_fwd: y needs ld % 4 == 0 and 16-B alignment")
+    _rows_ok(news, nseq, H, "news")
+    _rows_ok(zout, nseq * seq_len, H, "zout")
+    if stats.numel() < 2 * nseq * seq_len or probs.numel() < nseq * seq_len:
+        raise L.HipError("mha_pool_fwd: stats/probs too small")
+    mp, mdt = mask_arg(mask, nseq * seq_len)
+    L.call("nr_mha_pool_fwd", L.ptr(y), y.stride(0), mp, mdt, nseq, seq_len, heads, dk, dv, L.ptr(gamma),
+           L.ptr(beta), eps, p_drop, seed, offset, L.ptr(q), L.ptr(news), news.stride(0), L.ptr(zout),
+           zout.stride(0) if zout is not None else 0, L.ptr(stats), L.ptr(probs), L.stream_ptr(y))
+
+
+def mha_pool_bwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, dbias, dq,
+                 dgamma, dbeta, p_drop=0.0, seed=0, offset=0, dz=None):
+    H = heads * dv
+    _f32(y, gamma, beta, q, stats, probs, dnews, dy, dbias, dq, dgamma, dbeta, dz)
+    _rows_ok(y, nseq * seq_len, heads * (dk + dv), "y")
+    _rows_ok(dy, nseq * seq_len, heads * (dk + dv), "dy")
+    _rows_ok(dnews, nseq, H, "dnews")
+    _rows_ok(dz, nseq * seq_len, H, "dz")
+    if dbias.numel() < heads * (dk + dv):
+        raise L.HipError("mha_pool_bwd: dbias too small")
+    mp, mdt = mask_arg(mask, nseq * seq_len)
+    L.call("nr_mha_pool_bwd", L.ptr(y), y.stride(0), mp, mdt, nseq, seq_len, heads, dk, dv, L.ptr(gamma),
+           L.ptr(beta), p_drop, seed, offset, L.ptr(q), L.ptr(stats), L.ptr(probs), L.ptr(dnews), dnews.stride(0),
+           L.ptr(dz), dz.stride(0) if dz is not None else 0, L.ptr(dy), dy.stride(0), L.ptr(dbias), L.ptr(dq),
+           L.ptr(dgamma), L.ptr(dbeta), L.stream_ptr(y))
