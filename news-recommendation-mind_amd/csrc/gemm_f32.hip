@@ -19,6 +19,8 @@
 // column tiles of one row panel run on the same XCD and share its L2.
 #include "common.h"
 #include "../../include/newsrec_hip.h"
+#include "gemm_fast.h"
+#include <stdlib.h>
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -285,6 +287,15 @@ int launch_kc(const Args& g, int ak, int bk, int splits, hipStream_t s) {
   return launch<BM, BN, false, false>(g, splits, s);
 }
 
+bool getenv_generic() {   // NR_GEMM_GENERIC=1 forces the generic kernel (A/B testing)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NR_GEMM_GENERIC");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 int pick_tile(int64_t n) {  // 64 or 128: least padding, ties -> 128
   const int64_t p64 = (n + 63) / 64 * 64, p128 = (n + 127) / 128 * 128;
   return p128 <= p64 ? 128 : 64;
@@ -316,6 +327,12 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
   if (g.kchunk == 0) g.kchunk = 32;
   const int splits = (int)((K + g.kchunk - 1) / g.kchunk) > 0 ? (int)((K + g.kchunk - 1) / g.kchunk) : 1;
 
+  if (!getenv_generic()) {
+    const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128) * splits;
+    const int fb = t128 >= 400 ? 128 : 64;
+    const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, fb, fb, stream);
+    if (rc != -1) return rc;
+  }
   int bm = pick_tile(M), bn = pick_tile(N);
   // small problems: prefer 64x64 tiles to fill the 256 CUs
   if ((int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * splits < 512) { bm = 64; bn = 64; }
