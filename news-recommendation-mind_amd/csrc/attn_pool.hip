@@ -30,6 +30,7 @@ struct PoolArgs {
   const float* gamma; const float* beta;  // NULL: no LayerNorm
   float eps;
   float p_drop; uint64_t seed; uint64_t offset;
+  uint32_t dkey, dthresh;                  // dropout key / threshold derived on the host
   int64_t nseq; int L; int D; float scale;
   float* out; int64_t ldo;
   float* zout; int64_t ldz;                // optional: write Z (the encoder's token output)
@@ -45,7 +46,7 @@ struct PoolArgs {
 
 __device__ __forceinline__ float drop_scale(const PoolArgs& g, int64_t elem) {
   if (g.p_drop <= 0.f) return 1.f;
-  return nr_dropout_keep(g.seed, g.offset + (uint64_t)elem, g.p_drop) ? 1.f / (1.f - g.p_drop) : 0.f;
+  return nr_dropout_keep(g.dkey, (uint32_t)elem, g.dthresh) ? 1.f / (1.f - g.p_drop) : 0.f;
 }
 
 // Stage Z rows of sequence `seq` in LDS (zs[l*D + d]); writes LN stats when `save`.
@@ -231,6 +232,7 @@ extern "C" int nr_attn_pool_fwd(const float* x, int64_t ldx, const float* key, i
   PoolArgs g{};
   g.x = x; g.ldx = ldx; g.key = key; g.ldk = ldk; g.q = q; g.mask = mask; g.mask_dt = mask_dtype;
   g.gamma = gamma; g.beta = beta; g.eps = eps; g.p_drop = p_drop; g.seed = seed; g.offset = offset;
+  g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop);
   g.nseq = nseq; g.L = L; g.D = D; g.scale = scale; g.out = out; g.ldo = ldo; g.stats = stats;
   g.probs = probs; g.zout = zout; g.ldz = ldz;
   if (smem_fwd(L, D) > 64 * 1024)
@@ -259,6 +261,7 @@ extern "C" int nr_attn_pool_bwd(const float* x, int64_t ldx, const float* key, i
   PoolArgs g{};
   g.x = x; g.ldx = ldx; g.key = key; g.ldk = ldk; g.q = q; g.mask = mask; g.mask_dt = mask_dtype;
   g.gamma = gamma; g.beta = beta; g.p_drop = p_drop; g.seed = seed; g.offset = offset;
+  g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop);
   g.nseq = nseq; g.L = L; g.D = D; g.scale = scale; g.stats = const_cast<float*>(stats);
   g.probs = const_cast<float*>(probs); g.dout = dout; g.lddo = lddo; g.dx = dx; g.lddx = lddx;
   g.dk = dk; g.lddk = lddk; g.key_tanh = key_tanh; g.dq = dq; g.dgamma = dgamma; g.dbeta = dbeta;

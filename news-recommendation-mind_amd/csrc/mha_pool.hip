@@ -22,6 +22,7 @@
 // tile, and accumulates the projection-bias gradient (column sums of dY) in the epilogue.
 #include "common.h"
 #include "../../include/newsrec_hip.h"
+#include <stdlib.h>
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -30,10 +31,11 @@ namespace {
 // row of accumulator register r in lane half h (32x32 C/D layout)
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// Orders one wave's LDS writes before its later LDS reads of other lanes' data.  A release
+// fence would also wait for every outstanding GLOBAL store of the wave (vmcnt(0)) and stall
+// the head loop on its own dY stores; only the LDS counter matters here.
 __device__ __forceinline__ void wave_lds_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 struct MPArgs {
@@ -43,6 +45,7 @@ struct MPArgs {
   float scale_attn, scale_pool;
   const float* gamma; const float* beta; float eps;
   float p_drop; uint64_t seed; uint64_t offset;
+  uint32_t dkey, dthresh;                  // dropout key / threshold derived on the host
   const float* q;                     // [H] query_words
   float* news; int64_t ldn;           // fwd out / bwd: dnews in (const)
   float* zout; int64_t ldz;           // fwd: optional token output Z
@@ -50,11 +53,12 @@ struct MPArgs {
   const float* dz; int64_t lddz;      // bwd: optional grad of Z
   float* dy; int64_t lddy;            // bwd: [T][heads*dk + heads*dv]
   float* dbias; float* dq; float* dgamma; float* dbeta;
+  int dbg;                            // timing-only ablations (NR_DEBUG_MHAPOOL): 1 = skip attention, 2 = skip LN/pool
 };
 
 __device__ __forceinline__ float drop_scale(const MPArgs& g, int64_t elem) {
   if (g.p_drop <= 0.f) return 1.f;
-  return nr_dropout_keep(g.seed, g.offset + (uint64_t)elem, g.p_drop) ? 1.f / (1.f - g.p_drop) : 0.f;
+  return nr_dropout_keep(g.dkey, (uint32_t)elem, g.dthresh) ? 1.f / (1.f - g.p_drop) : 0.f;
 }
 
 __device__ __forceinline__ uint64_t token_bits(const MPArgs& g, int64_t seq) {
@@ -63,23 +67,33 @@ __device__ __forceinline__ uint64_t token_bits(const MPArgs& g, int64_t seq) {
   return __ballot(m);
 }
 
-// S and P of one head for this lane's row c = lane & 31; returns P in p[16] (C layout).
+// Loads this lane's half of key row c = lane & 31 for one head (see below for the order).
 template <int DK>
-__device__ __forceinline__ void head_probs(const MPArgs& g, int64_t seq, int head, uint64_t bits, float (&p)[16]) {
+__device__ __forceinline__ void load_krow(const MPArgs& g, int64_t seq, int head, float (&a)[DK / 2]) {
   const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
   constexpr int HK = DK / 2;
-  float a[HK];
-  if (c < g.L) {
-    const float* kr = g.y + (seq * g.L + c) * g.ldy + head * DK + h * HK;
+  {
+    // lane (c, h) takes the 16-B chunks 2*s4 + h of row c: the two halves of the wave read the
+    // two halves of the same 32-B span (the k order inside S = K Kᵀ is free).  Rows past L are
+    // clamped and zeroed by a select, never a branch: a branch around a load makes hipcc wait
+    // for it at the join, serialising the whole load stream.
+    const bool ok = c < g.L;
+    const float* kr = g.y + (seq * g.L + (ok ? c : 0)) * g.ldy + head * DK + 4 * h;
 #pragma unroll
     for (int s = 0; s < HK; s += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(kr + s);
-      a[s] = v.x; a[s + 1] = v.y; a[s + 2] = v.z; a[s + 3] = v.w;
+      const float4 v = *reinterpret_cast<const float4*>(kr + 2 * s);
+      a[s] = ok ? v.x : 0.f; a[s + 1] = ok ? v.y : 0.f; a[s + 2] = ok ? v.z : 0.f; a[s + 3] = ok ? v.w : 0.f;
     }
-  } else {
-#pragma unroll
-    for (int s = 0; s < HK; ++s) a[s] = 0.f;
   }
+}
+
+// S and P of one head for this lane's row c = lane & 31 from its key half-row a[];
+// returns P in p[16] (C layout).
+template <int DK>
+__device__ __forceinline__ void head_probs_from(const MPArgs& g, uint64_t bits, const float (&a)[DK / 2],
+                                                float (&p)[16]) {
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  constexpr int HK = DK / 2;
   f32x16 S;
 #pragma unroll
   for (int r = 0; r < 16; ++r) S[r] = 0.f;
@@ -107,23 +121,40 @@ __device__ __forceinline__ void head_probs(const MPArgs& g, int64_t seq, int hea
   for (int r = 0; r < 16; ++r) p[r] *= inv;
 }
 
-// O_h = P V_h into the LDS image os[32][so] at columns head*DV ..
+template <int DK>
+__device__ __forceinline__ void head_probs(const MPArgs& g, int64_t seq, int head, uint64_t bits, float (&p)[16]) {
+  float a[DK / 2];
+  load_krow<DK>(g, seq, head, a);
+  head_probs_from<DK>(g, bits, a, p);
+}
+
+// V operand of O = P V: lane (c, h) needs V[crow(s, h)][vb*32 + c] (rows past L -> 0)
 template <int DK, int DV>
-__device__ __forceinline__ void head_out(const MPArgs& g, int64_t seq, int head, const float (&p)[16], float* os,
-                                         int so) {
+__device__ __forceinline__ void load_vop(const MPArgs& g, int64_t seq, int head, float (&bv)[DV / 2]) {
   const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
   const int nq = g.heads * DK;
+#pragma unroll
+  for (int vb = 0; vb < DV / 32; ++vb)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = crow(s, h);
+      const float v = g.y[(seq * g.L + (k < g.L ? k : 0)) * g.ldy + nq + head * DV + vb * 32 + c];
+      bv[vb * 16 + s] = k < g.L ? v : 0.f;
+    }
+}
+
+// O_h = P V_h into the LDS image os[32][so] at columns head*DV ..
+template <int DK, int DV>
+__device__ __forceinline__ void head_out(const float (&bv)[DV / 2], int head, const float (&p)[16], float* os,
+                                         int so) {
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int vb = 0; vb < DV / 32; ++vb) {
     f32x16 O;
 #pragma unroll
     for (int r = 0; r < 16; ++r) O[r] = 0.f;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int k = crow(s, h);
-      const float bv = k < g.L ? g.y[(seq * g.L + k) * g.ldy + nq + head * DV + vb * 32 + c] : 0.f;
-      O = __builtin_amdgcn_mfma_f32_32x32x2f32(p[s], bv, O, 0, 0, 0);
-    }
+    for (int s = 0; s < 16; ++s) O = __builtin_amdgcn_mfma_f32_32x32x2f32(p[s], bv[vb * 16 + s], O, 0, 0, 0);
 #pragma unroll
     for (int r = 0; r < 16; ++r) os[crow(r, h) * so + head * DV + vb * 32 + c] = O[r];
   }
@@ -133,26 +164,38 @@ template <int DK, int DV>
 __device__ void attention_to_lds(const MPArgs& g, int64_t seq, uint64_t bits, float* os, int so) {
   const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int head = w; head < g.heads; head += nw) {
+    // issue the key and value loads together: one memory latency per head, not two
+    float a[DK / 2], bv[DV / 2];
+    load_krow<DK>(g, seq, head, a);
+    load_vop<DK, DV>(g, seq, head, bv);
     float p[16];
-    head_probs<DK>(g, seq, head, bits, p);
-    head_out<DK, DV>(g, seq, head, p, os, so);
+    head_probs_from<DK>(g, bits, a, p);
+    head_out<DK, DV>(bv, head, p, os, so);
   }
 }
 
 template <int DK, int DV, int NH64>
-__global__ __launch_bounds__(256) void mha_pool_fwd_kernel(MPArgs g) {
+__global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int H = NH64 * 64;
   constexpr int SO = H + 1;
   float* os = sm;                       // [32][SO]  O, then Z
   float* sc = os + 32 * SO;             // [32] scores -> probs
   const int64_t seq = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
   const uint64_t bits = token_bits(g, seq);
-  attention_to_lds<DK, DV>(g, seq, bits, os, SO);
+  float gam[NH64], bet[NH64], qv[NH64];
+#pragma unroll
+  for (int k = 0; k < NH64; ++k) {
+    gam[k] = g.gamma[lane + 64 * k];
+    bet[k] = g.beta[lane + 64 * k];
+    qv[k] = g.q[lane + 64 * k];
+  }
+  if (!(g.dbg & 1)) attention_to_lds<DK, DV>(g, seq, bits, os, SO);
   __syncthreads();
+  if (g.dbg & 2) return;
   // LayerNorm + dropout in place, scores; one wave per row
-  for (int l = w; l < g.L; l += 4) {
+  for (int l = w; l < g.L; l += nw) {
     const int64_t row = seq * g.L + l;
     float x[NH64];
     float s = 0.f;
@@ -167,10 +210,10 @@ __global__ __launch_bounds__(256) void mha_pool_fwd_kernel(MPArgs g) {
 #pragma unroll
     for (int k = 0; k < NH64; ++k) {
       const int d = lane + 64 * k;
-      const float z = ((x[k] - mean) * rstd * g.gamma[d] + g.beta[d]) * drop_scale(g, row * H + d);
+      const float z = ((x[k] - mean) * rstd * gam[k] + bet[k]) * drop_scale(g, row * H + d);
       os[l * SO + d] = z;
       if (g.zout) g.zout[row * g.ldz + d] = z;
-      dot = fmaf(g.q[d], z, dot);
+      dot = fmaf(qv[k], z, dot);
     }
     dot = nr_wave_sum(dot);
     if (lane == 0) {
@@ -193,7 +236,7 @@ __global__ __launch_bounds__(256) void mha_pool_fwd_kernel(MPArgs g) {
     }
   }
   __syncthreads();
-  for (int d = tid; d < H; d += 256) {
+  for (int d = tid; d < H; d += nt) {
     float acc = 0.f;
     for (int l = 0; l < g.L; ++l) acc = fmaf(sc[l], os[l * SO + d], acc);
     g.news[seq * g.ldn + d] = acc;
@@ -201,37 +244,45 @@ __global__ __launch_bounds__(256) void mha_pool_fwd_kernel(MPArgs g) {
 }
 
 template <int DK, int DV, int NH64>
-__global__ __launch_bounds__(256) void mha_pool_bwd_kernel(MPArgs g) {
+__global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int H = NH64 * 64;
   constexpr int SO = H + 1;
+  const int nw = blockDim.x >> 6, nt = blockDim.x;
   float* os = sm;                       // [32][SO]  O, then dO
-  float* ts = os + 32 * SO;             // [4][32][33] per-wave transpose tiles
-  float* ps = ts + 4 * 32 * 33;         // [32] pooling probs
+  float* ps = os + 32 * SO;             // [32] pooling probs
   float* ds = ps + 32;                  // [32] dp -> ds
   float* st = ds + 32;                  // [32][2] mean, rstd
-  float* red = st + 64;                 // [4][2][H] per-wave dgamma / dbeta partials
+  float* ts = st + 64;                  // [nw][32][33] per-wave transpose tiles
+  float* red = ts;                      // [nw][2][H] dgamma / dbeta partials (before ts is used)
   const int64_t seq = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
   const uint64_t bits = token_bits(g, seq);
-  attention_to_lds<DK, DV>(g, seq, bits, os, SO);
+  float gam[NH64], bet[NH64], qv[NH64], dnv[NH64];
+#pragma unroll
+  for (int k = 0; k < NH64; ++k) {
+    gam[k] = g.gamma[lane + 64 * k];
+    bet[k] = g.beta[lane + 64 * k];
+    qv[k] = g.q[lane + 64 * k];
+    dnv[k] = g.news[seq * g.ldn + lane + 64 * k];
+  }
+  if (!(g.dbg & 1)) attention_to_lds<DK, DV>(g, seq, bits, os, SO);
   if (tid < 32) {
     ps[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
     st[2 * tid] = tid < g.L ? g.stats[2 * (seq * g.L + tid)] : 0.f;
     st[2 * tid + 1] = tid < g.L ? g.stats[2 * (seq * g.L + tid) + 1] : 0.f;
   }
   __syncthreads();
-  const float* dnews = g.news + seq * g.ldn;
   // (B1) dp_l = dnews · Z_l
-  for (int l = w; l < g.L; l += 4) {
+  for (int l = w; l < g.L; l += nw) {
     const int64_t row = seq * g.L + l;
     const float mean = st[2 * l], rstd = st[2 * l + 1];
     float dot = 0.f;
 #pragma unroll
     for (int k = 0; k < NH64; ++k) {
       const int d = lane + 64 * k;
-      const float z = ((os[l * SO + d] - mean) * rstd * g.gamma[d] + g.beta[d]) * drop_scale(g, row * H + d);
-      dot = fmaf(dnews[d], z, dot);
+      const float z = ((os[l * SO + d] - mean) * rstd * gam[k] + bet[k]) * drop_scale(g, row * H + d);
+      dot = fmaf(dnv[k], z, dot);
     }
     dot = nr_wave_sum(dot);
     if (lane == 0) ds[l] = dot;
@@ -245,10 +296,11 @@ __global__ __launch_bounds__(256) void mha_pool_bwd_kernel(MPArgs g) {
   }
   __syncthreads();
   // (B3) dq[d] += Σ_l ds_l Z_l[d]
-  for (int d = tid; d < H; d += 256) {
+  for (int d = tid; d < H; d += nt) {
     float acc = 0.f;
+    const float gd = g.gamma[d], bd = g.beta[d];
     for (int l = 0; l < g.L; ++l) {
-      const float z = ((os[l * SO + d] - st[2 * l]) * st[2 * l + 1] * g.gamma[d] + g.beta[d]) *
+      const float z = ((os[l * SO + d] - st[2 * l]) * st[2 * l + 1] * gd + bd) *
                       drop_scale(g, (seq * g.L + l) * H + d);
       acc = fmaf(ds[l], z, acc);
     }
@@ -259,7 +311,7 @@ __global__ __launch_bounds__(256) void mha_pool_bwd_kernel(MPArgs g) {
   float dgam[NH64], dbet[NH64];
 #pragma unroll
   for (int k = 0; k < NH64; ++k) { dgam[k] = 0.f; dbet[k] = 0.f; }
-  for (int l = w; l < g.L; l += 4) {
+  for (int l = w; l < g.L; l += nw) {
     const int64_t row = seq * g.L + l;
     const float mean = st[2 * l], rstd = st[2 * l + 1], pl = ps[l], dsl = ds[l];
     float xh[NH64], dyv[NH64];
@@ -267,11 +319,11 @@ __global__ __launch_bounds__(256) void mha_pool_bwd_kernel(MPArgs g) {
 #pragma unroll
     for (int k = 0; k < NH64; ++k) {
       const int d = lane + 64 * k;
-      float dz = fmaf(pl, dnews[d], dsl * g.q[d]);
+      float dz = fmaf(pl, dnv[k], dsl * qv[k]);
       if (g.dz) dz += g.dz[row * g.lddz + d];
       dyv[k] = dz * drop_scale(g, row * H + d);
       xh[k] = (os[l * SO + d] - mean) * rstd;
-      const float gg = dyv[k] * g.gamma[d];
+      const float gg = dyv[k] * gam[k];
       sg += gg;
       sgx = fmaf(gg, xh[k], sgx);
       dgam[k] = fmaf(dyv[k], xh[k], dgam[k]);
@@ -282,7 +334,7 @@ __global__ __launch_bounds__(256) void mha_pool_bwd_kernel(MPArgs g) {
 #pragma unroll
     for (int k = 0; k < NH64; ++k) {
       const int d = lane + 64 * k;
-      os[l * SO + d] = rstd * (dyv[k] * g.gamma[d] - sg - xh[k] * sgx);
+      os[l * SO + d] = rstd * (dyv[k] * gam[k] - sg - xh[k] * sgx);
     }
   }
 #pragma unroll
@@ -291,45 +343,75 @@ __global__ __launch_bounds__(256) void mha_pool_bwd_kernel(MPArgs g) {
     red[(w * 2 + 1) * H + lane + 64 * k] = dbet[k];
   }
   __syncthreads();
-  for (int d = tid; d < H; d += 256) {
+  for (int d = tid; d < H; d += nt) {
     float a = 0.f, b = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww) { a += red[(ww * 2) * H + d]; b += red[(ww * 2 + 1) * H + d]; }
+    for (int ww = 0; ww < nw; ++ww) { a += red[(ww * 2) * H + d]; b += red[(ww * 2 + 1) * H + d]; }
     atomicAdd(&g.dgamma[d], a);
     atomicAdd(&g.dbeta[d], b);
   }
+  __syncthreads();   // red aliases the transpose tiles
+  if (g.dbg & 4) return;
   // (C) attention backward per head
   const int nq = g.heads * DK;
   float* tw = ts + w * 32 * 33;
-  for (int head = w; head < g.heads; head += 4) {
+  for (int head = w; head < g.heads; head += nw) {
     float p[16];
     head_probs<DK>(g, seq, head, bits, p);
-    // dPᵀ = V dOᵀ  (lane (c, h): V[c][h*DV/2 + s], dO[c][h*DV/2 + s])
-    f32x16 dpt;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dpt[r] = 0.f;
+    // dVp = Pᵀ dO first (P is live anyway): Pᵀ through the transpose tile, dO from LDS
     {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tw[c * 33 + crow(r, h)] = p[r];
+      wave_lds_fence();
+      float pt[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) pt[s] = tw[crow(s, h) * 33 + c];
+      wave_lds_fence();
+#pragma unroll
+      for (int vb = 0; vb < DV / 32; ++vb) {
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pt[s], os[crow(s, h) * SO + head * DV + vb * 32 + c], acc, 0, 0, 0);
+        float cs = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = crow(r, h);
+          if (i < g.L) g.dy[(seq * g.L + i) * g.lddy + nq + head * DV + vb * 32 + c] = acc[r];
+          cs += acc[r];
+        }
+        cs += __shfl_xor(cs, 32, 64);
+        if (h == 0) atomicAdd(&g.dbias[nq + head * DV + vb * 32 + c], cs);
+      }
+    }
+    // dPᵀ = V dOᵀ  (lane (c, h): V[c][k], dO[c][k] over the interleaved k order)
+    float dsv[16];
+    {
+      f32x16 dpt;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dpt[r] = 0.f;
       constexpr int HV = DV / 2;
-      const float* vr = g.y + (seq * g.L + c) * g.ldy + nq + head * DV + h * HV;
+      const float* vr = g.y + (seq * g.L + c) * g.ldy + nq + head * DV + 4 * h;
       const bool rv = c < g.L;
+      const float* vrr = rv ? vr : vr - (int64_t)c * g.ldy;   // clamp to row 0, zero by select
 #pragma unroll
       for (int s = 0; s < HV; s += 4) {
-        float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (rv) v4 = *reinterpret_cast<const float4*>(vr + s);
-        const float* dor = os + c * SO + head * DV + h * HV + s;
+        float4 v4 = *reinterpret_cast<const float4*>(vrr + 2 * s);
+        if (!rv) v4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float* dor = os + c * SO + head * DV + 4 * h + 2 * s;
         dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.x, dor[0], dpt, 0, 0, 0);
         dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.y, dor[1], dpt, 0, 0, 0);
         dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.z, dor[2], dpt, 0, 0, 0);
         dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.w, dor[3], dpt, 0, 0, 0);
       }
+      float rs = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) rs = fmaf(p[r], dpt[r], rs);
+      rs += __shfl_xor(rs, 32, 64);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dsv[r] = p[r] * (dpt[r] - rs) * g.scale_attn;
     }
-    float rs = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) rs = fmaf(p[r], dpt[r], rs);
-    rs += __shfl_xor(rs, 32, 64);
-    float dsv[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dsv[r] = p[r] * (dpt[r] - rs) * g.scale_attn;
     // W = dS + dSᵀ via the per-wave transpose tile
 #pragma unroll
     for (int r = 0; r < 16; ++r) tw[c * 33 + crow(r, h)] = dsv[r];
@@ -340,15 +422,18 @@ __global__ __launch_bounds__(256) void mha_pool_bwd_kernel(MPArgs g) {
     // dKp = W Kp  -> dY[:, head*DK ..]
 #pragma unroll
     for (int kb = 0; kb < DK / 32; ++kb) {
+      float bk[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int k = crow(s, h);
+        const float v = g.y[(seq * g.L + (k < g.L ? k : 0)) * g.ldy + head * DK + kb * 32 + c];
+        bk[s] = k < g.L ? v : 0.f;
+      }
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int k = crow(s, h);
-        const float bk = k < g.L ? g.y[(seq * g.L + k) * g.ldy + head * DK + kb * 32 + c] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(dsv[s], bk, acc, 0, 0, 0);
-      }
+      for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(dsv[s], bk[s], acc, 0, 0, 0);
       float cs = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -359,53 +444,33 @@ __global__ __launch_bounds__(256) void mha_pool_bwd_kernel(MPArgs g) {
       cs += __shfl_xor(cs, 32, 64);
       if (h == 0) atomicAdd(&g.dbias[head * DK + kb * 32 + c], cs);
     }
-    // dVp = Pᵀ dO: Pᵀ through the transpose tile, dO from the LDS image
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tw[c * 33 + crow(r, h)] = p[r];
-    wave_lds_fence();
-    float pt[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) pt[s] = tw[crow(s, h) * 33 + c];
-    wave_lds_fence();
-#pragma unroll
-    for (int vb = 0; vb < DV / 32; ++vb) {
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-      for (int s = 0; s < 16; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pt[s], os[crow(s, h) * SO + head * DV + vb * 32 + c], acc, 0, 0, 0);
-      float cs = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = crow(r, h);
-        if (i < g.L) g.dy[(seq * g.L + i) * g.lddy + nq + head * DV + vb * 32 + c] = acc[r];
-        cs += acc[r];
-      }
-      cs += __shfl_xor(cs, 32, 64);
-      if (h == 0) atomicAdd(&g.dbias[nq + head * DV + vb * 32 + c], cs);
-    }
   }
 }
 
 size_t fwd_smem(int H) { return (size_t)(32 * (H + 1) + 32) * sizeof(float); }
-size_t bwd_smem(int H) { return (size_t)(32 * (H + 1) + 4 * 32 * 33 + 32 + 32 + 64 + 8 * H) * sizeof(float); }
+size_t bwd_smem(int H, int nw) {
+  const size_t tiles = (size_t)nw * 32 * 33, red = (size_t)nw * 2 * H;
+  return (size_t)(32 * (H + 1) + 32 + 32 + 64 + (tiles > red ? tiles : red)) * sizeof(float);
+}
 
 template <int DK, int DV, int NH64>
 int launch(const MPArgs& g, bool bwd, hipStream_t s) {
   const int H = NH64 * 64;
+  // forward: one wave per head (>= 4 waves for the LN phase); backward: one wave per two heads
+  // (its per-head state needs ~200 VGPRs, more than a 12-wave workgroup can give a wave)
+  const int nw = bwd ? ((g.heads + 1) / 2 < 4 ? 4 : (g.heads + 1) / 2) : (g.heads < 4 ? 4 : g.heads);
   if (bwd) {
-    const size_t sz = bwd_smem(H);
+    const size_t sz = bwd_smem(H, nw);
     if (sz > 64 * 1024)
-      hipFuncSetAttribute((const void*)mha_pool_bwd_kernel<DK, DV, NH64>,
+      (void)hipFuncSetAttribute((const void*)mha_pool_bwd_kernel<DK, DV, NH64>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)sz);
-    hipLaunchKernelGGL((mha_pool_bwd_kernel<DK, DV, NH64>), dim3((unsigned)g.nseq), dim3(256), sz, s, g);
+    hipLaunchKernelGGL((mha_pool_bwd_kernel<DK, DV, NH64>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
   } else {
     const size_t sz = fwd_smem(H);
     if (sz > 64 * 1024)
-      hipFuncSetAttribute((const void*)mha_pool_fwd_kernel<DK, DV, NH64>,
+      (void)hipFuncSetAttribute((const void*)mha_pool_fwd_kernel<DK, DV, NH64>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)sz);
-    hipLaunchKernelGGL((mha_pool_fwd_kernel<DK, DV, NH64>), dim3((unsigned)g.nseq), dim3(256), sz, s, g);
+    hipLaunchKernelGGL((mha_pool_fwd_kernel<DK, DV, NH64>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
   }
   NR_LAUNCH_CHECK();
   return NR_OK;
@@ -434,15 +499,20 @@ extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const void* mask, in
                                const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset,
                                const float* q, float* news, int64_t ldn, float* zout, int64_t ldz, float* stats,
                                float* probs, hipStream_t stream) {
-  if (L < 1 || L > 32 || heads < 1) return NR_EINVAL(0);
+  if (L < 1 || L > 32 || heads < 1 || heads > 12) return NR_EINVAL(0);
   if (!y || !mask || !gamma || !beta || !q || !news || !stats || !probs) return NR_EINVAL(1);
   if ((ldy & 3) || !al16(y)) return NR_EINVAL(2);
   if (nseq == 0) return NR_OK;
   MPArgs g{};
   g.y = y; g.ldy = ldy; g.mask = mask; g.mask_dt = mask_dtype; g.nseq = nseq; g.L = L; g.heads = heads;
   g.scale_attn = 1.0f / sqrtf((float)dk); g.scale_pool = 1.0f / sqrtf((float)(heads * dv));
-  g.gamma = gamma; g.beta = beta; g.eps = eps; g.p_drop = p_drop; g.seed = seed; g.offset = offset; g.q = q;
+  g.gamma = gamma; g.beta = beta; g.eps = eps; g.p_drop = p_drop; g.seed = seed; g.offset = offset;
+  g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop); g.q = q;
   g.news = news; g.ldn = ldn; g.zout = zout; g.ldz = ldz; g.stats = stats; g.probs = probs;
+  {
+    const char* e = getenv("NR_DEBUG_MHAPOOL");
+    g.dbg = e ? atoi(e) : 0;
+  }
   return dispatch(g, dk, dv, false, stream);
 }
 
@@ -452,7 +522,7 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const void* mask, in
                                const float* stats, const float* probs, const float* dnews, int64_t ldn,
                                const float* dz, int64_t lddz, float* dy, int64_t lddy, float* dbias, float* dq,
                                float* dgamma, float* dbeta, hipStream_t stream) {
-  if (L < 1 || L > 32 || heads < 1) return NR_EINVAL(0);
+  if (L < 1 || L > 32 || heads < 1 || heads > 12) return NR_EINVAL(0);
   if (!y || !mask || !gamma || !beta || !q || !stats || !probs || !dnews || !dy || !dbias || !dq || !dgamma ||
       !dbeta)
     return NR_EINVAL(1);
@@ -461,9 +531,14 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const void* mask, in
   MPArgs g{};
   g.y = y; g.ldy = ldy; g.mask = mask; g.mask_dt = mask_dtype; g.nseq = nseq; g.L = L; g.heads = heads;
   g.scale_attn = 1.0f / sqrtf((float)dk); g.scale_pool = 1.0f / sqrtf((float)(heads * dv));
-  g.gamma = gamma; g.beta = beta; g.p_drop = p_drop; g.seed = seed; g.offset = offset; g.q = q;
+  g.gamma = gamma; g.beta = beta; g.p_drop = p_drop; g.seed = seed; g.offset = offset;
+  g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop); g.q = q;
   g.news = const_cast<float*>(dnews); g.ldn = ldn; g.stats = const_cast<float*>(stats);
   g.probs = const_cast<float*>(probs); g.dz = dz; g.lddz = lddz; g.dy = dy; g.lddy = lddy; g.dbias = dbias;
   g.dq = dq; g.dgamma = dgamma; g.dbeta = dbeta;
+  {
+    const char* e = getenv("NR_DEBUG_MHAPOOL");
+    g.dbg = e ? atoi(e) : 0;
+  }
   return dispatch(g, dk, dv, true, stream);
 }

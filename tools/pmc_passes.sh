@@ -1,0 +1,17 @@
+#!/bin/bash
+# Collect PMC counters for a python command in separate rocprofv3 passes (kernel-trace only,
+# never combined with sys/runtime traces).  Usage: tools/pmc_passes.sh OUTDIR cmd...
+set -e
+OUT=$1; shift
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM SQ_WAVES"
+P2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU"
+P3="TCC_EA0_RDREQ TCC_EA0_WRREQ TCC_HIT TCC_MISS"
+P4="FETCH_SIZE"
+P5="WRITE_SIZE GRBM_GUI_ACTIVE"
+i=0
+for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
+  i=$((i+1))
+  timeout -k 10 200 rocprofv3 --pmc $P --output-format csv -d "$OUT/p$i" -o run -- "$@" > "$OUT/p$i.log" 2>&1
+done
