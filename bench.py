@@ -70,19 +70,15 @@ def make_optim(model):
     return get_optim(model)
 
 
-def train_step(model, opt, x, world):
+def train_step(model, opt, x, sync):
+    """utils/Manager.py:636-647 with the DDP gradient mean (GradSync: the word-table gradient's
+    all-reduce starts inside the backward; 1/world folded into Adam)."""
     opt.zero_grad(set_to_none=True)
     logits, _ = model(x)
     loss = torch.nn.functional.nll_loss(logits, x["label"])
     loss.backward()
-    if world > 1:
-        works = [dist.all_reduce(p.grad, async_op=True) for p in model.parameters() if p.grad is not None]
-        for w in works:
-            w.wait()
-        for p in model.parameters():
-            if p.grad is not None:
-                p.grad.mul_(1.0 / world)
-    opt.step()
+    scale = sync() if sync is not None else 1.0
+    opt.step(grad_scale=scale)
     return loss
 
 
@@ -121,11 +117,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU over RCCL; NR_DIST_BACKEND=gloo lets a 1-GPU box rehearse the N > 1 path
+    backend = os.environ.get("NR_DIST_BACKEND", "nccl")
+    dev_index = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev_index)
+        kw = {"device_id": torch.device("cuda", dev_index)} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    dev = torch.device("cuda", dev_index)
+    from newsrec_amd.dist import GradSync
     torch.cuda.set_device(dev)
 
     from newsrec_amd import functions as F
@@ -136,11 +137,12 @@ def main():
             for p in model.parameters():
                 dist.broadcast(p, 0)
     opt = make_optim(model)
+    sync = GradSync(model) if world > 1 else None
     gen = torch.Generator().manual_seed(1234 + rank)
     batches = [synth_batch(gen, dev) for _ in range(4)]
 
     for i in range(a.warmup):
-        train_step(model, opt, batches[i % len(batches)], world)
+        train_step(model, opt, batches[i % len(batches)], sync)
     torch.cuda.synchronize()
 
     # per-launch timing of the dominant kernel (the fused gather + key/value projection GEMM)
@@ -150,7 +152,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        train_step(model, opt, batches[i % len(batches)], world)
+        train_step(model, opt, batches[i % len(batches)], sync)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

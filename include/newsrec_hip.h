@@ -185,10 +185,12 @@ int nr_score_bwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
                  hipStream_t stream);
 
 /* One torch.optim.Adam step (amsgrad=False) on n contiguous fp32 elements; `step` is the
- * 1-based step count after increment (bias corrections as torch).  Manager.py:404-413,647. */
+ * 1-based step count after increment (bias corrections as torch).  The gradient is read as
+ * grad * grad_scale (1/world_size folds the data-parallel mean into the update).
+ * Manager.py:404-413,647. */
 int nr_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
             float lr, float beta1, float beta2, float eps, float weight_decay, int64_t step,
-            hipStream_t stream);
+            float grad_scale, hipStream_t stream);
 
 /* out[i] = table[idx[i]] rows of E floats (E % 4 == 0).  BERT_Embedding.forward, BERT.py:39. */
 int nr_embedding_fwd(const float* table, int64_t V, int64_t E, const int64_t* idx, int64_t n,

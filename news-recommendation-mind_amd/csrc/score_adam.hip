@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void score_bwd_kernel(const float* cdd, int64_
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                    float step, float b1, float b2, float eps,
-                                                   float bc2_sqrt, float wd) {
+                                                   float bc2_sqrt, float wd, float gscale) {
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     float4 vv = reinterpret_cast<float4*>(v)[i];
 #define NR_ADAM1(c)                                            \
     {                                                          \
-      float gc = gg.c;                                         \
+      float gc = gg.c * gscale;                                \
       if (wd != 0.f) gc = fmaf(wd, pp.c, gc);                  \
       mm.c = fmaf(1.f - b1, gc - mm.c, mm.c);                  \
       vv.c = fmaf(vv.c, b2, (1.f - b2) * gc * gc);             \
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     reinterpret_cast<float4*>(v)[i] = vv;
   }
   for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    float gc = g[i];
+    float gc = g[i] * gscale;
     if (wd != 0.f) gc = fmaf(wd, p[i], gc);
     m[i] = fmaf(1.f - b1, gc - m[i], m[i]);
     v[i] = fmaf(v[i], b2, (1.f - b2) * gc * gc);
@@ -185,7 +185,7 @@ extern "C" int nr_score_bwd(const float* cdd, int64_t ldc, const float* user, in
 
 extern "C" int nr_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                        float lr, float beta1, float beta2, float eps, float weight_decay, int64_t step,
-                       hipStream_t stream) {
+                       float grad_scale, hipStream_t stream) {
   if (n < 0 || step < 1) return NR_EINVAL(0);
   if (!param || !grad || !exp_avg || !exp_avg_sq) return NR_EINVAL(1);
   if ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
@@ -199,7 +199,7 @@ extern "C" int nr_adam(float* param, const float* grad, float* exp_avg, float* e
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, param, grad, exp_avg,
-                     exp_avg_sq, n, (float)((double)lr / bc1), beta1, beta2, eps, (float)sqrt(bc2), weight_decay);
+                     exp_avg_sq, n, (float)((double)lr / bc1), beta1, beta2, eps, (float)sqrt(bc2), weight_decay, grad_scale);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

@@ -54,7 +54,7 @@ _SIGS = {
     "nr_score_fwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i64, c_i32, c_i32, c_i32, c_ptr, c_ptr],
     "nr_score_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i32, c_i32, c_i32, c_ptr, c_i64, c_ptr,
                      c_i64, c_ptr],
-    "nr_adam": [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_ptr],
+    "nr_adam": [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_f32, c_ptr],
     "nr_embedding_fwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr],
     "nr_embedding_bwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_ptr],
     "nr_colsum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr],

@@ -80,6 +80,25 @@ class _Probe:
 PROBE = _Probe()
 
 
+class _TableGradHook:
+    """Optional callback ``hook(table_param, dtable) -> bool`` run inside a news-tower backward
+    as soon as the dense word-table gradient exists (before the weight-gradient GEMMs).  When it
+    returns True it has taken ownership (e.g. started an async all-reduce and will install the
+    gradient itself) and the Function returns None for the table."""
+
+    def __init__(self):
+        self.fn = None
+
+    def set(self, fn):
+        self.fn = fn
+
+    def __call__(self, table, dtable):
+        return bool(self.fn(table, dtable)) if self.fn is not None else False
+
+
+TABLE_GRAD_HOOK = _TableGradHook()
+
+
 # ---------------------------------------------------------------------- MHA news encoder
 
 class MHANewsFn(torch.autograd.Function):
@@ -118,6 +137,7 @@ class MHANewsFn(torch.autograd.Function):
                             p_drop=p_drop, seed=seed, offset=offset, zout=tok)
         ctx.save_for_backward(table, ids, mask, w_cat, gamma, beta, query, Y, O, probs, stats)
         ctx.cfg = (heads, dk, dv, seq_len, pad_row, p_drop, seed, offset, fused)
+        ctx.table_ref = table
         return news, tok
 
     @staticmethod
@@ -151,6 +171,8 @@ class MHANewsFn(torch.autograd.Function):
             dtable = torch.zeros(V, E, device=table.device)
             K.gemm(T, E, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dtable,
                    epilogue=L.EPI_SCATTER, c_rows=K.rows_map(ids, L.ROWS_GATHER), pad_row=pad_row)
+            if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
+                dtable = None
         dw = torch.zeros(NY, E, device=table.device)
         _proj_wgrad(dY, K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dw, None, T)
         return (dtable, None, None, dw, db, dgamma, dbeta, dq.view_as(query), None, None, None, None, None,
@@ -181,6 +203,7 @@ class CNNNewsFn(torch.autograd.Function):
         K.attn_pool_fwd(C, query, mask, n, seq_len, news, probs, key=Kq)
         ctx.save_for_backward(table, ids, mask, w3, wq, query, C, Kq, probs)
         ctx.cfg = (seq_len, pad_row)
+        ctx.table_ref = table
         return news, C
 
     @staticmethod
@@ -214,6 +237,8 @@ class CNNNewsFn(torch.autograd.Function):
             K.gemm(T, 3 * E, H, K.operand(dC, L.KCONTIG), K.operand(w3, L.MNCONTIG), dtable,
                    epilogue=L.EPI_SCATTER, c_rows=K.rows_map(ids, L.ROWS_CONV3, seq_len=seq_len, seg=E),
                    pad_row=pad_row)
+            if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
+                dtable = None
         return dtable, None, None, dw3, dconv_b, dwq, dbq, dq.view_as(query), None, None
 
 

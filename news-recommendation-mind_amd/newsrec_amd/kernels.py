@@ -221,14 +221,14 @@ def score_bwd(cdd, user, logits, dlogits, B, C, H, mode, dcdd, duser):
            L.stream_ptr(user))
 
 
-def adam(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step):
+def adam(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
     _f32(param, grad, exp_avg, exp_avg_sq)
     n = param.numel()
     for t in (param, grad, exp_avg, exp_avg_sq):
         if not t.is_contiguous() or t.numel() != n:
             raise L.HipError("adam: tensors must be contiguous with equal numel")
     L.call("nr_adam", L.ptr(param), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), n, lr, beta1, beta2, eps,
-           weight_decay, step, L.stream_ptr(param))
+           weight_decay, step, grad_scale, L.stream_ptr(param))
 
 
 def embedding_fwd(table, idx, out):

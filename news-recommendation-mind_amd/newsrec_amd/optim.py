@@ -11,7 +11,9 @@ class FusedAdam(torch.optim.Optimizer):
         super().__init__(params, defaults)
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, grad_scale=1.0):
+        """``grad_scale`` multiplies every gradient as it is read (the data-parallel 1/world
+        mean of GradSync), saving a separate scaling pass over the gradients."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -29,5 +31,5 @@ class FusedAdam(torch.optim.Optimizer):
                 st["step"] += 1
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                 K.adam(p, g, st["exp_avg"], st["exp_avg_sq"], group["lr"], b1, b2, group["eps"],
-                       group["weight_decay"], st["step"])
+                       group["weight_decay"], st["step"], grad_scale)
         return loss

@@ -1,0 +1,106 @@
+"""Data-parallel plumbing on CPU with the gloo backend, world_size 2 (the GPU path uses the
+same code over RCCL): gradient mean incl. the in-backward word-table hook, the reference's
+strided train sharding and contiguous eval partitions."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from newsrec_amd import dist as D
+from newsrec_amd import functions as F
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class Tiny(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.table = torch.nn.Parameter(torch.randn(10, 4))
+        self.lin = torch.nn.Linear(4, 3)
+
+
+def _grads(model, x, use_hook):
+    """loss = sum(lin(table[x])**2); the table grad goes through TABLE_GRAD_HOOK when asked."""
+    class Gather(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, table, idx):
+            ctx.save_for_backward(idx)
+            ctx.table_ref = table
+            return table[idx]
+
+        @staticmethod
+        def backward(ctx, g):
+            (idx,) = ctx.saved_tensors
+            dt = torch.zeros_like(ctx.table_ref).index_add_(0, idx, g)
+            if use_hook and F.TABLE_GRAD_HOOK(ctx.table_ref, dt):
+                dt = None
+            return dt, None
+    model.zero_grad(set_to_none=True)
+    out = model.lin(Gather.apply(model.table, x))
+    (out ** 2).sum().backward()
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    D.setup(rank, world, backend="gloo", master_port=str(port))
+    model = Tiny()
+    x = torch.tensor([rank, rank + 3, 7])
+    sync = D.GradSync(model)
+    _grads(model, x, use_hook=True)
+    scale = sync()
+    sync.close()
+    q.put((rank, scale, {n: (p.grad * scale).clone() for n, p in model.named_parameters()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_sync_mean_gloo_world2():
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # reference: per-rank grads computed serially, averaged
+    want = {}
+    for r in range(world):
+        m = Tiny()
+        _grads(m, torch.tensor([r, r + 3, 7]), use_hook=False)
+        for n, p in m.named_parameters():
+            want[n] = want.get(n, 0) + p.grad / world
+    for rank, scale, g in res:
+        assert scale == 0.5
+        for n in want:
+            torch.testing.assert_close(g[n], want[n], rtol=1e-6, atol=1e-6)
+
+
+def test_shard_train_matches_distributed_sampler():
+    from torch.utils.data.distributed import DistributedSampler
+    ds = list(range(11))
+    for world in (1, 2, 3, 4):
+        for shuffle in (False, True):
+            for r in range(world):
+                s = DistributedSampler(ds, num_replicas=world, rank=r, shuffle=shuffle, seed=5)
+                s.set_epoch(2)
+                assert D.shard_train(len(ds), world, r, shuffle=shuffle, seed=5, epoch=2) == list(iter(s))
+
+
+def test_partition_sampler_contiguous():
+    ds = list(range(10))
+    parts = [list(D.Partition_Sampler(ds, 3, r)) for r in range(3)]
+    assert parts == [[0, 1, 2], [3, 4, 5], [6, 7, 8, 9]]
