@@ -58,6 +58,11 @@ def conv():
 
 
 fl = 2 * T * NQKV * E
+ONLY = os.environ.get("PROBE_ONLY")
+if ONLY == "fwd":
+    ms = timeit(fwd, n=int(os.environ.get("ITERS", "20")))
+    print("%-22s %8.3f ms  %7.1f TF/s" % ("proj fwd gather", ms, fl / ms / 1e9), flush=True)
+    sys.exit(0)
 for name, fn, flops in [("proj fwd gather", fwd, fl), ("proj dgrad scatter", dgrad, fl),
                         ("proj wgrad sk6", wgrad(6), fl), ("proj wgrad sk12", wgrad(12), fl),
                         ("proj wgrad sk24", wgrad(24), fl), ("conv3 fwd H150", conv, 2 * T * Hc * 3 * E)]:
