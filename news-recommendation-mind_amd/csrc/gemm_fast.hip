@@ -15,6 +15,8 @@
 // Requirements (checked by the dispatcher, else the generic kernel runs): data 16-B aligned,
 // ld % 4 == 0, MN-contiguous operands with ld >= round4(M or N) (reads stay inside padded
 // rows), conv3 seg % 32 == 0 and seg % BN == 0 where the taps run along N.
+#include <stdlib.h>
+
 #include "common.h"
 #include "../../include/newsrec_hip.h"
 #include "gemm_fast.h"
@@ -45,6 +47,8 @@ struct Args {
   int epi;
   int64_t pad_row;
   int64_t kchunk;
+  int vec;   // float4 epilogue: N, ldc (and aux ld) % 4 == 0, C (and aux) 16-B aligned
+  int dbg;   // NR_GEMM_DEBUG bits (timing experiments only): 1 = skip the output stores
 };
 
 // Register-staged tile loader for an operand of R rows (the M or N extent) x 32 k.
@@ -180,23 +184,256 @@ struct Loader {
   }
 };
 
-template <int BM, int BN, int AM, int BMODE>
-__global__ __launch_bounds__(256, 2) void gemm_fast_kernel(Args g) {
+// Output-tile epilogue.  The MFMAs run with the operands swapped (B tile as the "A" operand),
+// so each accumulator holds a Cᵀ tile: lane (c, h) owns output row m = c of the 32x32 tile
+// and, in register group q = r >> 2, the four consecutive columns n = 8q + 4h .. +3 — one
+// float4 per group.  Per wave: TI*TJ*4 vector stores (vs 64 scalar stores in the C-major
+// layout), one bias float4 per group, one token-id lookup per row for the scatter.
+template <int EPI>
+__device__ __forceinline__ float4 epi_combine(const Args& g, float4 v, float4 b, const float* crow, const float* arow,
+                                              int64_t n) {
+  if (EPI == NR_EPI_STORE) return make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
+  if (EPI == NR_EPI_STORE_RELU)
+    return make_float4(fmaxf(v.x + b.x, 0.f), fmaxf(v.y + b.y, 0.f), fmaxf(v.z + b.z, 0.f), fmaxf(v.w + b.w, 0.f));
+  if (EPI == NR_EPI_STORE_TANH) return make_float4(tanhf(v.x + b.x), tanhf(v.y + b.y), tanhf(v.z + b.z), tanhf(v.w + b.w));
+  if (EPI == NR_EPI_ACCUM) {
+    const float4 o = *reinterpret_cast<const float4*>(crow + n);
+    return make_float4(o.x + v.x + b.x, o.y + v.y + b.y, o.z + v.z + b.z, o.w + v.w + b.w);
+  }
+  // NR_EPI_ACCUM_GATE
+  const float4 o = *reinterpret_cast<const float4*>(crow + n);
+  const float4 a = *reinterpret_cast<const float4*>(arow + n);
+  return make_float4(a.x > 0.f ? o.x + v.x : 0.f, a.y > 0.f ? o.y + v.y : 0.f, a.z > 0.f ? o.z + v.z : 0.f,
+                     a.w > 0.f ? o.w + v.w : 0.f);
+}
+
+template <int EPI>
+__device__ __forceinline__ float epi_combine1(const Args& g, float v, float b, const float* crow, const float* arow,
+                                              int64_t n) {
+  if (EPI == NR_EPI_STORE) return v + b;
+  if (EPI == NR_EPI_STORE_RELU) return fmaxf(v + b, 0.f);
+  if (EPI == NR_EPI_STORE_TANH) return tanhf(v + b);
+  if (EPI == NR_EPI_ACCUM) return crow[n] + v + b;
+  return arow[n] > 0.f ? crow[n] + v : 0.f;
+}
+
+template <int EPI, int TI, int TJ>
+__device__ __forceinline__ void epilogue_t(const Args& g, f32x16 (&acc)[TI][TJ], int64_t m0, int64_t n0, int wm,
+                                           int wn, int h, int c, bool vec) {
+  const bool has_bias = g.bias && (EPI == NR_EPI_STORE || EPI == NR_EPI_STORE_RELU || EPI == NR_EPI_STORE_TANH ||
+                                   EPI == NR_EPI_ACCUM);
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int64_t row = m0 + wm + 32 * i + c;
+    if (row >= g.M) continue;
+    float* crow = g.C + row * g.ldc;
+    const float* arow = EPI == NR_EPI_ACCUM_GATE ? g.Cm.base + row * g.Cm.ld : nullptr;
+    int64_t tok = 0, nbase = 0;
+    int tpos = 0;
+    if (EPI == NR_EPI_SCATTER) {
+      if (g.Cm.L == 1) {
+        tok = g.Cm.idx[row];
+      } else {
+        nbase = row / g.Cm.L;
+        tpos = (int)(row - nbase * g.Cm.L);
+        nbase *= g.Cm.L;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t n = n0 + wn + 32 * j + 8 * q + 4 * h;
+        if (n >= g.N) continue;
+        const float4 v = make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+        if (EPI == NR_EPI_ATOMIC || EPI == NR_EPI_SCATTER) {
+          float* dst;
+          int64_t t = tok;
+          int64_t sn = n;
+          if (EPI == NR_EPI_ATOMIC) {
+            dst = crow;
+          } else {
+            if (g.Cm.L != 1) {   // conv3 row map: column tap sj of token t + sj - 1
+              const int sj = (int)(n / g.Cm.seg);
+              sn = n - (int64_t)sj * g.Cm.seg;
+              const int t2 = tpos + sj - 1;
+              if (t2 < 0 || t2 >= g.Cm.L) continue;
+              t = g.Cm.idx[nbase + t2];
+            }
+            if (t == g.pad_row) continue;
+            dst = g.C + t * g.ldc;
+          }
+          const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (n + u < g.N) atomicAdd(dst + sn + u, e[u]);
+        } else if (vec && n + 3 < g.N) {
+          const float4 b = has_bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+          *reinterpret_cast<float4*>(crow + n) = epi_combine<EPI>(g, v, b, crow, arow, n);
+        } else {
+          const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (n + u < g.N) crow[n + u] = epi_combine1<EPI>(g, e[u], has_bias ? g.bias[n + u] : 0.f, crow, arow, n + u);
+        }
+      }
+  }
+}
+
+// Atomic epilogues in the C-major accumulator layout (operands not swapped): lane c owns
+// column n = c, register r row (r & 3) + 8 (r >> 2) + 4h — each atomic instruction covers 32
+// consecutive columns of two rows (two cache lines), 16x fewer line transactions than the
+// transposed layout would issue.
+template <int EPI, int TI, int TJ>
+__device__ __forceinline__ void epilogue_cmajor(const Args& g, f32x16 (&acc)[TI][TJ], int64_t m0, int64_t n0, int wm,
+                                                int wn, int h, int c) {
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int64_t col = n0 + wn + 32 * j + c;
+      if (col >= g.N) continue;
+      int sj = 0;
+      int64_t scol = col;
+      if (EPI == NR_EPI_SCATTER && g.Cm.L != 1) {
+        sj = (int)(col / g.Cm.seg);
+        scol = col - (int64_t)sj * g.Cm.seg;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= g.M) continue;
+        const float v = acc[i][j][r];
+        if (EPI == NR_EPI_ATOMIC) {
+          atomicAdd(&g.C[row * g.ldc + col], v);
+        } else {
+          int64_t tok;
+          if (g.Cm.L == 1) {
+            tok = g.Cm.idx[row];
+          } else {
+            const int64_t n = row / g.Cm.L;
+            const int t2 = (int)(row - n * g.Cm.L) + sj - 1;
+            if (t2 < 0 || t2 >= g.Cm.L) continue;
+            tok = g.Cm.idx[n * g.Cm.L + t2];
+          }
+          if (tok == g.pad_row) continue;
+          atomicAdd(&g.C[tok * g.ldc + scol], v);
+        }
+      }
+    }
+}
+
+template <int TI, int TJ>
+__device__ __forceinline__ void epilogue(const Args& g, f32x16 (&acc)[TI][TJ], int64_t m0, int64_t n0, int wm,
+                                         int wn, int h, int c) {
+  if (g.dbg & 1) {   // timing experiment: keep the accumulators live, store nothing
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s += acc[i][j][r];
+    if (s == 1234.5678f) g.C[0] = s;
+    return;
+  }
+  const bool vec = g.vec;
+  switch (g.epi) {
+    case NR_EPI_STORE: epilogue_t<NR_EPI_STORE, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_STORE_RELU: epilogue_t<NR_EPI_STORE_RELU, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_STORE_TANH: epilogue_t<NR_EPI_STORE_TANH, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_ACCUM: epilogue_t<NR_EPI_ACCUM, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_ACCUM_GATE: epilogue_t<NR_EPI_ACCUM_GATE, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_ATOMIC: epilogue_t<NR_EPI_ATOMIC, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    default: epilogue_t<NR_EPI_SCATTER, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+  }
+}
+
+template <bool TR, int TI, int TJ>
+__device__ __forceinline__ void epilogue_any(const Args& g, f32x16 (&acc)[TI][TJ], int64_t m0, int64_t n0, int wm,
+                                             int wn, int h, int c) {
+  if (TR) {
+    epilogue<TI, TJ>(g, acc, m0, n0, wm, wn, h, c);
+  } else if (g.epi == NR_EPI_ATOMIC) {
+    epilogue_cmajor<NR_EPI_ATOMIC, TI, TJ>(g, acc, m0, n0, wm, wn, h, c);
+  } else {
+    epilogue_cmajor<NR_EPI_SCATTER, TI, TJ>(g, acc, m0, n0, wm, wn, h, c);
+  }
+}
+
+// A work unit = one BM x BN output tile x one K split.
+struct Unit {
+  int64_t m0, n0, kbeg;
+  int nt;   // 32-deep k-tiles
+};
+
+// Virtual block id -> unit.  Ids congruent mod 8 run on the same XCD (the hardware deals
+// workgroups round-robin over the 8 XCDs); each XCD gets a contiguous run of units, n fastest,
+// so the blocks resident on one XCD at a time share A row panels (and all of B) in its L2.
+__device__ __forceinline__ Unit decode_unit(const Args& g, int id, int units, int ntiles, int gn, int BM, int BN) {
+  const int xcd = id & 7, q8 = units >> 3, rr = units & 7;
+  const int u = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (id >> 3);
+  const int tile = u % ntiles, split = u / ntiles;
+  Unit r;
+  r.m0 = (int64_t)(tile / gn) * BM;
+  r.n0 = (int64_t)(tile % gn) * BN;
+  r.kbeg = (int64_t)split * g.kchunk;
+  const int64_t kend = r.kbeg + g.kchunk < g.K ? r.kbeg + g.kchunk : g.K;
+  r.nt = kend > r.kbeg ? (int)((kend - r.kbeg + 31) / 32) : 0;
+  return r;
+}
+
+// Position in a block's flattened (unit, k-tile) sequence.
+struct Cursor {
+  int id;   // virtual block id (units of this block: blockIdx.x + j * gridDim.x)
+  int kt;   // k-tile within the unit
+  Unit u;
+};
+
+// Persistent GEMM: a grid of (resident blocks) walks the units with stride gridDim.x, and the
+// k-loop runs over the flattened (unit, k-tile) sequence.  Two-deep pipeline per block: while
+// the MFMAs consume k-tile P from LDS, tile P+1 sits in registers and is written to the other
+// LDS buffer after the first quarter of P's MFMAs, and the global loads of P+2 are issued right
+// behind that write — so a load has a whole iteration to land, the LDS write never waits, and
+// each iteration ends in a bare barrier.  Unit boundaries are invisible to the pipeline: the
+// next unit's first tiles load during the current unit's last ones, and the finished unit's
+// epilogue stores go out behind them.  A grid of `units` blocks is the plain one-tile-per-block
+// kernel.
+template <int BM, int BN, int AM, int BMODE, bool TR>
+__global__ __launch_bounds__(256, 2) void gemm_fast_kernel(Args g, int units) {
   using LA = Loader<BM, AM>;
   using LB = Loader<BN, BMODE>;
   __shared__ __attribute__((aligned(16))) float As[2][LA::LDS_FLOATS];
   __shared__ __attribute__((aligned(16))) float Bs[2][LB::LDS_FLOATS];
+  constexpr bool IDX_AHEAD = AM == MN_GATHER || BMODE == MN_GATHER;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
-  const int64_t gm = (g.M + BM - 1) / BM, gn = (g.N + BN - 1) / BN;
-  const int nwg = (int)(gm * gn);
-  const int id = blockIdx.x;
-  const int xcd = id & 7, q8 = nwg >> 3, rr = nwg & 7;
-  const int wg = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (id >> 3);
-  const int64_t m0 = (wg / gn) * BM, n0 = (wg % gn) * BN;
-  const int64_t kbeg = (int64_t)blockIdx.y * g.kchunk;
-  const int64_t kend = kbeg + g.kchunk < g.K ? kbeg + g.kchunk : g.K;
-  const int nt = kend > kbeg ? (int)((kend - kbeg + 31) / 32) : 0;
+  const int gn = (int)((g.N + BN - 1) / BN);
+  const int ntiles = (int)((g.M + BM - 1) / BM) * gn;
+  const int G = gridDim.x;
+  if ((int)blockIdx.x >= units) return;
+
+  // cursor advance: false when the block's sequence is exhausted
+  auto advance = [&](Cursor& p) -> bool {
+    if (p.kt + 1 < p.u.nt) { ++p.kt; return true; }
+    const int nid = p.id + G;
+    if (nid >= units) return false;
+    p.id = nid;
+    p.kt = 0;
+    p.u = decode_unit(g, nid, units, ntiles, gn, BM, BN);
+    return p.u.nt > 0;
+  };
+  auto kof = [](const Cursor& p) -> int64_t { return p.u.kbeg + (int64_t)p.kt * 32; };
+  auto peek_k = [&](const Cursor& p) -> int64_t {   // k of the position after p, or -1
+    if (p.kt + 1 < p.u.nt) return kof(p) + 32;
+    const int nid = p.id + G;
+    return nid < units ? decode_unit(g, nid, units, ntiles, gn, BM, BN).kbeg : -1;
+  };
+
+  Cursor cp;   // compute position
+  cp.id = blockIdx.x;
+  cp.kt = 0;
+  cp.u = decode_unit(g, cp.id, units, ntiles, gn, BM, BN);
 
   constexpr int TI = BM / 64, TJ = BN / 64;
   const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
@@ -207,38 +444,67 @@ __global__ __launch_bounds__(256, 2) void gemm_fast_kernel(Args g) {
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  if (cp.u.nt <= 0) {   // K == 0 (only the last split can be empty, and then every unit is)
+    epilogue_any<TR, TI, TJ>(g, acc, cp.u.m0, cp.u.n0, wm, wn, h, c);
+    return;
+  }
 
   LA la;
   LB lb;
-  la.init(g.A, m0, g.M, tid);
-  lb.init(g.B, n0, g.N, tid);
-  if (nt > 0) {
-    la.prefetch_idx(g.A, kbeg, g.K, tid);
-    lb.prefetch_idx(g.B, kbeg, g.K, tid);
-    la.load(g.A, m0, g.M, kbeg, tid);
-    lb.load(g.B, n0, g.N, kbeg, tid);
-    if (nt > 1) {
-      la.prefetch_idx(g.A, kbeg + 32, g.K, tid);
-      lb.prefetch_idx(g.B, kbeg + 32, g.K, tid);
+  Cursor lp = cp;   // load position
+  la.init(g.A, lp.u.m0, g.M, tid);
+  lb.init(g.B, lp.u.n0, g.N, tid);
+  auto issue = [&](const Cursor& p) {
+    const int64_t k = kof(p);
+    la.load(g.A, p.u.m0, g.M, k, tid);
+    lb.load(g.B, p.u.n0, g.N, k, tid);
+    if (IDX_AHEAD) {   // token ids of the position after p, one load ahead of its data
+      const int64_t pk = peek_k(p);
+      if (pk >= 0) {
+        la.prefetch_idx(g.A, pk, g.K, tid);
+        lb.prefetch_idx(g.B, pk, g.K, tid);
+      }
     }
-    la.store(As[0], tid);
-    lb.store(Bs[0], tid);
+  };
+  auto step_load = [&]() -> bool {   // move lp one position and issue its loads
+    const int old = lp.id;
+    if (!advance(lp)) return false;
+    if (lp.id != old) {
+      la.init(g.A, lp.u.m0, g.M, tid);
+      lb.init(g.B, lp.u.n0, g.N, tid);
+    }
+    issue(lp);
+    return true;
+  };
+
+  // prologue: P0 -> LDS[0], P1 -> registers
+  if (IDX_AHEAD) {
+    la.prefetch_idx(g.A, kof(lp), g.K, tid);
+    lb.prefetch_idx(g.B, kof(lp), g.K, tid);
   }
+  issue(lp);
+  la.store(As[0], tid);
+  lb.store(Bs[0], tid);
+  bool staged = step_load();   // registers hold the position after cp
   __syncthreads();
 
-  for (int t = 0; t < nt; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nt) {
-      const int64_t k1 = kbeg + (int64_t)(t + 1) * 32;
-      la.load(g.A, m0, g.M, k1, tid);
-      lb.load(g.B, n0, g.N, k1, tid);
-      if (t + 2 < nt) {
-        la.prefetch_idx(g.A, k1 + 32, g.K, tid);
-        lb.prefetch_idx(g.B, k1 + 32, g.K, tid);
-      }
+  bool pending = false;
+  int64_t pm0 = 0, pn0 = 0;
+  int buf = 0;
+  for (;;) {
+    if (pending) {   // previous unit's output, behind this unit's first loads
+      epilogue_any<TR, TI, TJ>(g, acc, pm0, pn0, wm, wn, h, c);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      pending = false;
     }
     const float* a_s = As[buf];
     const float* b_s = Bs[buf];
+    const bool had_staged = staged;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float4 a[TI], b[TJ];
@@ -250,85 +516,90 @@ __global__ __launch_bounds__(256, 2) void gemm_fast_kernel(Args g) {
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+          acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x2f32(b[j].x, a[i].x, acc[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x2f32(b[j].y, a[i].y, acc[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x2f32(b[j].z, a[i].z, acc[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+          acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x2f32(b[j].w, a[i].w, acc[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
         }
-    }
-    if (t + 1 < nt) {
-      la.store(As[buf ^ 1], tid);
-      lb.store(Bs[buf ^ 1], tid);
+      if (q == 0 && had_staged) {   // publish P+1 (its buffer's readers passed the last barrier)
+        la.store(As[buf ^ 1], tid);
+        lb.store(Bs[buf ^ 1], tid);
+        staged = step_load();       // and start P+2
+      }
     }
     __syncthreads();
-  }
-
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int64_t col = n0 + wn + 32 * j + c;
-      if (col >= g.N) continue;
-      const bool has_bias = g.bias && (g.epi == NR_EPI_STORE || g.epi == NR_EPI_STORE_RELU ||
-                                       g.epi == NR_EPI_STORE_TANH || g.epi == NR_EPI_ACCUM);
-      const float bcol = has_bias ? g.bias[col] : 0.f;
-      int sj = 0;
-      int64_t scol = col;
-      if (g.epi == NR_EPI_SCATTER && g.Cm.L > 0 && g.Cm.seg > 0 && g.Cm.idx && g.Cm.L != 1) {
-        sj = (int)(col / g.Cm.seg);
-        scol = col - (int64_t)sj * g.Cm.seg;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row >= g.M) continue;
-        const float v = acc[i][j][r];
-        const int64_t o = row * g.ldc + col;
-        switch (g.epi) {
-          case NR_EPI_STORE: g.C[o] = v + bcol; break;
-          case NR_EPI_STORE_RELU: g.C[o] = fmaxf(v + bcol, 0.f); break;
-          case NR_EPI_STORE_TANH: g.C[o] = tanhf(v + bcol); break;
-          case NR_EPI_ACCUM: g.C[o] += v + bcol; break;
-          case NR_EPI_ACCUM_GATE: g.C[o] = g.Cm.base[row * g.Cm.ld + col] > 0.f ? g.C[o] + v : 0.f; break;
-          case NR_EPI_ATOMIC: atomicAdd(&g.C[o], v); break;
-          default: {   // NR_EPI_SCATTER through a GATHER (L == 1) or CONV3 row map
-            int64_t tok;
-            if (g.Cm.L == 1) {
-              tok = g.Cm.idx[row];
-            } else {
-              const int64_t n = row / g.Cm.L;
-              const int t2 = (int)(row - n * g.Cm.L) + sj - 1;
-              if (t2 < 0 || t2 >= g.Cm.L) continue;
-              tok = g.Cm.idx[n * g.Cm.L + t2];
-            }
-            if (tok == g.pad_row) continue;
-            atomicAdd(&g.C[tok * g.ldc + scol], v);
-          }
-        }
-      }
+    buf ^= 1;
+    const int old = cp.id;
+    const int64_t om0 = cp.u.m0, on0 = cp.u.n0;
+    if (!had_staged) break;         // cp was the block's last position
+    advance(cp);
+    if (cp.id != old) {
+      pending = true;
+      pm0 = om0;
+      pn0 = on0;
     }
+  }
+  epilogue_any<TR, TI, TJ>(g, acc, cp.u.m0, cp.u.n0, wm, wn, h, c);
 }
 
-template <int BM, int BN, int AM, int BMODE>
+// Resident-block slots for a kernel instantiation (CUs x occupancy), cached per device.
+template <typename Kern>
+int resident_slots(Kern k) {
+  static int cache[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  if (cache[dev] == 0) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 256, 0) != hipSuccess) return 0;
+    cache[dev] = cus * per;
+  }
+  return cache[dev];
+}
+
+static bool persistent_disabled() {   // NR_GEMM_NOPERSIST=1: one unit per block (A/B testing)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NR_GEMM_NOPERSIST");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
+template <int BM, int BN, int AM, int BMODE, bool TR>
 int launch(const Args& g, int splits, hipStream_t s) {
   const int64_t gm = (g.M + BM - 1) / BM, gn = (g.N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_fast_kernel<BM, BN, AM, BMODE>), dim3((unsigned)(gm * gn), (unsigned)splits), dim3(256),
-                     0, s, g);
+  const int64_t units = gm * gn * splits;
+  if (units <= 0) return NR_OK;
+  if (units > 0x7fffffff) return NR_EINVAL(0);
+  int grid = (int)units;
+  if (!persistent_disabled()) {
+    const int slots = resident_slots(gemm_fast_kernel<BM, BN, AM, BMODE, TR>);
+    if (slots > 0 && slots < grid) grid = slots;
+  }
+  hipLaunchKernelGGL((gemm_fast_kernel<BM, BN, AM, BMODE, TR>), dim3((unsigned)grid), dim3(256), 0, s, g, (int)units);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
 
 template <int BM, int BN>
 int launch_modes(const Args& g, int am, int bm, int splits, hipStream_t s) {
-#define NR_AB(A_, B_) \
-  if (am == A_ && bm == B_) return launch<BM, BN, A_, B_>(g, splits, s);
-  NR_AB(KC_GATHER, KC_PLAIN)   // fused gather + projection (fwd)
-  NR_AB(KC_CONV3, KC_PLAIN)    // conv as K = 3E GEMM (fwd)
-  NR_AB(KC_PLAIN, KC_PLAIN)    // plain y = x Wᵀ
-  NR_AB(KC_PLAIN, MN_PLAIN)    // dgrad dx = dy W
-  NR_AB(MN_PLAIN, MN_GATHER)   // wgrad dW = dyᵀ table[ids]
-  NR_AB(MN_PLAIN, MN_CONV3)    // conv wgrad
-  NR_AB(MN_PLAIN, MN_PLAIN)    // wgrad dW = dyᵀ x
+#define NR_AB(A_, B_, TR_) \
+  if (am == A_ && bm == B_ && atomic_epi == !TR_) return launch<BM, BN, A_, B_, TR_>(g, splits, s);
+  // transposed accumulators (float4 stores) for store epilogues, C-major for atomic ones
+  const bool atomic_epi = g.epi == NR_EPI_ATOMIC || g.epi == NR_EPI_SCATTER;
+  NR_AB(KC_GATHER, KC_PLAIN, true)    // fused gather + projection (fwd)
+  NR_AB(KC_CONV3, KC_PLAIN, true)     // conv as K = 3E GEMM (fwd)
+  NR_AB(KC_PLAIN, KC_PLAIN, true)     // plain y = x Wᵀ
+  NR_AB(KC_PLAIN, MN_PLAIN, true)     // dgrad dx = dy W
+  NR_AB(KC_PLAIN, MN_PLAIN, false)    // dgrad scattered into the word-table gradient
+  NR_AB(MN_PLAIN, MN_GATHER, false)   // wgrad dW = dyᵀ table[ids]
+  NR_AB(MN_PLAIN, MN_CONV3, false)    // conv wgrad
+  NR_AB(MN_PLAIN, MN_PLAIN, false)    // wgrad dW = dyᵀ x
 #undef NR_AB
   return -1;
 }
@@ -369,6 +640,20 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   if (epilogue == NR_EPI_SCATTER && c_rows && c_rows->map == NR_ROWS_PLAIN) return -1;
   if (epilogue == NR_EPI_SCATTER && c_rows && c_rows->map == NR_ROWS_CONV3 && c_rows->seq_len == 1) return -1;
   g.C = C; g.ldc = ldc; g.bias = bias; g.epi = epilogue; g.pad_row = pad_row;
+  {
+    static int dbg = -1;
+    if (dbg < 0) {
+      const char* e = getenv("NR_GEMM_DEBUG");
+      dbg = e ? atoi(e) : 0;
+    }
+    g.dbg = dbg;
+  }
+  {
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    bool v = N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!bias || al16(bias));
+    if (epilogue == NR_EPI_ACCUM_GATE) v = v && c_rows && c_rows->ld % 4 == 0 && al16(c_rows->data);
+    g.vec = v ? 1 : 0;
+  }
   g.kchunk = (K + split_k - 1) / split_k;
   g.kchunk = (g.kchunk + 31) / 32 * 32;
   if (g.kchunk == 0) g.kchunk = 32;

@@ -64,8 +64,10 @@ if ONLY == "fwd":
     print("%-22s %8.3f ms  %7.1f TF/s" % ("proj fwd gather", ms, fl / ms / 1e9), flush=True)
     sys.exit(0)
 for name, fn, flops in [("proj fwd gather", fwd, fl), ("proj dgrad scatter", dgrad, fl),
-                        ("proj wgrad sk6", wgrad(6), fl), ("proj wgrad sk12", wgrad(12), fl),
-                        ("proj wgrad sk24", wgrad(24), fl), ("conv3 fwd H150", conv, 2 * T * Hc * 3 * E)]:
+                        ("proj wgrad sk6", wgrad(6), fl), ("proj wgrad sk9", wgrad(9), fl),
+                        ("proj wgrad sk12", wgrad(12), fl), ("proj wgrad sk19", wgrad(19), fl),
+                        ("proj wgrad sk24", wgrad(24), fl), ("proj wgrad sk28", wgrad(28), fl),
+                        ("proj wgrad sk38", wgrad(38), fl), ("proj wgrad sk48", wgrad(48), fl), ("conv3 fwd H150", conv, 2 * T * Hc * 3 * E)]:
     ms = timeit(fn)
     print("%-22s %8.3f ms  %7.1f TF/s" % (name, ms, flops / ms / 1e9), flush=True)
 ref = lambda: torch.matmul(table[tok], W.t())
