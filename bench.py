@@ -181,7 +181,10 @@ def main():
         ms = el / a.steps * 1e3
         value = world * B * a.steps / el
         gemm_ms = probe.get("proj_fwd_ms")
-        gemm_flops = 2.0 * B * (C + NH) * L * E * (E + H)     # per launch: [T,768] x [768,1152]
+        # per launch: [rows, 768] x [768, 1152], rows = the distinct word rows of the batch
+        # (device-side count, read back after the timed region) or T tokens without dedup
+        gemm_rows = probe.get("proj_fwd_rows", float(B * (C + NH) * L))
+        gemm_flops = 2.0 * gemm_rows * E * (E + H)
         achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms else None
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_proj_fwd.json")
@@ -202,7 +205,8 @@ def main():
                          "achieved": round(achieved, 2) if achieved else None, "peak": FP32_MFMA_PEAK_TF,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TF, 4) if achieved else None,
                          "traffic": traffic, "launch_ms": round(gemm_ms, 4) if gemm_ms else None,
-                         "flops_per_launch": gemm_flops},
+                         "flops_per_launch": gemm_flops, "rows_per_launch": gemm_rows,
+                         "tokens_per_launch": B * (C + NH) * L},
         }
         if not a.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)

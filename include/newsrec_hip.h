@@ -61,7 +61,9 @@ enum nr_epilogue {
   NR_EPI_STORE_TANH = 4, /* C[m][n] = tanh(acc + bias[n])                   (CNN.py:46)      */
   NR_EPI_ACCUM_GATE = 5, /* C[m][n] = aux[m][n] > 0 ? C[m][n] + acc : 0, aux = c_rows->data
                             (ld c_rows->ld): adds a second gradient path, then ReLU's mask   */
-  NR_EPI_ACCUM = 6       /* C[m][n] += acc + bias[n]  (row tiles are block-exclusive)         */
+  NR_EPI_ACCUM = 6,      /* C[m][n] += acc + bias[n]  (row tiles are block-exclusive)         */
+  NR_EPI_SCATTER_STORE = 7 /* C[c_rows(m)][n] = acc for DISTINCT GATHER rows (pad_row skipped):
+                            the table gradient over nr_unique_rows' ids, plain vector stores */
 };
 
 /* C (op)= A(m,k) * B(k,n) over k in [0,K), fp32 on the f32-input MFMA.
@@ -73,6 +75,42 @@ int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_o
                 float* C, int64_t ldc, const float* bias, int32_t epilogue,
                 const nr_operand* c_rows, int64_t pad_row, int32_t split_k,
                 hipStream_t stream);
+
+/* nr_gemm_f32 with device-resident extents: M and K are host upper bounds (grid sizing) and
+ * the kernel reads the actual values from m_dev / k_dev (either may be NULL), so a row count
+ * produced on the GPU (nr_unique_rows) sizes the GEMM without a host synchronisation.
+ * Fast-path operands only (16-B aligned, ld % 4 == 0); K and *k_dev multiples of 32. */
+int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B,
+                    float* C, int64_t ldc, const float* bias, int32_t epilogue,
+                    const nr_operand* c_rows, int64_t pad_row, int32_t split_k,
+                    const int32_t* m_dev, const int32_t* k_dev, hipStream_t stream);
+
+/* ------------------------------------------------------------------ distinct token rows */
+
+/* Distinct ids of a token batch (the news tower projects each word-table row once, not once
+ * per token: BERT.py:39 + Attention.py:107-108 commute with the gather).  Outputs:
+ *   uids[U_pad]      distinct ids ascending, padded with fill_row up to U_pad = ceil32(U)
+ *   inv[T]           uids[inv[t]] == ids[t]
+ *   seg_off[U_pad+1], seg_tok[T], seg_of[T]   CSR of the tokens of each distinct id (pad
+ *                    rows empty); seg_of[p] = the distinct row owning CSR position p
+ *   counts[3]        {U, U_pad, bad} (bad = 1 if an id fell outside [0, V))
+ * fill_row is also the "hot" id (the padding row) whose tokens are counted per wave.
+ * work: 4*V int32.  Capacity: uids / seg_off hold ceil32(min(T, V)) (+1) entries. */
+int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t fill_row, int32_t* work,
+                   int64_t* uids, int64_t* inv, int32_t* seg_off, int32_t* seg_tok,
+                   int32_t* seg_of, int32_t* counts, hipStream_t stream);
+
+/* Bytes of `work` nr_segment_rows_sum needs for T tokens of `width` floats. */
+int64_t nr_segment_rows_sum_workspace(int64_t T, int64_t width);
+
+/* dst[u][:] = Σ_{t in segment u} src[t][:]  for u < counts[0]; zero rows up to counts[1].
+ * The per-distinct-row gradient of the projection (what embedding_dense_backward sums after
+ * the dgrad, summed before it).  No atomics.  width, lds, ldd multiples of 4; rows_max >=
+ * counts[1]; src, dst, work 16-B aligned. */
+int nr_segment_rows_sum(const float* src, int64_t lds, int64_t width, int64_t T,
+                        const int32_t* seg_off, const int32_t* seg_tok, const int32_t* seg_of,
+                        const int32_t* counts, int64_t rows_max, float* work, float* dst,
+                        int64_t ldd, hipStream_t stream);
 
 /* ------------------------------------------------------------------ attention */
 
@@ -100,16 +138,20 @@ int nr_mha_attn_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v
  * LayerNorm (eps) -> dropout(p, counter RNG) -> learned-query pooling, all in LDS.
  * y = [T][heads*dk | heads*dv] projections.  (dk, dv, heads*dv) in {(64,32,384), (64,64,768),
  * (64,32,256), (32,32,384)}.  Replaces MultiheadAttention.forward :125-147 + MHA.py:37-38.
- * Saves stats [T][2] and probs [T]; zout (optional) receives Z = the encoder's token output. */
-int nr_mha_pool_fwd(const float* y, int64_t ldy, const void* mask, int32_t mask_dtype, int64_t nseq,
+ * Saves stats [T][2] and probs [T]; zout (optional) receives Z = the encoder's token output.
+ * yrows (optional): token t reads projection row yrows[t] (distinct-row projections). */
+int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,
+                    int32_t mask_dtype, int64_t nseq,
                     int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
                     const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset,
                     const float* q, float* news, int64_t ldn, float* zout, int64_t ldz,
                     float* stats, float* probs, hipStream_t stream);
 
 /* Backward of nr_mha_pool_fwd (recomputes the attention): writes dy [T][heads*(dk+dv)] and
- * ATOMICALLY ACCUMULATES dbias (= column sums of dy), dq, dgamma, dbeta (caller zeroes). */
-int nr_mha_pool_bwd(const float* y, int64_t ldy, const void* mask, int32_t mask_dtype, int64_t nseq,
+ * ATOMICALLY ACCUMULATES dbias (= column sums of dy), dq, dgamma, dbeta (caller zeroes).
+ * dy stays per token (row t) when yrows is given. */
+int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,
+                    int32_t mask_dtype, int64_t nseq,
                     int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
                     const float* beta, float p_drop, uint64_t seed, uint64_t offset,
                     const float* q, const float* stats, const float* probs, const float* dnews,

@@ -327,12 +327,16 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
   if (g.kchunk == 0) g.kchunk = 32;
   const int splits = (int)((K + g.kchunk - 1) / g.kchunk) > 0 ? (int)((K + g.kchunk - 1) / g.kchunk) : 1;
 
+  if (epilogue == NR_EPI_SCATTER_STORE && (!c_rows || c_rows->map != NR_ROWS_GATHER || !c_rows->rows))
+    return NR_EINVAL(4);
   if (!getenv_generic()) {
     const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128) * splits;
     const int fb = t128 >= 400 ? 128 : 64;
-    const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, fb, fb, stream);
+    const int rc =
+        nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, fb, fb, nullptr, nullptr, stream);
     if (rc != -1) return rc;
   }
+  if (epilogue == NR_EPI_SCATTER_STORE) g.epi = NR_EPI_SCATTER;   // generic kernel: same sums via atomics
   int bm = pick_tile(M), bn = pick_tile(N);
   // small problems: prefer 64x64 tiles to fill the 256 CUs
   if ((int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * splits < 512) { bm = 64; bn = 64; }
@@ -351,4 +355,27 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
   if (bm == 128 && bn == 64) return launch_kc<128, 64>(g, ak, bk, splits, stream);
   if (bm == 64 && bn == 128) return launch_kc<64, 128>(g, ak, bk, splits, stream);
   return launch_kc<64, 64>(g, ak, bk, splits, stream);
+}
+
+// Device-resident extents: M and K are upper bounds (grid sizing); the kernel reads the actual
+// values from m_dev / k_dev (either may be null).  Fast-path operand shapes only (K-contiguous
+// or MN-contiguous rows, 16-B aligned, ld % 4 == 0); the device K must be a multiple of 32.
+extern "C" int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B,
+                               float* C, int64_t ldc, const float* bias, int32_t epilogue,
+                               const nr_operand* c_rows, int64_t pad_row, int32_t split_k, const int32_t* m_dev,
+                               const int32_t* k_dev, hipStream_t stream) {
+  if (M < 0 || N < 0 || K < 0 || (K % 32)) return NR_EINVAL(0);
+  if (!A || !B || !C || !A->data || !B->data) return NR_EINVAL(1);
+  if ((A->ld & 3) || (B->ld & 3)) return NR_EINVAL(2);
+  if (epilogue == NR_EPI_SCATTER && (!c_rows || (c_rows->map != NR_ROWS_PLAIN && !c_rows->rows)))
+    return NR_EINVAL(4);
+  if (epilogue == NR_EPI_ACCUM_GATE && (!c_rows || !c_rows->data)) return NR_EINVAL(4);
+  if (epilogue == NR_EPI_SCATTER_STORE && (!c_rows || c_rows->map != NR_ROWS_GATHER || !c_rows->rows))
+    return NR_EINVAL(4);
+  if (split_k < 1) split_k = 1;
+  if (split_k > 1 && epilogue != NR_EPI_ATOMIC && epilogue != NR_EPI_SCATTER) return NR_EINVAL(5);
+  if (M == 0 || N == 0 || K == 0) return NR_OK;
+  const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, 128, 128, m_dev,
+                              k_dev, stream);
+  return rc == -1 ? NR_EINVAL(7) : rc;
 }

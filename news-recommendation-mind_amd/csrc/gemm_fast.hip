@@ -48,6 +48,9 @@ struct Args {
   int64_t pad_row;
   int64_t kchunk;
   int vec;   // float4 epilogue: N, ldc (and aux ld) % 4 == 0, C (and aux) 16-B aligned
+  int splits;
+  const int32_t* mdyn;   // device-resident M (<= M), or null
+  const int32_t* kdyn;   // device-resident K (<= K), or null
   int dbg;   // NR_GEMM_DEBUG bits (timing experiments only): 1 = skip the output stores
 };
 
@@ -227,6 +230,11 @@ __device__ __forceinline__ void epilogue_t(const Args& g, f32x16 (&acc)[TI][TJ],
     const int64_t row = m0 + wm + 32 * i + c;
     if (row >= g.M) continue;
     float* crow = g.C + row * g.ldc;
+    if (EPI == NR_EPI_SCATTER_STORE) {   // distinct destination rows: plain stores
+      const int64_t tok = g.Cm.idx[row];
+      if (tok == g.pad_row) continue;
+      crow = g.C + tok * g.ldc;
+    }
     const float* arow = EPI == NR_EPI_ACCUM_GATE ? g.Cm.base + row * g.Cm.ld : nullptr;
     int64_t tok = 0, nbase = 0;
     int tpos = 0;
@@ -267,6 +275,15 @@ __device__ __forceinline__ void epilogue_t(const Args& g, f32x16 (&acc)[TI][TJ],
 #pragma unroll
           for (int u = 0; u < 4; ++u)
             if (n + u < g.N) atomicAdd(dst + sn + u, e[u]);
+        } else if (EPI == NR_EPI_SCATTER_STORE) {
+          if (vec && n + 3 < g.N) {
+            *reinterpret_cast<float4*>(crow + n) = v;
+          } else {
+            const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (n + u < g.N) crow[n + u] = e[u];
+          }
         } else if (vec && n + 3 < g.N) {
           const float4 b = has_bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
           *reinterpret_cast<float4*>(crow + n) = epi_combine<EPI>(g, v, b, crow, arow, n);
@@ -345,6 +362,7 @@ __device__ __forceinline__ void epilogue(const Args& g, f32x16 (&acc)[TI][TJ], i
     case NR_EPI_ACCUM: epilogue_t<NR_EPI_ACCUM, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
     case NR_EPI_ACCUM_GATE: epilogue_t<NR_EPI_ACCUM_GATE, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
     case NR_EPI_ATOMIC: epilogue_t<NR_EPI_ATOMIC, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_SCATTER_STORE: epilogue_t<NR_EPI_SCATTER_STORE, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
     default: epilogue_t<NR_EPI_SCATTER, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
   }
 }
@@ -400,40 +418,62 @@ struct Cursor {
 // epilogue stores go out behind them.  A grid of `units` blocks is the plain one-tile-per-block
 // kernel.
 template <int BM, int BN, int AM, int BMODE, bool TR>
-__global__ __launch_bounds__(256, 2) void gemm_fast_kernel(Args g, int units) {
+__global__ __launch_bounds__(256, 2) void gemm_fast_kernel(Args g) {
   using LA = Loader<BM, AM>;
   using LB = Loader<BN, BMODE>;
   __shared__ __attribute__((aligned(16))) float As[2][LA::LDS_FLOATS];
   __shared__ __attribute__((aligned(16))) float Bs[2][LB::LDS_FLOATS];
   constexpr bool IDX_AHEAD = AM == MN_GATHER || BMODE == MN_GATHER;
 
+  // device-resident extents (row counts produced on the GPU, e.g. nr_unique_rows): the host
+  // sizes were upper bounds for the grid
+  if (g.mdyn) {
+    const int64_t m = *g.mdyn;
+    g.M = m < g.M ? (m > 0 ? m : 0) : g.M;
+  }
+  if (g.kdyn) {
+    const int64_t k = *g.kdyn;
+    g.K = k < g.K ? (k > 0 ? k : 0) : g.K;
+    const int64_t kc = (g.K + g.splits - 1) / g.splits;
+    g.kchunk = kc > 0 ? (kc + 31) / 32 * 32 : 32;
+  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
   const int gn = (int)((g.N + BN - 1) / BN);
   const int ntiles = (int)((g.M + BM - 1) / BM) * gn;
+  const int units = ntiles * g.splits;
   const int G = gridDim.x;
-  if ((int)blockIdx.x >= units) return;
 
+  // first non-empty unit at or after virtual id `id` in this block's sequence (a split past a
+  // device-resident K is empty), or `units`
+  auto skip_empty = [&](int id, Unit& u) -> int {
+    for (; id < units; id += G) {
+      u = decode_unit(g, id, units, ntiles, gn, BM, BN);
+      if (u.nt > 0) return id;
+    }
+    return units;
+  };
   // cursor advance: false when the block's sequence is exhausted
   auto advance = [&](Cursor& p) -> bool {
     if (p.kt + 1 < p.u.nt) { ++p.kt; return true; }
-    const int nid = p.id + G;
+    Unit u;
+    const int nid = skip_empty(p.id + G, u);
     if (nid >= units) return false;
     p.id = nid;
     p.kt = 0;
-    p.u = decode_unit(g, nid, units, ntiles, gn, BM, BN);
-    return p.u.nt > 0;
+    p.u = u;
+    return true;
   };
   auto kof = [](const Cursor& p) -> int64_t { return p.u.kbeg + (int64_t)p.kt * 32; };
   auto peek_k = [&](const Cursor& p) -> int64_t {   // k of the position after p, or -1
     if (p.kt + 1 < p.u.nt) return kof(p) + 32;
-    const int nid = p.id + G;
-    return nid < units ? decode_unit(g, nid, units, ntiles, gn, BM, BN).kbeg : -1;
+    Unit u;
+    return skip_empty(p.id + G, u) < units ? u.kbeg : -1;
   };
 
   Cursor cp;   // compute position
-  cp.id = blockIdx.x;
   cp.kt = 0;
-  cp.u = decode_unit(g, cp.id, units, ntiles, gn, BM, BN);
+  cp.id = skip_empty(blockIdx.x, cp.u);
+  if (cp.id >= units) return;
 
   constexpr int TI = BM / 64, TJ = BN / 64;
   const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
@@ -444,10 +484,6 @@ __global__ __launch_bounds__(256, 2) void gemm_fast_kernel(Args g, int units) {
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  if (cp.u.nt <= 0) {   // K == 0 (only the last split can be empty, and then every unit is)
-    epilogue_any<TR, TI, TJ>(g, acc, cp.u.m0, cp.u.n0, wm, wn, h, c);
-    return;
-  }
 
   LA la;
   LB lb;
@@ -581,7 +617,9 @@ int launch(const Args& g, int splits, hipStream_t s) {
     const int slots = resident_slots(gemm_fast_kernel<BM, BN, AM, BMODE, TR>);
     if (slots > 0 && slots < grid) grid = slots;
   }
-  hipLaunchKernelGGL((gemm_fast_kernel<BM, BN, AM, BMODE, TR>), dim3((unsigned)grid), dim3(256), 0, s, g, (int)units);
+  Args a = g;
+  a.splits = splits;
+  hipLaunchKernelGGL((gemm_fast_kernel<BM, BN, AM, BMODE, TR>), dim3((unsigned)grid), dim3(256), 0, s, a);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
@@ -609,8 +647,9 @@ int launch_modes(const Args& g, int am, int bm, int splits, hipStream_t s) {
 // Returns -1 if the shape/operands are not eligible (the caller falls back), else a status.
 int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B, float* C,
                  int64_t ldc, const float* bias, int32_t epilogue, const nr_operand* c_rows, int64_t pad_row,
-                 int32_t split_k, int bm, int bn, hipStream_t stream) {
+                 int32_t split_k, int bm, int bn, const int32_t* m_dev, const int32_t* k_dev, hipStream_t stream) {
   using namespace nrfast;
+  if (K <= 0) return -1;
   auto aligned = [](const nr_operand* o) {
     return (o->ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(o->data) & 15) == 0);
   };
@@ -638,8 +677,10 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   g.Cm = Op{c_rows ? c_rows->data : nullptr, c_rows ? c_rows->ld : 0, c_rows ? c_rows->rows : nullptr,
             c_rows ? (c_rows->map == NR_ROWS_CONV3 ? c_rows->seq_len : 1) : 1, c_rows ? c_rows->seg : 1};
   if (epilogue == NR_EPI_SCATTER && c_rows && c_rows->map == NR_ROWS_PLAIN) return -1;
+  if (epilogue == NR_EPI_SCATTER_STORE && (!c_rows || c_rows->map != NR_ROWS_GATHER || !c_rows->rows)) return -1;
   if (epilogue == NR_EPI_SCATTER && c_rows && c_rows->map == NR_ROWS_CONV3 && c_rows->seq_len == 1) return -1;
   g.C = C; g.ldc = ldc; g.bias = bias; g.epi = epilogue; g.pad_row = pad_row;
+  g.mdyn = m_dev; g.kdyn = k_dev; g.splits = 1;
   {
     static int dbg = -1;
     if (dbg < 0) {

@@ -40,6 +40,7 @@ __device__ __forceinline__ void wave_lds_fence() {
 
 struct MPArgs {
   const float* y; int64_t ldy;        // [T][heads*dk + heads*dv] projections
+  const int64_t* yrows;               // optional: projection row of token t
   const void* mask; int mask_dt;      // [nseq][L]
   int64_t nseq; int L; int heads;
   float scale_attn, scale_pool;
@@ -55,6 +56,24 @@ struct MPArgs {
   float* dbias; float* dq; float* dgamma; float* dbeta;
   int dbg;                            // timing-only ablations (NR_DEBUG_MHAPOOL): 1 = skip attention, 2 = skip LN/pool
 };
+
+// Projection row of position l of the workgroup's title.  The row indices (yrows[token], or
+// the token index itself) are staged once per title in the first 32 words of the dynamic LDS
+// (stage_rows), so the per-head K/V loads never wait on an index load.
+__device__ __forceinline__ const float* yrow(const MPArgs& g, int l) {
+  extern __shared__ int32_t nr_mp_rows[];
+  return g.y + (int64_t)nr_mp_rows[l] * g.ldy;
+}
+
+__device__ __forceinline__ void stage_rows(const MPArgs& g, int64_t seq) {
+  extern __shared__ int32_t nr_mp_rows[];
+  const int tid = threadIdx.x;
+  if (tid < 32) {
+    const int64_t tok = seq * g.L + (tid < g.L ? tid : 0);
+    nr_mp_rows[tid] = (int32_t)(g.yrows ? g.yrows[tok] : tok);
+  }
+  __syncthreads();
+}
 
 __device__ __forceinline__ float drop_scale(const MPArgs& g, int64_t elem) {
   if (g.p_drop <= 0.f) return 1.f;
@@ -78,7 +97,7 @@ __device__ __forceinline__ void load_krow(const MPArgs& g, int64_t seq, int head
     // clamped and zeroed by a select, never a branch: a branch around a load makes hipcc wait
     // for it at the join, serialising the whole load stream.
     const bool ok = c < g.L;
-    const float* kr = g.y + (seq * g.L + (ok ? c : 0)) * g.ldy + head * DK + 4 * h;
+    const float* kr = yrow(g, ok ? c : 0) + head * DK + 4 * h;
 #pragma unroll
     for (int s = 0; s < HK; s += 4) {
       const float4 v = *reinterpret_cast<const float4*>(kr + 2 * s);
@@ -138,7 +157,7 @@ __device__ __forceinline__ void load_vop(const MPArgs& g, int64_t seq, int head,
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const int k = crow(s, h);
-      const float v = g.y[(seq * g.L + (k < g.L ? k : 0)) * g.ldy + nq + head * DV + vb * 32 + c];
+      const float v = yrow(g, k < g.L ? k : 0)[nq + head * DV + vb * 32 + c];
       bv[vb * 16 + s] = k < g.L ? v : 0.f;
     }
 }
@@ -179,7 +198,7 @@ __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int H = NH64 * 64;
   constexpr int SO = H + 1;
-  float* os = sm;                       // [32][SO]  O, then Z
+  float* os = sm + 32;                  // [32][SO]  O, then Z (sm[0..32): staged rows, yrow)
   float* sc = os + 32 * SO;             // [32] scores -> probs
   const int64_t seq = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
@@ -191,6 +210,7 @@ __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
     bet[k] = g.beta[lane + 64 * k];
     qv[k] = g.q[lane + 64 * k];
   }
+  stage_rows(g, seq);
   if (!(g.dbg & 1)) attention_to_lds<DK, DV>(g, seq, bits, os, SO);
   __syncthreads();
   if (g.dbg & 2) return;
@@ -249,7 +269,7 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
   constexpr int H = NH64 * 64;
   constexpr int SO = H + 1;
   const int nw = blockDim.x >> 6, nt = blockDim.x;
-  float* os = sm;                       // [32][SO]  O, then dO
+  float* os = sm + 32;                  // [32][SO]  O, then dO (sm[0..32): staged rows, yrow)
   float* ps = os + 32 * SO;             // [32] pooling probs
   float* ds = ps + 32;                  // [32] dp -> ds
   float* st = ds + 32;                  // [32][2] mean, rstd
@@ -266,6 +286,7 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
     qv[k] = g.q[lane + 64 * k];
     dnv[k] = g.news[seq * g.ldn + lane + 64 * k];
   }
+  stage_rows(g, seq);
   if (!(g.dbg & 1)) attention_to_lds<DK, DV>(g, seq, bits, os, SO);
   if (tid < 32) {
     ps[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
@@ -392,9 +413,8 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) dpt[r] = 0.f;
       constexpr int HV = DV / 2;
-      const float* vr = g.y + (seq * g.L + c) * g.ldy + nq + head * DV + 4 * h;
       const bool rv = c < g.L;
-      const float* vrr = rv ? vr : vr - (int64_t)c * g.ldy;   // clamp to row 0, zero by select
+      const float* vrr = yrow(g, rv ? c : 0) + nq + head * DV + 4 * h;   // clamp, zero by select
 #pragma unroll
       for (int s = 0; s < HV; s += 4) {
         float4 v4 = *reinterpret_cast<const float4*>(vrr + 2 * s);
@@ -426,7 +446,7 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         const int k = crow(s, h);
-        const float v = g.y[(seq * g.L + (k < g.L ? k : 0)) * g.ldy + head * DK + kb * 32 + c];
+        const float v = yrow(g, k < g.L ? k : 0)[head * DK + kb * 32 + c];
         bk[s] = k < g.L ? v : 0.f;
       }
       f32x16 acc;
@@ -447,10 +467,10 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
   }
 }
 
-size_t fwd_smem(int H) { return (size_t)(32 * (H + 1) + 32) * sizeof(float); }
+size_t fwd_smem(int H) { return (size_t)(32 + 32 * (H + 1) + 32) * sizeof(float); }
 size_t bwd_smem(int H, int nw) {
   const size_t tiles = (size_t)nw * 32 * 33, red = (size_t)nw * 2 * H;
-  return (size_t)(32 * (H + 1) + 32 + 32 + 64 + (tiles > red ? tiles : red)) * sizeof(float);
+  return (size_t)(32 + 32 * (H + 1) + 32 + 32 + 64 + (tiles > red ? tiles : red)) * sizeof(float);
 }
 
 template <int DK, int DV, int NH64>
@@ -494,7 +514,8 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
 
-extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const void* mask, int32_t mask_dtype, int64_t nseq,
+extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,
+                               int32_t mask_dtype, int64_t nseq,
                                int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
                                const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset,
                                const float* q, float* news, int64_t ldn, float* zout, int64_t ldz, float* stats,
@@ -504,7 +525,7 @@ extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const void* mask, in
   if ((ldy & 3) || !al16(y)) return NR_EINVAL(2);
   if (nseq == 0) return NR_OK;
   MPArgs g{};
-  g.y = y; g.ldy = ldy; g.mask = mask; g.mask_dt = mask_dtype; g.nseq = nseq; g.L = L; g.heads = heads;
+  g.y = y; g.ldy = ldy; g.yrows = yrows; g.mask = mask; g.mask_dt = mask_dtype; g.nseq = nseq; g.L = L; g.heads = heads;
   g.scale_attn = 1.0f / sqrtf((float)dk); g.scale_pool = 1.0f / sqrtf((float)(heads * dv));
   g.gamma = gamma; g.beta = beta; g.eps = eps; g.p_drop = p_drop; g.seed = seed; g.offset = offset;
   g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop); g.q = q;
@@ -516,7 +537,8 @@ extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const void* mask, in
   return dispatch(g, dk, dv, false, stream);
 }
 
-extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const void* mask, int32_t mask_dtype, int64_t nseq,
+extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,
+                               int32_t mask_dtype, int64_t nseq,
                                int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
                                const float* beta, float p_drop, uint64_t seed, uint64_t offset, const float* q,
                                const float* stats, const float* probs, const float* dnews, int64_t ldn,
@@ -529,7 +551,7 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const void* mask, in
   if ((ldy & 3) || !al16(y)) return NR_EINVAL(2);
   if (nseq == 0) return NR_OK;
   MPArgs g{};
-  g.y = y; g.ldy = ldy; g.mask = mask; g.mask_dt = mask_dtype; g.nseq = nseq; g.L = L; g.heads = heads;
+  g.y = y; g.ldy = ldy; g.yrows = yrows; g.mask = mask; g.mask_dt = mask_dtype; g.nseq = nseq; g.L = L; g.heads = heads;
   g.scale_attn = 1.0f / sqrtf((float)dk); g.scale_pool = 1.0f / sqrtf((float)(heads * dv));
   g.gamma = gamma; g.beta = beta; g.p_drop = p_drop; g.seed = seed; g.offset = offset;
   g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop); g.q = q;

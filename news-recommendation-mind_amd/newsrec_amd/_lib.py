@@ -24,7 +24,7 @@ ROWS_PLAIN, ROWS_GATHER, ROWS_CONV3 = 0, 1, 2
 KCONTIG, MNCONTIG = 0, 1
 EPI_STORE, EPI_STORE_RELU, EPI_ATOMIC, EPI_SCATTER = 0, 1, 2, 3
 MASK_U8, MASK_I64, MASK_F64, MASK_F32 = 0, 1, 2, 3
-EPI_STORE_TANH, EPI_ACCUM_GATE, EPI_ACCUM = 4, 5, 6
+EPI_STORE_TANH, EPI_ACCUM_GATE, EPI_ACCUM, EPI_SCATTER_STORE = 4, 5, 6, 7
 CELL_LSTM, CELL_GRU = 0, 1
 SCORE_RAW, SCORE_LOG_SOFTMAX, SCORE_SIGMOID = 0, 1, 2
 
@@ -34,10 +34,16 @@ class nr_operand(ctypes.Structure):
                 ("map", c_i32), ("seq_len", c_i32), ("seg", c_i32), ("layout", c_i32)]
 
 
-# name -> argtypes (restype is always int32)
+# name -> argtypes (restype int32 unless listed in _RESTYPES)
 _SIGS = {
     "nr_gemm_f32": [c_i64, c_i64, c_i64, ctypes.POINTER(nr_operand), ctypes.POINTER(nr_operand),
                     c_ptr, c_i64, c_ptr, c_i32, ctypes.POINTER(nr_operand), c_i64, c_i32, c_ptr],
+    "nr_gemm_f32_dyn": [c_i64, c_i64, c_i64, ctypes.POINTER(nr_operand), ctypes.POINTER(nr_operand),
+                        c_ptr, c_i64, c_ptr, c_i32, ctypes.POINTER(nr_operand), c_i64, c_i32, c_ptr, c_ptr, c_ptr],
+    "nr_unique_rows": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+    "nr_segment_rows_sum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
+                            c_ptr],
+    "nr_segment_rows_sum_workspace": [c_i64, c_i64],
     "nr_mha_attn_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
                         c_f32, c_ptr, c_i64, c_ptr],
     "nr_mha_attn_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
@@ -58,12 +64,14 @@ _SIGS = {
     "nr_embedding_fwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr],
     "nr_embedding_bwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_ptr],
     "nr_colsum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr],
-    "nr_mha_pool_fwd": [c_ptr, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_f32,
+    "nr_mha_pool_fwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_f32,
                         c_u64, c_u64, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr],
-    "nr_mha_pool_bwd": [c_ptr, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_u64,
+    "nr_mha_pool_bwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_u64,
                         c_u64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
                         c_ptr, c_ptr],
 }
+
+_RESTYPES = {"nr_segment_rows_sum_workspace": c_i64}
 
 _lib = None
 
@@ -82,7 +90,7 @@ def load():
         for name, argtypes in _SIGS.items():
             fn = getattr(lib, name)
             fn.argtypes = argtypes
-            fn.restype = c_i32
+            fn.restype = _RESTYPES.get(name, c_i32)
         _lib = lib
     return _lib
 

@@ -9,6 +9,8 @@ operand loader) and scatter the table gradient straight out of the dgrad GEMM, s
 [T, 768] embedding activations are never materialised.  A standalone ``encoderN(emb, mask)``
 call uses the same functions with the embeddings as the "table" and identity row ids.
 """
+import os
+
 import torch
 
 from . import _lib as L
@@ -65,19 +67,28 @@ class _Probe:
         e.record()
         return e
 
-    def add(self, name, start, end):
+    def add(self, name, start, end, ur=None):
+        """``ur``: the launch's UniqueRows — its device-side row count (U_pad, the GEMM's M) is
+        read back at collect() time for the launch's algorithmic FLOPs."""
         if start is not None:
-            self.events.append((name, start, end))
+            self.events.append((name, start, end, ur.counts if ur is not None else None))
 
     def collect(self):
         torch.cuda.synchronize()
-        out = {}
-        for name, s, e in self.events:
+        out, rows = {}, {}
+        for name, s, e, cnt in self.events:
             out.setdefault(name, []).append(s.elapsed_time(e))
-        return {k + "_ms": sum(v) / len(v) for k, v in out.items()}
+            if cnt is not None:
+                rows.setdefault(name, []).append(int(cnt[1].item()))
+        res = {k + "_ms": sum(v) / len(v) for k, v in out.items()}
+        res.update({k + "_rows": sum(v) / len(v) for k, v in rows.items()})
+        return res
 
 
 PROBE = _Probe()
+
+# Distinct-row projection in the MHA news tower (NR_DEDUP_ROWS=0 projects every token row).
+DEDUP_ROWS = os.environ.get("NR_DEDUP_ROWS", "1") != "0"
 
 
 class _TableGradHook:
@@ -111,25 +122,34 @@ class MHANewsFn(torch.autograd.Function):
                 pad_row, p_drop, seed, offset, want_tokens):
         T = ids.numel()
         n = T // seq_len
-        E = table.shape[1]
+        V, E = table.shape
         H = heads * dv
         NQ = heads * dk
         NY = NQ + H
-        Y = _empty(T, NY, table)
-        ev0 = PROBE.record()
-        K.gemm(T, NY, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(w_cat, L.KCONTIG),
-               Y, bias=b_cat)
-        PROBE.add("proj_fwd", ev0, PROBE.record())
+        fused = K.mha_pool_supported(seq_len, heads, dk, dv)
+        ur = None
+        if fused and DEDUP_ROWS:
+            # project each distinct word-table row once (Y rows = distinct ids, read through inv)
+            ur = K.UniqueRows(ids, V, fill_row=pad_row if 0 <= pad_row < V else 0)
+            Y = _empty(ur.cap, NY, table)
+            ev0 = PROBE.record()
+            K.gemm_dyn(ur.cap, NY, E, K.operand(table, L.KCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER),
+                       K.operand(w_cat, L.KCONTIG), Y, m_dev=ur.u_pad, bias=b_cat)
+        else:
+            Y = _empty(T, NY, table)
+            ev0 = PROBE.record()
+            K.gemm(T, NY, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER),
+                   K.operand(w_cat, L.KCONTIG), Y, bias=b_cat)
+        PROBE.add("proj_fwd", ev0, PROBE.record(), ur)
         news = _empty(n, H, table)
         probs = torch.empty(T, device=table.device)
         stats = torch.empty(T, 2, device=table.device)
         tok = _empty(T, H, table) if want_tokens else None
-        fused = K.mha_pool_supported(seq_len, heads, dk, dv)
         if fused:
             # attention + LN + dropout + pooling in one kernel per title; O stays in LDS
             O = None
             K.mha_pool_fwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, news, stats, probs,
-                           p_drop=p_drop, seed=seed, offset=offset, zout=tok)
+                           p_drop=p_drop, seed=seed, offset=offset, zout=tok, yrows=ur.inv if ur else None)
         else:
             O = _empty(T, H, table)
             K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, O)
@@ -138,6 +158,7 @@ class MHANewsFn(torch.autograd.Function):
         ctx.save_for_backward(table, ids, mask, w_cat, gamma, beta, query, Y, O, probs, stats)
         ctx.cfg = (heads, dk, dv, seq_len, pad_row, p_drop, seed, offset, fused)
         ctx.table_ref = table
+        ctx.ur = ur
         return news, tok
 
     @staticmethod
@@ -157,9 +178,11 @@ class MHANewsFn(torch.autograd.Function):
         dY = _empty(T, NY, table)
         dz = dtok.contiguous() if dtok is not None else None
         db = torch.zeros(NY, device=table.device)
+        ur = ctx.ur
         if fused:
             K.mha_pool_bwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, stats, probs, dnews, dY, db, dq,
-                           dgamma, dbeta, p_drop=p_drop, seed=seed, offset=offset, dz=dz)
+                           dgamma, dbeta, p_drop=p_drop, seed=seed, offset=offset, dz=dz,
+                           yrows=ur.inv if ur else None)
         else:
             dO = _empty(T, H, table)
             K.attn_pool_bwd(O, query, mask, n, seq_len, probs, dnews, dO, dq, gamma=gamma, beta=beta, stats=stats,
@@ -167,14 +190,30 @@ class MHANewsFn(torch.autograd.Function):
             K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
             K.colsum(dY, T, NY, db)
         dtable = None
-        if ctx.needs_input_grad[0]:
-            dtable = torch.zeros(V, E, device=table.device)
-            K.gemm(T, E, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dtable,
-                   epilogue=L.EPI_SCATTER, c_rows=K.rows_map(ids, L.ROWS_GATHER), pad_row=pad_row)
-            if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
-                dtable = None
         dw = torch.zeros(NY, E, device=table.device)
-        _proj_wgrad(dY, K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dw, None, T)
+        if ur is not None:
+            # per-distinct-row gradient, then the two GEMMs over U rows instead of T tokens
+            dYu = _empty(ur.cap, NY, table)
+            ur.segment_sum(dY, dYu)
+            if ctx.needs_input_grad[0]:
+                dtable = torch.zeros(V, E, device=table.device)
+                # distinct rows (M = U, not U_pad: no duplicate pad ids): plain row stores
+                K.gemm_dyn(ur.cap, E, NY, K.operand(dYu, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dtable,
+                           m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_STORE,
+                           c_rows=K.rows_map(ur.uids, L.ROWS_GATHER), pad_row=pad_row)
+                if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
+                    dtable = None
+            K.gemm_dyn(NY, E, ur.cap, K.operand(dYu, L.MNCONTIG),
+                       K.operand(table, L.MNCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER), dw, k_dev=ur.u_pad,
+                       epilogue=L.EPI_ATOMIC, split_k=_split_k(NY, E, ur.cap))
+        else:
+            if ctx.needs_input_grad[0]:
+                dtable = torch.zeros(V, E, device=table.device)
+                K.gemm(T, E, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dtable,
+                       epilogue=L.EPI_SCATTER, c_rows=K.rows_map(ids, L.ROWS_GATHER), pad_row=pad_row)
+                if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
+                    dtable = None
+            _proj_wgrad(dY, K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dw, None, T)
         return (dtable, None, None, dw, db, dgamma, dbeta, dq.view_as(query), None, None, None, None, None,
                 None, None, None, None)
 

@@ -30,6 +30,65 @@ def gemm(M, N, K, A, B, C, ldc=None, bias=None, epilogue=L.EPI_STORE, c_rows=Non
            L.ptr(bias), epilogue, c_rows, pad_row, split_k, L.stream_ptr(C))
 
 
+def gemm_dyn(M, N, K, A, B, C, m_dev=None, k_dev=None, ldc=None, bias=None, epilogue=L.EPI_STORE,
+             c_rows=None, pad_row=-1, split_k=1):
+    """``gemm`` with device-resident extents: M, K are upper bounds, the kernel reads the actual
+    M / K from the int32 CUDA scalars ``m_dev`` / ``k_dev`` (e.g. ``UniqueRows.counts[1:2]``)."""
+    _f32(C, bias)
+    for t in (m_dev, k_dev):
+        if t is not None and (t.dtype != torch.int32 or not t.is_cuda):
+            raise L.HipError("gemm_dyn: device extents must be int32 CUDA tensors")
+    if bias is not None and bias.numel() < N:
+        raise L.HipError("gemm_dyn: bias has %d < N=%d entries" % (bias.numel(), N))
+    if K % 32:
+        raise L.HipError("gemm_dyn: K must be a multiple of 32")
+    L.call("nr_gemm_f32_dyn", M, N, K, A, B, L.ptr(C), ldc if ldc is not None else C.stride(0),
+           L.ptr(bias), epilogue, c_rows, pad_row, split_k, L.ptr(m_dev), L.ptr(k_dev), L.stream_ptr(C))
+
+
+def _ceil32(n):
+    return (n + 31) // 32 * 32
+
+
+class UniqueRows:
+    """Distinct ids of a token batch (``nr_unique_rows``), sizes left on the device.
+
+    uids [cap] int64 (valid prefix counts[1], ascending, padded with fill_row), inv [T] int64,
+    seg_off [cap + 1] / seg_tok [T] int32 CSR, counts [3] int32 = (U, U_pad, bad);
+    cap = ceil32(min(T, V)) is the host-side upper bound of U_pad."""
+
+    def __init__(self, ids, vocab, fill_row=0):
+        _check_rows(ids, None, "unique_rows")
+        T = ids.numel()
+        dev = ids.device
+        self.T, self.vocab = T, vocab
+        self.cap = max(32, _ceil32(min(T, vocab)))
+        i32 = dict(device=dev, dtype=torch.int32)
+        work = torch.empty(4 * vocab, **i32)
+        self.uids = torch.empty(self.cap, device=dev, dtype=torch.int64)
+        self.inv = torch.empty(T, device=dev, dtype=torch.int64)
+        self.seg_off = torch.empty(self.cap + 1, **i32)
+        self.seg_tok = torch.empty(max(T, 1), **i32)
+        self.seg_of = torch.empty(max(T, 1), **i32)
+        self.counts = torch.empty(3, **i32)
+        L.call("nr_unique_rows", L.ptr(ids), T, vocab, fill_row, L.ptr(work), L.ptr(self.uids), L.ptr(self.inv),
+               L.ptr(self.seg_off), L.ptr(self.seg_tok), L.ptr(self.seg_of), L.ptr(self.counts), L.stream_ptr(ids))
+        self.n_rows = self.counts[0:1]  # device scalar: U
+        self.u_pad = self.counts[1:2]   # device scalar: U_pad, the GEMM extent
+
+    def segment_sum(self, src, dst):
+        """dst[u] = Σ src[t] over the tokens t of distinct row u (zeros on pad rows)."""
+        _f32(src, dst)
+        _rows_ok(src, self.T, src.shape[1], "segment_sum src")
+        _rows_ok(dst, self.cap, src.shape[1], "segment_sum dst")
+        width = src.shape[1]
+        nbytes = L.load().nr_segment_rows_sum_workspace(self.T, width)
+        work = torch.empty(max(1, nbytes // 4), device=src.device, dtype=torch.float32)
+        L.call("nr_segment_rows_sum", L.ptr(src), src.stride(0), width, self.T, L.ptr(self.seg_off),
+               L.ptr(self.seg_tok), L.ptr(self.seg_of), L.ptr(self.counts), self.cap, L.ptr(work), L.ptr(dst),
+               dst.stride(0), L.stream_ptr(src))
+
+
 def operand(t, layout, rows=None, mapping=L.ROWS_PLAIN, seq_len=1, seg=1, ld=None):
     """Describe a stored matrix ``t`` (2-D, row-major, ld % 4 == 0, 16-B aligned)."""
     _f32(t)
@@ -265,12 +324,23 @@ def mha_pool_supported(seq_len, heads, dk, dv):
     return seq_len <= 32 and (dk, dv, heads * dv) in MHA_POOL_SHAPES
 
 
+def _yrows_ok(y, yrows, T, ncols, name):
+    if yrows is None:
+        _rows_ok(y, T, ncols, name)
+    else:
+        _check_rows(yrows, None, name)
+        if yrows.numel() < T:
+            raise L.HipError("%s: yrows has %d < %d entries" % (name, yrows.numel(), T))
+        _rows_ok(y, 1, ncols, name)
+
+
 def mha_pool_fwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, news, stats, probs, eps=1e-5,
-                 p_drop=0.0, seed=0, offset=0, zout=None):
-    """Fused tied-QK attention + LayerNorm + dropout + query pooling per title."""
+                 p_drop=0.0, seed=0, offset=0, zout=None, yrows=None):
+    """Fused tied-QK attention + LayerNorm + dropout + query pooling per title.  ``yrows``:
+    token t reads projection row yrows[t] (distinct-row projections)."""
     H = heads * dv
     _f32(y, gamma, beta, q, news, stats, probs, zout)
-    _rows_ok(y, nseq * seq_len, heads * (dk + dv), "y")
+    _yrows_ok(y, yrows, nseq * seq_len, heads * (dk + dv), "y")
     if y.stride(0) % 4 or y.data_ptr() % 16:
         raise L.HipError("mha_pool_fwd: y needs ld % 4 == 0 and 16-B alignment")
     _rows_ok(news, nseq, H, "news")
@@ -278,23 +348,23 @@ def mha_pool_fwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, news, st
     if stats.numel() < 2 * nseq * seq_len or probs.numel() < nseq * seq_len:
         raise L.HipError("mha_pool_fwd: stats/probs too small")
     mp, mdt = mask_arg(mask, nseq * seq_len)
-    L.call("nr_mha_pool_fwd", L.ptr(y), y.stride(0), mp, mdt, nseq, seq_len, heads, dk, dv, L.ptr(gamma),
+    L.call("nr_mha_pool_fwd", L.ptr(y), y.stride(0), L.ptr(yrows), mp, mdt, nseq, seq_len, heads, dk, dv, L.ptr(gamma),
            L.ptr(beta), eps, p_drop, seed, offset, L.ptr(q), L.ptr(news), news.stride(0), L.ptr(zout),
            zout.stride(0) if zout is not None else 0, L.ptr(stats), L.ptr(probs), L.stream_ptr(y))
 
 
 def mha_pool_bwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, dbias, dq,
-                 dgamma, dbeta, p_drop=0.0, seed=0, offset=0, dz=None):
+                 dgamma, dbeta, p_drop=0.0, seed=0, offset=0, dz=None, yrows=None):
     H = heads * dv
     _f32(y, gamma, beta, q, stats, probs, dnews, dy, dbias, dq, dgamma, dbeta, dz)
-    _rows_ok(y, nseq * seq_len, heads * (dk + dv), "y")
+    _yrows_ok(y, yrows, nseq * seq_len, heads * (dk + dv), "y")
     _rows_ok(dy, nseq * seq_len, heads * (dk + dv), "dy")
     _rows_ok(dnews, nseq, H, "dnews")
     _rows_ok(dz, nseq * seq_len, H, "dz")
     if dbias.numel() < heads * (dk + dv):
         raise L.HipError("mha_pool_bwd: dbias too small")
     mp, mdt = mask_arg(mask, nseq * seq_len)
-    L.call("nr_mha_pool_bwd", L.ptr(y), y.stride(0), mp, mdt, nseq, seq_len, heads, dk, dv, L.ptr(gamma),
+    L.call("nr_mha_pool_bwd", L.ptr(y), y.stride(0), L.ptr(yrows), mp, mdt, nseq, seq_len, heads, dk, dv, L.ptr(gamma),
            L.ptr(beta), p_drop, seed, offset, L.ptr(q), L.ptr(stats), L.ptr(probs), L.ptr(dnews), dnews.stride(0),
            L.ptr(dz), dz.stride(0) if dz is not None else 0, L.ptr(dy), dy.stride(0), L.ptr(dbias), L.ptr(dq),
            L.ptr(dgamma), L.ptr(dbeta), L.stream_ptr(y))

@@ -13,7 +13,17 @@ HEADER = os.path.join(ROOT, "include", "newsrec_hip.h")
 
 def declared():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^int\s+(nr_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t)\s+(nr_\w+)\s*\(", txt, flags=re.M)))
+
+
+def declared_arity():
+    """name -> number of parameters, from the prototypes in the header."""
+    txt = open(HEADER).read()
+    out = {}
+    for m in re.finditer(r"^(?:int|int64_t)\s+(nr_\w+)\s*\(([^)]*)\)\s*;", txt, flags=re.M):
+        params = [p for p in m.group(2).replace("\n", " ").split(",") if p.strip()]
+        out[m.group(1)] = len(params)
+    return out
 
 
 def test_header_declares_entry_points():
@@ -34,6 +44,11 @@ def test_library_exports_every_declared_symbol():
 def test_bindings_match_header():
     from newsrec_amd import _lib
     assert sorted(_lib.declared_symbols()) == declared()
+    arity = declared_arity()
+    assert sorted(arity) == declared()
+    for name in declared():
+        assert len(_lib._SIGS[name]) == arity[name], "%s: %d ctypes args vs %d in the header" % (
+            name, len(_lib._SIGS[name]), arity[name])
 
 
 def test_product_path_fails_loudly_without_gpu():

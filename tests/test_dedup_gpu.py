@@ -1,0 +1,165 @@
+"""Distinct-row projection path: nr_unique_rows / nr_segment_rows_sum / nr_gemm_f32_dyn and the
+yrows indirection of the fused MHA pool kernels, each against a plain torch / numpy statement
+of the same operation; then the MHA news Function with and without dedup on the same inputs."""
+import numpy as np
+import pytest
+import torch
+
+from newsrec_amd import _lib as L
+from newsrec_amd import functions as F
+from newsrec_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _ids(T, V, seed, pad_frac=0.4):
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(1, V, (T,), generator=g)
+    ids[torch.rand(T, generator=g) < pad_frac] = 0
+    return ids
+
+
+@pytest.mark.parametrize("T,V", [(1, 5), (37, 7), (1000, 30522), (52800, 30522), (4096, 100)])
+def test_unique_rows(T, V):
+    ids = _ids(T, V, T + V)
+    ur = K.UniqueRows(ids.cuda(), V, fill_row=0)
+    torch.cuda.synchronize()
+    U, Up, bad = ur.counts.tolist()
+    ref = np.unique(ids.numpy())
+    assert bad == 0 and U == len(ref) and Up == (U + 31) // 32 * 32
+    uids = ur.uids.cpu().numpy()
+    assert (uids[:U] == ref).all() and (uids[U:Up] == 0).all()
+    inv = ur.inv.cpu().numpy()
+    assert (uids[inv] == ids.numpy()).all()
+    off = ur.seg_off.cpu().numpy()
+    tok = ur.seg_tok.cpu().numpy()
+    assert off[0] == 0 and off[Up] == T and (off[U:Up + 1] == T).all()
+    for u in np.random.default_rng(0).choice(U, size=min(U, 200), replace=False):
+        seg = np.sort(tok[off[u]:off[u + 1]])
+        assert (seg == np.nonzero(ids.numpy() == uids[u])[0]).all()
+
+
+def test_unique_rows_flags_bad_ids():
+    ids = torch.tensor([0, 3, 9, 2], dtype=torch.int64)
+    ur = K.UniqueRows(ids.cuda(), 5)
+    torch.cuda.synchronize()
+    U, Up, bad = ur.counts.tolist()
+    assert bad == 1 and U == 3
+
+
+@pytest.mark.parametrize("T,V,W", [(300, 50, 1152), (52800, 30522, 1152), (33, 4, 4)])
+def test_segment_sum(T, V, W):
+    ids = _ids(T, V, 7 * T)
+    ur = K.UniqueRows(ids.cuda(), V)
+    src = torch.randn(T, W, device="cuda")
+    dst = torch.full((ur.cap, W), float("nan"), device="cuda")
+    ur.segment_sum(src, dst)
+    torch.cuda.synchronize()
+    U, Up, _ = ur.counts.tolist()
+    ref = torch.zeros(ur.cap, W, dtype=torch.float64, device="cuda")
+    ref.index_add_(0, ur.inv, src.double())
+    # fp32 sums of n unit-variance terms: tolerance grows with the segment length n
+    n = torch.bincount(ur.inv, minlength=ur.cap)[:U].double()[:, None]
+    err = (dst[:U].double() - ref[:U]).abs()
+    assert (err <= 1e-5 + 1e-6 * n).all(), float((err - 1e-6 * n).max())
+    assert (dst[U:Up] == 0).all()
+
+
+def test_gemm_dyn_rows_and_k():
+    torch.manual_seed(0)
+    V, E, N = 2000, 256, 384
+    table = torch.randn(V, E, device="cuda")
+    W = torch.randn(N, E, device="cuda") * 0.05
+    b = torch.randn(N, device="cuda")
+    ids = _ids(5000, V, 3).cuda()
+    ur = K.UniqueRows(ids, V)
+    Y = torch.full((ur.cap, N), float("nan"), device="cuda")
+    K.gemm_dyn(ur.cap, N, E, K.operand(table, L.KCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER),
+               K.operand(W, L.KCONTIG), Y, m_dev=ur.u_pad, bias=b)
+    torch.cuda.synchronize()
+    Up = int(ur.counts[1])
+    ref = table[ur.uids[:Up]].double() @ W.double().t() + b.double()
+    torch.testing.assert_close(Y[:Up].double(), ref, rtol=1e-4, atol=1e-4)
+    assert torch.isnan(Y[Up:]).all()   # rows past the device extent untouched
+    # K from the device: dW = dYuᵀ table[uids] over U_pad rows, split-K atomic
+    dYu = torch.randn(ur.cap, N, device="cuda")
+    dW = torch.zeros(N, E, device="cuda")
+    K.gemm_dyn(N, E, ur.cap, K.operand(dYu, L.MNCONTIG), K.operand(table, L.MNCONTIG, rows=ur.uids,
+               mapping=L.ROWS_GATHER), dW, k_dev=ur.u_pad, epilogue=L.EPI_ATOMIC, split_k=7)
+    torch.cuda.synchronize()
+    ref = dYu[:Up].double().t() @ table[ur.uids[:Up]].double()
+    torch.testing.assert_close(dW.double(), ref, rtol=1e-4, atol=1e-3)
+    # scatter dgrad into a table gradient over the distinct rows
+    dtab = torch.zeros(V, E, device="cuda")
+    K.gemm_dyn(ur.cap, E, N, K.operand(dYu, L.KCONTIG), K.operand(W, L.MNCONTIG), dtab, m_dev=ur.u_pad,
+               epilogue=L.EPI_SCATTER, c_rows=K.rows_map(ur.uids, L.ROWS_GATHER), pad_row=0)
+    torch.cuda.synchronize()
+    ref = torch.zeros(V, E, dtype=torch.float64, device="cuda")
+    ref.index_add_(0, ur.uids[:Up], dYu[:Up].double() @ W.double())
+    ref[0] = 0
+    torch.testing.assert_close(dtab.double(), ref, rtol=1e-4, atol=1e-4)
+    # the same through plain row stores over the U distinct rows
+    dtab2 = torch.zeros(V, E, device="cuda")
+    K.gemm_dyn(ur.cap, E, N, K.operand(dYu, L.KCONTIG), K.operand(W, L.MNCONTIG), dtab2, m_dev=ur.n_rows,
+               epilogue=L.EPI_SCATTER_STORE, c_rows=K.rows_map(ur.uids, L.ROWS_GATHER), pad_row=0)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dtab2.double(), ref, rtol=1e-4, atol=1e-4)
+
+
+def test_mha_pool_yrows_matches_gathered():
+    torch.manual_seed(1)
+    n, Lq, heads, dk, dv = 64, 30, 12, 64, 32
+    T, NY, H = n * Lq, heads * (dk + dv), heads * dv
+    ids = _ids(T, 500, 11).cuda()
+    ur = K.UniqueRows(ids, 500)
+    Yu = torch.randn(ur.cap, NY, device="cuda") * 0.3
+    Yt = Yu[ur.inv].contiguous()
+    mask = (torch.rand(n, Lq, device="cuda") < 0.8).long()
+    mask[:, 0] = 1
+    gamma = 1 + 0.1 * torch.randn(H, device="cuda")
+    beta = 0.1 * torch.randn(H, device="cuda")
+    q = torch.randn(H, device="cuda")
+    outs = []
+    for Y, yrows in ((Yt, None), (Yu, ur.inv)):
+        news = torch.empty(n, H, device="cuda")
+        stats = torch.empty(T, 2, device="cuda")
+        probs = torch.empty(T, device="cuda")
+        K.mha_pool_fwd(Y, mask, n, Lq, heads, dk, dv, gamma, beta, q, news, stats, probs, p_drop=0.2, seed=5,
+                       offset=9, yrows=yrows)
+        dnews = torch.ones(n, H, device="cuda")
+        dy = torch.empty(T, NY, device="cuda")
+        db, dq, dg, dbt = (torch.zeros(NY, device="cuda"), torch.zeros(H, device="cuda"),
+                           torch.zeros(H, device="cuda"), torch.zeros(H, device="cuda"))
+        K.mha_pool_bwd(Y, mask, n, Lq, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, db, dq, dg, dbt,
+                       p_drop=0.2, seed=5, offset=9, yrows=yrows)
+        outs.append((news, dy))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])   # same rows, same arithmetic: bitwise
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_mha_news_dedup_vs_tokenwise(monkeypatch):
+    torch.manual_seed(2)
+    V, E, heads, dk, dv, Lq, n = 3000, 768, 12, 64, 32, 30, 96
+    H, NY = heads * dv, heads * (dk + dv)
+    table = (torch.randn(V, E, device="cuda") * 0.5).requires_grad_()
+    ids = _ids(n * Lq, V, 21).cuda()
+    mask = (ids != 0).long().view(n, Lq)
+    mask[:, 0] = 1
+    w = (torch.randn(NY, E, device="cuda") * 0.03).requires_grad_()
+    b = (torch.randn(NY, device="cuda") * 0.1).requires_grad_()
+    gamma = torch.ones(H, device="cuda", requires_grad=True)
+    beta = torch.zeros(H, device="cuda", requires_grad=True)
+    q = torch.randn(1, H, device="cuda", requires_grad=True)
+    res = []
+    for dedup in (False, True):
+        monkeypatch.setattr(F, "DEDUP_ROWS", dedup)
+        for t in (table, w, b, gamma, beta, q):
+            t.grad = None
+        news, _ = F.MHANewsFn.apply(table, ids, mask, w, b, gamma, beta, q, heads, dk, dv, Lq, 0, 0.2, 3, 4, False)
+        (news * torch.linspace(-1, 1, H, device="cuda")).sum().backward()
+        res.append([news.detach().clone()] + [t.grad.clone() for t in (table, w, b, gamma, beta, q)])
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0])   # forward: identical rows, identical arithmetic
+    for a, c in zip(res[0][1:], res[1][1:]):   # backward: same sums, different fp32 order
+        torch.testing.assert_close(c, a, rtol=1e-4, atol=5e-5)
