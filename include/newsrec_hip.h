@@ -91,19 +91,23 @@ int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand* A, const 
  * per token: BERT.py:39 + Attention.py:107-108 commute with the gather).  Outputs:
  *   uids[U_pad]      distinct ids ascending, padded with fill_row up to U_pad = ceil32(U)
  *   inv[T]           uids[inv[t]] == ids[t]
- *   seg_off[U_pad+1], seg_tok[T], seg_of[T]   CSR of the tokens of each distinct id (pad
- *                    rows empty); seg_of[p] = the distinct row owning CSR position p
- *   counts[3]        {U, U_pad, bad} (bad = 1 if an id fell outside [0, V))
- * fill_row is also the "hot" id (the padding row) whose tokens are counted per wave.
- * work: 4*V int32.  Capacity: uids / seg_off hold ceil32(min(T, V)) (+1) entries. */
-int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t fill_row, int32_t* work,
-                   int64_t* uids, int64_t* inv, int32_t* seg_off, int32_t* seg_tok,
-                   int32_t* seg_of, int32_t* counts, hipStream_t stream);
+ *   seg_off[U_pad+1], seg_tok[T], seg_of[T]   CSR of the tokens of each distinct id whose
+ *                    grad_mask is nonzero (grad_mask NULL: every token); seg_of[p] = the
+ *                    distinct row owning CSR position p.  Leave a token out only when its
+ *                    gradient row is zero (masked tokens of nr_mha_pool_bwd: exactly zero).
+ *   counts[4]        {U, U_pad, bad, T_csr} (bad = 1 if an id fell outside [0, V))
+ * Equal ids are aggregated per workgroup (LDS hash) before the global atomics.
+ * work: 5*V int32.  Capacity: uids / seg_off hold ceil32(min(T, V)) (+1) entries. */
+int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t fill_row,
+                   const void* grad_mask, int32_t mask_dtype, int32_t* work, int64_t* uids,
+                   int64_t* inv, int32_t* seg_off, int32_t* seg_tok, int32_t* seg_of,
+                   int32_t* counts, hipStream_t stream);
 
 /* Bytes of `work` nr_segment_rows_sum needs for T tokens of `width` floats. */
 int64_t nr_segment_rows_sum_workspace(int64_t T, int64_t width);
 
-/* dst[u][:] = Σ_{t in segment u} src[t][:]  for u < counts[0]; zero rows up to counts[1].
+/* dst[u][:] = Σ_{t in segment u} src[t][:]  for u < counts[0] (zero for an empty segment),
+ * zero rows up to counts[1]; the CSR holds counts[3] <= T positions.
  * The per-distinct-row gradient of the projection (what embedding_dense_backward sums after
  * the dgrad, summed before it).  No atomics.  width, lds, ldd multiples of 4; rows_max >=
  * counts[1]; src, dst, work 16-B aligned. */

@@ -9,12 +9,15 @@
 // nn.Embedding), taken before the GEMM instead of after it.
 //
 // nr_unique_rows  : ids[T] -> uids[U_pad] (ascending), inv[T] (uids[inv[t]] == ids[t]),
-//                   CSR seg_off[U_pad + 1] / seg_tok[T] of the tokens of each distinct id,
-//                   counts = {U, U_pad}; U_pad = U rounded up to 32 (pad entries = fill_row,
-//                   empty segments).  Sizes stay on the device: no host synchronisation.
-// nr_segment_rows_sum : dst[u] = sum over t in segment u of src[t]   (zero for pad rows);
-//                   two passes over the CSR, no atomics: ranges of 64 positions, then the
-//                   segments cut by a range boundary (a long padding segment spans many).
+//                   CSR seg_off[U_pad + 1] / seg_tok / seg_of of the tokens of each distinct
+//                   id whose grad_mask is set (all tokens without a mask: masked-out tokens of
+//                   the fused MHA tail receive an exactly-zero dY, so leaving them out of the
+//                   sums changes nothing and drops the long padding segment),
+//                   counts = {U, U_pad, bad, T_csr}; U_pad = U rounded up to 32 (pad entries =
+//                   fill_row, empty segments).  Sizes stay on the device: no host sync.
+// nr_segment_rows_sum : dst[u] = sum over t in segment u of src[t]   (zero for empty / pad
+//                   rows); two passes over the CSR, no atomics: ranges of 64 positions, then
+//                   the segments cut by a range boundary.
 #include "common.h"
 #include "../../include/newsrec_hip.h"
 
@@ -22,27 +25,52 @@ namespace {
 
 constexpr int SCAN_THREADS = 1024;
 constexpr int SEG_RANGE = 64;   // CSR positions per segment-sum workgroup
-
-// Tokens equal to the hot id (the padding row: most of a padded title batch) are counted per
-// workgroup (ballot popcounts into LDS, one global atomic per block) — same-address global
-// atomics serialise at one L2 channel, ~825 of them took ~25 us.
 constexpr int CNT_THREADS = 1024;
+constexpr int HASH_SLOTS = 2048;
 
+// Per-workgroup aggregation of equal ids: an open-addressing hash table in LDS (1024 tokens ->
+// 2048 slots) collects (id, count); one global atomic per distinct id of the block.  Frequent
+// ids (padding, [CLS], [SEP]: once per title) would otherwise serialise thousands of
+// same-address atomics at one L2 channel.  Returns the slot; `rank` = the token's arrival
+// order among the block's tokens of that id counted in `hcnt` (unique, order not fixed).
+__device__ __forceinline__ int hash_slot(int32_t* hkey, int32_t v) {
+  uint32_t h = ((uint32_t)v * 0x9E3779B1u) >> (32 - 11);   // 11 bits: HASH_SLOTS
+  for (;;) {
+    const int32_t old = atomicCAS(&hkey[h], -1, v);
+    if (old == -1 || old == v) return (int)h;
+    h = (h + 1) & (HASH_SLOTS - 1);
+  }
+}
+
+__device__ __forceinline__ bool grad_on(const void* gm, int dt, int64_t t) {
+  return gm == nullptr || nr_mask_at(gm, dt, t);
+}
+
+// cnt_all[v]: tokens of id v (distinctness), cnt_csr[v]: those with grad_mask set (segments)
 __global__ __launch_bounds__(CNT_THREADS) void count_kernel(const int64_t* __restrict__ ids, int64_t T, int64_t V,
-                                                            int64_t hot, int32_t* __restrict__ cnt,
+                                                            const void* gm, int gm_dt, int32_t* __restrict__ cnt_all,
+                                                            int32_t* __restrict__ cnt_csr,
                                                             int32_t* __restrict__ counts) {
-  __shared__ int32_t hot_n;
-  if (threadIdx.x == 0) hot_n = 0;
+  __shared__ int32_t hkey[HASH_SLOTS], hall[HASH_SLOTS], hcsr[HASH_SLOTS];
+  for (int i = threadIdx.x; i < HASH_SLOTS; i += blockDim.x) { hkey[i] = -1; hall[i] = 0; hcsr[i] = 0; }
   __syncthreads();
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t v = t < T ? ids[t] : -1;
-  const bool bad = t < T && (v < 0 || v >= V);
-  if (bad) counts[2] = 1;   // out-of-range id: flagged, token dropped
-  const uint64_t hb = __ballot(t < T && v == hot);
-  if (hb && (threadIdx.x & 63) == __builtin_ctzll(hb)) atomicAdd(&hot_n, __builtin_popcountll(hb));
-  if (t < T && !bad && v != hot) atomicAdd(&cnt[v], 1);
+  if (t < T) {
+    const int64_t v = ids[t];
+    if (v < 0 || v >= V) {
+      counts[2] = 1;   // out-of-range id: flagged, token dropped
+    } else {
+      const int h = hash_slot(hkey, (int32_t)v);
+      atomicAdd(&hall[h], 1);
+      if (grad_on(gm, gm_dt, t)) atomicAdd(&hcsr[h], 1);
+    }
+  }
   __syncthreads();
-  if (threadIdx.x == 0 && hot_n) atomicAdd(&cnt[hot], hot_n);
+  for (int i = threadIdx.x; i < HASH_SLOTS; i += blockDim.x)
+    if (hkey[i] >= 0) {
+      atomicAdd(&cnt_all[hkey[i]], hall[i]);
+      if (hcsr[i]) atomicAdd(&cnt_csr[hkey[i]], hcsr[i]);
+    }
 }
 
 // Inclusive wave scan (Hillis-Steele over the 64 lanes).
@@ -56,26 +84,56 @@ __device__ __forceinline__ int32_t wave_scan_incl(int32_t x) {
   return x;
 }
 
-// One workgroup walks the vocabulary in coalesced tiles of 4 x 1024 entries (4 consecutive per
-// thread): exclusive scans of (cnt[v] > 0) -> pos[v] and of cnt[v] -> off[v], and the
-// compaction uids[pos[v]] = v, seg_off[pos[v]] = off[v].
-__global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(const int32_t* __restrict__ cnt, int64_t V,
+// One workgroup scans the vocabulary in tiles of SCAN_PER x 1024 entries: coalesced loads into
+// LDS, each thread scans SCAN_PER consecutive entries read back from LDS (1-word row pad: no
+// bank conflicts), block scan of the thread totals, and every output leaves through LDS with
+// coalesced stores.  Exclusive scans of (cnt_all[v] > 0) -> pos[v] and of cnt_csr[v] ->
+// off[v]; compaction uids[pos[v]] = v, seg_off[pos[v]] = off[v].
+constexpr int SCAN_PER = 16;
+constexpr int SCAN_TILE = SCAN_PER * SCAN_THREADS;
+constexpr int SCAN_LDS_WORDS = SCAN_TILE + SCAN_TILE / SCAN_PER;
+
+__device__ __forceinline__ int scan_lds_index(int v) { return v + v / SCAN_PER; }
+
+__device__ __forceinline__ void scan_load(int32_t* tile, const int32_t* __restrict__ src, int64_t base, int nv) {
+  const int tid = threadIdx.x;
+  int32_t ld[SCAN_PER];   // all loads in flight before the first LDS store
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) {
+    const int i = tid + k * SCAN_THREADS;
+    ld[k] = i < nv ? src[base + i] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) tile[scan_lds_index(tid + k * SCAN_THREADS)] = ld[k];
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(const int32_t* __restrict__ cnt_all,
+                                                            const int32_t* __restrict__ cnt_csr, int64_t V,
                                                             int32_t* __restrict__ pos, int32_t* __restrict__ off,
                                                             int64_t* __restrict__ uids, int32_t* __restrict__ seg_off,
                                                             int32_t* __restrict__ counts, int64_t fill_row) {
+  extern __shared__ int32_t tile[];   // SCAN_LDS_WORDS
   __shared__ int32_t wu[SCAN_THREADS / 64], wc[SCAN_THREADS / 64];
   __shared__ int32_t carry[2];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (tid == 0) carry[0] = carry[1] = 0;
-  __syncthreads();
-  for (int64_t base = 0; base < V; base += 4 * SCAN_THREADS) {
-    const int64_t v0 = base + 4 * tid;
-    int32_t c[4];
+  for (int64_t base = 0; base < V; base += SCAN_TILE) {
+    const int nv = (int)(V - base < SCAN_TILE ? V - base : SCAN_TILE);
+    int32_t f[SCAN_PER], c[SCAN_PER];   // f: id present, c: segment length
+    scan_load(tile, cnt_all, base, nv);
+    __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 4; ++k) c[k] = v0 + k < V ? cnt[v0 + k] : 0;
+    for (int k = 0; k < SCAN_PER; ++k) f[k] = tile[scan_lds_index(SCAN_PER * tid + k)] > 0 ? 1 : 0;
+    __syncthreads();
+    scan_load(tile, cnt_csr, base, nv);
+    __syncthreads();
     int32_t fu = 0, fc = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { fu += c[k] > 0; fc += c[k]; }
+    for (int k = 0; k < SCAN_PER; ++k) {
+      c[k] = tile[scan_lds_index(SCAN_PER * tid + k)];
+      fu += f[k];
+      fc += c[k];
+    }
     const int32_t iu = wave_scan_incl(fu), ic = wave_scan_incl(fc);
     if (lane == 63) { wu[w] = iu; wc[w] = ic; }
     __syncthreads();
@@ -83,22 +141,45 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(const int32_t* __res
     for (int k = 0; k < w; ++k) { pu += wu[k]; pc += wc[k]; }
     pu += iu - fu;   // exclusive
     pc += ic - fc;
+    const int32_t pu0 = pu, pc0 = pc, ubase = carry[0];
+    __syncthreads();   // every thread has read carry
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t v = v0 + k;
-      if (v < V) {
-        pos[v] = pu;
-        off[v] = pc;
-        if (c[k] > 0) {
-          uids[pu] = v;
-          seg_off[pu] = pc;
-        }
-      }
-      pu += c[k] > 0;
+    for (int k = 0; k < SCAN_PER; ++k) {
+      tile[scan_lds_index(SCAN_PER * tid + k)] = pu;
+      pu += f[k];
+    }
+    __syncthreads();
+    for (int i = tid; i < nv; i += SCAN_THREADS) pos[base + i] = tile[scan_lds_index(i)];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; ++k) {
+      tile[scan_lds_index(SCAN_PER * tid + k)] = pc;
       pc += c[k];
     }
     __syncthreads();
+    for (int i = tid; i < nv; i += SCAN_THREADS) off[base + i] = tile[scan_lds_index(i)];
+    __syncthreads();
+    pu = pu0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; ++k) {   // compacted ids (tile-local positions)
+      if (f[k]) tile[pu - ubase] = SCAN_PER * tid + k;
+      pu += f[k];
+    }
     if (tid == SCAN_THREADS - 1) { carry[0] = pu; carry[1] = pc; }
+    __syncthreads();
+    const int tu = carry[0] - ubase;
+    for (int i = tid; i < tu; i += SCAN_THREADS) uids[ubase + i] = base + tile[i];
+    __syncthreads();
+    pu = pu0;
+    pc = pc0;
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; ++k) {
+      if (f[k]) tile[pu - ubase] = pc;
+      pu += f[k];
+      pc += c[k];
+    }
+    __syncthreads();
+    for (int i = tid; i < tu; i += SCAN_THREADS) seg_off[ubase + i] = tile[i];
     __syncthreads();
   }
   if (tid == 0) {
@@ -106,6 +187,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(const int32_t* __res
     const int32_t Up = (U + 31) / 32 * 32;
     counts[0] = U;
     counts[1] = Up;
+    counts[3] = Tv;
     for (int32_t u = U; u < Up; ++u) {
       uids[u] = fill_row;
       seg_off[u] = Tv;
@@ -114,195 +196,241 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(const int32_t* __res
   }
 }
 
-// CSR fill: token t goes to a slot of its id's segment; seg_of[p] = the distinct row of CSR
-// position p.  Hot-id tokens take consecutive slots: wave offsets from an LDS scan, one global
-// atomic per workgroup.
+// inv[t] for every token; CSR slots for the tokens with grad_mask set: slot = (block base of its
+// id) + (its rank in the block), one global atomic per distinct id of the block.
+// seg_of[p] = the distinct row of CSR position p.
 __global__ __launch_bounds__(CNT_THREADS) void fill_kernel(const int64_t* __restrict__ ids, int64_t T, int64_t V,
-                                                           int64_t hot, const int32_t* __restrict__ pos,
+                                                           const void* gm, int gm_dt,
+                                                           const int32_t* __restrict__ pos,
                                                            const int32_t* __restrict__ off,
                                                            int32_t* __restrict__ cursor, int64_t* __restrict__ inv,
                                                            int32_t* __restrict__ seg_tok,
                                                            int32_t* __restrict__ seg_of) {
-  __shared__ int32_t wn[CNT_THREADS / 64];
-  __shared__ int32_t hot_base;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ int32_t hkey[HASH_SLOTS], hcnt[HASH_SLOTS];
+  for (int i = threadIdx.x; i < HASH_SLOTS; i += blockDim.x) { hkey[i] = -1; hcnt[i] = 0; }
+  __syncthreads();
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t v = t < T ? ids[t] : -1;
   const bool ok = t < T && v >= 0 && v < V;
-  if (t < T && !ok) inv[t] = 0;
-  const uint64_t hb = __ballot(ok && v == hot);
-  if (lane == 0) wn[w] = __builtin_popcountll(hb);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int32_t n = 0;
-    for (int k = 0; k < CNT_THREADS / 64; ++k) n += wn[k];
-    hot_base = n ? atomicAdd(&cursor[hot], n) : 0;
+  const bool seg = ok && grad_on(gm, gm_dt, t);
+  if (t < T) inv[t] = ok ? pos[v] : 0;
+  int h = -1;
+  int32_t rank = 0;
+  if (seg) {
+    h = hash_slot(hkey, (int32_t)v);
+    rank = atomicAdd(&hcnt[h], 1);
   }
   __syncthreads();
-  int32_t slot = 0;
-  if (ok && v == hot) {
-    int32_t before = 0;
-    for (int k = 0; k < w; ++k) before += wn[k];
-    slot = hot_base + before + __builtin_popcountll(hb & ((1ull << lane) - 1));
-  }
-  if (!ok) return;
-  if (v != hot) slot = atomicAdd(&cursor[v], 1);
-  const int32_t u = pos[v];
-  const int32_t p = off[v] + slot;
-  inv[t] = u;
+  for (int i = threadIdx.x; i < HASH_SLOTS; i += blockDim.x)   // counts -> block bases (in place)
+    if (hkey[i] >= 0) hcnt[i] = atomicAdd(&cursor[hkey[i]], hcnt[i]);
+  __syncthreads();
+  if (!seg) return;
+  const int32_t p = off[v] + hcnt[h] + rank;
   seg_tok[p] = (int32_t)t;
-  seg_of[p] = u;
+  seg_of[p] = pos[v];
 }
 
 // Segment sum, pass 1: workgroup b sums the CSR positions [b*R, (b+1)*R) piece by piece (a
 // piece = the part of one segment inside the range).  Whole segments are stored to dst; a
 // segment cut by a range boundary leaves its pieces in part[b][slot] (slot 0: the block's
-// first piece, slot 1: a later one) for pass 2.  The piece table is built once in LDS; the
-// sum loop per (piece, float4 column) has no branches and 4 loads in flight.
-__global__ __launch_bounds__(256) void segsum_pieces_kernel(const float* __restrict__ src, int64_t lds, int64_t w4,
-                                                            const int32_t* __restrict__ seg_off,
-                                                            const int32_t* __restrict__ seg_tok,
-                                                            const int32_t* __restrict__ seg_of, int64_t T,
-                                                            float4* __restrict__ part, float* __restrict__ dst,
-                                                            int64_t ldd) {
+// first piece, slot 1: a later one) for pass 2.  A table in LDS marks each piece's last
+// position and destination; one thread per float4 column streams the range 8 rows at a time
+// (8 independent loads in flight), flushing at piece ends (block-uniform branches).
+__global__ __launch_bounds__(1024) void segsum_pieces_kernel(const float* __restrict__ src, int64_t lds, int64_t w4,
+                                                             const int32_t* __restrict__ seg_off,
+                                                             const int32_t* __restrict__ seg_tok,
+                                                             const int32_t* __restrict__ seg_of,
+                                                             const int32_t* __restrict__ counts,
+                                                             float4* __restrict__ part, float* __restrict__ dst,
+                                                             int64_t ldd) {
+  const int64_t T = counts[3];   // positions in the CSR
   const int64_t b = blockIdx.x, p0 = b * SEG_RANGE;
+  if (p0 >= T) return;
   const int64_t p1 = p0 + SEG_RANGE < T ? p0 + SEG_RANGE : T;
   const int n = (int)(p1 - p0);
-  __shared__ int32_t s_tok[SEG_RANGE], s_seg[SEG_RANGE];
-  __shared__ int32_t pc_beg[SEG_RANGE + 1], pc_u[SEG_RANGE];
-  __shared__ int64_t pc_dst[SEG_RANGE];   // float4 index of the piece's destination
-  __shared__ int32_t npieces;
+  __shared__ int32_t s_tok[SEG_RANGE], s_seg[SEG_RANGE + 1];
+  __shared__ int64_t s_dst[SEG_RANGE];   // at a piece's last position: its float4 destination
   const int tid = threadIdx.x;
   if (tid < n) {
     s_tok[tid] = seg_tok[p0 + tid];
     s_seg[tid] = seg_of[p0 + tid];
   }
+  if (tid == 0) s_seg[n] = -1;
   __syncthreads();
-  if (tid < 64) {   // one wave: piece starts = positions whose segment differs from the previous
-    const bool start = tid < n && (tid == 0 || s_seg[tid] != s_seg[tid - 1]);
-    const uint64_t sb = __ballot(start);
-    if (start) {
-      const int k = __builtin_popcountll(sb & ((1ull << tid) - 1));
-      const int32_t u = s_seg[tid];
-      const int64_t gb = seg_off[u], ge = seg_off[u + 1];
-      int64_t d;
-      if (gb >= p0 && ge <= p1) d = u * (ldd / 4);                    // whole segment -> dst row
-      else d = -1 - ((b * 2 + (gb > p0 ? 1 : 0)) * w4);               // cut -> part slot (encoded)
-      pc_beg[k] = tid;
-      pc_u[k] = u;
-      pc_dst[k] = d;
-    }
-    if (tid == 0) {
-      const int np = __builtin_popcountll(sb);
-      npieces = np;
-      pc_beg[np] = n;
-    }
+  if (tid < n && s_seg[tid + 1] != s_seg[tid]) {   // last position of a piece
+    const int32_t u = s_seg[tid];
+    const int64_t gb = seg_off[u], ge = seg_off[u + 1];
+    int64_t d;
+    if (gb >= p0 && ge <= p1) d = u * (ldd / 4);                    // whole segment -> dst row
+    else d = -1 - ((b * 2 + (gb > p0 ? 1 : 0)) * w4);               // cut -> part slot (encoded)
+    s_dst[tid] = d;
   }
   __syncthreads();
-  const int np = npieces;
   float4* dst4 = reinterpret_cast<float4*>(dst);
-  for (int k = 0; k < np; ++k) {
-    const int i0 = pc_beg[k], i1 = pc_beg[k + 1];
-    const int64_t d = pc_dst[k];
-    float4* out = d >= 0 ? dst4 + d : part + (-1 - d);
-    for (int64_t j = tid; j < w4; j += blockDim.x) {
-      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-      int i = i0;
-      for (; i + 4 <= i1; i += 4) {
-        const float4 x0 = reinterpret_cast<const float4*>(src + (int64_t)s_tok[i] * lds)[j];
-        const float4 x1 = reinterpret_cast<const float4*>(src + (int64_t)s_tok[i + 1] * lds)[j];
-        const float4 x2 = reinterpret_cast<const float4*>(src + (int64_t)s_tok[i + 2] * lds)[j];
-        const float4 x3 = reinterpret_cast<const float4*>(src + (int64_t)s_tok[i + 3] * lds)[j];
-        s.x += x0.x; s.y += x0.y; s.z += x0.z; s.w += x0.w;
-        s.x += x1.x; s.y += x1.y; s.z += x1.z; s.w += x1.w;
-        s.x += x2.x; s.y += x2.y; s.z += x2.z; s.w += x2.w;
-        s.x += x3.x; s.y += x3.y; s.z += x3.z; s.w += x3.w;
+  for (int64_t j = tid; j < w4; j += blockDim.x) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i0 = 0; i0 < n; i0 += 8) {
+      float4 x[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = i0 + k < n ? i0 + k : n - 1;
+        x[k] = reinterpret_cast<const float4*>(src + (int64_t)s_tok[i] * lds)[j];
       }
-      for (; i < i1; ++i) {
-        const float4 x = reinterpret_cast<const float4*>(src + (int64_t)s_tok[i] * lds)[j];
-        s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = i0 + k;
+        if (i < n) {
+          s.x += x[k].x; s.y += x[k].y; s.z += x[k].z; s.w += x[k].w;
+          if (s_seg[i + 1] != s_seg[i]) {
+            const int64_t d = s_dst[i];
+            (d >= 0 ? dst4 + d : part + (-1 - d))[j] = s;
+            s = make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
       }
-      out[j] = s;
     }
   }
 }
 
-// Pass 2, one workgroup per distinct row: a cut segment sums its pieces in range order (the
-// long padding segment: hundreds of pieces, split over thread groups then combined in LDS);
-// pad rows [U, U_pad) are zeroed; whole segments were written by pass 1.
+// Pass 2: workgroups stride over the distinct rows in chunks of FIX_THREADS and compact the
+// rows that need work into LDS: segments cut by a range boundary (sum their pieces in range
+// order), empty segments and pad rows [U, U_pad) (zero).  Whole segments were written by pass
+// 1.  One wave per row for short cuts; a cut with many pieces (a long segment) takes the whole
+// workgroup, pieces split over thread groups and combined in LDS.
 constexpr int FIX_THREADS = 1024;
+constexpr int FIX_BLOCKS = 256;
+constexpr int FIX_WAVE_PIECES = 8;
+
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
 
 __global__ __launch_bounds__(FIX_THREADS) void segsum_fix_kernel(int64_t w4, const int32_t* __restrict__ seg_off,
                                                                  const int32_t* __restrict__ counts,
                                                                  const float4* __restrict__ part,
                                                                  float* __restrict__ dst, int64_t ldd) {
   __shared__ float4 acc_s[FIX_THREADS];
-  const int64_t u = blockIdx.x;
+  __shared__ int32_t todo_w[FIX_THREADS], todo_b[FIX_THREADS];
+  __shared__ int32_t nw_todo, nb_todo;
   const int32_t U = counts[0], Up = counts[1];
-  if (u >= Up) return;
-  float4* drow = reinterpret_cast<float4*>(dst + u * ldd);
-  if (u >= U) {
-    for (int64_t j = threadIdx.x; j < w4; j += blockDim.x) drow[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    return;
-  }
-  const int64_t sb = seg_off[u], se = seg_off[u + 1];
-  const int64_t b0 = sb / SEG_RANGE, b1 = (se - 1) / SEG_RANGE;
-  if (b0 == b1) return;
-  // groups of w4 threads each take every G-th piece; w4 > FIX_THREADS: one group, column loop
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nwv = FIX_THREADS / 64;
   const int G = w4 <= FIX_THREADS ? (int)(FIX_THREADS / w4) : 1;
-  const int g = (int)(threadIdx.x / (w4 < FIX_THREADS ? w4 : FIX_THREADS));
-  const int64_t j0 = threadIdx.x - (int64_t)g * (w4 < FIX_THREADS ? w4 : FIX_THREADS);
-  for (int64_t jb = 0; jb < w4; jb += FIX_THREADS) {
-    const int64_t j = jb + j0;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (g < G && j < w4) {
-      for (int64_t b = b0 + g; b <= b1; b += G) {
-        const int slot = (b == b0 && sb > b0 * SEG_RANGE) ? 1 : 0;
-        const float4 x = part[(b * 2 + slot) * w4 + j];
-        s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+  const int64_t gw = w4 < FIX_THREADS ? w4 : FIX_THREADS;
+  const int g = (int)(tid / gw);
+  const int64_t j0 = tid - (int64_t)g * gw;
+  for (int64_t c0 = (int64_t)blockIdx.x * FIX_THREADS; c0 < Up; c0 += (int64_t)gridDim.x * FIX_THREADS) {
+    if (tid == 0) nw_todo = nb_todo = 0;
+    __syncthreads();
+    {
+      const int64_t u = c0 + tid;
+      if (u < Up) {
+        bool wave_item = false, block_item = false;
+        if (u >= U) {
+          wave_item = true;   // pad row: zero
+        } else {
+          const int64_t sb = seg_off[u], se = seg_off[u + 1];
+          if (se == sb) {
+            wave_item = true;   // no token with a gradient: zero
+          } else {
+            const int64_t b0 = sb / SEG_RANGE, b1 = (se - 1) / SEG_RANGE;
+            if (b0 != b1) (b1 - b0 + 1 > FIX_WAVE_PIECES ? block_item : wave_item) = true;
+          }
+        }
+        if (wave_item) todo_w[atomicAdd(&nw_todo, 1)] = (int32_t)u;
+        if (block_item) todo_b[atomicAdd(&nb_todo, 1)] = (int32_t)u;
       }
     }
-    if (G > 1) {
-      acc_s[threadIdx.x] = s;
-      __syncthreads();
-      if (g == 0 && j < w4) {
-        for (int k = 1; k < G; ++k) {
-          const float4 x = acc_s[k * w4 + j0];
-          s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+    __syncthreads();
+    const int nw = nw_todo, nb = nb_todo;
+    for (int k = wv; k < nw; k += nwv) {   // one wave per row
+      const int64_t u = todo_w[k];
+      float4* drow = reinterpret_cast<float4*>(dst + u * ldd);
+      int64_t sb = 0, se = 0;
+      if (u < U) { sb = seg_off[u]; se = seg_off[u + 1]; }
+      for (int64_t j = lane; j < w4; j += 64) {
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (se > sb) {
+          const int64_t b0 = sb / SEG_RANGE, b1 = (se - 1) / SEG_RANGE;
+          s = part[(b0 * 2 + (sb > b0 * SEG_RANGE ? 1 : 0)) * w4 + j];
+          for (int64_t b = b0 + 1; b <= b1; ++b) s = f4add(s, part[(b * 2) * w4 + j]);
         }
         drow[j] = s;
       }
-      __syncthreads();
-    } else if (j < w4) {
-      drow[j] = s;
     }
+    for (int k = 0; k < nb; ++k) {   // long segments: the whole workgroup
+      const int64_t u = todo_b[k];
+      float4* drow = reinterpret_cast<float4*>(dst + u * ldd);
+      const int64_t sb = seg_off[u], se = seg_off[u + 1];
+      const int64_t b0 = sb / SEG_RANGE, b1 = (se - 1) / SEG_RANGE;
+      for (int64_t jb = 0; jb < w4; jb += FIX_THREADS) {
+        const int64_t j = jb + j0;
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (g < G && j < w4) {
+          int64_t b = b0 + g;
+          if (b == b0) {   // the first piece may sit in slot 1
+            s = part[(b * 2 + (sb > b0 * SEG_RANGE ? 1 : 0)) * w4 + j];
+            b += G;
+          }
+          for (; b + 3 * G <= b1; b += 4 * G) {   // later pieces: slot 0, four loads in flight
+            const float4 x0 = part[(b * 2) * w4 + j];
+            const float4 x1 = part[((b + G) * 2) * w4 + j];
+            const float4 x2 = part[((b + 2 * G) * 2) * w4 + j];
+            const float4 x3 = part[((b + 3 * G) * 2) * w4 + j];
+            s = f4add(s, x0); s = f4add(s, x1); s = f4add(s, x2); s = f4add(s, x3);
+          }
+          for (; b <= b1; b += G) s = f4add(s, part[(b * 2) * w4 + j]);
+        }
+        if (G > 1) {
+          acc_s[tid] = s;
+          __syncthreads();
+          if (g == 0 && j < w4) {
+            for (int q = 1; q < G; ++q) s = f4add(s, acc_s[q * w4 + j0]);
+            drow[j] = s;
+          }
+          __syncthreads();
+        } else if (j < w4) {
+          drow[j] = s;
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
 }  // namespace
 
-extern "C" int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t fill_row, int32_t* work,
-                              int64_t* uids, int64_t* inv, int32_t* seg_off, int32_t* seg_tok, int32_t* seg_of,
-                              int32_t* counts, hipStream_t stream) {
+extern "C" int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t fill_row, const void* grad_mask,
+                              int32_t mask_dtype, int32_t* work, int64_t* uids, int64_t* inv, int32_t* seg_off,
+                              int32_t* seg_tok, int32_t* seg_of, int32_t* counts, hipStream_t stream) {
   if (T < 0 || V < 1 || V > 0x7fffffff || T > 0x7fffffff) return NR_EINVAL(0);
   if (!ids || !work || !uids || !inv || !seg_off || !seg_tok || !seg_of || !counts) return NR_EINVAL(1);
   if (fill_row < 0 || fill_row >= V) return NR_EINVAL(2);
-  int32_t* cnt = work;
-  int32_t* cursor = work + V;
-  int32_t* pos = work + 2 * V;
-  int32_t* off = work + 3 * V;
-  hipError_t e = hipMemsetAsync(work, 0, sizeof(int32_t) * 2 * V, stream);
+  if (grad_mask && (mask_dtype < NR_MASK_U8 || mask_dtype > NR_MASK_F32)) return NR_EINVAL(5);
+  int32_t* cnt_all = work;
+  int32_t* cnt_csr = work + V;
+  int32_t* cursor = work + 2 * V;
+  int32_t* pos = work + 3 * V;
+  int32_t* off = work + 4 * V;
+  hipError_t e = hipMemsetAsync(work, 0, sizeof(int32_t) * 3 * V, stream);
   if (e != hipSuccess) return -(int)e;
-  e = hipMemsetAsync(counts, 0, sizeof(int32_t) * 3, stream);
+  e = hipMemsetAsync(counts, 0, sizeof(int32_t) * 4, stream);
   if (e != hipSuccess) return -(int)e;
   const unsigned gb = (unsigned)((T + CNT_THREADS - 1) / CNT_THREADS);
   if (T > 0)
-    hipLaunchKernelGGL(count_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, fill_row, cnt, counts);
-  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, cnt, V, pos, off, uids, seg_off, counts,
-                     fill_row);
+    hipLaunchKernelGGL(count_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, grad_mask, mask_dtype, cnt_all,
+                       cnt_csr, counts);
+  const size_t scan_lds = sizeof(int32_t) * SCAN_LDS_WORDS;
+  static bool scan_attr = false;
+  if (!scan_attr) {
+    e = hipFuncSetAttribute((const void*)scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds);
+    if (e != hipSuccess) return -(int)e;
+    scan_attr = true;
+  }
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(SCAN_THREADS), scan_lds, stream, cnt_all, cnt_csr, V, pos, off, uids,
+                     seg_off, counts, fill_row);
   if (T > 0)
-    hipLaunchKernelGGL(fill_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, fill_row, pos, off, cursor,
-                       inv, seg_tok, seg_of);
+    hipLaunchKernelGGL(fill_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, grad_mask, mask_dtype, pos, off,
+                       cursor, inv, seg_tok, seg_of);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
@@ -322,10 +450,13 @@ extern "C" int nr_segment_rows_sum(const float* src, int64_t lds, int64_t width,
   if (rows_max == 0 || width == 0) return NR_OK;
   const int64_t w4 = width / 4;
   if (T > 0)
-    hipLaunchKernelGGL(segsum_pieces_kernel, dim3((unsigned)((T + SEG_RANGE - 1) / SEG_RANGE)), dim3(256), 0, stream,
-                       src, lds, w4, seg_off, seg_tok, seg_of, T, reinterpret_cast<float4*>(work), dst, ldd);
-  hipLaunchKernelGGL(segsum_fix_kernel, dim3((unsigned)rows_max), dim3(FIX_THREADS), 0, stream, w4, seg_off, counts,
-                     reinterpret_cast<const float4*>(work), dst, ldd);
+    hipLaunchKernelGGL(segsum_pieces_kernel, dim3((unsigned)((T + SEG_RANGE - 1) / SEG_RANGE)),
+                       dim3((unsigned)(w4 >= 1024 ? 1024 : (w4 < SEG_RANGE ? SEG_RANGE : (w4 + 63) / 64 * 64))), 0,
+                       stream, src, lds, w4, seg_off, seg_tok, seg_of, counts, reinterpret_cast<float4*>(work), dst,
+                       ldd);
+  const int64_t fb = (rows_max + FIX_THREADS - 1) / FIX_THREADS;
+  hipLaunchKernelGGL(segsum_fix_kernel, dim3((unsigned)(fb < FIX_BLOCKS ? fb : FIX_BLOCKS)), dim3(FIX_THREADS), 0,
+                     stream, w4, seg_off, counts, reinterpret_cast<const float4*>(work), dst, ldd);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

@@ -129,8 +129,10 @@ class MHANewsFn(torch.autograd.Function):
         fused = K.mha_pool_supported(seq_len, heads, dk, dv)
         ur = None
         if fused and DEDUP_ROWS:
-            # project each distinct word-table row once (Y rows = distinct ids, read through inv)
-            ur = K.UniqueRows(ids, V, fill_row=pad_row if 0 <= pad_row < V else 0)
+            # project each distinct word-table row once (Y rows = distinct ids, read through inv);
+            # the backward sums dY per distinct row over the unmasked tokens only — the fused
+            # tail gives masked tokens an exactly-zero dY (their P rows and columns are zero)
+            ur = K.UniqueRows(ids, V, fill_row=pad_row if 0 <= pad_row < V else 0, grad_mask=mask)
             Y = _empty(ur.cap, NY, table)
             ev0 = PROBE.record()
             K.gemm_dyn(ur.cap, NY, E, K.operand(table, L.KCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER),

@@ -54,25 +54,28 @@ class UniqueRows:
     """Distinct ids of a token batch (``nr_unique_rows``), sizes left on the device.
 
     uids [cap] int64 (valid prefix counts[1], ascending, padded with fill_row), inv [T] int64,
-    seg_off [cap + 1] / seg_tok [T] int32 CSR, counts [3] int32 = (U, U_pad, bad);
-    cap = ceil32(min(T, V)) is the host-side upper bound of U_pad."""
+    seg_off [cap + 1] / seg_tok [T] / seg_of [T] int32 CSR of the tokens with ``grad_mask`` set
+    (all tokens if None), counts [4] int32 = (U, U_pad, bad, T_csr); cap = ceil32(min(T, V))
+    is the host-side upper bound of U_pad."""
 
-    def __init__(self, ids, vocab, fill_row=0):
+    def __init__(self, ids, vocab, fill_row=0, grad_mask=None):
         _check_rows(ids, None, "unique_rows")
         T = ids.numel()
         dev = ids.device
         self.T, self.vocab = T, vocab
         self.cap = max(32, _ceil32(min(T, vocab)))
         i32 = dict(device=dev, dtype=torch.int32)
-        work = torch.empty(4 * vocab, **i32)
+        work = torch.empty(5 * vocab, **i32)
         self.uids = torch.empty(self.cap, device=dev, dtype=torch.int64)
         self.inv = torch.empty(T, device=dev, dtype=torch.int64)
         self.seg_off = torch.empty(self.cap + 1, **i32)
         self.seg_tok = torch.empty(max(T, 1), **i32)
         self.seg_of = torch.empty(max(T, 1), **i32)
-        self.counts = torch.empty(3, **i32)
-        L.call("nr_unique_rows", L.ptr(ids), T, vocab, fill_row, L.ptr(work), L.ptr(self.uids), L.ptr(self.inv),
-               L.ptr(self.seg_off), L.ptr(self.seg_tok), L.ptr(self.seg_of), L.ptr(self.counts), L.stream_ptr(ids))
+        self.counts = torch.empty(4, **i32)
+        mp, mdt = mask_arg(grad_mask, T) if grad_mask is not None else (None, 0)
+        L.call("nr_unique_rows", L.ptr(ids), T, vocab, fill_row, mp, mdt, L.ptr(work), L.ptr(self.uids),
+               L.ptr(self.inv), L.ptr(self.seg_off), L.ptr(self.seg_tok), L.ptr(self.seg_of), L.ptr(self.counts),
+               L.stream_ptr(ids))
         self.n_rows = self.counts[0:1]  # device scalar: U
         self.u_pad = self.counts[1:2]   # device scalar: U_pad, the GEMM extent
 

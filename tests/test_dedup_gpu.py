@@ -24,7 +24,7 @@ def test_unique_rows(T, V):
     ids = _ids(T, V, T + V)
     ur = K.UniqueRows(ids.cuda(), V, fill_row=0)
     torch.cuda.synchronize()
-    U, Up, bad = ur.counts.tolist()
+    U, Up, bad, Tc = ur.counts.tolist()
     ref = np.unique(ids.numpy())
     assert bad == 0 and U == len(ref) and Up == (U + 31) // 32 * 32
     uids = ur.uids.cpu().numpy()
@@ -39,12 +39,37 @@ def test_unique_rows(T, V):
         assert (seg == np.nonzero(ids.numpy() == uids[u])[0]).all()
 
 
+def test_unique_rows_grad_mask_segments():
+    T, V = 5000, 700
+    ids = _ids(T, V, 99)
+    gm = (torch.rand(T, generator=torch.Generator().manual_seed(5)) < 0.6)
+    gm[ids == 0] = False
+    ur = K.UniqueRows(ids.cuda(), V, fill_row=0, grad_mask=gm.long().cuda())
+    torch.cuda.synchronize()
+    U, Up, bad, Tc = ur.counts.tolist()
+    assert U == len(np.unique(ids.numpy())) and Tc == int(gm.sum())
+    uids, off, tok = ur.uids.cpu().numpy(), ur.seg_off.cpu().numpy(), ur.seg_tok.cpu().numpy()
+    assert off[Up] == Tc
+    for u in range(U):
+        seg = np.sort(tok[off[u]:off[u + 1]])
+        want = np.nonzero((ids.numpy() == uids[u]) & gm.numpy())[0]
+        assert (seg == want).all()
+    src = torch.randn(T, 64, device="cuda")
+    dst = torch.full((ur.cap, 64), float("nan"), device="cuda")
+    ur.segment_sum(src, dst)
+    ref = torch.zeros(ur.cap, 64, dtype=torch.float64, device="cuda")
+    g = gm.cuda()
+    ref.index_add_(0, ur.inv[g], src[g].double())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dst[:Up].double(), ref[:Up], rtol=1e-5, atol=1e-5)   # empty segments: 0
+
+
 def test_unique_rows_flags_bad_ids():
     ids = torch.tensor([0, 3, 9, 2], dtype=torch.int64)
     ur = K.UniqueRows(ids.cuda(), 5)
     torch.cuda.synchronize()
-    U, Up, bad = ur.counts.tolist()
-    assert bad == 1 and U == 3
+    U, Up, bad, Tc = ur.counts.tolist()
+    assert bad == 1 and U == 3 and Tc == 3
 
 
 @pytest.mark.parametrize("T,V,W", [(300, 50, 1152), (52800, 30522, 1152), (33, 4, 4)])
@@ -55,7 +80,7 @@ def test_segment_sum(T, V, W):
     dst = torch.full((ur.cap, W), float("nan"), device="cuda")
     ur.segment_sum(src, dst)
     torch.cuda.synchronize()
-    U, Up, _ = ur.counts.tolist()
+    U, Up, _, _ = ur.counts.tolist()
     ref = torch.zeros(ur.cap, W, dtype=torch.float64, device="cuda")
     ref.index_add_(0, ur.inv, src.double())
     # fp32 sums of n unit-variance terms: tolerance grows with the segment length n
