@@ -65,9 +65,40 @@ def build(device):
     return build_model("mha", "mha", H, vocab=V, device=device, user_num=USERS_LARGE, dropout_p=0.2)
 
 
-def make_optim(model):
+def make_optim(model, capturable=False):
     from newsrec_amd.manager import get_optim
-    return get_optim(model)
+    return get_optim(model, capturable=capturable)
+
+
+class GraphedStep:
+    """The whole train step (forward, NLL, backward, Adam) captured once as a HIP graph and
+    replayed: the ~80 kernels of a step launch back to back with no host work between them.
+    Each step copies its batch into the captured input buffers first (the data feed); dropout
+    draws and Adam step counts advance on the device, so replays are real training steps."""
+
+    def __init__(self, model, opt, batches, sync, warmup):
+        self.static = {k: v.clone() for k, v in batches[0].items()}
+        self.batches = batches
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):   # warm-up off the default stream (allocator, lazy init)
+            for i in range(max(2, warmup)):
+                self.feed(i)
+                train_step(model, opt, self.static, sync)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.loss = train_step(model, opt, self.static, sync)
+        torch.cuda.synchronize()
+
+    def feed(self, i):
+        for k, v in self.batches[i % len(self.batches)].items():
+            self.static[k].copy_(v, non_blocking=True)
+
+    def __call__(self, i):
+        self.feed(i)
+        self.graph.replay()
 
 
 def train_step(model, opt, x, sync):
@@ -112,6 +143,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="replay the train step as a HIP graph (auto: single GPU)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -136,27 +169,37 @@ def main():
         with torch.no_grad():
             for p in model.parameters():
                 dist.broadcast(p, 0)
-    opt = make_optim(model)
+    use_graph = a.graph == "on" or (a.graph == "auto" and world == 1)
+    opt = make_optim(model, capturable=use_graph)
     sync = GradSync(model) if world > 1 else None
     gen = torch.Generator().manual_seed(1234 + rank)
     batches = [synth_batch(gen, dev) for _ in range(4)]
 
-    for i in range(a.warmup):
-        train_step(model, opt, batches[i % len(batches)], sync)
+    if use_graph:
+        step_fn = GraphedStep(model, opt, batches, sync, a.warmup)
+    else:
+        def step_fn(i):
+            train_step(model, opt, batches[i % len(batches)], sync)
+        for i in range(a.warmup):
+            step_fn(i)
     torch.cuda.synchronize()
 
-    # per-launch timing of the dominant kernel (the fused gather + key/value projection GEMM)
-    F.PROBE.enable()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        train_step(model, opt, batches[i % len(batches)], sync)
+        step_fn(i)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+
+    # per-launch timing of the dominant kernel (the fused gather + key/value projection GEMM),
+    # HIP events on its stream, over a few eager steps (events cannot sit inside a replay)
+    F.PROBE.enable()
+    for i in range(3):
+        train_step(model, opt, batches[i % len(batches)], sync)
     probe = F.PROBE.collect()
     F.PROBE.disable()
     if world > 1:
@@ -197,6 +240,7 @@ def main():
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (MIND-large-shaped, random-init weights)",
             "config": {"workload": "NRMS train step: MHA news encoder + MHA user encoder, H=384, 12 heads, "
                                    "V=30522 word table (trainable), dropout 0.2, Adam",
+                       "launch": "hipGraph replay of the whole step" if use_graph else "eager",
                        "global_batch": B * world, "per_gpu_batch": B, "candidates": C, "history": NH,
                        "seq_len": L, "parallelism": "dp%d" % world},
             "eval": {"candidates_per_s": round(world * B * C * ne / el_eval, 1),

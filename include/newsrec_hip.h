@@ -143,12 +143,15 @@ int nr_mha_attn_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v
  * y = [T][heads*dk | heads*dv] projections.  (dk, dv, heads*dv) in {(64,32,384), (64,64,768),
  * (64,32,256), (32,32,384)}.  Replaces MultiheadAttention.forward :125-147 + MHA.py:37-38.
  * Saves stats [T][2] and probs [T]; zout (optional) receives Z = the encoder's token output.
- * yrows (optional): token t reads projection row yrows[t] (distinct-row projections). */
+ * yrows (optional): token t reads projection row yrows[t] (distinct-row projections).
+ * rng (optional, all dropout entries): the dropout key comes from the device pair
+ * (rng[0], rng[1] + offset) instead of (seed, offset), so a replayed graph draws new masks. */
 int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,
                     int32_t mask_dtype, int64_t nseq,
                     int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
                     const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset,
-                    const float* q, float* news, int64_t ldn, float* zout, int64_t ldz,
+                    const uint64_t* rng, const float* q, float* news, int64_t ldn, float* zout,
+                    int64_t ldz,
                     float* stats, float* probs, hipStream_t stream);
 
 /* Backward of nr_mha_pool_fwd (recomputes the attention): writes dy [T][heads*(dk+dv)] and
@@ -158,7 +161,8 @@ int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const voi
                     int32_t mask_dtype, int64_t nseq,
                     int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
                     const float* beta, float p_drop, uint64_t seed, uint64_t offset,
-                    const float* q, const float* stats, const float* probs, const float* dnews,
+                    const uint64_t* rng, const float* q, const float* stats, const float* probs,
+                    const float* dnews,
                     int64_t ldn, const float* dz, int64_t lddz, float* dy, int64_t lddy,
                     float* dbias, float* dq, float* dgamma, float* dbeta, hipStream_t stream);
 
@@ -174,8 +178,9 @@ int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const voi
  * zout (optional) receives Z, the encoder's per-token output. */
 int nr_attn_pool_fwd(const float* x, int64_t ldx, const float* key, int64_t ldk, const float* q,
                      const void* mask, int32_t mask_dtype, const float* gamma, const float* beta,
-                     float eps, float p_drop, uint64_t seed, uint64_t offset, int64_t nseq,
-                     int32_t L, int32_t D, float scale, float* out, int64_t ldo, float* zout,
+                     float eps, float p_drop, uint64_t seed, uint64_t offset, const uint64_t* rng,
+                     int64_t nseq, int32_t L, int32_t D, float scale, float* out, int64_t ldo,
+                     float* zout,
                      int64_t ldz, float* stats, float* probs, hipStream_t stream);
 
 /* Backward of nr_attn_pool_fwd (dz: optional upstream grad of Z, added to the pooling's):
@@ -184,8 +189,9 @@ int nr_attn_pool_fwd(const float* x, int64_t ldx, const float* key, int64_t ldk,
  * dbeta[D] (caller zeroes them). */
 int nr_attn_pool_bwd(const float* x, int64_t ldx, const float* key, int64_t ldk, const float* q,
                      const void* mask, int32_t mask_dtype, const float* gamma, const float* beta,
-                     float p_drop, uint64_t seed, uint64_t offset, int64_t nseq, int32_t L,
-                     int32_t D, float scale, const float* stats, const float* probs,
+                     float p_drop, uint64_t seed, uint64_t offset, const uint64_t* rng,
+                     int64_t nseq, int32_t L, int32_t D, float scale, const float* stats,
+                     const float* probs,
                      const float* dout, int64_t lddo, const float* dz, int64_t lddz, float* dx,
                      int64_t lddx, float* dk, int64_t lddk, int32_t key_tanh, float* dq,
                      float* dgamma, float* dbeta, hipStream_t stream);
@@ -232,11 +238,12 @@ int nr_score_bwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
 
 /* One torch.optim.Adam step (amsgrad=False) on n contiguous fp32 elements; `step` is the
  * 1-based step count after increment (bias corrections as torch).  The gradient is read as
- * grad * grad_scale (1/world_size folds the data-parallel mean into the update).
+ * grad * grad_scale (1/world_size folds the data-parallel mean into the update).  step_dev
+ * (optional): the step count read on the device instead (graph replays).
  * Manager.py:404-413,647. */
 int nr_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
             float lr, float beta1, float beta2, float eps, float weight_decay, int64_t step,
-            float grad_scale, hipStream_t stream);
+            const int64_t* step_dev, float grad_scale, hipStream_t stream);
 
 /* out[i] = table[idx[i]] rows of E floats (E % 4 == 0).  BERT_Embedding.forward, BERT.py:39. */
 int nr_embedding_fwd(const float* table, int64_t V, int64_t E, const int64_t* idx, int64_t n,

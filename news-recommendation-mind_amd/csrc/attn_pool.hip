@@ -31,6 +31,7 @@ struct PoolArgs {
   float eps;
   float p_drop; uint64_t seed; uint64_t offset;
   uint32_t dkey, dthresh;                  // dropout key / threshold derived on the host
+  const uint64_t* rng;                     // device (seed, offset base): key derived in the kernel
   int64_t nseq; int L; int D; float scale;
   float* out; int64_t ldo;
   float* zout; int64_t ldz;                // optional: write Z (the encoder's token output)
@@ -84,6 +85,7 @@ __device__ __forceinline__ const float* key_row(const PoolArgs& g, const float* 
 }
 
 __global__ __launch_bounds__(256) void attn_pool_fwd_kernel(PoolArgs g) {
+  if (g.rng) g.dkey = nr_dropout_key(g.rng[0], g.rng[1] + g.offset);   // graph-replay RNG
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* zs = smem;                       // [L][D]
   float* sc = smem + (size_t)g.L * g.D;   // [64]
@@ -124,6 +126,7 @@ __global__ __launch_bounds__(256) void attn_pool_fwd_kernel(PoolArgs g) {
 }
 
 __global__ __launch_bounds__(256) void attn_pool_bwd_kernel(PoolArgs g) {
+  if (g.rng) g.dkey = nr_dropout_key(g.rng[0], g.rng[1] + g.offset);   // graph-replay RNG
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* zs = smem;                         // [L][D]
   float* ps = smem + (size_t)g.L * g.D;     // [64] p
@@ -221,7 +224,7 @@ size_t smem_bwd(int L, int D) { return ((size_t)L * D + 128 + 2 * (size_t)D) * s
 extern "C" int nr_attn_pool_fwd(const float* x, int64_t ldx, const float* key, int64_t ldk,
                                 const float* q, const void* mask, int32_t mask_dtype,
                                 const float* gamma, const float* beta, float eps, float p_drop,
-                                uint64_t seed, uint64_t offset, int64_t nseq, int32_t L, int32_t D,
+                                uint64_t seed, uint64_t offset, const uint64_t* rng, int64_t nseq, int32_t L, int32_t D,
                                 float scale, float* out, int64_t ldo, float* zout, int64_t ldz,
                                 float* stats, float* probs, hipStream_t stream) {
   if (L < 1 || L > 64 || D < 1) return NR_EINVAL(0);
@@ -232,7 +235,7 @@ extern "C" int nr_attn_pool_fwd(const float* x, int64_t ldx, const float* key, i
   PoolArgs g{};
   g.x = x; g.ldx = ldx; g.key = key; g.ldk = ldk; g.q = q; g.mask = mask; g.mask_dt = mask_dtype;
   g.gamma = gamma; g.beta = beta; g.eps = eps; g.p_drop = p_drop; g.seed = seed; g.offset = offset;
-  g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop);
+  g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop); g.rng = rng;
   g.nseq = nseq; g.L = L; g.D = D; g.scale = scale; g.out = out; g.ldo = ldo; g.stats = stats;
   g.probs = probs; g.zout = zout; g.ldz = ldz;
   if (smem_fwd(L, D) > 64 * 1024)
@@ -246,8 +249,8 @@ extern "C" int nr_attn_pool_fwd(const float* x, int64_t ldx, const float* key, i
 extern "C" int nr_attn_pool_bwd(const float* x, int64_t ldx, const float* key, int64_t ldk,
                                 const float* q, const void* mask, int32_t mask_dtype,
                                 const float* gamma, const float* beta, float p_drop, uint64_t seed,
-                                uint64_t offset, int64_t nseq, int32_t L, int32_t D, float scale,
-                                const float* stats, const float* probs, const float* dout,
+                                uint64_t offset, const uint64_t* rng, int64_t nseq, int32_t L, int32_t D,
+                                float scale, const float* stats, const float* probs, const float* dout,
                                 int64_t lddo, const float* dz, int64_t lddz, float* dx, int64_t lddx,
                                 float* dk, int64_t lddk,
                                 int32_t key_tanh, float* dq, float* dgamma, float* dbeta,
@@ -261,7 +264,7 @@ extern "C" int nr_attn_pool_bwd(const float* x, int64_t ldx, const float* key, i
   PoolArgs g{};
   g.x = x; g.ldx = ldx; g.key = key; g.ldk = ldk; g.q = q; g.mask = mask; g.mask_dt = mask_dtype;
   g.gamma = gamma; g.beta = beta; g.p_drop = p_drop; g.seed = seed; g.offset = offset;
-  g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop);
+  g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop); g.rng = rng;
   g.nseq = nseq; g.L = L; g.D = D; g.scale = scale; g.stats = const_cast<float*>(stats);
   g.probs = const_cast<float*>(probs); g.dout = dout; g.lddo = lddo; g.dx = dx; g.lddx = lddx;
   g.dk = dk; g.lddk = lddk; g.key_tanh = key_tanh; g.dq = dq; g.dgamma = dgamma; g.dbeta = dbeta;

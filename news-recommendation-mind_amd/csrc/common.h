@@ -80,10 +80,11 @@ __device__ __forceinline__ float nr_wave_max(float v) {
 }
 
 // Counter-based RNG for dropout.  Each call derives a 32-bit key from (seed, offset) on the
-// host (splitmix64, nr_dropout_key); each element's keep bit is a 32-bit hash (lowbias32) of
+// host, or in the kernel from a device-resident (seed, offset) pair when the call sits in a
+// replayed graph (splitmix64, nr_dropout_key); each element's keep bit is a 32-bit hash (lowbias32) of
 // key + index, compared with a 32-bit threshold.  Stateless: the backward regenerates the
 // forward's mask exactly, nothing is stored.
-static inline uint32_t nr_dropout_key(uint64_t seed, uint64_t offset) {
+__host__ __device__ static inline uint32_t nr_dropout_key(uint64_t seed, uint64_t offset) {
   uint64_t z = seed * 0x9E3779B97F4A7C15ull + offset * 0xD1B54A32D192ED03ull + 0x632BE59BD9B4E019ull;
   z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
   z ^= z >> 27; z *= 0x94D049BB133111EBull;

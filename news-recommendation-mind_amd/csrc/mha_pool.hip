@@ -47,6 +47,7 @@ struct MPArgs {
   const float* gamma; const float* beta; float eps;
   float p_drop; uint64_t seed; uint64_t offset;
   uint32_t dkey, dthresh;                  // dropout key / threshold derived on the host
+  const uint64_t* rng;                     // device (seed, offset base): key derived in the kernel
   const float* q;                     // [H] query_words
   float* news; int64_t ldn;           // fwd out / bwd: dnews in (const)
   float* zout; int64_t ldz;           // fwd: optional token output Z
@@ -195,6 +196,7 @@ __device__ void attention_to_lds(const MPArgs& g, int64_t seq, uint64_t bits, fl
 
 template <int DK, int DV, int NH64>
 __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
+  if (g.rng) g.dkey = nr_dropout_key(g.rng[0], g.rng[1] + g.offset);   // graph-replay RNG
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int H = NH64 * 64;
   constexpr int SO = H + 1;
@@ -265,6 +267,7 @@ __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
 
 template <int DK, int DV, int NH64>
 __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
+  if (g.rng) g.dkey = nr_dropout_key(g.rng[0], g.rng[1] + g.offset);   // graph-replay RNG
   extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int H = NH64 * 64;
   constexpr int SO = H + 1;
@@ -517,7 +520,7 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,
                                int32_t mask_dtype, int64_t nseq,
                                int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
-                               const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset,
+                               const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset, const uint64_t* rng,
                                const float* q, float* news, int64_t ldn, float* zout, int64_t ldz, float* stats,
                                float* probs, hipStream_t stream) {
   if (L < 1 || L > 32 || heads < 1 || heads > 12) return NR_EINVAL(0);
@@ -528,7 +531,7 @@ extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows
   g.y = y; g.ldy = ldy; g.yrows = yrows; g.mask = mask; g.mask_dt = mask_dtype; g.nseq = nseq; g.L = L; g.heads = heads;
   g.scale_attn = 1.0f / sqrtf((float)dk); g.scale_pool = 1.0f / sqrtf((float)(heads * dv));
   g.gamma = gamma; g.beta = beta; g.eps = eps; g.p_drop = p_drop; g.seed = seed; g.offset = offset;
-  g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop); g.q = q;
+  g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop); g.rng = rng; g.q = q;
   g.news = news; g.ldn = ldn; g.zout = zout; g.ldz = ldz; g.stats = stats; g.probs = probs;
   {
     const char* e = getenv("NR_DEBUG_MHAPOOL");
@@ -540,7 +543,7 @@ extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows
 extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,
                                int32_t mask_dtype, int64_t nseq,
                                int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
-                               const float* beta, float p_drop, uint64_t seed, uint64_t offset, const float* q,
+                               const float* beta, float p_drop, uint64_t seed, uint64_t offset, const uint64_t* rng, const float* q,
                                const float* stats, const float* probs, const float* dnews, int64_t ldn,
                                const float* dz, int64_t lddz, float* dy, int64_t lddy, float* dbias, float* dq,
                                float* dgamma, float* dbeta, hipStream_t stream) {
@@ -554,7 +557,7 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
   g.y = y; g.ldy = ldy; g.yrows = yrows; g.mask = mask; g.mask_dt = mask_dtype; g.nseq = nseq; g.L = L; g.heads = heads;
   g.scale_attn = 1.0f / sqrtf((float)dk); g.scale_pool = 1.0f / sqrtf((float)(heads * dv));
   g.gamma = gamma; g.beta = beta; g.p_drop = p_drop; g.seed = seed; g.offset = offset;
-  g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop); g.q = q;
+  g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop); g.rng = rng; g.q = q;
   g.news = const_cast<float*>(dnews); g.ldn = ldn; g.stats = const_cast<float*>(stats);
   g.probs = const_cast<float*>(probs); g.dz = dz; g.lddz = lddz; g.dy = dy; g.lddy = lddy; g.dbias = dbias;
   g.dq = dq; g.dgamma = dgamma; g.dbeta = dbeta;

@@ -87,10 +87,25 @@ __global__ __launch_bounds__(256) void score_bwd_kernel(const float* cdd, int64_
 // torch.optim.Adam (foreach=False, maximize=False, amsgrad=False) per element:
 //   g += wd * p;  m = lerp(m, g, 1 - b1);  v = b2 v + (1 - b2) g²
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+// step_dev (graph replays): the step count lives on the device and the bias corrections are
+// formed per workgroup in double, as torch forms them in Python floats.
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                    float step, float b1, float b2, float eps,
-                                                   float bc2_sqrt, float wd, float gscale) {
+                                                   float bc2_sqrt, float wd, float gscale,
+                                                   const int64_t* __restrict__ step_dev, float lr) {
+  if (step_dev) {
+    __shared__ float sc[2];
+    if (threadIdx.x == 0) {
+      const double t = (double)*step_dev;
+      const double bc1 = 1.0 - pow((double)b1, t), bc2 = 1.0 - pow((double)b2, t);
+      sc[0] = (float)((double)lr / bc1);
+      sc[1] = (float)sqrt(bc2);
+    }
+    __syncthreads();
+    step = sc[0];
+    bc2_sqrt = sc[1];
+  }
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -185,21 +200,22 @@ extern "C" int nr_score_bwd(const float* cdd, int64_t ldc, const float* user, in
 
 extern "C" int nr_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                        float lr, float beta1, float beta2, float eps, float weight_decay, int64_t step,
-                       float grad_scale, hipStream_t stream) {
-  if (n < 0 || step < 1) return NR_EINVAL(0);
+                       const int64_t* step_dev, float grad_scale, hipStream_t stream) {
+  if (n < 0 || (step < 1 && !step_dev)) return NR_EINVAL(0);
   if (!param || !grad || !exp_avg || !exp_avg_sq) return NR_EINVAL(1);
   if ((reinterpret_cast<uintptr_t>(param) | reinterpret_cast<uintptr_t>(grad) |
        reinterpret_cast<uintptr_t>(exp_avg) | reinterpret_cast<uintptr_t>(exp_avg_sq)) & 15)
     return NR_EINVAL(2);
   if (n == 0) return NR_OK;
   // bias corrections in double, as torch computes them in Python floats
-  const double bc1 = 1.0 - pow((double)beta1, (double)step);
-  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  const double bc1 = 1.0 - pow((double)beta1, (double)(step < 1 ? 1 : step));
+  const double bc2 = 1.0 - pow((double)beta2, (double)(step < 1 ? 1 : step));
   int64_t blocks = (n / 4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, param, grad, exp_avg,
-                     exp_avg_sq, n, (float)((double)lr / bc1), beta1, beta2, eps, (float)sqrt(bc2), weight_decay, grad_scale);
+                     exp_avg_sq, n, (float)((double)lr / bc1), beta1, beta2, eps, (float)sqrt(bc2), weight_decay, grad_scale,
+                     step_dev, lr);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

@@ -50,9 +50,9 @@ _SIGS = {
     "nr_mha_attn_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
                         c_f32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr],
     "nr_attn_pool_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_ptr, c_ptr, c_f32, c_f32, c_u64,
-                         c_u64, c_i64, c_i32, c_i32, c_f32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr],
+                         c_u64, c_ptr, c_i64, c_i32, c_i32, c_f32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr],
     "nr_attn_pool_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_ptr, c_ptr, c_f32, c_u64, c_u64,
-                         c_i64, c_i32, c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64,
+                         c_ptr, c_i64, c_i32, c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64,
                          c_ptr, c_i64, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
     "nr_rnn_fwd": [c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i32, c_i64, c_i32,
                    c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr],
@@ -61,14 +61,14 @@ _SIGS = {
     "nr_score_fwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i64, c_i32, c_i32, c_i32, c_ptr, c_ptr],
     "nr_score_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i32, c_i32, c_i32, c_ptr, c_i64, c_ptr,
                      c_i64, c_ptr],
-    "nr_adam": [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_f32, c_ptr],
+    "nr_adam": [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_ptr, c_f32, c_ptr],
     "nr_embedding_fwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr],
     "nr_embedding_bwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_ptr],
     "nr_colsum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr],
     "nr_mha_pool_fwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_f32,
-                        c_u64, c_u64, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr],
+                        c_u64, c_u64, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr],
     "nr_mha_pool_bwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_u64,
-                        c_u64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
+                        c_u64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
                         c_ptr, c_ptr],
 }
 

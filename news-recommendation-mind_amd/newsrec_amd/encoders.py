@@ -28,16 +28,25 @@ def _mask_rows(mask, rows):
 
 class _DropoutStream:
     """Stateless counter RNG bookkeeping for the fused dropout: a fixed seed and an offset that
-    advances by the number of elements each training forward consumes."""
+    advances by the number of elements each training forward consumes.  The pair lives on the
+    device: each forward snapshots it (the kernels read the snapshot; the backward reuses it)
+    and advances it with a device add, so a captured train step replayed as a graph draws a
+    fresh mask every replay."""
 
     def __init__(self):
         self.seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFF
         self.offset = 0
+        self.state = None
 
-    def take(self, n):
+    def take(self, n, device):
+        """-> (seed, offset, rng): rng = int64 CUDA (seed, offset) snapshot for the kernels."""
+        if self.state is None or self.state.device != device:
+            self.state = torch.tensor([self.seed, self.offset], dtype=torch.int64, device=device)
+        snap = self.state.clone()
+        self.state[1:].add_(int(n))
         off = self.offset
-        self.offset += int(n)
-        return self.seed, off
+        self.offset += int(n)   # host mirror (eager bookkeeping; replays advance only the device pair)
+        return self.seed, off, snap
 
 
 class CNN_Encoder(nn.Module):
@@ -102,12 +111,12 @@ class MHA_Encoder(nn.Module):
         seq_len = token_ids.shape[-1]
         T = token_ids.numel()
         p = float(self.dropOut.p) if self.training else 0.0
-        seed, off = self._rng.take(T * self.hidden_dim) if p > 0 else (0, 0)
+        seed, off, rng = self._rng.take(T * self.hidden_dim, table.device) if p > 0 else (0, 0, None)
         w, b = self.mha.fused_weight()
         news, tok = MHANewsFn.apply(table, token_ids.reshape(T), _mask_rows(attn_mask, T), w, b,
                                     self.layerNorm.weight, self.layerNorm.bias, self.query_words, self.head_num,
                                     self.mha.key_dim, self.mha.value_dim, seq_len, pad_row, p, seed, off,
-                                    want_tokens)
+                                    want_tokens, rng)
         tok = tok.reshape(*lead, seq_len, self.hidden_dim) if tok is not None else None
         return tok, news.reshape(*lead, self.hidden_dim)
 

@@ -119,7 +119,7 @@ class MHANewsFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, table, ids, mask, w_cat, b_cat, gamma, beta, query, heads, dk, dv, seq_len,
-                pad_row, p_drop, seed, offset, want_tokens):
+                pad_row, p_drop, seed, offset, want_tokens, rng=None):
         T = ids.numel()
         n = T // seq_len
         V, E = table.shape
@@ -150,17 +150,20 @@ class MHANewsFn(torch.autograd.Function):
         if fused:
             # attention + LN + dropout + pooling in one kernel per title; O stays in LDS
             O = None
+            # rng (device (seed, offset) snapshot) supersedes the host pair: kernel offset 0
             K.mha_pool_fwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, news, stats, probs,
-                           p_drop=p_drop, seed=seed, offset=offset, zout=tok, yrows=ur.inv if ur else None)
+                           p_drop=p_drop, seed=seed, offset=0 if rng is not None else offset, zout=tok,
+                           yrows=ur.inv if ur else None, rng=rng)
         else:
             O = _empty(T, H, table)
             K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, O)
             K.attn_pool_fwd(O, query, mask, n, seq_len, news, probs, gamma=gamma, beta=beta, stats=stats,
-                            p_drop=p_drop, seed=seed, offset=offset, zout=tok)
+                            p_drop=p_drop, seed=seed, offset=0 if rng is not None else offset, zout=tok, rng=rng)
         ctx.save_for_backward(table, ids, mask, w_cat, gamma, beta, query, Y, O, probs, stats)
         ctx.cfg = (heads, dk, dv, seq_len, pad_row, p_drop, seed, offset, fused)
         ctx.table_ref = table
         ctx.ur = ur
+        ctx.rng = rng
         return news, tok
 
     @staticmethod
@@ -183,12 +186,13 @@ class MHANewsFn(torch.autograd.Function):
         ur = ctx.ur
         if fused:
             K.mha_pool_bwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, stats, probs, dnews, dY, db, dq,
-                           dgamma, dbeta, p_drop=p_drop, seed=seed, offset=offset, dz=dz,
-                           yrows=ur.inv if ur else None)
+                           dgamma, dbeta, p_drop=p_drop, seed=seed, offset=0 if ctx.rng is not None else offset,
+                           dz=dz, yrows=ur.inv if ur else None, rng=ctx.rng)
         else:
             dO = _empty(T, H, table)
             K.attn_pool_bwd(O, query, mask, n, seq_len, probs, dnews, dO, dq, gamma=gamma, beta=beta, stats=stats,
-                            dgamma=dgamma, dbeta=dbeta, p_drop=p_drop, seed=seed, offset=offset, dz=dz)
+                            dgamma=dgamma, dbeta=dbeta, p_drop=p_drop, seed=seed,
+                            offset=0 if ctx.rng is not None else offset, dz=dz, rng=ctx.rng)
             K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
             K.colsum(dY, T, NY, db)
         dtable = None
@@ -217,7 +221,7 @@ class MHANewsFn(torch.autograd.Function):
                     dtable = None
             _proj_wgrad(dY, K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dw, None, T)
         return (dtable, None, None, dw, db, dgamma, dbeta, dq.view_as(query), None, None, None, None, None,
-                None, None, None, None)
+                None, None, None, None, None)
 
 
 # ---------------------------------------------------------------------- CNN news encoder

@@ -179,8 +179,13 @@ def _rows_ok(t, rows, ncols, name):
                          % (name, rows, ncols, tuple(t.shape), t.stride()))
 
 
+def _rng_ok(rng):
+    if rng is not None and (rng.dtype != torch.int64 or not rng.is_cuda or rng.numel() < 2):
+        raise L.HipError("rng must be an int64 CUDA tensor holding (seed, offset)")
+
+
 def attn_pool_fwd(x, q, mask, nseq, seq_len, out, probs, key=None, gamma=None, beta=None, stats=None,
-                  eps=1e-5, p_drop=0.0, seed=0, offset=0, scale=None, zout=None):
+                  eps=1e-5, p_drop=0.0, seed=0, offset=0, scale=None, zout=None, rng=None):
     D = q.numel()
     _f32(x, q, out, probs, key, gamma, beta, stats, zout)
     _rows_ok(zout, nseq * seq_len, D, "zout")
@@ -192,14 +197,14 @@ def attn_pool_fwd(x, q, mask, nseq, seq_len, out, probs, key=None, gamma=None, b
     mp, mdt = mask_arg(mask, nseq * seq_len)
     scale = 1.0 / float(D) ** 0.5 if scale is None else scale
     L.call("nr_attn_pool_fwd", L.ptr(x), x.stride(0), L.ptr(key), key.stride(0) if key is not None else 0,
-           L.ptr(q), mp, mdt, L.ptr(gamma), L.ptr(beta), eps, p_drop, seed, offset, nseq, seq_len, D,
-           scale, L.ptr(out), out.stride(0), L.ptr(zout), zout.stride(0) if zout is not None else 0,
+           L.ptr(q), mp, mdt, L.ptr(gamma), L.ptr(beta), eps, p_drop, seed, offset, L.ptr(rng), nseq, seq_len,
+           D, scale, L.ptr(out), out.stride(0), L.ptr(zout), zout.stride(0) if zout is not None else 0,
            L.ptr(stats), L.ptr(probs), L.stream_ptr(x))
 
 
 def attn_pool_bwd(x, q, mask, nseq, seq_len, probs, dout, dx, dq, key=None, dk=None, key_tanh=False,
                   gamma=None, beta=None, stats=None, dgamma=None, dbeta=None, p_drop=0.0, seed=0, offset=0,
-                  scale=None, dz=None):
+                  scale=None, dz=None, rng=None):
     D = q.numel()
     _f32(x, q, probs, dout, dx, dq, key, dk, gamma, beta, stats, dgamma, dbeta, dz)
     _rows_ok(dz, nseq * seq_len, D, "dz")
@@ -211,8 +216,8 @@ def attn_pool_bwd(x, q, mask, nseq, seq_len, probs, dout, dx, dq, key=None, dk=N
     mp, mdt = mask_arg(mask, nseq * seq_len)
     scale = 1.0 / float(D) ** 0.5 if scale is None else scale
     L.call("nr_attn_pool_bwd", L.ptr(x), x.stride(0), L.ptr(key), key.stride(0) if key is not None else 0,
-           L.ptr(q), mp, mdt, L.ptr(gamma), L.ptr(beta), p_drop, seed, offset, nseq, seq_len, D, scale,
-           L.ptr(stats), L.ptr(probs), L.ptr(dout), dout.stride(0), L.ptr(dz),
+           L.ptr(q), mp, mdt, L.ptr(gamma), L.ptr(beta), p_drop, seed, offset, L.ptr(rng), nseq, seq_len, D,
+           scale, L.ptr(stats), L.ptr(probs), L.ptr(dout), dout.stride(0), L.ptr(dz),
            dz.stride(0) if dz is not None else 0, L.ptr(dx), dx.stride(0), L.ptr(dk),
            dk.stride(0) if dk is not None else 0, int(key_tanh), L.ptr(dq), L.ptr(dgamma), L.ptr(dbeta),
            L.stream_ptr(x))
@@ -284,13 +289,19 @@ def score_bwd(cdd, user, logits, dlogits, B, C, H, mode, dcdd, duser):
 
 
 def adam(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
+    """``step``: an int (host count) or an int64 CUDA scalar tensor (device count, graph replays)."""
     _f32(param, grad, exp_avg, exp_avg_sq)
+    step_dev = None
+    if torch.is_tensor(step):
+        if step.dtype != torch.int64 or not step.is_cuda:
+            raise L.HipError("adam: a device step count must be an int64 CUDA tensor")
+        step_dev, step = step, 0
     n = param.numel()
     for t in (param, grad, exp_avg, exp_avg_sq):
         if not t.is_contiguous() or t.numel() != n:
             raise L.HipError("adam: tensors must be contiguous with equal numel")
     L.call("nr_adam", L.ptr(param), L.ptr(grad), L.ptr(exp_avg), L.ptr(exp_avg_sq), n, lr, beta1, beta2, eps,
-           weight_decay, step, grad_scale, L.stream_ptr(param))
+           weight_decay, step, L.ptr(step_dev), grad_scale, L.stream_ptr(param))
 
 
 def embedding_fwd(table, idx, out):
@@ -338,9 +349,11 @@ def _yrows_ok(y, yrows, T, ncols, name):
 
 
 def mha_pool_fwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, news, stats, probs, eps=1e-5,
-                 p_drop=0.0, seed=0, offset=0, zout=None, yrows=None):
+                 p_drop=0.0, seed=0, offset=0, zout=None, yrows=None, rng=None):
     """Fused tied-QK attention + LayerNorm + dropout + query pooling per title.  ``yrows``:
-    token t reads projection row yrows[t] (distinct-row projections)."""
+    token t reads projection row yrows[t] (distinct-row projections).  ``rng``: int64 CUDA
+    (seed, offset base) read by the kernel (graph replays draw fresh masks)."""
+    _rng_ok(rng)
     H = heads * dv
     _f32(y, gamma, beta, q, news, stats, probs, zout)
     _yrows_ok(y, yrows, nseq * seq_len, heads * (dk + dv), "y")
@@ -352,12 +365,13 @@ def mha_pool_fwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, news, st
         raise L.HipError("mha_pool_fwd: stats/probs too small")
     mp, mdt = mask_arg(mask, nseq * seq_len)
     L.call("nr_mha_pool_fwd", L.ptr(y), y.stride(0), L.ptr(yrows), mp, mdt, nseq, seq_len, heads, dk, dv, L.ptr(gamma),
-           L.ptr(beta), eps, p_drop, seed, offset, L.ptr(q), L.ptr(news), news.stride(0), L.ptr(zout),
+           L.ptr(beta), eps, p_drop, seed, offset, L.ptr(rng), L.ptr(q), L.ptr(news), news.stride(0), L.ptr(zout),
            zout.stride(0) if zout is not None else 0, L.ptr(stats), L.ptr(probs), L.stream_ptr(y))
 
 
 def mha_pool_bwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, dbias, dq,
-                 dgamma, dbeta, p_drop=0.0, seed=0, offset=0, dz=None, yrows=None):
+                 dgamma, dbeta, p_drop=0.0, seed=0, offset=0, dz=None, yrows=None, rng=None):
+    _rng_ok(rng)
     H = heads * dv
     _f32(y, gamma, beta, q, stats, probs, dnews, dy, dbias, dq, dgamma, dbeta, dz)
     _yrows_ok(y, yrows, nseq * seq_len, heads * (dk + dv), "y")
@@ -368,6 +382,6 @@ def mha_pool_bwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, stats, p
         raise L.HipError("mha_pool_bwd: dbias too small")
     mp, mdt = mask_arg(mask, nseq * seq_len)
     L.call("nr_mha_pool_bwd", L.ptr(y), y.stride(0), L.ptr(yrows), mp, mdt, nseq, seq_len, heads, dk, dv, L.ptr(gamma),
-           L.ptr(beta), p_drop, seed, offset, L.ptr(q), L.ptr(stats), L.ptr(probs), L.ptr(dnews), dnews.stride(0),
+           L.ptr(beta), p_drop, seed, offset, L.ptr(rng), L.ptr(q), L.ptr(stats), L.ptr(probs), L.ptr(dnews), dnews.stride(0),
            L.ptr(dz), dz.stride(0) if dz is not None else 0, L.ptr(dy), dy.stride(0), L.ptr(dbias), L.ptr(dq),
            L.ptr(dgamma), L.ptr(dbeta), L.stream_ptr(y))

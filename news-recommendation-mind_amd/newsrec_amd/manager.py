@@ -45,14 +45,15 @@ def build_model(encN, encU, hidden, vocab=30522, device="cuda", user_num=40, dro
     return TwoTower(m, emb, en, eu).to(device)
 
 
-def get_optim(model, lr=1e-4, bert_lr=6e-6):
-    """Manager._get_optim: names containing 'bert' -> bert_lr, the rest -> lr."""
+def get_optim(model, lr=1e-4, bert_lr=6e-6, capturable=False):
+    """Manager._get_optim: names containing 'bert' -> bert_lr, the rest -> lr.  ``capturable``:
+    step counts on the device (the step can be captured in a graph)."""
     from .optim import FusedAdam
     import re
     base, bert = [], []
     for name, p in model.named_parameters():
         (bert if re.search("bert", name) else base).append(p)
-    return FusedAdam([{"params": base, "lr": lr}, {"params": bert, "lr": bert_lr}])
+    return FusedAdam([{"params": base, "lr": lr}, {"params": bert, "lr": bert_lr}], capturable=capturable)
 
 
 def train_step(model, optimizer, x, grad_sync=None):
