@@ -142,7 +142,9 @@ int nr_mha_attn_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v
  * LayerNorm (eps) -> dropout(p, counter RNG) -> learned-query pooling, all in LDS.
  * y = [T][heads*dk | heads*dv] projections.  (dk, dv, heads*dv) in {(64,32,384), (64,64,768),
  * (64,32,256), (32,32,384)}.  Replaces MultiheadAttention.forward :125-147 + MHA.py:37-38.
- * Saves stats [T][2] and probs [T]; zout (optional) receives Z = the encoder's token output.
+ * Saves stats [T][2] and probs [T]; zout (optional) receives Z = the encoder's token output;
+ * oout (optional, ldo >= heads*dv) receives O, the attention output before the LayerNorm
+ * (training: lets nr_mha_pool_bwd skip the attention recompute).
  * yrows (optional): token t reads projection row yrows[t] (distinct-row projections).
  * rng (optional, all dropout entries): the dropout key comes from the device pair
  * (rng[0], rng[1] + offset) instead of (seed, offset), so a replayed graph draws new masks. */
@@ -151,19 +153,23 @@ int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows, const voi
                     int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
                     const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset,
                     const uint64_t* rng, const float* q, float* news, int64_t ldn, float* zout,
-                    int64_t ldz,
-                    float* stats, float* probs, hipStream_t stream);
+                    int64_t ldz, float* oout, int64_t ldo, float* stats, float* probs,
+                    hipStream_t stream);
 
-/* Backward of nr_mha_pool_fwd (recomputes the attention): writes dy [T][heads*(dk+dv)] and
- * ATOMICALLY ACCUMULATES dbias (= column sums of dy), dq, dgamma, dbeta (caller zeroes).
- * dy stays per token (row t) when yrows is given. */
+/* Backward of nr_mha_pool_fwd: writes dy [T][heads*(dk+dv)] and ATOMICALLY ACCUMULATES dbias
+ * (= column sums of dy), dq, dgamma, dbeta (caller zeroes).  dy stays per token (row t) when
+ * yrows is given; rows of masked tokens are exactly zero.  With o (the forward's oout) the
+ * backward runs split: a per-title pooling/LN pass writes dO into dob [T][heads*dv] (caller's
+ * workspace), then a per-(title, head) attention pass at high occupancy; without o one fused
+ * kernel recomputes the attention. */
 int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,
                     int32_t mask_dtype, int64_t nseq,
                     int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
                     const float* beta, float p_drop, uint64_t seed, uint64_t offset,
                     const uint64_t* rng, const float* q, const float* stats, const float* probs,
                     const float* dnews,
-                    int64_t ldn, const float* dz, int64_t lddz, float* dy, int64_t lddy,
+                    int64_t ldn, const float* dz, int64_t lddz, const float* o, int64_t ldo,
+                    float* dob, int64_t lddob, float* dy, int64_t lddy,
                     float* dbias, float* dq, float* dgamma, float* dbeta, hipStream_t stream);
 
 /* ------------------------------------------------------------------ pooling */

@@ -56,23 +56,38 @@ struct MPArgs {
   float* dy; int64_t lddy;            // bwd: [T][heads*dk + heads*dv]
   float* dbias; float* dq; float* dgamma; float* dbeta;
   int dbg;                            // timing-only ablations (NR_DEBUG_MHAPOOL): 1 = skip attention, 2 = skip LN/pool
+  float* o; int64_t ldo;              // fwd: optional saved attention output O (pre-LN); bwd: its input
+  float* dob; int64_t lddob;          // split bwd: dO rows (kernel 1 writes, kernel 2 reads)
+  int rows_per_wave;                  // staged row indices per wave (split bwd kernel 2) or per block
 };
 
-// Projection row of position l of the workgroup's title.  The row indices (yrows[token], or
-// the token index itself) are staged once per title in the first 32 words of the dynamic LDS
-// (stage_rows), so the per-head K/V loads never wait on an index load.
+// Projection rows of the workgroup's title are staged once per title as 32-bit BYTE offsets
+// from y (yrows[token] * ldy * 4, or the token's own row) in the first 32 words of the dynamic
+// LDS (per wave in the split backward), so the per-head K/V loads never wait on an index load
+// and address as 64-bit SGPR base + 32-bit VGPR offset (one VGPR per address, not two).
+// Requires (rows of y) * ldy * 4 < 2^32.
+__device__ __forceinline__ uint32_t yrow_off(const MPArgs& g, int l) {
+  extern __shared__ uint32_t nr_mp_rows[];
+  const int base = g.rows_per_wave ? (int)(threadIdx.x >> 6) * 32 : 0;
+  return nr_mp_rows[base + l];
+}
+
+__device__ __forceinline__ float ld_off(const float* base, uint32_t byte_off) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
 __device__ __forceinline__ const float* yrow(const MPArgs& g, int l) {
-  extern __shared__ int32_t nr_mp_rows[];
-  return g.y + (int64_t)nr_mp_rows[l] * g.ldy;
+  return reinterpret_cast<const float*>(reinterpret_cast<const char*>(g.y) + yrow_off(g, l));
+}
+
+__device__ __forceinline__ uint32_t row_byte_off(const MPArgs& g, int64_t tok) {
+  return (uint32_t)((g.yrows ? g.yrows[tok] : tok) * g.ldy * 4);
 }
 
 __device__ __forceinline__ void stage_rows(const MPArgs& g, int64_t seq) {
-  extern __shared__ int32_t nr_mp_rows[];
+  extern __shared__ uint32_t nr_mp_rows[];
   const int tid = threadIdx.x;
-  if (tid < 32) {
-    const int64_t tok = seq * g.L + (tid < g.L ? tid : 0);
-    nr_mp_rows[tid] = (int32_t)(g.yrows ? g.yrows[tok] : tok);
-  }
+  if (tid < 32) nr_mp_rows[tid] = row_byte_off(g, seq * g.L + (tid < g.L ? tid : 0));
   __syncthreads();
 }
 
@@ -158,7 +173,7 @@ __device__ __forceinline__ void load_vop(const MPArgs& g, int64_t seq, int head,
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const int k = crow(s, h);
-      const float v = yrow(g, k < g.L ? k : 0)[nq + head * DV + vb * 32 + c];
+      const float v = ld_off(g.y, yrow_off(g, k < g.L ? k : 0) + 4u * (uint32_t)(nq + head * DV + vb * 32 + c));
       bv[vb * 16 + s] = k < g.L ? v : 0.f;
     }
 }
@@ -223,6 +238,10 @@ __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < NH64; ++k) { x[k] = os[l * SO + lane + 64 * k]; s += x[k]; }
+    if (g.o) {   // saved attention output for the split backward
+#pragma unroll
+      for (int k = 0; k < NH64; ++k) g.o[row * g.ldo + lane + 64 * k] = x[k];
+    }
     const float mean = nr_wave_sum(s) * (1.f / H);
     float v = 0.f;
 #pragma unroll
@@ -265,22 +284,17 @@ __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
   }
 }
 
-template <int DK, int DV, int NH64>
-__global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
-  if (g.rng) g.dkey = nr_dropout_key(g.rng[0], g.rng[1] + g.offset);   // graph-replay RNG
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+// Pooling + dropout + LayerNorm backward of one title (B1..B4).  On entry os[l][*] holds the
+// attention output O rows (rows >= L zero), ps / st the saved pooling probabilities and LN
+// (mean, rstd).  On exit os holds dO (rows < L; rows >= L untouched); dq, dgamma, dbeta
+// accumulate atomically; dob (optional) receives the dO rows in global memory too.  `red`
+// ([nw][2][H]) may alias scratch that is free until the trailing barrier.
+template <int NH64>
+__device__ __forceinline__ void pool_ln_bwd(const MPArgs& g, int64_t seq, float* os, const float* ps, float* ds,
+                                            const float* st, float* red, float* dob, int64_t lddob) {
   constexpr int H = NH64 * 64;
   constexpr int SO = H + 1;
-  const int nw = blockDim.x >> 6, nt = blockDim.x;
-  float* os = sm + 32;                  // [32][SO]  O, then dO (sm[0..32): staged rows, yrow)
-  float* ps = os + 32 * SO;             // [32] pooling probs
-  float* ds = ps + 32;                  // [32] dp -> ds
-  float* st = ds + 32;                  // [32][2] mean, rstd
-  float* ts = st + 64;                  // [nw][32][33] per-wave transpose tiles
-  float* red = ts;                      // [nw][2][H] dgamma / dbeta partials (before ts is used)
-  const int64_t seq = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
-  const uint64_t bits = token_bits(g, seq);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
   float gam[NH64], bet[NH64], qv[NH64], dnv[NH64];
 #pragma unroll
   for (int k = 0; k < NH64; ++k) {
@@ -289,14 +303,6 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
     qv[k] = g.q[lane + 64 * k];
     dnv[k] = g.news[seq * g.ldn + lane + 64 * k];
   }
-  stage_rows(g, seq);
-  if (!(g.dbg & 1)) attention_to_lds<DK, DV>(g, seq, bits, os, SO);
-  if (tid < 32) {
-    ps[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
-    st[2 * tid] = tid < g.L ? g.stats[2 * (seq * g.L + tid)] : 0.f;
-    st[2 * tid + 1] = tid < g.L ? g.stats[2 * (seq * g.L + tid) + 1] : 0.f;
-  }
-  __syncthreads();
   // (B1) dp_l = dnews · Z_l
   for (int l = w; l < g.L; l += nw) {
     const int64_t row = seq * g.L + l;
@@ -358,7 +364,9 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
 #pragma unroll
     for (int k = 0; k < NH64; ++k) {
       const int d = lane + 64 * k;
-      os[l * SO + d] = rstd * (dyv[k] * gam[k] - sg - xh[k] * sgx);
+      const float v = rstd * (dyv[k] * gam[k] - sg - xh[k] * sgx);
+      os[l * SO + d] = v;
+      if (dob) dob[row * lddob + d] = v;
     }
   }
 #pragma unroll
@@ -373,101 +381,261 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
     atomicAdd(&g.dgamma[d], a);
     atomicAdd(&g.dbeta[d], b);
   }
-  __syncthreads();   // red aliases the transpose tiles
-  if (g.dbg & 4) return;
-  // (C) attention backward per head
+  __syncthreads();   // red may alias later scratch
+}
+
+// dO of one head for the attention backward: from the workgroup's LDS image (fused kernel:
+// rows >= L are zero there) or from the global dO rows (split form: clamp + zero by select).
+template <int DV>
+struct DoSource {
+  const float* base;   // row 0, column head*DV
+  int64_t ld;
+  int L;
+  bool global;
+  __device__ __forceinline__ float at(int l, int col) const {
+    if (!global) return base[l * ld + col];
+    const float v = ld_off(base, 4u * (uint32_t)((l < L ? l : 0) * (int)ld + col));
+    return l < L ? v : 0.f;
+  }
+};
+
+// Attention backward of one (title, head) by one wave (the title's projection rows staged by
+// stage_rows*): recompute P from the key rows, dV = Pᵀ dO, dPᵀ = V dOᵀ, dS (XSoftmax
+// backward), W = dS + dSᵀ (tied Q = K), dK = W K; dV / dK rows to dy, their column sums added
+// to cs[] (dbias: cs[vb] for the value columns, cs[DV/32 + kb] for the key columns).
+template <int DK, int DV>
+__device__ __forceinline__ void head_bwd(const MPArgs& g, int64_t seq, int head, uint64_t bits, float* tw,
+                                         const DoSource<DV>& dO, float (&cs)[DV / 32 + DK / 32]) {
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
   const int nq = g.heads * DK;
-  float* tw = ts + w * 32 * 33;
-  for (int head = w; head < g.heads; head += nw) {
-    float p[16];
-    head_probs<DK>(g, seq, head, bits, p);
-    // dVp = Pᵀ dO first (P is live anyway): Pᵀ through the transpose tile, dO from LDS
-    {
+  float* dyt = g.dy + seq * g.L * g.lddy;   // the title's dy rows (wave-uniform base)
+  float p[16];
+  head_probs<DK>(g, seq, head, bits, p);
+  // phase fences: keep each phase's loads inside it (hoisting them all to the top costs more
+  // registers than the latency they would hide; the split kernel runs 4 waves per SIMD)
+  __builtin_amdgcn_sched_barrier(0);
+  // dVp = Pᵀ dO first (P is live anyway): Pᵀ through the transpose tile
+  {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) tw[c * 33 + crow(r, h)] = p[r];
-      wave_lds_fence();
-      float pt[16];
+    for (int r = 0; r < 16; ++r) tw[c * 33 + crow(r, h)] = p[r];
+    wave_lds_fence();
+    float pt[16];
 #pragma unroll
-      for (int s = 0; s < 16; ++s) pt[s] = tw[crow(s, h) * 33 + c];
-      wave_lds_fence();
-#pragma unroll
-      for (int vb = 0; vb < DV / 32; ++vb) {
-        f32x16 acc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-        for (int s = 0; s < 16; ++s)
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pt[s], os[crow(s, h) * SO + head * DV + vb * 32 + c], acc, 0, 0, 0);
-        float cs = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int i = crow(r, h);
-          if (i < g.L) g.dy[(seq * g.L + i) * g.lddy + nq + head * DV + vb * 32 + c] = acc[r];
-          cs += acc[r];
-        }
-        cs += __shfl_xor(cs, 32, 64);
-        if (h == 0) atomicAdd(&g.dbias[nq + head * DV + vb * 32 + c], cs);
-      }
-    }
-    // dPᵀ = V dOᵀ  (lane (c, h): V[c][k], dO[c][k] over the interleaved k order)
-    float dsv[16];
-    {
-      f32x16 dpt;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dpt[r] = 0.f;
-      constexpr int HV = DV / 2;
-      const bool rv = c < g.L;
-      const float* vrr = yrow(g, rv ? c : 0) + nq + head * DV + 4 * h;   // clamp, zero by select
-#pragma unroll
-      for (int s = 0; s < HV; s += 4) {
-        float4 v4 = *reinterpret_cast<const float4*>(vrr + 2 * s);
-        if (!rv) v4 = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float* dor = os + c * SO + head * DV + 4 * h + 2 * s;
-        dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.x, dor[0], dpt, 0, 0, 0);
-        dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.y, dor[1], dpt, 0, 0, 0);
-        dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.z, dor[2], dpt, 0, 0, 0);
-        dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.w, dor[3], dpt, 0, 0, 0);
-      }
-      float rs = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) rs = fmaf(p[r], dpt[r], rs);
-      rs += __shfl_xor(rs, 32, 64);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dsv[r] = p[r] * (dpt[r] - rs) * g.scale_attn;
-    }
-    // W = dS + dSᵀ via the per-wave transpose tile
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tw[c * 33 + crow(r, h)] = dsv[r];
+    for (int s = 0; s < 16; ++s) pt[s] = tw[crow(s, h) * 33 + c];
     wave_lds_fence();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dsv[r] += tw[crow(r, h) * 33 + c];
-    wave_lds_fence();
-    // dKp = W Kp  -> dY[:, head*DK ..]
+    for (int vb = 0; vb < DV / 32; ++vb) {
+      float bo[16];
 #pragma unroll
-    for (int kb = 0; kb < DK / 32; ++kb) {
-      float bk[16];
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int k = crow(s, h);
-        const float v = yrow(g, k < g.L ? k : 0)[head * DK + kb * 32 + c];
-        bk[s] = k < g.L ? v : 0.f;
-      }
+      for (int s = 0; s < 16; ++s) bo[s] = dO.at(crow(s, h), vb * 32 + c);
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(dsv[s], bk[s], acc, 0, 0, 0);
-      float cs = 0.f;
+      for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pt[s], bo[s], acc, 0, 0, 0);
+      float sum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int j = crow(r, h);
-        if (j < g.L) g.dy[(seq * g.L + j) * g.lddy + head * DK + kb * 32 + c] = acc[r];
-        cs += acc[r];
+        const int i = crow(r, h);
+        if (i < g.L) dyt[(uint32_t)(i * (int)g.lddy + nq + head * DV + vb * 32 + c)] = acc[r];
+        sum += acc[r];
       }
-      cs += __shfl_xor(cs, 32, 64);
-      if (h == 0) atomicAdd(&g.dbias[head * DK + kb * 32 + c], cs);
+      cs[vb] += sum;
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
+  // dPᵀ = V dOᵀ  (lane (c, h): V[c][k], dO[c][k] over the interleaved k order)
+  float dsv[16];
+  {
+    f32x16 dpt;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dpt[r] = 0.f;
+    constexpr int HV = DV / 2;
+    const bool rv = c < g.L;
+    const float* vrr = yrow(g, rv ? c : 0) + nq + head * DV + 4 * h;   // clamp, zero by select
+#pragma unroll
+    for (int s = 0; s < HV; s += 4) {
+      float4 v4 = *reinterpret_cast<const float4*>(vrr + 2 * s);
+      if (!rv) v4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int col = 4 * h + 2 * s;
+      dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.x, dO.at(c, col), dpt, 0, 0, 0);
+      dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.y, dO.at(c, col + 1), dpt, 0, 0, 0);
+      dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.z, dO.at(c, col + 2), dpt, 0, 0, 0);
+      dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.w, dO.at(c, col + 3), dpt, 0, 0, 0);
+    }
+    float rs = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rs = fmaf(p[r], dpt[r], rs);
+    rs += __shfl_xor(rs, 32, 64);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dsv[r] = p[r] * (dpt[r] - rs) * g.scale_attn;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // W = dS + dSᵀ via the per-wave transpose tile
+#pragma unroll
+  for (int r = 0; r < 16; ++r) tw[c * 33 + crow(r, h)] = dsv[r];
+  wave_lds_fence();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dsv[r] += tw[crow(r, h) * 33 + c];
+  wave_lds_fence();
+  // dKp = W Kp  -> dY[:, head*DK ..]
+#pragma unroll
+  for (int kb = 0; kb < DK / 32; ++kb) {
+    float bk[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = crow(s, h);
+      const float v = ld_off(g.y, yrow_off(g, k < g.L ? k : 0) + 4u * (uint32_t)(head * DK + kb * 32 + c));
+      bk[s] = k < g.L ? v : 0.f;
+    }
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(dsv[s], bk[s], acc, 0, 0, 0);
+    float sum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = crow(r, h);
+      if (j < g.L) dyt[(uint32_t)(j * (int)g.lddy + head * DK + kb * 32 + c)] = acc[r];
+      sum += acc[r];
+    }
+    cs[DV / 32 + kb] += sum;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// dbias column sums of one head: lanes of the two halves hold partial sums of the same column
+template <int DK, int DV>
+__device__ __forceinline__ void flush_dbias(const MPArgs& g, int head, float (&cs)[DV / 32 + DK / 32]) {
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  const int nq = g.heads * DK;
+#pragma unroll
+  for (int i = 0; i < DV / 32 + DK / 32; ++i) {
+    const float v = cs[i] + __shfl_xor(cs[i], 32, 64);
+    const int col = i < DV / 32 ? nq + head * DV + i * 32 + c : head * DK + (i - DV / 32) * 32 + c;
+    if (h == 0) atomicAdd(&g.dbias[col], v);
+    cs[i] = 0.f;
+  }
+}
+
+// Fused backward (no saved O): recompute the attention into LDS, pooling/LN backward in
+// place, then the attention backward of every head with dO from LDS.
+template <int DK, int DV, int NH64>
+__global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
+  if (g.rng) g.dkey = nr_dropout_key(g.rng[0], g.rng[1] + g.offset);   // graph-replay RNG
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int H = NH64 * 64;
+  constexpr int SO = H + 1;
+  const int nw = blockDim.x >> 6;
+  float* os = sm + 32;                  // [32][SO]  O, then dO (sm[0..32): staged rows, yrow)
+  float* ps = os + 32 * SO;             // [32] pooling probs
+  float* ds = ps + 32;                  // [32] dp -> ds
+  float* st = ds + 32;                  // [32][2] mean, rstd
+  float* ts = st + 64;                  // [nw][32][33] per-wave transpose tiles
+  float* red = ts;                      // [nw][2][H] dgamma / dbeta partials (before ts is used)
+  const int64_t seq = blockIdx.x;
+  const int tid = threadIdx.x, w = tid >> 6;
+  const uint64_t bits = token_bits(g, seq);
+  stage_rows(g, seq);
+  if (!(g.dbg & 1)) attention_to_lds<DK, DV>(g, seq, bits, os, SO);
+  if (tid < 32) {
+    ps[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
+    st[2 * tid] = tid < g.L ? g.stats[2 * (seq * g.L + tid)] : 0.f;
+    st[2 * tid + 1] = tid < g.L ? g.stats[2 * (seq * g.L + tid) + 1] : 0.f;
+  }
+  __syncthreads();
+  pool_ln_bwd<NH64>(g, seq, os, ps, ds, st, red, nullptr, 0);
+  if (g.dbg & 4) return;
+  float* tw = ts + w * 32 * 33;
+  for (int head = w; head < g.heads; head += nw) {
+    DoSource<DV> dO{os + head * DV, SO, g.L, false};
+    float cs[DV / 32 + DK / 32];
+#pragma unroll
+    for (int i = 0; i < DV / 32 + DK / 32; ++i) cs[i] = 0.f;
+    head_bwd<DK, DV>(g, seq, head, bits, tw, dO, cs);
+    flush_dbias<DK, DV>(g, head, cs);
+  }
+}
+
+// Split backward, kernel 1 (forward saved O): pooling/LN backward per title from the saved O
+// rows; dO rows to global.
+template <int NH64>
+__global__ __launch_bounds__(256) void mha_ln_bwd_kernel(MPArgs g) {
+  if (g.rng) g.dkey = nr_dropout_key(g.rng[0], g.rng[1] + g.offset);   // graph-replay RNG
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int H = NH64 * 64;
+  constexpr int SO = H + 1;
+  float* os = sm;                       // [32][SO]  O, then dO
+  float* ps = os + 32 * SO;             // [32]
+  float* ds = ps + 32;                  // [32]
+  float* st = ds + 32;                  // [32][2]
+  float* red = st + 64;                 // [nw][2][H]
+  const int64_t seq = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+  for (int l = w; l < g.L; l += nw) {   // O rows: coalesced float loads
+    const float* orow = g.o + (seq * g.L + l) * g.ldo;
+#pragma unroll
+    for (int k = 0; k < NH64; ++k) os[l * SO + lane + 64 * k] = orow[lane + 64 * k];
+  }
+  if (tid < 32) {
+    ps[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
+    st[2 * tid] = tid < g.L ? g.stats[2 * (seq * g.L + tid)] : 0.f;
+    st[2 * tid + 1] = tid < g.L ? g.stats[2 * (seq * g.L + tid) + 1] : 0.f;
+  }
+  __syncthreads();
+  pool_ln_bwd<NH64>(g, seq, os, ps, ds, st, red, g.dob, g.lddob);
+}
+
+// Split backward, kernel 2: attention backward, one wave per head, HB_TITLES titles per
+// workgroup in sequence (the dbias column sums accumulate in registers across them: one
+// atomic per column per workgroup instead of per title).  Each wave stages its title's
+// projection-row indices in a private slice of LDS.
+constexpr int HB_TITLES = 1;
+
+template <int DK, int DV>
+__global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int head = blockIdx.y * nw + w;
+  if (head >= g.heads) return;   // no block-wide barrier below
+  uint32_t* rows = reinterpret_cast<uint32_t*>(sm) + 32 * w;   // this wave's staged row offsets (yrow)
+  float* tw = sm + 32 * nw + w * 32 * 33;                     // this wave's transpose tile
+  float* dot = sm + 32 * nw + nw * 32 * 33 + w * 32 * (DV + 1);   // this wave's dO slice [32][DV+1]
+  float cs[DV / 32 + DK / 32];
+#pragma unroll
+  for (int i = 0; i < DV / 32 + DK / 32; ++i) cs[i] = 0.f;
+  const int64_t s0 = (int64_t)blockIdx.x * HB_TITLES;
+#pragma unroll 1
+  for (int64_t seq = s0; seq < s0 + HB_TITLES && seq < g.nseq; ++seq) {
+    if (lane < 32) rows[lane] = row_byte_off(g, seq * g.L + (lane < g.L ? lane : 0));
+    wave_lds_fence();
+    {   // the head's dO slice into LDS (rows >= L zero): coalesced float4 loads, all in flight
+      constexpr int F4 = DV / 4;                 // float4 per row
+      constexpr int PER = 32 * F4 / 64;          // per lane
+      const float* src = g.dob + (seq * g.L) * g.lddob + head * DV;
+      float4 v[PER];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int e = lane + 64 * i, r = e / F4, c4 = e % F4;
+        v[i] = *reinterpret_cast<const float4*>(
+            reinterpret_cast<const char*>(src) + 4u * (uint32_t)((r < g.L ? r : 0) * (int)g.lddob + 4 * c4));
+        if (r >= g.L) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int e = lane + 64 * i, r = e / F4, c4 = e % F4;
+        float* d = dot + r * (DV + 1) + 4 * c4;
+        d[0] = v[i].x; d[1] = v[i].y; d[2] = v[i].z; d[3] = v[i].w;
+      }
+    }
+    wave_lds_fence();
+    const uint64_t bits = token_bits(g, seq);
+    DoSource<DV> dO{dot, DV + 1, g.L, false};
+    head_bwd<DK, DV>(g, seq, head, bits, tw, dO, cs);
+    wave_lds_fence();   // the next title's row indices / dO overwrite these
+  }
+  flush_dbias<DK, DV>(g, head, cs);
 }
 
 size_t fwd_smem(int H) { return (size_t)(32 + 32 * (H + 1) + 32) * sizeof(float); }
@@ -476,35 +644,50 @@ size_t bwd_smem(int H, int nw) {
   return (size_t)(32 + 32 * (H + 1) + 32 + 32 + 64 + (tiles > red ? tiles : red)) * sizeof(float);
 }
 
+size_t ln_bwd_smem(int H, int nw) { return (size_t)(32 * (H + 1) + 32 + 32 + 64 + nw * 2 * H) * sizeof(float); }
+size_t head_bwd_smem(int nw, int dv) { return (size_t)(32 * nw + nw * 32 * 33 + nw * 32 * (dv + 1)) * sizeof(float); }
+
+enum Pass { FWD = 0, BWD_FUSED = 1, BWD_SPLIT = 2 };
+
+template <typename K>
+void allow_smem(K kern, size_t sz) {
+  if (sz > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sz);
+}
+
 template <int DK, int DV, int NH64>
-int launch(const MPArgs& g, bool bwd, hipStream_t s) {
+int launch(const MPArgs& g, Pass pass, hipStream_t s) {
   const int H = NH64 * 64;
-  // forward: one wave per head (>= 4 waves for the LN phase); backward: one wave per two heads
-  // (its per-head state needs ~200 VGPRs, more than a 12-wave workgroup can give a wave)
-  const int nw = bwd ? ((g.heads + 1) / 2 < 4 ? 4 : (g.heads + 1) / 2) : (g.heads < 4 ? 4 : g.heads);
-  if (bwd) {
+  if (pass == FWD) {   // one wave per head (>= 4 waves for the LN phase)
+    const int nw = g.heads < 4 ? 4 : g.heads;
+    const size_t sz = fwd_smem(H);
+    allow_smem(mha_pool_fwd_kernel<DK, DV, NH64>, sz);
+    hipLaunchKernelGGL((mha_pool_fwd_kernel<DK, DV, NH64>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
+  } else if (pass == BWD_FUSED) {
+    // one wave per two heads (its per-head state needs ~200 VGPRs, more than a 12-wave
+    // workgroup can give a wave)
+    const int nw = (g.heads + 1) / 2 < 4 ? 4 : (g.heads + 1) / 2;
     const size_t sz = bwd_smem(H, nw);
-    if (sz > 64 * 1024)
-      (void)hipFuncSetAttribute((const void*)mha_pool_bwd_kernel<DK, DV, NH64>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)sz);
+    allow_smem(mha_pool_bwd_kernel<DK, DV, NH64>, sz);
     hipLaunchKernelGGL((mha_pool_bwd_kernel<DK, DV, NH64>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
   } else {
-    const size_t sz = fwd_smem(H);
-    if (sz > 64 * 1024)
-      (void)hipFuncSetAttribute((const void*)mha_pool_fwd_kernel<DK, DV, NH64>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)sz);
-    hipLaunchKernelGGL((mha_pool_fwd_kernel<DK, DV, NH64>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
+    const size_t s1 = ln_bwd_smem(H, 4);
+    allow_smem(mha_ln_bwd_kernel<NH64>, s1);
+    hipLaunchKernelGGL((mha_ln_bwd_kernel<NH64>), dim3((unsigned)g.nseq), dim3(256), s1, s, g);
+    MPArgs g2 = g;
+    g2.rows_per_wave = 1;
+    const unsigned gx = (unsigned)((g.nseq + HB_TITLES - 1) / HB_TITLES), gy = (unsigned)((g.heads + 3) / 4);
+    hipLaunchKernelGGL((mha_head_bwd_kernel<DK, DV>), dim3(gx, gy), dim3(256), head_bwd_smem(4, DV), s, g2);
   }
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
 
-int dispatch(const MPArgs& g, int dk, int dv, bool bwd, hipStream_t s) {
+int dispatch(const MPArgs& g, int dk, int dv, Pass pass, hipStream_t s) {
   const int H = g.heads * dv;
   if (H % 64) return NR_EINVAL(9);
   const int nh64 = H / 64;
 #define NR_CASE(K, V, N) \
-  if (dk == K && dv == V && nh64 == N) return launch<K, V, N>(g, bwd, s);
+  if (dk == K && dv == V && nh64 == N) return launch<K, V, N>(g, pass, s);
   NR_CASE(64, 32, 6)    // NRMS news encoder: E=768 -> 12 heads x 64, H = 384
   NR_CASE(64, 64, 12)   // H = 768
   NR_CASE(64, 32, 4)    // H = 256 (8 heads)
@@ -521,8 +704,8 @@ extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows
                                int32_t mask_dtype, int64_t nseq,
                                int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
                                const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset, const uint64_t* rng,
-                               const float* q, float* news, int64_t ldn, float* zout, int64_t ldz, float* stats,
-                               float* probs, hipStream_t stream) {
+                               const float* q, float* news, int64_t ldn, float* zout, int64_t ldz, float* oout,
+                               int64_t ldo, float* stats, float* probs, hipStream_t stream) {
   if (L < 1 || L > 32 || heads < 1 || heads > 12) return NR_EINVAL(0);
   if (!y || !mask || !gamma || !beta || !q || !news || !stats || !probs) return NR_EINVAL(1);
   if ((ldy & 3) || !al16(y)) return NR_EINVAL(2);
@@ -533,11 +716,13 @@ extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows
   g.gamma = gamma; g.beta = beta; g.eps = eps; g.p_drop = p_drop; g.seed = seed; g.offset = offset;
   g.dkey = nr_dropout_key(seed, offset); g.dthresh = nr_dropout_threshold(p_drop); g.rng = rng; g.q = q;
   g.news = news; g.ldn = ldn; g.zout = zout; g.ldz = ldz; g.stats = stats; g.probs = probs;
+  g.o = oout; g.ldo = ldo;
+  if (oout && ((ldo & 3) || ldo < (int64_t)heads * dv)) return NR_EINVAL(3);
   {
     const char* e = getenv("NR_DEBUG_MHAPOOL");
     g.dbg = e ? atoi(e) : 0;
   }
-  return dispatch(g, dk, dv, false, stream);
+  return dispatch(g, dk, dv, FWD, stream);
 }
 
 extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,
@@ -545,8 +730,9 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
                                int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
                                const float* beta, float p_drop, uint64_t seed, uint64_t offset, const uint64_t* rng, const float* q,
                                const float* stats, const float* probs, const float* dnews, int64_t ldn,
-                               const float* dz, int64_t lddz, float* dy, int64_t lddy, float* dbias, float* dq,
-                               float* dgamma, float* dbeta, hipStream_t stream) {
+                               const float* dz, int64_t lddz, const float* o, int64_t ldo, float* dob,
+                               int64_t lddob, float* dy, int64_t lddy, float* dbias, float* dq, float* dgamma,
+                               float* dbeta, hipStream_t stream) {
   if (L < 1 || L > 32 || heads < 1 || heads > 12) return NR_EINVAL(0);
   if (!y || !mask || !gamma || !beta || !q || !stats || !probs || !dnews || !dy || !dbias || !dq || !dgamma ||
       !dbeta)
@@ -561,9 +747,11 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
   g.news = const_cast<float*>(dnews); g.ldn = ldn; g.stats = const_cast<float*>(stats);
   g.probs = const_cast<float*>(probs); g.dz = dz; g.lddz = lddz; g.dy = dy; g.lddy = lddy; g.dbias = dbias;
   g.dq = dq; g.dgamma = dgamma; g.dbeta = dbeta;
+  g.o = const_cast<float*>(o); g.ldo = ldo; g.dob = dob; g.lddob = lddob;
+  if (o && (!dob || lddob < (int64_t)heads * dv || ldo < (int64_t)heads * dv)) return NR_EINVAL(3);
   {
     const char* e = getenv("NR_DEBUG_MHAPOOL");
     g.dbg = e ? atoi(e) : 0;
   }
-  return dispatch(g, dk, dv, true, stream);
+  return dispatch(g, dk, dv, o ? BWD_SPLIT : BWD_FUSED, stream);
 }

@@ -76,3 +76,40 @@ def test_fused_mha_news_encoder(p_drop):
                "encoderN.query_words": Pd[k].grad}.get(k, Pd[k].grad)
         torch.testing.assert_close(got.cpu().double(), ref, rtol=0, atol=3e-4 * max(ref.abs().max().item(), 1e-3),
                                    msg=k)
+
+
+@pytest.mark.parametrize("p_drop", [0.0, 0.2])
+def test_mha_pool_split_backward_matches_fused(p_drop):
+    """The split backward (forward saves O; pooling/LN pass + per-head attention pass) against
+    the fused one (recomputes the attention) on the same inputs."""
+    from newsrec_amd import kernels as K
+    torch.manual_seed(11)
+    n, Lq, heads, dk, dv = 97, 30, 12, 64, 32
+    T, NY, H = n * Lq, heads * (dk + dv), heads * dv
+    y = torch.randn(T, NY, device="cuda") * 0.3
+    mask = (torch.rand(n, Lq, device="cuda") < 0.8).long()
+    mask[:, 0] = 1
+    mask[5] = 0   # a fully masked title
+    gamma = 1 + 0.1 * torch.randn(H, device="cuda")
+    beta = 0.1 * torch.randn(H, device="cuda")
+    q = torch.randn(H, device="cuda")
+    dnews = torch.randn(n, H, device="cuda")
+    outs = []
+    for split in (False, True):
+        news = torch.empty(n, H, device="cuda")
+        stats = torch.empty(T, 2, device="cuda")
+        probs = torch.empty(T, device="cuda")
+        O = torch.empty(T, H, device="cuda") if split else None
+        K.mha_pool_fwd(y, mask, n, Lq, heads, dk, dv, gamma, beta, q, news, stats, probs, p_drop=p_drop, seed=9,
+                       offset=3, oout=O)
+        dy = torch.zeros(T, NY, device="cuda")
+        db, dq, dg, dbt = (torch.zeros(NY, device="cuda"), torch.zeros(H, device="cuda"),
+                           torch.zeros(H, device="cuda"), torch.zeros(H, device="cuda"))
+        dob = torch.empty(T, H, device="cuda") if split else None
+        K.mha_pool_bwd(y, mask, n, Lq, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, db, dq, dg, dbt,
+                       p_drop=p_drop, seed=9, offset=3, o=O, dob=dob)
+        outs.append((news, dy, db, dq, dg, dbt))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-4)   # dbias: atomic order

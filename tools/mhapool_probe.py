@@ -30,6 +30,14 @@ def timeit(fn, n=int(os.environ.get("ITERS", "20"))):
     return s.elapsed_time(e) / n * 1e3
 
 
+O = torch.empty(T, H, device="cuda")
+dob = torch.empty(T, H, device="cuda")
+for p in (0.0, 0.2):
+    f2 = lambda: K.mha_pool_fwd(y, mask, n, L, heads, dk, dv, gamma, beta, q, news, stats, probs, p_drop=p, seed=1,
+                                oout=O)
+    b2 = lambda: K.mha_pool_bwd(y, mask, n, L, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, db, dq, dg,
+                                dbt, p_drop=p, seed=1, o=O, dob=dob)
+    print("p=%.1f split: fwd+O %.1f us  bwd %.1f us" % (p, timeit(f2), timeit(b2)), flush=True)
 for p in (0.0, 0.2):
     f = lambda: K.mha_pool_fwd(y, mask, n, L, heads, dk, dv, gamma, beta, q, news, stats, probs, p_drop=p, seed=1)
     b = lambda: K.mha_pool_bwd(y, mask, n, L, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, db, dq, dg, dbt,
