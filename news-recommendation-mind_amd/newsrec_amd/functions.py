@@ -89,6 +89,9 @@ PROBE = _Probe()
 
 # Distinct-row projection in the MHA news tower (NR_DEDUP_ROWS=0 projects every token row).
 DEDUP_ROWS = os.environ.get("NR_DEDUP_ROWS", "1") != "0"
+# Training forward saves the attention output; the backward runs split (NR_SPLIT_BWD=0: fused
+# backward that recomputes the attention).
+SPLIT_BWD = os.environ.get("NR_SPLIT_BWD", "1") != "0"
 
 
 class _TableGradHook:
@@ -148,12 +151,13 @@ class MHANewsFn(torch.autograd.Function):
         stats = torch.empty(T, 2, device=table.device)
         tok = _empty(T, H, table) if want_tokens else None
         if fused:
-            # attention + LN + dropout + pooling in one kernel per title; O stays in LDS
-            O = None
+            # attention + LN + dropout + pooling in one kernel per title; when a backward will
+            # run, the attention output O is saved too (the backward then skips recomputing it)
+            O = _empty(T, H, table) if SPLIT_BWD and any(ctx.needs_input_grad) else None
             # rng (device (seed, offset) snapshot) supersedes the host pair: kernel offset 0
             K.mha_pool_fwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, news, stats, probs,
                            p_drop=p_drop, seed=seed, offset=0 if rng is not None else offset, zout=tok,
-                           yrows=ur.inv if ur else None, rng=rng)
+                           yrows=ur.inv if ur else None, rng=rng, oout=O)
         else:
             O = _empty(T, H, table)
             K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, O)
@@ -185,9 +189,10 @@ class MHANewsFn(torch.autograd.Function):
         db = torch.zeros(NY, device=table.device)
         ur = ctx.ur
         if fused:
+            dob = _empty(T, H, table) if O is not None else None
             K.mha_pool_bwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, stats, probs, dnews, dY, db, dq,
                            dgamma, dbeta, p_drop=p_drop, seed=seed, offset=0 if ctx.rng is not None else offset,
-                           dz=dz, yrows=ur.inv if ur else None, rng=ctx.rng)
+                           dz=dz, yrows=ur.inv if ur else None, rng=ctx.rng, o=O, dob=dob)
         else:
             dO = _empty(T, H, table)
             K.attn_pool_bwd(O, query, mask, n, seq_len, probs, dnews, dO, dq, gamma=gamma, beta=beta, stats=stats,
