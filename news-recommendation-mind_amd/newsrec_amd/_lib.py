@@ -10,7 +10,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libnewsrec_hip.so")
+# NR_LIB_PATH: load another build of the library (A/B timing of two builds in one session)
+LIB_PATH = os.environ.get("NR_LIB_PATH") or os.path.join(_HERE, "lib", "libnewsrec_hip.so")
 
 c_f32p = ctypes.c_void_p
 c_i64 = ctypes.c_int64
