@@ -284,17 +284,23 @@ __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
   }
 }
 
-// Pooling + dropout + LayerNorm backward of one title (B1..B4).  On entry os[l][*] holds the
-// attention output O rows (rows >= L zero), ps / st the saved pooling probabilities and LN
-// (mean, rstd).  On exit os holds dO (rows < L; rows >= L untouched); dq, dgamma, dbeta
-// accumulate atomically; dob (optional) receives the dO rows in global memory too.  `red`
-// ([nw][2][H]) may alias scratch that is free until the trailing barrier.
+// Pooling + dropout + LayerNorm backward of one title.  On entry os[l][*] holds the attention
+// output O rows (rows >= L zero), ps / st the saved pooling probabilities and LN (mean, rstd).
+// On exit os holds dO (rows < L; rows >= L untouched); dq, dgamma, dbeta accumulate
+// atomically; dob (optional) receives the dO rows in global memory too.  Two row passes, one
+// wave per row: (1) dp_l = dnews · Z_l, keeping the row's dropout keep-bits in LDS (one hash
+// per element for the whole backward); (2) after the pooling-softmax backward, dZ -> dropout ->
+// LayerNorm backward with per-lane partials of dq, dgamma, dbeta, reduced across the waves
+// through `red` ([nw][3][H]; may alias scratch that is free until the trailing barrier).
 template <int NH64>
 __device__ __forceinline__ void pool_ln_bwd(const MPArgs& g, int64_t seq, float* os, const float* ps, float* ds,
-                                            const float* st, float* red, float* dob, int64_t lddob) {
+                                            const float* st, float* red, uint64_t* kbits, float* dob,
+                                            int64_t lddob) {
   constexpr int H = NH64 * 64;
   constexpr int SO = H + 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
+  const bool drop = g.p_drop > 0.f;
+  const float dsc = drop ? 1.f / (1.f - g.p_drop) : 1.f;
   float gam[NH64], bet[NH64], qv[NH64], dnv[NH64];
 #pragma unroll
   for (int k = 0; k < NH64; ++k) {
@@ -303,7 +309,7 @@ __device__ __forceinline__ void pool_ln_bwd(const MPArgs& g, int64_t seq, float*
     qv[k] = g.q[lane + 64 * k];
     dnv[k] = g.news[seq * g.ldn + lane + 64 * k];
   }
-  // (B1) dp_l = dnews · Z_l
+  // (1) dp_l = dnews · Z_l; keep-bits of row l -> kbits[l][k]
   for (int l = w; l < g.L; l += nw) {
     const int64_t row = seq * g.L + l;
     const float mean = st[2 * l], rstd = st[2 * l + 1];
@@ -311,36 +317,27 @@ __device__ __forceinline__ void pool_ln_bwd(const MPArgs& g, int64_t seq, float*
 #pragma unroll
     for (int k = 0; k < NH64; ++k) {
       const int d = lane + 64 * k;
-      const float z = ((os[l * SO + d] - mean) * rstd * gam[k] + bet[k]) * drop_scale(g, row * H + d);
+      const bool keep = !drop || nr_dropout_keep(g.dkey, (uint32_t)(row * H + d), g.dthresh);
+      const uint64_t b = __ballot(keep);
+      if (lane == 0) kbits[l * NH64 + k] = b;
+      const float z = keep ? ((os[l * SO + d] - mean) * rstd * gam[k] + bet[k]) * dsc : 0.f;
       dot = fmaf(dnv[k], z, dot);
     }
     dot = nr_wave_sum(dot);
     if (lane == 0) ds[l] = dot;
   }
   __syncthreads();
-  if (w == 0) {
+  if (w == 0) {   // pooling softmax backward: ds_l = p_l (dp_l - Σ p dp) / sqrt(H)
     const float pl = lane < 32 ? ps[lane & 31] : 0.f;
     const float dp = lane < g.L ? ds[lane & 31] : 0.f;
     const float r = nr_wave_sum(pl * dp);
     if (lane < g.L) ds[lane] = pl * (dp - r) * g.scale_pool;
   }
   __syncthreads();
-  // (B3) dq[d] += Σ_l ds_l Z_l[d]
-  for (int d = tid; d < H; d += nt) {
-    float acc = 0.f;
-    const float gd = g.gamma[d], bd = g.beta[d];
-    for (int l = 0; l < g.L; ++l) {
-      const float z = ((os[l * SO + d] - st[2 * l]) * st[2 * l + 1] * gd + bd) *
-                      drop_scale(g, (seq * g.L + l) * H + d);
-      acc = fmaf(ds[l], z, acc);
-    }
-    atomicAdd(&g.dq[d], acc);
-  }
-  __syncthreads();
-  // (B4) dZ -> dropout -> LayerNorm backward; dO overwrites O row by row
-  float dgam[NH64], dbet[NH64];
+  // (2) dq += ds_l Z_l;  dZ = p_l dnews + ds_l q (+ dz) -> dropout -> LayerNorm backward
+  float dgam[NH64], dbet[NH64], dqp[NH64];
 #pragma unroll
-  for (int k = 0; k < NH64; ++k) { dgam[k] = 0.f; dbet[k] = 0.f; }
+  for (int k = 0; k < NH64; ++k) { dgam[k] = 0.f; dbet[k] = 0.f; dqp[k] = 0.f; }
   for (int l = w; l < g.L; l += nw) {
     const int64_t row = seq * g.L + l;
     const float mean = st[2 * l], rstd = st[2 * l + 1], pl = ps[l], dsl = ds[l];
@@ -349,10 +346,12 @@ __device__ __forceinline__ void pool_ln_bwd(const MPArgs& g, int64_t seq, float*
 #pragma unroll
     for (int k = 0; k < NH64; ++k) {
       const int d = lane + 64 * k;
+      const float s = ((kbits[l * NH64 + k] >> lane) & 1ull) ? dsc : 0.f;
+      xh[k] = (os[l * SO + d] - mean) * rstd;
+      dqp[k] = fmaf(dsl, (xh[k] * gam[k] + bet[k]) * s, dqp[k]);
       float dz = fmaf(pl, dnv[k], dsl * qv[k]);
       if (g.dz) dz += g.dz[row * g.lddz + d];
-      dyv[k] = dz * drop_scale(g, row * H + d);
-      xh[k] = (os[l * SO + d] - mean) * rstd;
+      dyv[k] = dz * s;
       const float gg = dyv[k] * gam[k];
       sg += gg;
       sgx = fmaf(gg, xh[k], sgx);
@@ -371,15 +370,21 @@ __device__ __forceinline__ void pool_ln_bwd(const MPArgs& g, int64_t seq, float*
   }
 #pragma unroll
   for (int k = 0; k < NH64; ++k) {
-    red[(w * 2) * H + lane + 64 * k] = dgam[k];
-    red[(w * 2 + 1) * H + lane + 64 * k] = dbet[k];
+    red[(w * 3) * H + lane + 64 * k] = dgam[k];
+    red[(w * 3 + 1) * H + lane + 64 * k] = dbet[k];
+    red[(w * 3 + 2) * H + lane + 64 * k] = dqp[k];
   }
   __syncthreads();
   for (int d = tid; d < H; d += nt) {
-    float a = 0.f, b = 0.f;
-    for (int ww = 0; ww < nw; ++ww) { a += red[(ww * 2) * H + d]; b += red[(ww * 2 + 1) * H + d]; }
+    float a = 0.f, b = 0.f, q = 0.f;
+    for (int ww = 0; ww < nw; ++ww) {
+      a += red[(ww * 3) * H + d];
+      b += red[(ww * 3 + 1) * H + d];
+      q += red[(ww * 3 + 2) * H + d];
+    }
     atomicAdd(&g.dgamma[d], a);
     atomicAdd(&g.dbeta[d], b);
+    atomicAdd(&g.dq[d], q);
   }
   __syncthreads();   // red may alias later scratch
 }
@@ -532,8 +537,9 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
   float* ps = os + 32 * SO;             // [32] pooling probs
   float* ds = ps + 32;                  // [32] dp -> ds
   float* st = ds + 32;                  // [32][2] mean, rstd
-  float* ts = st + 64;                  // [nw][32][33] per-wave transpose tiles
-  float* red = ts;                      // [nw][2][H] dgamma / dbeta partials (before ts is used)
+  uint64_t* kb = reinterpret_cast<uint64_t*>(st + 64);   // [32][NH64] dropout keep-bits
+  float* ts = st + 64 + 2 * 32 * NH64;  // [nw][32][33] per-wave transpose tiles
+  float* red = ts;                      // [nw][3][H] dgamma / dbeta / dq partials (before ts is used)
   const int64_t seq = blockIdx.x;
   const int tid = threadIdx.x, w = tid >> 6;
   const uint64_t bits = token_bits(g, seq);
@@ -545,7 +551,7 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
     st[2 * tid + 1] = tid < g.L ? g.stats[2 * (seq * g.L + tid) + 1] : 0.f;
   }
   __syncthreads();
-  pool_ln_bwd<NH64>(g, seq, os, ps, ds, st, red, nullptr, 0);
+  pool_ln_bwd<NH64>(g, seq, os, ps, ds, st, red, kb, nullptr, 0);
   if (g.dbg & 4) return;
   float* tw = ts + w * 32 * 33;
   for (int head = w; head < g.heads; head += nw) {
@@ -570,13 +576,26 @@ __global__ __launch_bounds__(256) void mha_ln_bwd_kernel(MPArgs g) {
   float* ps = os + 32 * SO;             // [32]
   float* ds = ps + 32;                  // [32]
   float* st = ds + 32;                  // [32][2]
-  float* red = st + 64;                 // [nw][2][H]
+  uint64_t* kb = reinterpret_cast<uint64_t*>(st + 64);   // [32][NH64]
+  float* red = st + 64 + 2 * 32 * NH64; // [nw][3][H]
   const int64_t seq = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
-  for (int l = w; l < g.L; l += nw) {   // O rows: coalesced float loads
-    const float* orow = g.o + (seq * g.L + l) * g.ldo;
+  {   // O rows (32 x H, rows >= L zero): every load in flight before the first LDS store
+    constexpr int PER = 32 * H / 4 / 256;   // float4 per thread (256 threads)
+    const float* o0 = g.o + seq * g.L * g.ldo;
+    float4 v[PER];
 #pragma unroll
-    for (int k = 0; k < NH64; ++k) os[l * SO + lane + 64 * k] = orow[lane + 64 * k];
+    for (int i = 0; i < PER; ++i) {
+      const int e = tid + 256 * i, r = e / (H / 4), c4 = e % (H / 4);
+      v[i] = *reinterpret_cast<const float4*>(o0 + (int64_t)(r < g.L ? r : 0) * g.ldo + 4 * c4);
+      if (r >= g.L) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = tid + 256 * i, r = e / (H / 4), c4 = e % (H / 4);
+      float* d = os + r * SO + 4 * c4;
+      d[0] = v[i].x; d[1] = v[i].y; d[2] = v[i].z; d[3] = v[i].w;
+    }
   }
   if (tid < 32) {
     ps[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
@@ -584,7 +603,7 @@ __global__ __launch_bounds__(256) void mha_ln_bwd_kernel(MPArgs g) {
     st[2 * tid + 1] = tid < g.L ? g.stats[2 * (seq * g.L + tid) + 1] : 0.f;
   }
   __syncthreads();
-  pool_ln_bwd<NH64>(g, seq, os, ps, ds, st, red, g.dob, g.lddob);
+  pool_ln_bwd<NH64>(g, seq, os, ps, ds, st, red, kb, g.dob, g.lddob);
 }
 
 // Split backward, kernel 2: attention backward, one wave per head, HB_TITLES titles per
@@ -608,13 +627,14 @@ __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
   const int64_t s0 = (int64_t)blockIdx.x * HB_TITLES;
 #pragma unroll 1
   for (int64_t seq = s0; seq < s0 + HB_TITLES && seq < g.nseq; ++seq) {
-    if (lane < 32) rows[lane] = row_byte_off(g, seq * g.L + (lane < g.L ? lane : 0));
-    wave_lds_fence();
-    {   // the head's dO slice into LDS (rows >= L zero): coalesced float4 loads, all in flight
-      constexpr int F4 = DV / 4;                 // float4 per row
-      constexpr int PER = 32 * F4 / 64;          // per lane
+    // every global load of the prologue in flight together: row ids, mask, the head's dO slice
+    const uint32_t roff = lane < 32 ? row_byte_off(g, seq * g.L + (lane < g.L ? lane : 0)) : 0u;
+    const uint64_t bits = token_bits(g, seq);
+    constexpr int F4 = DV / 4;                 // float4 per dO row
+    constexpr int PER = 32 * F4 / 64;          // per lane
+    float4 v[PER];
+    {
       const float* src = g.dob + (seq * g.L) * g.lddob + head * DV;
-      float4 v[PER];
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int e = lane + 64 * i, r = e / F4, c4 = e % F4;
@@ -622,15 +642,15 @@ __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
             reinterpret_cast<const char*>(src) + 4u * (uint32_t)((r < g.L ? r : 0) * (int)g.lddob + 4 * c4));
         if (r >= g.L) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
+    }
+    if (lane < 32) rows[lane] = roff;
 #pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const int e = lane + 64 * i, r = e / F4, c4 = e % F4;
-        float* d = dot + r * (DV + 1) + 4 * c4;
-        d[0] = v[i].x; d[1] = v[i].y; d[2] = v[i].z; d[3] = v[i].w;
-      }
+    for (int i = 0; i < PER; ++i) {   // dO slice into LDS, rows >= L zero
+      const int e = lane + 64 * i, r = e / F4, c4 = e % F4;
+      float* d = dot + r * (DV + 1) + 4 * c4;
+      d[0] = v[i].x; d[1] = v[i].y; d[2] = v[i].z; d[3] = v[i].w;
     }
     wave_lds_fence();
-    const uint64_t bits = token_bits(g, seq);
     DoSource<DV> dO{dot, DV + 1, g.L, false};
     head_bwd<DK, DV>(g, seq, head, bits, tw, dO, cs);
     wave_lds_fence();   // the next title's row indices / dO overwrite these
@@ -640,11 +660,13 @@ __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
 
 size_t fwd_smem(int H) { return (size_t)(32 + 32 * (H + 1) + 32) * sizeof(float); }
 size_t bwd_smem(int H, int nw) {
-  const size_t tiles = (size_t)nw * 32 * 33, red = (size_t)nw * 2 * H;
-  return (size_t)(32 + 32 * (H + 1) + 32 + 32 + 64 + (tiles > red ? tiles : red)) * sizeof(float);
+  const size_t tiles = (size_t)nw * 32 * 33, red = (size_t)nw * 3 * H;
+  return (size_t)(32 + 32 * (H + 1) + 32 + 32 + 64 + 2 * 32 * (H / 64) + (tiles > red ? tiles : red)) * sizeof(float);
 }
 
-size_t ln_bwd_smem(int H, int nw) { return (size_t)(32 * (H + 1) + 32 + 32 + 64 + nw * 2 * H) * sizeof(float); }
+size_t ln_bwd_smem(int H, int nw) {
+  return (size_t)(32 * (H + 1) + 32 + 32 + 64 + 2 * 32 * (H / 64) + nw * 3 * H) * sizeof(float);
+}
 size_t head_bwd_smem(int nw, int dv) { return (size_t)(32 * nw + nw * 32 * 33 + nw * 32 * (dv + 1)) * sizeof(float); }
 
 enum Pass { FWD = 0, BWD_FUSED = 1, BWD_SPLIT = 2 };
@@ -748,7 +770,8 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
   g.probs = const_cast<float*>(probs); g.dz = dz; g.lddz = lddz; g.dy = dy; g.lddy = lddy; g.dbias = dbias;
   g.dq = dq; g.dgamma = dgamma; g.dbeta = dbeta;
   g.o = const_cast<float*>(o); g.ldo = ldo; g.dob = dob; g.lddob = lddob;
-  if (o && (!dob || lddob < (int64_t)heads * dv || ldo < (int64_t)heads * dv)) return NR_EINVAL(3);
+  if (o && (!dob || lddob < (int64_t)heads * dv || ldo < (int64_t)heads * dv || (ldo & 3) || !al16(o)))
+    return NR_EINVAL(3);
   {
     const char* e = getenv("NR_DEBUG_MHAPOOL");
     g.dbg = e ? atoi(e) : 0;

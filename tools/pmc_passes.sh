@@ -3,6 +3,7 @@
 # never combined with sys/runtime traces).  Usage: tools/pmc_passes.sh OUTDIR cmd...
 set -e
 OUT=$1; shift
+mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM SQ_WAVES"
