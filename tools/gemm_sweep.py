@@ -23,8 +23,10 @@ def timeit(fn, n=10):
     return s.elapsed_time(e) / n
 
 
-shapes = [(52800, 1152, 768), (65536, 1024, 768), (65536, 1024, 1536), (65536, 1024, 3072),
-          (32768, 1024, 768), (8192, 8192, 4096), (4096, 4096, 4096)]
+shapes = [(24608, 1152, 768), (24608, 1152, 3072), (24576, 1024, 768), (32768, 1152, 768), (49152, 1152, 768),
+          (24608, 768, 1152), (65536, 1024, 768), (65536, 1024, 3072), (4096, 4096, 4096)]
+if os.environ.get("SWEEP_SHAPES"):
+    shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ["SWEEP_SHAPES"].split(",")]
 for M, N, Kd in shapes:
     A = torch.randn(M, Kd, device="cuda")
     B = torch.randn(N, Kd, device="cuda")
