@@ -264,6 +264,70 @@ int nr_embedding_bwd(const float* dout, int64_t V, int64_t E, const int64_t* idx
 int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out,
               hipStream_t stream);
 
+/* ---------------------------------------------------------------- device-side MIND data path
+ * (csrc/mind_batch.hip).  The dataset lives in HBM as CSR arrays:
+ *   tok, attn    [n_news, L] int32   encoded_news / attn_mask truncated to L columns with the
+ *                                    last column forced to [SEP] (utils/MIND.py:103-108)
+ *   his_off/ids  CSR of every impression's click history (behaviors.pkl "histories")
+ *   neg_off/ids  CSR of every train impression's unclicked news ("negatives")
+ *   imprs        [P, 2] int32 (impression index, clicked news) train samples ("imprs")
+ *   uindex       [I] int32 user index per impression ("uindexes")
+ * status: int32 word OR-ed with 1 (sample index out of range), 2 (news id out of range),
+ * 4 (candidate row / user row out of range); the caller zeroes it and checks it when it wants. */
+enum nr_batch_flags { NR_BATCH_REVERSE_HISTORY = 1, NR_BATCH_SHUFFLE_POS = 2 };
+
+/* One collated train batch of B impressions: MIND.__getitem__ train branch
+ * (utils/MIND.py:311-365) with newsample (utils/utils.py:83-98) for every sample_idx[b] in [0, P),
+ * then the DataLoader default collate.  Negatives: a uniform npratio-subset in uniform random
+ * order drawn from the counter RNG (seed, offset [+ b * 4C + d]); or the rng device pair
+ * {seed, offset} when non-null.  Outputs (C = npratio + 1): cdd_id [B,C] i64, his_id [B,his_size]
+ * i64, cdd_tok/cdd_attn [B,C,L] i64, his_tok/his_attn [B,his_size,L] i64, cdd_mask [B,C] f64,
+ * his_mask [B,his_size] f64, user_id [B] i64, label [B] i64.  Replaces the Python
+ * `random.sample` / `np.random.shuffle` streams (parity: structure exact, draws from this RNG). */
+int nr_form_train_batch(const int64_t* sample_idx, int64_t B, const int32_t* imprs, int64_t P,
+                        const int64_t* his_off, const int32_t* his_ids, const int64_t* neg_off,
+                        const int32_t* neg_ids, const int32_t* uindex, const int32_t* tok,
+                        const int32_t* attn, int64_t n_news, int32_t L, int32_t npratio,
+                        int32_t his_size, int32_t flags, uint64_t seed, uint64_t offset,
+                        const uint64_t* rng, int64_t* cdd_id, int64_t* his_id, int64_t* cdd_tok,
+                        int64_t* cdd_attn, int64_t* his_tok, int64_t* his_attn, double* cdd_mask,
+                        double* his_mask, int64_t* user_id, int64_t* label, int32_t* status,
+                        hipStream_t stream);
+
+/* History side of B consecutive dev/test impression chunks chunk0 .. chunk0+B-1
+ * (utils/MIND.py:367-449; chunk_impr[c] = impression of chunk c).  his_tok/his_attn may be null
+ * (fast eval reads history representations from the news table instead).  impr_index[b] =
+ * impression + 1 as the reference returns it. */
+int nr_form_eval_batch(int64_t chunk0, int64_t B, const int32_t* chunk_impr, int64_t n_chunks,
+                       const int64_t* his_off, const int32_t* his_ids, const int32_t* uindex,
+                       const int32_t* tok, const int32_t* attn, int64_t n_news, int32_t L,
+                       int32_t his_size, int32_t flags, int64_t* his_id, int64_t* his_tok,
+                       int64_t* his_attn, double* his_mask, int64_t* user_id, int64_t* impr_index,
+                       int32_t* status, hipStream_t stream);
+
+/* out_tok[i, :] = tok[ids[i], :], out_attn likewise (int32 table -> int64 rows). */
+int nr_gather_news_rows(const int64_t* ids, int64_t n, const int32_t* tok, const int32_t* attn,
+                        int64_t n_news, int32_t L, int64_t* out_tok, int64_t* out_attn,
+                        int32_t* status, hipStream_t stream);
+
+/* predict_fast over a packed ragged candidate list (models/TwoTowerBaseModel.py:78-83):
+ * out[c] = f(table[cand_ids[c]] . user[cand_seg[c] - seg_base] / sqrt(H)), f = sigmoid
+ * (NR_SCORE_SIGMOID) or identity (NR_SCORE_RAW). */
+int nr_score_ragged(const float* table, int64_t ldt, int64_t n_rows, const int64_t* cand_ids,
+                    const int32_t* cand_seg, int64_t seg_base, int64_t n, const float* user,
+                    int64_t ldu, int64_t n_users, int32_t H, int32_t mode, float* out,
+                    int32_t* status, hipStream_t stream);
+
+/* Per-impression ranking metrics of cal_metric (utils/Manager.py:1205-1273, 1276-1345) for G
+ * groups preds/labels[grp_off[g] .. grp_off[g+1]): out [G, 2 + 2*nk] f64 =
+ * {roc_auc, mrr, ndcg@ks[0..nk), hit@ks[0..nk)}; nk <= 8.  Ties in the score order follow a
+ * stable argsort reversed (the later index ranks first).  flags[g]: NR_METRIC_ONE_CLASS (auc
+ * undefined: sklearn raises), NR_METRIC_NONBINARY (labels outside {0,1}: auc undefined). */
+enum nr_metric_flags { NR_METRIC_ONE_CLASS = 1, NR_METRIC_NONBINARY = 2 };
+int nr_impression_metrics(const float* preds, const int32_t* labels, const int64_t* grp_off,
+                          int64_t G, const int32_t* ks, int32_t nk, double* out, int32_t* flags,
+                          hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,9 +71,22 @@ _SIGS = {
     "nr_mha_pool_bwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_u64,
                         c_u64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64,
                         c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+    "nr_form_train_batch": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
+                            c_i32, c_i32, c_i32, c_i32, c_u64, c_u64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+                            c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+    "nr_form_eval_batch": [c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_i32, c_i32,
+                           c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+    "nr_gather_news_rows": [c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
+    "nr_score_ragged": [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i32, c_i32, c_ptr,
+                        c_ptr, c_ptr],
+    "nr_impression_metrics": [c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i32, c_ptr, c_ptr, c_ptr],
 }
 
 _RESTYPES = {"nr_segment_rows_sum_workspace": c_i64}
+
+# enum nr_batch_flags / nr_metric_flags
+BATCH_REVERSE_HISTORY, BATCH_SHUFFLE_POS = 1, 2
+METRIC_ONE_CLASS, METRIC_NONBINARY = 1, 2
 
 _lib = None
 
