@@ -2,13 +2,20 @@
 12 heads) two-tower TRAIN step on synthetic MIND-large-shaped impressions.
 
 One step = one batch of B=32 impressions per GPU (1 clicked + 4 negative candidates, a
-50-click history, 30-token titles) through forward (fused embedding gather,
+50-click history, 30-token titles), FORMED ON THE DEVICE from a MIND-large-shaped
+train split resident in HBM (nr_form_train_batch: sampler indices -> impression -> news ids ->
+token rows, negative sampling from a device RNG; --data resident feeds pre-formed batches
+instead), through forward (fused embedding gather,
 news tower over 55 titles per impression, user tower, scorer + log-softmax), NLL loss,
 backward, gradient all-reduce (N > 1) and Adam (two groups, lr 1e-4 / 6e-6 for the 23.4 M
 parameter word table), exactly as utils/Manager.py:636-647.  Inputs are resident in HBM
 before the timed region.  fp32 storage and arithmetic (the reference's precision).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+The eval leg is the fast-eval pipeline (Manager._eval_fast): the 72,024-row MIND-large dev news
+table encoded (sharded over ranks + RCCL all-gather), batched predict_fast over a synthetic
+MIND-large-shaped dev split (376,471 impressions, ~37 candidates each), and cal_metric on the GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--data device|resident]
 
 Rank 0 prints ONE JSON line.  For N > 1 launch with torch.distributed.run (one rank/GPU).
 """
@@ -26,7 +33,9 @@ import torch
 import torch.distributed as dist
 
 B, C, NH, L, V, E, H, HEADS = 32, 5, 50, 30, 30522, 768, 384, 12
-USERS_LARGE, NEWS_LARGE_DEV = 876956, 72023
+USERS_LARGE, NEWS_LARGE_DEV, NEWS_LARGE_TRAIN = 876956, 72023, 101527
+DEV_IMPR_LARGE = 376471            # MIND-large dev impressions
+TRAIN_IMPR_SYNTH = 262144          # train impressions resident for the synthetic split (a subset of 2.23 M)
 FP32_MFMA_PEAK_TF = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = f32 vector peak
 HBM_PEAK_GBS = 8000.0
 
@@ -70,34 +79,73 @@ def make_optim(model, capturable=False):
     return get_optim(model, capturable=capturable)
 
 
-class GraphedStep:
-    """The whole train step (forward, NLL, backward, Adam) captured once as a HIP graph and
-    replayed: the ~80 kernels of a step launch back to back with no host work between them.
-    Each step copies its batch into the captured input buffers first (the data feed); dropout
-    draws and Adam step counts advance on the device, so replays are real training steps."""
+class ResidentFeed:
+    """Pre-formed synthetic batches already in HBM; step i copies batch i into the static inputs."""
 
-    def __init__(self, model, opt, batches, sync, warmup):
-        self.static = {k: v.clone() for k, v in batches[0].items()}
+    def __init__(self, batches):
         self.batches = batches
+        self.x = {k: v.clone() for k, v in batches[0].items()}
+
+    def feed(self, i):
+        for k, v in self.batches[i % len(self.batches)].items():
+            self.x[k].copy_(v, non_blocking=True)
+
+    def form(self):
+        return self.x
+
+
+class DeviceFeed:
+    """Batches formed on the device each step from a MIND-large-shaped train split in HBM
+    (MINDStore + nr_form_train_batch).  The sampler's epoch order (DistributedSampler: shuffled,
+    strided over ranks) is uploaded once; feed(i) copies step i's B indices into a static buffer
+    and form() launches the formation kernel, which draws negatives from the device RNG pair
+    (captured in the graph, every replay draws fresh negatives)."""
+
+    def __init__(self, device, world, rank, b=B, n_impr=TRAIN_IMPR_SYNTH):
+        from newsrec_amd.dist import shard_train
+        from newsrec_amd.mind import MINDStore, synthetic_arrays
+        self.store = MINDStore.from_arrays(
+            synthetic_arrays("train", NEWS_LARGE_TRAIN + 1, n_impr, vocab=V, users=USERS_LARGE, seed=99),
+            "train", seed=1234 + rank, device=device)
+        order = shard_train(len(self.store), world, rank, shuffle=True, seed=0)
+        self.order = torch.tensor(order, dtype=torch.int64, device=device)
+        self.b = b
+        self.idx = self.order[:b].clone()
+        self.x = self.store.train_batch(self.idx, device_rng=True)
+
+    def feed(self, i):
+        n = self.order.numel() // self.b
+        s = (i % n) * self.b
+        self.idx.copy_(self.order[s:s + self.b], non_blocking=True)
+
+    def form(self):
+        return self.store.train_batch(self.idx, out=self.x, device_rng=True)
+
+
+class GraphedStep:
+    """The whole train step (batch formation, forward, NLL, backward, Adam) captured once as a
+    HIP graph and replayed: the ~80 kernels of a step launch back to back with no host work
+    between them.  Each step first feeds its sampler indices (or resident batch) into the
+    captured input buffers; dropout draws, negative sampling and Adam step counts advance on the
+    device, so replays are real training steps."""
+
+    def __init__(self, model, opt, feed, sync, warmup):
+        self.feed = feed
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):   # warm-up off the default stream (allocator, lazy init)
             for i in range(max(2, warmup)):
-                self.feed(i)
-                train_step(model, opt, self.static, sync)
+                feed.feed(i)
+                train_step(model, opt, feed.form(), sync)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.loss = train_step(model, opt, self.static, sync)
+            self.loss = train_step(model, opt, feed.form(), sync)
         torch.cuda.synchronize()
 
-    def feed(self, i):
-        for k, v in self.batches[i % len(self.batches)].items():
-            self.static[k].copy_(v, non_blocking=True)
-
     def __call__(self, i):
-        self.feed(i)
+        self.feed.feed(i)
         self.graph.replay()
 
 
@@ -111,6 +159,48 @@ def train_step(model, opt, x, sync):
     scale = sync() if sync is not None else 1.0
     opt.step(grad_scale=scale)
     return loss
+
+
+def fast_eval_leg(model, dev, world, rank, n_impr):
+    """Manager._eval_fast + evaluate on a synthetic MIND-large-shaped dev split resident in HBM:
+    (1) encode the 72,024-row news table (rank shards + all-gather), (2) batched predict_fast over
+    the rank's Partition_Sampler chunks (history representations read from the table), predictions
+    gathered to rank 0, (3) cal_metric (auc, mean_mrr, ndcg@5;10) on the GPU.  Every phase is
+    bracketed by a barrier + synchronize; times are rank 0's (phases end in collectives)."""
+    from newsrec_amd import evaluate as EV
+    from newsrec_amd.mind import MINDStore, synthetic_arrays
+    st = MINDStore.from_arrays(synthetic_arrays("dev", NEWS_LARGE_DEV + 1, n_impr, vocab=V, users=USERS_LARGE,
+                                                seed=2024), "dev", device=dev)
+    n_cand = int(st.cand_off_host[-1])
+
+    def sync():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # warm-up: kernels, allocator
+    small = MINDStore.from_arrays(synthetic_arrays("dev", 2048, 256, vocab=V, seed=1), "dev", device=dev)
+    EV.evaluate(model, small, batch_impr=128)
+    sync()
+    t0 = time.perf_counter()
+    table = EV.encode_news_table(model, st)
+    sync()
+    t1 = time.perf_counter()
+    preds, labels, grp = EV.eval_fast(model, st, batch_impr=2048, news_table=table)
+    sync()
+    t2 = time.perf_counter()
+    res = EV.cal_metric_packed(preds, labels, grp, ["auc", "mean_mrr", "ndcg@5;10"]) if rank == 0 else None
+    t3 = time.perf_counter()
+    enc, pred, met = t1 - t0, t2 - t1, t3 - t2
+    return {"mode": "fast eval (Manager._eval_fast + evaluate): sharded news-table encode + RCCL all-gather, "
+                    "batched predict_fast (ragged scorer), cal_metric on the GPU",
+            "news": st.n_news, "impressions": n_impr, "candidates": n_cand,
+            "news_encode_ms": round(enc * 1e3, 2), "news_per_s": round(st.n_news / enc, 1),
+            "predict_ms": round(pred * 1e3, 2), "candidates_per_s": round(n_cand / pred, 1),
+            "metric_ms": round(met * 1e3, 2),
+            "end_to_end_ms": round((enc + pred + met) * 1e3, 2),
+            "end_to_end_candidates_per_s": round(n_cand / (enc + pred + met), 1),
+            "metrics_random_model": res}
 
 
 def cpu_baseline(seconds=20.0):
@@ -143,6 +233,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--data", choices=["device", "resident"], default="device",
+                    help="device: form each batch on the GPU from a resident MIND split; resident: pre-formed")
+    ap.add_argument("--eval-impr", type=int, default=DEV_IMPR_LARGE,
+                    help="dev impressions of the fast-eval leg (0 skips it)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the train step as a HIP graph (auto: single GPU)")
     a = ap.parse_args()
@@ -173,13 +267,15 @@ def main():
     opt = make_optim(model, capturable=use_graph)
     sync = GradSync(model) if world > 1 else None
     gen = torch.Generator().manual_seed(1234 + rank)
-    batches = [synth_batch(gen, dev) for _ in range(4)]
+    feed = DeviceFeed(dev, world, rank) if a.data == "device" else \
+        ResidentFeed([synth_batch(gen, dev) for _ in range(4)])
 
     if use_graph:
-        step_fn = GraphedStep(model, opt, batches, sync, a.warmup)
+        step_fn = GraphedStep(model, opt, feed, sync, a.warmup)
     else:
         def step_fn(i):
-            train_step(model, opt, batches[i % len(batches)], sync)
+            feed.feed(i)
+            train_step(model, opt, feed.form(), sync)
         for i in range(a.warmup):
             step_fn(i)
     torch.cuda.synchronize()
@@ -194,12 +290,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if a.data == "device":
+        feed.store.check_status()
 
     # per-launch timing of the dominant kernel (the fused gather + key/value projection GEMM),
     # HIP events on its stream, over a few eager steps (events cannot sit inside a replay)
     F.PROBE.enable()
     for i in range(3):
-        train_step(model, opt, batches[i % len(batches)], sync)
+        feed.feed(a.steps + i)
+        train_step(model, opt, feed.form(), sync)
     probe = F.PROBE.collect()
     F.PROBE.disable()
     if world > 1:
@@ -207,18 +306,25 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    # eval: forward in eval mode (sigmoid) over the same batch shape -> candidates scored/s
+    # eval (a): forward in eval mode (sigmoid) over train-shaped batches -> candidates scored/s
     model.eval()
+    evb = []
+    for i in range(4):
+        feed.feed(i)
+        evb.append({k: v.clone() for k, v in feed.form().items()})
     with torch.no_grad():
         for i in range(3):
-            model(batches[i % len(batches)])
+            model(evb[i % len(evb)])
         torch.cuda.synchronize()
         ne = max(5, a.steps // 2)
         t1 = time.perf_counter()
         for i in range(ne):
-            model(batches[i % len(batches)])
+            model(evb[i % len(evb)])
         torch.cuda.synchronize()
         el_eval = time.perf_counter() - t1
+    del evb
+    # eval (b): the fast-eval pipeline over a MIND-large-shaped dev split
+    fast = fast_eval_leg(model, dev, world, rank, a.eval_impr) if a.eval_impr > 0 else None
 
     if rank == 0:
         ms = el / a.steps * 1e3
@@ -241,10 +347,14 @@ def main():
             "config": {"workload": "NRMS train step: MHA news encoder + MHA user encoder, H=384, 12 heads, "
                                    "V=30522 word table (trainable), dropout 0.2, Adam",
                        "launch": "hipGraph replay of the whole step" if use_graph else "eager",
+                       "batches": ("formed on the device each step from a synthetic MIND-large-shaped train split "
+                                   "in HBM (%d impressions, 101,528-news token table)" % TRAIN_IMPR_SYNTH)
+                       if a.data == "device" else "pre-formed synthetic batches resident in HBM",
                        "global_batch": B * world, "per_gpu_batch": B, "candidates": C, "history": NH,
                        "seq_len": L, "parallelism": "dp%d" % world},
-            "eval": {"candidates_per_s": round(world * B * C * ne / el_eval, 1),
-                     "impressions_per_s": round(world * B * ne / el_eval, 1), "mode": "forward, eval (sigmoid)"},
+            "eval": dict(fast or {}, forward={"candidates_per_s": round(world * B * C * ne / el_eval, 1),
+                                              "impressions_per_s": round(world * B * ne / el_eval, 1),
+                                              "mode": "model(x) in eval mode (sigmoid) on train-shaped batches"}),
             "roofline": {"kernel": "gemm_f32 gather+key/value projection (fwd)", "bound": "mfma",
                          "achieved": round(achieved, 2) if achieved else None, "peak": FP32_MFMA_PEAK_TF,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TF, 4) if achieved else None,

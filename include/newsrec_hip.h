@@ -123,9 +123,11 @@ int nr_segment_rows_sum(const float* src, int64_t lds, int64_t width, int64_t T,
  * Replaces MultiheadAttention.forward after the projections (models/Modules/Attention.py:
  * 125-147), get_attn_mask (:33-53) and XSoftmax.forward (:66-74).  (dk, dv) in
  * {(64,32),(32,32),(64,64),(64,16),(16,16)} for L <= 32, {(32,32),(64,64),(16,16),(64,32)}
- * for L <= 64.  mask: [nseq, L] of enum nr_mask_dtype (0=u8, 1=i64, 2=f64, 3=f32). */
+ * for L <= 64.  mask: [nseq, L] of enum nr_mask_dtype (0=u8, 1=i64, 2=f64, 3=f32).
+ * rows (optional): token s*L+j reads qk / v row rows[s*L+j] (projections computed once per
+ * distinct row, e.g. the fast-eval news table, and gathered inside the kernel). */
 int nr_mha_attn_fwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v,
-                    const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L,
+                    const int64_t* rows, const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L,
                     int32_t heads, int32_t dk, int32_t dv, float scale, float* out,
                     int64_t ld_out, hipStream_t stream);
 

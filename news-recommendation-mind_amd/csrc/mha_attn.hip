@@ -25,6 +25,7 @@ struct AttnArgs {
   const float* dout; int64_t ld_dout;   // bwd: dO
   float* out; int64_t ld_out;           // fwd: O         bwd: dKp
   float* dv; int64_t ld_dv;             // bwd: dVp
+  const int64_t* rows;                  // fwd: physical qk / v row of token (seq*L + j), or null
 };
 
 template <int LMAX, int DK, int DV>
@@ -32,13 +33,21 @@ struct Smem {
   static constexpr int HPW = 64 / LMAX;          // heads per wave
   float k[HPW][LMAX][DK];
   float v[HPW][LMAX][DV];
-  float p[HPW][LMAX][LMAX + 1];                  // P (fwd: unused) then dS (bwd)
+  float p[HPW][LMAX][LMAX + 1];                  // P then dS (bwd)
   float d[HPW][LMAX][DV];                        // dO (bwd)
 };
 
+// forward: K/V rows only (16 KB at L <= 64, dk = dv = 32 instead of 41 KB: 2.5x the resident
+// waves per CU)
 template <int LMAX, int DK, int DV>
-__device__ __forceinline__ void load_rows(Smem<LMAX, DK, DV>& sm, const AttnArgs& g, int64_t seq,
-                                          int head0, bool with_dout) {
+struct SmemF {
+  static constexpr int HPW = 64 / LMAX;
+  float k[HPW][LMAX][DK];
+  float v[HPW][LMAX][DV];
+};
+
+template <bool WITH_DOUT, int LMAX, int DK, int DV, class S>
+__device__ __forceinline__ void load_rows(S& sm, const AttnArgs& g, int64_t seq, int head0) {
   constexpr int HPW = 64 / LMAX;
   const int lane = threadIdx.x;
   // K rows: HPW heads x L rows x DK floats, as float4
@@ -46,8 +55,10 @@ __device__ __forceinline__ void load_rows(Smem<LMAX, DK, DV>& sm, const AttnArgs
   for (int e = lane; e < HPW * LMAX * K4; e += 64) {
     const int hh = e / (LMAX * K4), rem = e % (LMAX * K4), j = rem / K4, c = rem % K4;
     float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (j < g.L && head0 + hh < g.heads)
-      x = *reinterpret_cast<const float4*>(g.qk + (seq * g.L + j) * g.ld_qk + (head0 + hh) * DK + 4 * c);
+    if (j < g.L && head0 + hh < g.heads) {
+      const int64_t r = g.rows ? g.rows[seq * g.L + j] : seq * g.L + j;
+      x = *reinterpret_cast<const float4*>(g.qk + r * g.ld_qk + (head0 + hh) * DK + 4 * c);
+    }
     *reinterpret_cast<float4*>(&sm.k[hh][j][4 * c]) = x;
   }
   for (int e = lane; e < HPW * LMAX * V4; e += 64) {
@@ -55,18 +66,19 @@ __device__ __forceinline__ void load_rows(Smem<LMAX, DK, DV>& sm, const AttnArgs
     float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 y = x;
     if (j < g.L && head0 + hh < g.heads) {
-      x = *reinterpret_cast<const float4*>(g.v + (seq * g.L + j) * g.ld_v + (head0 + hh) * DV + 4 * c);
-      if (with_dout)
+      const int64_t r = g.rows ? g.rows[seq * g.L + j] : seq * g.L + j;
+      x = *reinterpret_cast<const float4*>(g.v + r * g.ld_v + (head0 + hh) * DV + 4 * c);
+      if constexpr (WITH_DOUT)
         y = *reinterpret_cast<const float4*>(g.dout + (seq * g.L + j) * g.ld_dout + (head0 + hh) * DV + 4 * c);
     }
     *reinterpret_cast<float4*>(&sm.v[hh][j][4 * c]) = x;
-    if (with_dout) *reinterpret_cast<float4*>(&sm.d[hh][j][4 * c]) = y;
+    if constexpr (WITH_DOUT) *reinterpret_cast<float4*>(&sm.d[hh][j][4 * c]) = y;
   }
 }
 
 // Row i of P for the lane's head: returns probabilities in p[], exact zeros where masked.
-template <int LMAX, int DK, int DV>
-__device__ __forceinline__ void softmax_row(const Smem<LMAX, DK, DV>& sm, const AttnArgs& g,
+template <int LMAX, int DK, int DV, class S>
+__device__ __forceinline__ void softmax_row(const S& sm, const AttnArgs& g,
                                             int64_t seq, int hh, int i, bool row_ok, float (&q)[DK],
                                             float (&p)[LMAX]) {
   float mx = -INFINITY;
@@ -98,12 +110,12 @@ __device__ __forceinline__ void softmax_row(const Smem<LMAX, DK, DV>& sm, const 
 template <int LMAX, int DK, int DV>
 __global__ __launch_bounds__(64) void mha_attn_fwd_kernel(AttnArgs g) {
   constexpr int HPW = 64 / LMAX;
-  __shared__ __attribute__((aligned(16))) Smem<LMAX, DK, DV> sm;
+  __shared__ __attribute__((aligned(16))) SmemF<LMAX, DK, DV> sm;
   const int64_t seq = blockIdx.x;
   const int head0 = blockIdx.y * HPW;
   const int lane = threadIdx.x, hh = lane / LMAX, i = lane % LMAX;
   const int head = head0 + hh;
-  load_rows<LMAX, DK, DV>(sm, g, seq, head0, false);
+  load_rows<false, LMAX, DK, DV>(sm, g, seq, head0);
   __syncthreads();
   if (head >= g.heads || i >= g.L) return;
   const bool row_ok = nr_mask_at(g.mask, g.mask_dt, seq * g.L + i);
@@ -138,7 +150,7 @@ __global__ __launch_bounds__(64) void mha_attn_bwd_kernel(AttnArgs g) {
   const int head0 = blockIdx.y * HPW;
   const int lane = threadIdx.x, hh = lane / LMAX, i = lane % LMAX;
   const int head = head0 + hh;
-  load_rows<LMAX, DK, DV>(sm, g, seq, head0, true);
+  load_rows<true, LMAX, DK, DV>(sm, g, seq, head0);
   __syncthreads();
   const bool active = head < g.heads && i < g.L;
   const bool row_ok = active && nr_mask_at(g.mask, g.mask_dt, seq * g.L + i);
@@ -245,7 +257,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 }  // namespace
 
 extern "C" int nr_mha_attn_fwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v,
-                               const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L,
+                               const int64_t* rows, const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L,
                                int32_t heads, int32_t dk, int32_t dv, float scale, float* out,
                                int64_t ld_out, hipStream_t stream) {
   if (L < 1 || L > 64 || heads < 1) return NR_EINVAL(0);
@@ -253,7 +265,7 @@ extern "C" int nr_mha_attn_fwd(const float* qk, int64_t ld_qk, const float* v, i
   if ((ld_qk | ld_v | ld_out) & 3 || !aligned16(qk) || !aligned16(v) || !aligned16(out)) return NR_EINVAL(2);
   if (nseq == 0) return NR_OK;
   AttnArgs g{qk, ld_qk, v, ld_v, mask, mask_dtype, nseq, L, heads, scale,
-             nullptr, 0, out, ld_out, nullptr, 0};
+             nullptr, 0, out, ld_out, nullptr, 0, rows};
   return dispatch(g, dk, dv, false, stream);
 }
 
@@ -269,6 +281,6 @@ extern "C" int nr_mha_attn_bwd(const float* qk, int64_t ld_qk, const float* v, i
     return NR_EINVAL(2);
   if (nseq == 0) return NR_OK;
   AttnArgs g{qk, ld_qk, v, ld_v, mask, mask_dtype, nseq, L, heads, scale,
-             dout, ld_dout, dqk, ld_dqk, dvout, ld_dv};
+             dout, ld_dout, dqk, ld_dqk, dvout, ld_dv, nullptr};
   return dispatch(g, dk, dv, true, stream);
 }

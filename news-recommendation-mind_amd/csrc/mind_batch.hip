@@ -244,7 +244,6 @@ __global__ __launch_bounds__(256) void score_ragged_kernel(const float* table, i
 
 // ---------------------------------------------------------------- per-impression metrics
 #define NR_METRIC_MAX_K 8
-#define NR_METRIC_LDS 2048
 
 template <typename T>
 __device__ __forceinline__ T wave_sum_t(T v) {
@@ -252,44 +251,44 @@ __device__ __forceinline__ T wave_sum_t(T v) {
   return v;
 }
 
-// ranks follow np.argsort(score)[::-1] with a stable ascending sort: descending score, ties
-// broken toward the LATER index (numpy's default sort is stable for these sizes only up to 16
-// elements; beyond that its tie order is unspecified)
+// One WAVE per impression group (MIND dev impressions average ~37 candidates: a 256-thread
+// block per group left most lanes idle and paid a block barrier per group).  Lane l owns
+// candidates l, l+64, ...; the O(n^2) rank counts read the group's scores / labels straight
+// from global memory (wave-uniform addresses: one broadcast load per j, L1/L2 resident).
+// Ranks follow np.argsort(score)[::-1] with a stable ascending sort: descending score, ties
+// broken toward the LATER index (numpy's default sort kind is not stable on SIMD builds, so the
+// reference's own tie order is machine-dependent).
 __global__ __launch_bounds__(256) void metrics_kernel(const float* preds, const int32_t* labels,
                                                       const int64_t* grp_off, int64_t G, const int32_t* ks,
                                                       int nk, double* out, int32_t* flags) {
-  __shared__ float s_p[NR_METRIC_LDS];
-  __shared__ int32_t s_y[NR_METRIC_LDS];
-  __shared__ double s_red[4][2 + 3 * NR_METRIC_MAX_K];
-  __shared__ unsigned long long s_cnt[4][4];
-  const int64_t g = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (g >= G) return;
   const int64_t o0 = grp_off[g];
   const int n = (int)(grp_off[g + 1] - o0);
-  const bool staged = n <= NR_METRIC_LDS;
   const float* P = preds + o0;
   const int32_t* Y = labels + o0;
-  if (staged) {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) { s_p[i] = P[i]; s_y[i] = Y[i]; }
-    __syncthreads();
-  }
   int kk[NR_METRIC_MAX_K];
   for (int q = 0; q < nk; ++q) kk[q] = ks[q] < n ? ks[q] : n;
   double mrr = 0.0, ysum = 0.0;
   double dcg[NR_METRIC_MAX_K], idcg[NR_METRIC_MAX_K], hit[NR_METRIC_MAX_K];
   for (int q = 0; q < NR_METRIC_MAX_K; ++q) { dcg[q] = 0.0; idcg[q] = 0.0; hit[q] = 0.0; }
   unsigned long long auc2 = 0, npos = 0, nneg = 0, nonbin = 0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const float pi = staged ? s_p[i] : P[i];
-    const int32_t yi = staged ? s_y[i] : Y[i];
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    const bool live = i < n;
+    const float pi = live ? P[i] : 0.f;
+    const int32_t yi = live ? Y[i] : 0;
     int rs = 0, ry = 0;
     unsigned long long a2 = 0;
     for (int j = 0; j < n; ++j) {
-      const float pj = staged ? s_p[j] : P[j];
-      const int32_t yj = staged ? s_y[j] : Y[j];
+      const float pj = P[j];
+      const int32_t yj = Y[j];
       rs += (pj > pi) | ((pj == pi) & (j > i));
       ry += (yj > yi) | ((yj == yi) & (j > i));
-      if (yi == 1 && yj == 0) a2 += (pi > pj) ? 2u : (pi == pj ? 1u : 0u);
+      a2 += (yi == 1 && yj == 0) ? ((pi > pj) ? 2u : (pi == pj ? 1u : 0u)) : 0u;
     }
+    if (!live) continue;
     auc2 += a2;
     npos += yi == 1;
     nneg += yi == 0;
@@ -303,38 +302,22 @@ __global__ __launch_bounds__(256) void metrics_kernel(const float* preds, const 
       if (yi == 1 && rs < ks[q]) hit[q] = 1.0;
     }
   }
-  // block reduction: waves via shuffles, then wave 0 over the 4 wave partials
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   mrr = wave_sum_t(mrr); ysum = wave_sum_t(ysum);
   auc2 = wave_sum_t(auc2); npos = wave_sum_t(npos); nneg = wave_sum_t(nneg); nonbin = wave_sum_t(nonbin);
   for (int q = 0; q < nk; ++q) { dcg[q] = wave_sum_t(dcg[q]); idcg[q] = wave_sum_t(idcg[q]); hit[q] = wave_sum_t(hit[q]); }
   if (lane == 0) {
-    s_red[w][0] = mrr; s_red[w][1] = ysum;
-    for (int q = 0; q < nk; ++q) { s_red[w][2 + q] = dcg[q]; s_red[w][2 + nk + q] = idcg[q]; s_red[w][2 + 2 * nk + q] = hit[q]; }
-    s_cnt[w][0] = auc2; s_cnt[w][1] = npos; s_cnt[w][2] = nneg; s_cnt[w][3] = nonbin;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int nw = blockDim.x >> 6;
-    double r[2 + 3 * NR_METRIC_MAX_K];
-    unsigned long long c[4] = {0, 0, 0, 0};
-    for (int t = 0; t < 2 + 3 * nk; ++t) r[t] = 0.0;
-    for (int v = 0; v < nw; ++v) {
-      for (int t = 0; t < 2 + 3 * nk; ++t) r[t] += s_red[v][t];
-      for (int t = 0; t < 4; ++t) c[t] += s_cnt[v][t];
-    }
     const int W = 2 + 2 * nk;
     double* o = out + g * W;
     int32_t f = 0;
     const double nanv = __builtin_nan("");
-    if (c[3]) f |= NR_METRIC_NONBINARY;
-    if (c[1] == 0 || c[2] == 0) f |= NR_METRIC_ONE_CLASS;
+    if (nonbin) f |= NR_METRIC_NONBINARY;
+    if (npos == 0 || nneg == 0) f |= NR_METRIC_ONE_CLASS;
     o[0] = (f & (NR_METRIC_NONBINARY | NR_METRIC_ONE_CLASS)) ? nanv
-           : (double)c[0] / (2.0 * (double)c[1] * (double)c[2]);
-    o[1] = r[0] / r[1];                                   // 0 / 0 -> nan as numpy
+           : (double)auc2 / (2.0 * (double)npos * (double)nneg);
+    o[1] = mrr / ysum;                                    // 0 / 0 -> nan as numpy
     for (int q = 0; q < nk; ++q) {
-      o[2 + q] = r[2 + q] / r[2 + nk + q];
-      o[2 + nk + q] = r[2 + 2 * nk + q] > 0.0 ? 1.0 : 0.0;
+      o[2 + q] = dcg[q] / idcg[q];
+      o[2 + nk + q] = hit[q] > 0.0 ? 1.0 : 0.0;
     }
     flags[g] = f;
   }
@@ -426,8 +409,8 @@ extern "C" int nr_impression_metrics(const float* preds, const int32_t* labels, 
   if (G < 0 || nk < 0 || nk > NR_METRIC_MAX_K) return NR_EINVAL(0);
   if (!preds || !labels || !grp_off || !out || !flags || (nk > 0 && !ks)) return NR_EINVAL(1);
   if (G == 0) return NR_OK;
-  if (G > 0x7FFFFFFF) return NR_EINVAL(2);
-  hipLaunchKernelGGL(metrics_kernel, dim3((unsigned)G), dim3(256), 0, stream, preds, labels, grp_off, G, ks, nk,
+  if ((G + 3) / 4 > 0x7FFFFFFF) return NR_EINVAL(2);
+  hipLaunchKernelGGL(metrics_kernel, dim3((unsigned)((G + 3) / 4)), dim3(256), 0, stream, preds, labels, grp_off, G, ks, nk,
                      out, flags);
   NR_LAUNCH_CHECK();
   return NR_OK;

@@ -46,7 +46,7 @@ _SIGS = {
     "nr_segment_rows_sum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
                             c_ptr],
     "nr_segment_rows_sum_workspace": [c_i64, c_i64],
-    "nr_mha_attn_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
+    "nr_mha_attn_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
                         c_f32, c_ptr, c_i64, c_ptr],
     "nr_mha_attn_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
                         c_f32, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr],

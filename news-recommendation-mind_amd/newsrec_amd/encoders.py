@@ -207,6 +207,31 @@ class MHA_User_Encoder(nn.Module):
                         self.mha.value_dim)
         return AttnPoolFn.apply(h, self.query_news, mask, B, N).unsqueeze(1)
 
+    @torch.no_grad()
+    def project_rows(self, x):
+        """keyProject / valueProject (Attention.py:107-108) of every row of x [R, H] ->
+        [R, heads*(dk+dv)].  Fast eval projects the news table once; forward_rows gathers."""
+        from . import kernels as K
+        w, b = self.mha.fused_weight()
+        x = x if x.stride(-1) == 1 and x.stride(0) % 4 == 0 else x.contiguous()
+        Y = torch.empty(x.shape[0], w.shape[0], device=x.device)
+        K.gemm(x.shape[0], w.shape[0], x.shape[1], K.operand(x, L.KCONTIG), K.operand(w, L.KCONTIG), Y, bias=b)
+        return Y
+
+    @torch.no_grad()
+    def forward_rows(self, Y, rows, his_mask, B, N):
+        """forward() (eval, no autograd) with the projections precomputed per distinct news:
+        history slot t reads Y[rows[t]] inside the attention kernel.  Same per-row GEMM, so the
+        result equals forward(table[rows])."""
+        from . import kernels as K
+        mha = self.mha
+        mask = _his_mask_rows(his_mask, B, N, Y.device)
+        NQ = mha.head_num * mha.key_dim
+        O = torch.empty(B * N, mha.head_num * mha.value_dim, device=Y.device)
+        K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:], mask, B, N, mha.head_num, mha.key_dim, mha.value_dim, O,
+                       rows=rows.reshape(-1).contiguous())
+        return AttnPoolFn.apply(O, self.query_news, mask, B, N).unsqueeze(1)
+
 
 class RNN_User_Encoder(nn.Module):
     """models/Encoders/RNN.py:36-73 (LSTM or GRU, packed by the history length)."""

@@ -99,20 +99,37 @@ def score_ragged(table, user, cand_ids, cand_seg, seg_base, out=None, mode=L.SCO
 
 
 @torch.no_grad()
-def predict_fast_batch(model, batch, history_from_table=True):
+def user_reprs(model, table, batch, history_from_table=True, cache=None):
+    """User representations [B, H] of a MINDStore.eval_batch.  history_from_table: the history
+    news representations are the table's rows; an MHA user encoder then reads its key / value
+    projections of the TABLE (computed once per table, kept in ``cache``) through the attention
+    kernel's row indirection instead of projecting B*N gathered rows."""
+    if not history_from_table:
+        user = model.encode_user(batch)[0]
+    else:
+        enc = model.encoderU
+        B, NH = batch["his_id"].shape
+        if hasattr(enc, "forward_rows"):
+            cache = {} if cache is None else cache
+            if cache.get("Y") is None:
+                cache["Y"] = enc.project_rows(table)
+            user = enc.forward_rows(cache["Y"], batch["his_id"], batch["his_mask"], B, NH)
+        else:
+            his = table.index_select(0, batch["his_id"].reshape(-1)).view(B, NH, -1)
+            user = model._user_from_his(his, batch)
+    user = user.reshape(user.shape[0], -1)
+    if user.stride(-1) != 1 or user.stride(0) != user.shape[1]:
+        user = user.contiguous()
+    return user
+
+
+@torch.no_grad()
+def predict_fast_batch(model, batch, history_from_table=True, cache=None):
     """TwoTowerBaseModel.predict_fast (:78-83) for a batch of impression chunks from
     MINDStore.eval_batch: user representations for the chunks, then the ragged scorer over all
     their candidates.  -> sigmoid scores [n] aligned with batch["cdd_id"]."""
     table = model.news_reprs.weight
-    if history_from_table:
-        B, NH = batch["his_id"].shape
-        his = table.index_select(0, batch["his_id"].reshape(-1)).view(B, NH, -1)
-        user = model._user_from_his(his, batch)
-    else:
-        user = model.encode_user(batch)[0]
-    user = user.reshape(user.shape[0], -1)
-    if user.stride(-1) != 1 or user.stride(0) != user.shape[1]:
-        user = user.contiguous()
+    user = user_reprs(model, table, batch, history_from_table, cache)
     preds, _ = score_ragged(table, user, batch["cdd_id"], batch["cand_seg"], batch["chunk0"])
     return preds
 
@@ -130,11 +147,14 @@ def eval_fast(model, store, batch_impr=1024, group=None, history_from_table=True
     c_lo, c_hi = _chunk_range(len(store), world, rank)
     o_lo, o_hi = int(store.cand_off_host[c_lo]), int(store.cand_off_host[c_hi])
     preds = torch.empty(o_hi - o_lo, dtype=torch.float32, device=store.device)
+    cache = {}
     for c0 in range(c_lo, c_hi, batch_impr):
         b = min(batch_impr, c_hi - c0)
         x = store.eval_batch(c0, b, with_tokens=not history_from_table)
         o0, o1 = x["cand_range"]
-        preds[o0 - o_lo:o1 - o_lo] = predict_fast_batch(model, x, history_from_table)
+        table = model.news_reprs.weight
+        user = user_reprs(model, table, x, history_from_table, cache)
+        score_ragged(table, user, x["cdd_id"], x["cand_seg"], c0, out=preds[o0 - o_lo:o1 - o_lo])
     model.destroy_embedding()
     model.train(was_training)
     if world > 1:

@@ -137,17 +137,24 @@ def _cols(t, need, name):
         raise L.HipError("%s: needs %d columns, has %d" % (name, need, t.shape[1]))
 
 
-def mha_attn_fwd(qk, v, mask, nseq, seq_len, heads, dk, dv, out):
+def mha_attn_fwd(qk, v, mask, nseq, seq_len, heads, dk, dv, out, rows=None):
     """Tied-QK multi-head attention core (Attention.py:115-147).  qk: [nseq*L, >=heads*dk]
-    (column views allowed), v: [nseq*L, >=heads*dv], mask: [nseq, L], out: [nseq*L, heads*dv]."""
+    (column views allowed), v: [nseq*L, >=heads*dv], mask: [nseq, L], out: [nseq*L, heads*dv].
+    rows (int64 [nseq*L], optional): token t reads qk / v row rows[t] (values < qk.shape[0])."""
     _f32(qk, v, out)
     for t, need, n in ((qk, heads * dk, "qk"), (v, heads * dv, "v"), (out, heads * dv, "out")):
         _cols(t, need, n)
-        if t.shape[0] != nseq * seq_len:
+        if rows is None and t.shape[0] != nseq * seq_len:
             raise L.HipError("%s has %d rows, expected %d" % (n, t.shape[0], nseq * seq_len))
+    if out.shape[0] != nseq * seq_len:
+        raise L.HipError("out has %d rows, expected %d" % (out.shape[0], nseq * seq_len))
+    if rows is not None:
+        _check_rows(rows, None, "rows")
+        if rows.numel() != nseq * seq_len or qk.shape[0] != v.shape[0]:
+            raise L.HipError("rows must hold nseq*L entries over qk / v of equal height")
     mp, mdt = mask_arg(mask, nseq * seq_len)
-    L.call("nr_mha_attn_fwd", L.ptr(qk), qk.stride(0), L.ptr(v), v.stride(0), mp, mdt, nseq, seq_len,
-           heads, dk, dv, 1.0 / float(dk) ** 0.5, L.ptr(out), out.stride(0), L.stream_ptr(out))
+    L.call("nr_mha_attn_fwd", L.ptr(qk), qk.stride(0), L.ptr(v), v.stride(0), L.ptr(rows), mp, mdt, nseq,
+           seq_len, heads, dk, dv, 1.0 / float(dk) ** 0.5, L.ptr(out), out.stride(0), L.stream_ptr(out))
 
 
 def mha_attn_bwd(qk, v, mask, nseq, seq_len, heads, dk, dv, dout, dqk, dvv):

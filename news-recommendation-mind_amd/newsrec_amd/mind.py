@@ -206,9 +206,14 @@ class MINDStore:
                 m for b, m in ((1, "sample index out of range"), (2, "news id out of range"),
                                (4, "candidate/user row out of range")) if s & b))
 
-    def train_batch(self, sample_idx):
+    def train_batch(self, sample_idx, out=None, device_rng=False):
         """Collated MIND.__getitem__ train outputs for the samples sample_idx (int64 [B],
-        device or host)."""
+        device or host).
+
+        out: a dict from an earlier call to fill in place (a captured graph's static inputs).
+        device_rng: draw from the device-resident (seed, offset) pair ``rng_state`` and advance
+        it on the device (graph-capturable: every replay draws fresh negatives) instead of the
+        host-side offset."""
         if self.mode != "train":
             raise ValueError("train_batch on a %s split" % self.mode)
         dev = self.device
@@ -219,23 +224,35 @@ class MINDStore:
             idx = idx.to(dev, non_blocking=True)
         idx = idx.contiguous()
         B, C, NH, Ls = idx.numel(), self.npratio + 1, self.his_size, self.signal_length
-        i64 = dict(dtype=torch.int64, device=dev)
-        x = {"user_id": torch.empty(B, **i64), "cdd_id": torch.empty(B, C, **i64),
-             "his_id": torch.empty(B, NH, **i64),
-             "cdd_encoded_index": torch.empty(B, C, Ls, **i64), "his_encoded_index": torch.empty(B, NH, Ls, **i64),
-             "cdd_attn_mask": torch.empty(B, C, Ls, **i64), "his_attn_mask": torch.empty(B, NH, Ls, **i64),
-             "cdd_mask": torch.empty(B, C, 1, dtype=torch.float64, device=dev),
-             "his_mask": torch.empty(B, NH, 1, dtype=torch.float64, device=dev),
-             "label": torch.empty(B, **i64)}
+        shapes = {"user_id": ((B,), torch.int64), "cdd_id": ((B, C), torch.int64), "his_id": ((B, NH), torch.int64),
+                  "cdd_encoded_index": ((B, C, Ls), torch.int64), "his_encoded_index": ((B, NH, Ls), torch.int64),
+                  "cdd_attn_mask": ((B, C, Ls), torch.int64), "his_attn_mask": ((B, NH, Ls), torch.int64),
+                  "cdd_mask": ((B, C, 1), torch.float64), "his_mask": ((B, NH, 1), torch.float64),
+                  "label": ((B,), torch.int64)}
+        if out is None:
+            x = {k: torch.empty(sh, dtype=dt, device=dev) for k, (sh, dt) in shapes.items()}
+        else:
+            x = out
+            for k, (sh, dt) in shapes.items():
+                t = x[k]
+                if tuple(t.shape) != sh or t.dtype != dt or not t.is_contiguous() or t.device != dev:
+                    raise ValueError("out[%r]: expected contiguous %s %s on %s" % (k, sh, dt, dev))
+        rng = None
+        if device_rng:
+            if getattr(self, "rng_state", None) is None:
+                self.rng_state = torch.tensor([self.seed, self.offset], dtype=torch.int64, device=dev)
+            rng = self.rng_state
         seed, off = self.seed, self.offset
         self.offset += B * 4 * C
         P = L.ptr
         L.call("nr_form_train_batch", P(idx), B, P(self.imprs), self.n_samples, P(self.his_off), P(self.his_ids),
                P(self.neg_off), P(self.neg_ids), P(self.uindex), P(self.tok), P(self.attn), self.n_news, Ls,
-               self.npratio, NH, self.flags, seed, off, None, P(x["cdd_id"]), P(x["his_id"]),
+               self.npratio, NH, self.flags, seed, off, P(rng), P(x["cdd_id"]), P(x["his_id"]),
                P(x["cdd_encoded_index"]), P(x["cdd_attn_mask"]), P(x["his_encoded_index"]), P(x["his_attn_mask"]),
                P(x["cdd_mask"]), P(x["his_mask"]), P(x["user_id"]), P(x["label"]), P(self.status),
                L.stream_ptr(idx))
+        if rng is not None:
+            rng[1:].add_(B * 4 * C)
         return x
 
     def eval_batch(self, chunk0, n_chunks, with_tokens=False):
@@ -322,3 +339,45 @@ class DeviceLoader:
             for s in range(0, stop, self.batch_size):
                 c0 = idx[s]
                 yield self.store.eval_batch(c0, min(self.batch_size, stop - s))
+
+
+def synthetic_arrays(mode, n_news, n_impr, his_len=(50, 100), neg_len=(4, 60), cand_len=(2, 75),
+                     signal_length=30, vocab=30522, users=876956, full_titles=True, seed=0):
+    """MIND-shaped synthetic split as ``MINDStore.from_arrays`` input: token ids
+    U[1000, vocab) with [CLS]=101 first and [SEP]=102 at the last real position (all positions
+    real when full_titles), row 0 = the padded "" news; histories / negatives / candidate lists
+    with lengths drawn from the given ranges; dev chunks get at least one click each."""
+    rng = np.random.default_rng(seed)
+    Ls = signal_length
+    tok = rng.integers(1000, vocab, (n_news, Ls), dtype=np.int64)
+    lens = np.full(n_news, Ls) if full_titles else rng.integers(5, Ls + 1, n_news)
+    msk = (np.arange(Ls)[None] < lens[:, None]).astype(np.int64)
+    tok *= msk
+    tok[:, 0] = 101
+    tok[np.arange(n_news), lens - 1] = 102
+    tok[0], msk[0] = 0, 0
+    tok[0, :2], msk[0, :2] = (101, 102), 1
+
+    def csr(lo_hi, n):
+        ln = rng.integers(lo_hi[0], lo_hi[1] + 1, n)
+        off = np.zeros(n + 1, np.int64)
+        off[1:] = np.cumsum(ln)
+        return off, rng.integers(1, n_news, int(off[-1]))
+
+    a = {"tok": tok, "attn": msk, "uindex": rng.integers(1, users + 1, n_impr)}
+    a["his_off"], a["his_ids"] = csr(his_len, n_impr)
+    if mode == "train":
+        a["neg_off"], a["neg_ids"] = csr(neg_len, n_impr)
+        a["imprs"] = np.stack([np.arange(n_impr), rng.integers(1, n_news, n_impr)], 1)
+    else:
+        a["chunk_impr"] = np.arange(n_impr)
+        a["cand_off"], a["cand_ids"] = csr(cand_len, n_impr)
+        if mode == "dev":
+            lab = (rng.random(int(a["cand_off"][-1])) < 0.04).astype(np.int64)
+            first = a["cand_off"][:-1] + rng.integers(0, np.diff(a["cand_off"]))
+            lab[first] = 1
+            off = a["cand_off"]
+            full = np.flatnonzero(np.add.reduceat(lab, off[:-1]) == np.diff(off))   # keep one unclicked
+            lab[off[full] + (first[full] - off[full] + 1) % (off[full + 1] - off[full])] = 0
+            a["cand_labels"] = lab
+    return a

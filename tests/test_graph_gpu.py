@@ -50,7 +50,7 @@ def test_graph_replay_matches_eager():
     # GraphedStep runs max(2, warmup) eager warm-up steps on batches 0, 1 before capturing
     for i in range(2):
         bench.train_step(m_eager, o_eager, batches[i], None)
-    g = bench.GraphedStep(m_graph, o_graph, batches, None, 2)
+    g = bench.GraphedStep(m_graph, o_graph, bench.ResidentFeed(batches), None, 2)
     for i in range(2, 4):
         bench.train_step(m_eager, o_eager, batches[i], None)
         g(i)

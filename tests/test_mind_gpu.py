@@ -218,7 +218,8 @@ def test_fast_eval_matches_model(data, encN, encU, H):
     p_table = predict_fast_batch(model, x, history_from_table=True)
     p_enc = predict_fast_batch(model, x, history_from_table=False)
     torch.testing.assert_close(p_table, p_enc, rtol=0, atol=1e-6)
-    user, _ = model.encode_user(x)
+    with torch.no_grad():
+        user, _ = model.encode_user(x)
     want = R.score_ragged(table.double().cpu(), user.reshape(len(st), -1).double().cpu(), x["cdd_id"].cpu(),
                           x["cand_seg"].cpu().long(), 0)
     np.testing.assert_allclose(p_enc.cpu().numpy(), want.numpy(), rtol=0, atol=1e-6)
@@ -231,3 +232,20 @@ def test_fast_eval_matches_model(data, encN, encU, H):
     gl = [ll[go[g]:go[g + 1]] for g in range(len(go) - 1)]
     gp = [pl[go[g]:go[g + 1]] for g in range(len(go) - 1)]
     assert res == R.cal_metric(gl, gp, ["auc", "mean_mrr", "ndcg@5;10"])
+
+
+def test_user_forward_rows_matches_forward():
+    """MHA_User_Encoder.forward_rows (table projected once, rows gathered inside the attention
+    kernel) equals forward() on the gathered history representations."""
+    model = _small_model()
+    g = torch.Generator().manual_seed(3)
+    table = torch.randn(300, 384, generator=g).to(DEV)
+    his_id = torch.randint(0, 300, (9, 50), generator=g).to(DEV)
+    hm = (torch.arange(50)[None] < torch.tensor([0, 1, 7, 50, 49, 23, 2, 50, 11])[:, None]).double()
+    hm[0, 0] = 1.0
+    hm = hm.unsqueeze(-1).to(DEV)
+    enc = model.encoderU
+    with torch.no_grad():
+        want = enc(table[his_id], his_mask=hm)
+        got = enc.forward_rows(enc.project_rows(table), his_id, hm, 9, 50)
+    torch.testing.assert_close(got, want, rtol=0, atol=1e-6)
