@@ -29,7 +29,7 @@ def regen_params(names_shapes, seed):
     for i, (name, shape) in enumerate(names_shapes):
         rng = np.random.default_rng([int(seed), i])
         z = rng.standard_normal(shape, dtype=np.float32)
-        if "layerNorm.weight" in name:
+        if "layerNorm.weight" in name or "LayerNorm.weight" in name:
             v = 1.0 + 0.1 * z
         else:
             v = z * np.float32(param_std(name, shape))

@@ -12,6 +12,9 @@ CONFIG_ENCODERS = {
     "cnn_attn": ("cnn", "attn"), "cnn_avg": ("cnn", "avg"), "cnn_lstm": ("cnn", "lstm"),
     "cnn_gru": ("cnn", "gru"), "cnn_lstur": ("cnn", "lstur"), "nrms": ("mha", "mha"),
 }
+# BERT-tower goldens (tests/golden/make_bert_golden.py): XFormer (one-tower user sequence) and
+# PLM (bert branch) with an Attention_Pooling user encoder.
+BERT_CONFIGS = {"xformer": ("bert", "xformer"), "plm": ("bert", "attn")}
 
 
 class Golden:
@@ -22,7 +25,8 @@ class Golden:
         self.names = [k[len("grad."):] for k in z.files if k.startswith("grad.")]
         shapes = [(n, self.z["grad." + n].shape) for n in self.names]
         self.params = regen_params(shapes, int(self.z["meta.seed"]))
-        self.encN, self.encU = CONFIG_ENCODERS[name]
+        self.encN, self.encU = {**CONFIG_ENCODERS, **BERT_CONFIGS}[name]
+        self.heads = int(self.z["meta.heads"]) if "meta.heads" in self.z else 12
         self.hidden = int(self.z["meta.hidden_dim"])
         for n in self.names:
             p = self.params[n].astype(np.float64)
