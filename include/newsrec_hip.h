@@ -62,8 +62,12 @@ enum nr_epilogue {
   NR_EPI_ACCUM_GATE = 5, /* C[m][n] = aux[m][n] > 0 ? C[m][n] + acc : 0, aux = c_rows->data
                             (ld c_rows->ld): adds a second gradient path, then ReLU's mask   */
   NR_EPI_ACCUM = 6,      /* C[m][n] += acc + bias[n]  (row tiles are block-exclusive)         */
-  NR_EPI_SCATTER_STORE = 7 /* C[c_rows(m)][n] = acc for DISTINCT GATHER rows (pad_row skipped):
+  NR_EPI_SCATTER_STORE = 7, /* C[c_rows(m)][n] = acc for DISTINCT GATHER rows (pad_row skipped):
                             the table gradient over nr_unique_rows' ids, plain vector stores */
+  NR_EPI_STORE_GELU = 8, /* aux[m][n] = acc + bias[n]; C[m][n] = gelu(aux[m][n]) (exact erf GELU,
+                            BertIntermediate); aux = c_rows->data, ld c_rows->ld               */
+  NR_EPI_GELU_GRAD = 9   /* C[m][n] = acc * gelu'(aux[m][n]), aux = c_rows->data (ld c_rows->ld):
+                            the dgrad of the intermediate dense through its GELU               */
 };
 
 /* C (op)= A(m,k) * B(k,n) over k in [0,K), fp32 on the f32-input MFMA.
@@ -329,6 +333,71 @@ enum nr_metric_flags { NR_METRIC_ONE_CLASS = 1, NR_METRIC_NONBINARY = 2 };
 int nr_impression_metrics(const float* preds, const int32_t* labels, const int64_t* grp_off,
                           int64_t G, const int32_t* ks, int32_t nk, double* out, int32_t* flags,
                           hipStream_t stream);
+
+/* ---------------------------------------------------------------- BERT towers (XFormer / PLM)
+ * transformers BertModel as models/XFormer.py:68,94 and models/PLM.py:102,121 call it (token
+ * type ids never passed: every token takes token_type_embeddings row 0).  The dense layers are
+ * nr_gemm_f32 calls (QKV, attention output, intermediate with NR_EPI_STORE_GELU, output, pooler
+ * with NR_EPI_STORE_TANH over the [CLS] rows); the entries below are the code between them.
+ * H % 4 == 0, H <= 1024; rows are float4-aligned.  Dropout uses the counter RNG of the other
+ * fused kernels ((seed, offset), or the device pair rng with offset added). */
+
+/* out[s*L+l] = Dropout_p(LayerNorm_eps(word[ids[s*L+l]] + pos[l] + type0)); saves stats [T][2]
+ * = (mean, rstd).  BertEmbeddings.forward.  status (optional): |= 2 on an id outside [0, V). */
+int nr_bert_embed_fwd(const float* word, int64_t V, const float* pos, int64_t P, const float* type0,
+                      const int64_t* ids, int64_t nseq, int32_t L, int32_t H, const float* gamma,
+                      const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset,
+                      const uint64_t* rng, float* out, int64_t ldo, float* stats, int32_t* status,
+                      hipStream_t stream);
+
+/* Backward of nr_bert_embed_fwd up to the LayerNorm input: ds [T][H] = dL/d(word+pos+type) (the
+ * table gradients are then nr_embedding_bwd / nr_colsum of ds); ATOMICALLY ACCUMULATES dgamma,
+ * dbeta (caller zeroes). */
+int nr_bert_embed_bwd(const float* word, int64_t V, const float* pos, const float* type0,
+                      const int64_t* ids, int64_t nseq, int32_t L, int32_t H, const float* gamma,
+                      float p_drop, uint64_t seed, uint64_t offset, const uint64_t* rng,
+                      const float* stats, const float* dout, int64_t ldd, float* ds, int64_t ldds,
+                      float* dgamma, float* dbeta, hipStream_t stream);
+
+/* out = LayerNorm_eps(Dropout_p(x) + res): BertSelfOutput / BertOutput (x = the dense output with
+ * its bias).  Saves stats [T][2]. */
+int nr_bert_add_ln_fwd(const float* x, int64_t ldx, const float* res, int64_t ldr, int64_t T, int32_t H,
+                       const float* gamma, const float* beta, float eps, float p_drop, uint64_t seed,
+                       uint64_t offset, const uint64_t* rng, float* out, int64_t ldo, float* stats,
+                       hipStream_t stream);
+
+/* Backward of nr_bert_add_ln_fwd (recomputes the LayerNorm input): dres = dL/dres (STORED),
+ * dx = dL/dx (stored), dgamma / dbeta ATOMICALLY ACCUMULATED. */
+int nr_bert_add_ln_bwd(const float* x, int64_t ldx, const float* res, int64_t ldr, int64_t T, int32_t H,
+                       const float* gamma, float p_drop, uint64_t seed, uint64_t offset,
+                       const uint64_t* rng, const float* stats, const float* dout, int64_t ldd,
+                       float* dres, int64_t lddr, float* dx, int64_t lddx, float* dgamma, float* dbeta,
+                       hipStream_t stream);
+
+/* BertSelfAttention core for nseq sequences of L tokens (any L), heads of 64 dims:
+ *   ctx[s*L+i][h*64:] = Σ_j Dropout_p(softmax_j(q_i·k_j / 8 + (1 - m_j) * FLT_MIN_NEG)) v_j
+ * with q / k / v at columns h*64, koff + h*64, voff + h*64 of qkv rows (ld ldq).  Fully masked
+ * rows are uniform over the L keys (the additive-mask arithmetic).  Saves ml [T][heads][2] =
+ * (row max, 1 / row sum) for the backward.  mask: [nseq, L] of enum nr_mask_dtype. */
+int nr_bert_attn_fwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
+                     int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, float p_drop,
+                     uint64_t seed, uint64_t offset, const uint64_t* rng, float* ctx, int64_t ldc,
+                     float* ml, hipStream_t stream);
+
+/* Bytes of `work` nr_bert_attn_bwd needs. */
+int64_t nr_bert_attn_bwd_workspace(int64_t nseq, int32_t L, int32_t heads);
+
+/* Backward of nr_bert_attn_fwd: writes dQ, dK, dV into dqkv at the columns of qkv (every column
+ * of the 3 * heads * 64 block is stored).  Deterministic (no atomics). */
+int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
+                     int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, float p_drop,
+                     uint64_t seed, uint64_t offset, const uint64_t* rng, const float* ctx, int64_t ldc,
+                     const float* ml, const float* dctx, int64_t ldd, float* work, float* dqkv,
+                     int64_t lddq, hipStream_t stream);
+
+/* dx = dy * (1 - y^2): the pooler's tanh backward (BertPooler). */
+int nr_tanh_bwd(const float* y, int64_t ldy, const float* dy, int64_t lddy, int64_t rows, int32_t cols,
+                float* dx, int64_t lddx, hipStream_t stream);
 
 #ifdef __cplusplus
 }

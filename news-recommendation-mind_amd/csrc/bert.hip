@@ -1,0 +1,820 @@
+// BERT tower kernels (transformers BertModel as XFormer / PLM call it: models/XFormer.py:68,94,
+// models/PLM.py:102,121).  The dense layers run on nr_gemm_f32 (QKV, attention output,
+// intermediate with a fused GELU epilogue, output, pooler with a tanh epilogue); this file holds
+// everything between the GEMMs:
+//
+//   nr_bert_embed_fwd / _bwd   word + position + token-type rows -> LayerNorm -> dropout
+//   nr_bert_add_ln_fwd / _bwd  LayerNorm(dropout(dense) + residual)     (BertSelfOutput/BertOutput)
+//   nr_bert_attn_fwd           softmax(Q Kᵀ / 8 + additive key mask) -> dropout -> · V per
+//                              (sequence, head), online softmax, f32 MFMA, L <= any
+//   nr_bert_attn_bwd           dQ, dK, dV from the saved per-query (max, 1/sum)
+//   nr_tanh_bwd                pooler tanh backward
+//
+// Attention tiling (head dim 64).  A wave owns 32 rows (queries in the forward / dQ pass, keys
+// in the dK/dV pass); the workgroup's waves share LDS-staged 32-row tiles of the other side.
+// Scores are formed TRANSPOSED where the softmax statistics are per query: Sᵀ = K Qᵀ puts the
+// query on the lane (column of the 32x32 C tile), so a query's max / sum / rescale is lane-local
+// up to one swap of the two lane halves, and the accumulator tile is directly the B operand of
+// the next MFMA (Oᵀ = Vᵀ Pᵀ): k-step s of that product takes key kr(s, h) = 8(s>>2) + 4h + (s&3),
+// which is the row accumulator register s of lane half h holds.  The contraction over the 64
+// head dims uses dim 32h + s in k-step s (the order is free), so every operand fragment is 32
+// consecutive floats of one row.
+#include "common.h"
+#include "../../include/newsrec_hip.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr float kNegMax = -3.4028234663852886e38f;   // torch.finfo(float32).min
+constexpr int kHD = 64;                               // head dim
+constexpr int kLS = 68;                               // LDS row stride (floats)
+
+__device__ __forceinline__ float xhalf_sum(float v) {   // v(lane) + v(lane ^ 32)
+  const unsigned x = __builtin_bit_cast(unsigned, v);
+  auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+__device__ __forceinline__ float xhalf_max(float v) {
+  const unsigned x = __builtin_bit_cast(unsigned, v);
+  auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+// row of 32x32 C tile held by accumulator register r in lane half h
+__device__ __forceinline__ int crow(int r, int h) { return 8 * (r >> 2) + 4 * h + (r & 3); }
+
+// ------------------------------------------------------------------------------------ LayerNorm rows
+// One wave per row of H floats (H % 4 == 0, H <= 256 * NV); lane owns float4 chunks lane + 64 j.
+
+struct LnArgs {
+  // inputs of the LayerNorm's argument s
+  const float* word; int64_t V; const float* pos; const float* type0; const int64_t* ids; int L;   // embed
+  const float* x; int64_t ldx; const float* res; int64_t ldr;                                      // add
+  int64_t T; int H;
+  const float* gamma; const float* beta; float eps;
+  float p; float pscale; uint32_t thresh; uint32_t key; const uint64_t* rng; uint64_t offset;
+  float* out; int64_t ldo; float* stats;   // stats written by the forward, read by the backward
+  // backward
+  const float* dout; int64_t ldd;
+  float* ds; int64_t ldds;     // embed: dL/ds ; add: dL/dres
+  float* dx; int64_t lddx;     // add: dL/d(dense)
+  float* dgamma; float* dbeta;
+  int32_t* status;
+};
+
+template <bool EMBED, int NV>
+__device__ __forceinline__ void load_s(const LnArgs& g, int64_t t, int lane, float4 (&v)[NV], uint32_t key) {
+  if (EMBED) {
+    int64_t id = g.ids[t];
+    if (id < 0 || id >= g.V) {
+      if (g.status && lane == 0) atomicOr(g.status, 2);
+      id = 0;
+    }
+    const int ps = (int)(t % g.L);
+    const float* w = g.word + id * g.H;
+    const float* pp = g.pos + (int64_t)ps * g.H;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      if (c < g.H) {
+        const float4 a = ld4(w + c), b = ld4(pp + c), e = ld4(g.type0 + c);
+        v[j] = make_float4(a.x + b.x + e.x, a.y + b.y + e.y, a.z + b.z + e.z, a.w + b.w + e.w);
+      } else {
+        v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  } else {
+    const float* xr = g.x + t * g.ldx;
+    const float* rr = g.res + t * g.ldr;
+    const uint32_t e0 = (uint32_t)(t * g.H);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      if (c < g.H) {
+        float4 a = ld4(xr + c);
+        const float4 b = ld4(rr + c);
+        if (g.p > 0.f) {
+          a.x = nr_dropout_keep(key, e0 + c, g.thresh) ? a.x * g.pscale : 0.f;
+          a.y = nr_dropout_keep(key, e0 + c + 1, g.thresh) ? a.y * g.pscale : 0.f;
+          a.z = nr_dropout_keep(key, e0 + c + 2, g.thresh) ? a.z * g.pscale : 0.f;
+          a.w = nr_dropout_keep(key, e0 + c + 3, g.thresh) ? a.w * g.pscale : 0.f;
+        }
+        v[j] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+      } else {
+        v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+}
+
+template <bool EMBED, int NV>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= g.T) return;
+  const uint32_t key = g.rng ? nr_dropout_key(g.rng[0], g.rng[1] + g.offset) : g.key;
+  float4 v[NV];
+  load_s<EMBED, NV>(g, t, lane, v, key);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) s += v[j].x + v[j].y + v[j].z + v[j].w;
+  const float invH = 1.f / (float)g.H;
+  const float mean = nr_wave_sum(s) * invH;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+    if (4 * (lane + 64 * j) < g.H) {
+      const float a = v[j].x - mean, b = v[j].y - mean, c = v[j].z - mean, d = v[j].w - mean;
+      q += a * a + b * b + c * c + d * d;
+    }
+  const float rstd = rsqrtf(nr_wave_sum(q) * invH + g.eps);
+  float* orow = g.out + t * g.ldo;
+  const uint32_t e0 = (uint32_t)(t * g.H);
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    if (c >= g.H) continue;
+    const float4 gm = ld4(g.gamma + c), bt = ld4(g.beta + c);
+    float4 y = make_float4((v[j].x - mean) * rstd * gm.x + bt.x, (v[j].y - mean) * rstd * gm.y + bt.y,
+                           (v[j].z - mean) * rstd * gm.z + bt.z, (v[j].w - mean) * rstd * gm.w + bt.w);
+    if (EMBED && g.p > 0.f) {   // BertEmbeddings.dropout after the LayerNorm
+      y.x = nr_dropout_keep(key, e0 + c, g.thresh) ? y.x * g.pscale : 0.f;
+      y.y = nr_dropout_keep(key, e0 + c + 1, g.thresh) ? y.y * g.pscale : 0.f;
+      y.z = nr_dropout_keep(key, e0 + c + 2, g.thresh) ? y.z * g.pscale : 0.f;
+      y.w = nr_dropout_keep(key, e0 + c + 3, g.thresh) ? y.w * g.pscale : 0.f;
+    }
+    st4(orow + c, y);
+  }
+  if (lane == 0) {
+    g.stats[2 * t] = mean;
+    g.stats[2 * t + 1] = rstd;
+  }
+}
+
+template <bool EMBED, int NV>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(LnArgs g) {
+  __shared__ float red[4][2][256 * NV];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t key = g.rng ? nr_dropout_key(g.rng[0], g.rng[1] + g.offset) : g.key;
+  float4 ag[NV], ab[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) ag[j] = ab[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float invH = 1.f / (float)g.H;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < g.T; t += (int64_t)gridDim.x * 4) {
+    float4 v[NV];
+    load_s<EMBED, NV>(g, t, lane, v, key);
+    const float mean = g.stats[2 * t], rstd = g.stats[2 * t + 1];
+    const float* drow = g.dout + t * g.ldd;
+    const uint32_t e0 = (uint32_t)(t * g.H);
+    float4 dy[NV], xh[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      if (c >= g.H) {
+        dy[j] = xh[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        continue;
+      }
+      float4 d = ld4(drow + c);
+      if (EMBED && g.p > 0.f) {
+        d.x = nr_dropout_keep(key, e0 + c, g.thresh) ? d.x * g.pscale : 0.f;
+        d.y = nr_dropout_keep(key, e0 + c + 1, g.thresh) ? d.y * g.pscale : 0.f;
+        d.z = nr_dropout_keep(key, e0 + c + 2, g.thresh) ? d.z * g.pscale : 0.f;
+        d.w = nr_dropout_keep(key, e0 + c + 3, g.thresh) ? d.w * g.pscale : 0.f;
+      }
+      dy[j] = d;
+      xh[j] = make_float4((v[j].x - mean) * rstd, (v[j].y - mean) * rstd, (v[j].z - mean) * rstd,
+                          (v[j].w - mean) * rstd);
+      const float4 gm = ld4(g.gamma + c);
+      const float4 dh = make_float4(d.x * gm.x, d.y * gm.y, d.z * gm.z, d.w * gm.w);
+      s1 += dh.x + dh.y + dh.z + dh.w;
+      s2 += dh.x * xh[j].x + dh.y * xh[j].y + dh.z * xh[j].z + dh.w * xh[j].w;
+      ag[j].x += d.x * xh[j].x; ag[j].y += d.y * xh[j].y; ag[j].z += d.z * xh[j].z; ag[j].w += d.w * xh[j].w;
+      ab[j].x += d.x; ab[j].y += d.y; ab[j].z += d.z; ab[j].w += d.w;
+    }
+    const float m1 = nr_wave_sum(s1) * invH, m2 = nr_wave_sum(s2) * invH;
+    float* srow = g.ds + t * g.ldds;
+    float* xrow = EMBED ? nullptr : g.dx + t * g.lddx;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      if (c >= g.H) continue;
+      const float4 gm = ld4(g.gamma + c);
+      const float4 gs = make_float4(rstd * (dy[j].x * gm.x - m1 - xh[j].x * m2),
+                                    rstd * (dy[j].y * gm.y - m1 - xh[j].y * m2),
+                                    rstd * (dy[j].z * gm.z - m1 - xh[j].z * m2),
+                                    rstd * (dy[j].w * gm.w - m1 - xh[j].w * m2));
+      st4(srow + c, gs);
+      if (!EMBED) {   // d(dense) = dropout mask * scale * gs
+        float4 dx = gs;
+        if (g.p > 0.f) {
+          dx.x = nr_dropout_keep(key, e0 + c, g.thresh) ? dx.x * g.pscale : 0.f;
+          dx.y = nr_dropout_keep(key, e0 + c + 1, g.thresh) ? dx.y * g.pscale : 0.f;
+          dx.z = nr_dropout_keep(key, e0 + c + 2, g.thresh) ? dx.z * g.pscale : 0.f;
+          dx.w = nr_dropout_keep(key, e0 + c + 3, g.thresh) ? dx.w * g.pscale : 0.f;
+        }
+        st4(xrow + c, dx);
+      }
+    }
+  }
+  // dgamma / dbeta: per-wave partials -> LDS -> one atomic per column per workgroup
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    red[wave][0][c] = ag[j].x; red[wave][0][c + 1] = ag[j].y; red[wave][0][c + 2] = ag[j].z; red[wave][0][c + 3] = ag[j].w;
+    red[wave][1][c] = ab[j].x; red[wave][1][c + 1] = ab[j].y; red[wave][1][c + 2] = ab[j].z; red[wave][1][c + 3] = ab[j].w;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < g.H; c += 256) {
+    atomicAdd(g.dgamma + c, red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c]);
+    atomicAdd(g.dbeta + c, red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c]);
+  }
+}
+
+template <bool EMBED, bool BWD>
+int launch_ln(const LnArgs& g, hipStream_t s) {
+  if (g.T == 0) return NR_OK;
+  const int nv = (g.H + 255) / 256;
+  dim3 grid;
+  if (BWD) {
+    int64_t nb = (g.T + 3) / 4;
+    grid = dim3((unsigned)(nb < 1024 ? nb : 1024));
+  } else {
+    grid = dim3((unsigned)((g.T + 3) / 4));
+  }
+#define NR_LN(NV)                                                                                    \
+  if (nv == NV) {                                                                                    \
+    if (BWD) hipLaunchKernelGGL((ln_bwd_kernel<EMBED, NV>), grid, dim3(256), 0, s, g);               \
+    else hipLaunchKernelGGL((ln_fwd_kernel<EMBED, NV>), grid, dim3(256), 0, s, g);                   \
+  }
+  NR_LN(1) else NR_LN(2) else NR_LN(3) else NR_LN(4) else return NR_EINVAL(9);
+#undef NR_LN
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+void set_drop(LnArgs& g, float p, uint64_t seed, uint64_t offset, const uint64_t* rng) {
+  g.p = p;
+  g.pscale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  g.thresh = nr_dropout_threshold(p);
+  g.key = nr_dropout_key(seed, offset);
+  g.rng = rng;
+  g.offset = offset;
+}
+
+// ------------------------------------------------------------------------------------ attention
+
+struct AttnArgs {
+  const float* qkv; int64_t ldq; int64_t koff, voff;   // Q at col head*64, K at koff + head*64, V at voff + ...
+  const void* mask; int mdt;
+  int64_t nseq; int L; int heads; int chunks;
+  float p; float pscale; uint32_t thresh; uint32_t key; const uint64_t* rng; uint64_t offset;
+  float* ctx; int64_t ldc;          // fwd output
+  float* ml;                        // [T][heads][2] = (max, 1/sum) per query
+  const float* dctx; int64_t ldd;   // bwd: upstream grad of ctx
+  const float* Dq;                  // bwd: [T][heads] rowsum(dctx * ctx)
+  float* dqkv; int64_t lddq;        // bwd output (same column layout as qkv)
+};
+
+__device__ __forceinline__ uint32_t attn_key(const AttnArgs& g, int64_t seq, int head) {
+  const uint32_t k = g.rng ? nr_dropout_key(g.rng[0], g.rng[1] + g.offset) : g.key;
+  return nr_hash32(k ^ (uint32_t)((seq * g.heads + head) * 0x85EBCA6Bull));
+}
+
+// stage rows r0 .. r0+31 of two 64-wide column blocks into LDS (zeros beyond L)
+__device__ __forceinline__ void stage2(float (*A)[kLS], float (*B)[kLS], const float* base, int64_t ld, int64_t row0,
+                                       int r0, int L, int64_t ca, int64_t cb) {
+  for (int f = threadIdx.x; f < 512; f += blockDim.x) {
+    const int r = f >> 4, cc = (f & 15) * 4;
+    const int j = r0 + r;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (j < L) {
+      const float* p = base + (row0 + j) * ld;
+      a = ld4(p + ca + cc);
+      b = ld4(p + cb + cc);
+    }
+    st4(&A[r][cc], a);
+    st4(&B[r][cc], b);
+  }
+}
+
+template <bool DROP>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs g) {
+  __shared__ float Ks[32][kLS];
+  __shared__ float Vs[32][kLS];
+  __shared__ float kadd[32];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, hh = lane >> 5;
+  const int nw = blockDim.x >> 6;
+  int64_t bid = blockIdx.x;
+  const int qc = (int)(bid % g.chunks);
+  bid /= g.chunks;
+  const int head = (int)(bid % g.heads);
+  const int64_t seq = bid / g.heads;
+  const int L = g.L;
+  const int64_t row0 = seq * L;
+  const int q0 = (qc * nw + wave) * 32;
+  const bool active = q0 < L;
+  const int q = q0 + c;
+  const uint32_t dkey = DROP ? attn_key(g, seq, head) : 0u;
+
+  float qf[32];   // B operand of Sᵀ = K Qᵀ: Q[q][32 hh + s] / 8 (exact power-of-two scale)
+  if (active && q < L) {
+    const float* qp = g.qkv + (row0 + q) * g.ldq + head * kHD + 32 * hh;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 x = ld4(qp + 4 * j);
+      qf[4 * j] = x.x * 0.125f; qf[4 * j + 1] = x.y * 0.125f; qf[4 * j + 2] = x.z * 0.125f; qf[4 * j + 3] = x.w * 0.125f;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 32; ++j) qf[j] = 0.f;
+  }
+  f32x16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o0[r] = o1[r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int nkb = (L + 31) / 32;
+  for (int kb = 0; kb < nkb; ++kb) {
+    __syncthreads();
+    stage2(Ks, Vs, g.qkv, g.ldq, row0, kb * 32, L, g.koff + head * kHD, g.voff + head * kHD);
+    if (threadIdx.x < 32) {
+      const int j = kb * 32 + threadIdx.x;
+      kadd[threadIdx.x] = j >= L ? -INFINITY : (nr_mask_at(g.mask, g.mdt, row0 + j) ? 0.f : kNegMax);
+    }
+    __syncthreads();
+    if (!active) continue;
+    f32x16 s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 a = ld4(&Ks[c][32 * hh + 4 * j]);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, qf[4 * j], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, qf[4 * j + 1], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, qf[4 * j + 2], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, qf[4 * j + 3], s, 0, 0, 0);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[r] = s[r] + kadd[crow(r, hh)];
+      mx = fmaxf(mx, s[r]);
+    }
+    mx = xhalf_max(mx);
+    const float mn = fmaxf(m, mx);
+    const float alpha = __expf(m - mn);
+    float ps = 0.f;
+    float pe[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      pe[r] = __expf(s[r] - mn);
+      ps += pe[r];
+    }
+    ps = xhalf_sum(ps);
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      o0[r] *= alpha;
+      o1[r] *= alpha;
+    }
+    if (DROP) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t e = (uint32_t)q * (uint32_t)L + (uint32_t)(kb * 32 + crow(r, hh));
+        pe[r] = nr_dropout_keep(dkey, e, g.thresh) ? pe[r] * g.pscale : 0.f;
+      }
+    }
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int kr = crow(st, hh);
+      o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(Vs[kr][c], pe[st], o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(Vs[kr][32 + c], pe[st], o1, 0, 0, 0);
+    }
+  }
+  if (!active || q >= L) return;
+  const float inv = 1.f / l;
+  float* op = g.ctx + (row0 + q) * g.ldc + head * kHD;
+#pragma unroll
+  for (int gq = 0; gq < 4; ++gq) {
+    const int d = 8 * gq + 4 * hh;
+    st4(op + d, make_float4(o0[4 * gq] * inv, o0[4 * gq + 1] * inv, o0[4 * gq + 2] * inv, o0[4 * gq + 3] * inv));
+    st4(op + 32 + d, make_float4(o1[4 * gq] * inv, o1[4 * gq + 1] * inv, o1[4 * gq + 2] * inv, o1[4 * gq + 3] * inv));
+  }
+  if (hh == 0) {
+    float* mp = g.ml + ((row0 + q) * g.heads + head) * 2;
+    mp[0] = m;
+    mp[1] = inv;
+  }
+}
+
+// D[t][h] = Σ_d dctx[t][h*64+d] * ctx[t][h*64+d]   (one thread per (token, head))
+__global__ void __launch_bounds__(256) attn_dsum_kernel(const float* dctx, int64_t ldd, const float* ctx, int64_t ldc,
+                                                        int64_t T, int heads, float* D) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= T * heads) return;
+  const int64_t t = i / heads;
+  const int h = (int)(i - t * heads);
+  const float* a = dctx + t * ldd + h * kHD;
+  const float* b = ctx + t * ldc + h * kHD;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const float4 x = ld4(a + 4 * j), y = ld4(b + 4 * j);
+    s += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+  }
+  D[i] = s;
+}
+
+// dK, dV: a wave owns 32 keys; query tiles (Q, dctx, stats) staged in LDS.
+template <bool DROP>
+__global__ void __launch_bounds__(256) attn_bwd_kv_kernel(AttnArgs g) {
+  __shared__ float Qs[32][kLS];
+  __shared__ float Os[32][kLS];   // dctx tile
+  __shared__ float qm[32], qi[32], qd[32];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, hh = lane >> 5;
+  const int nw = blockDim.x >> 6;
+  int64_t bid = blockIdx.x;
+  const int kc = (int)(bid % g.chunks);
+  bid /= g.chunks;
+  const int head = (int)(bid % g.heads);
+  const int64_t seq = bid / g.heads;
+  const int L = g.L;
+  const int64_t row0 = seq * L;
+  const int k0 = (kc * nw + wave) * 32;
+  const bool active = k0 < L;
+  const int key = k0 + c;
+  const uint32_t dkey = DROP ? attn_key(g, seq, head) : 0u;
+
+  float kf[32], vf[32];
+  float kadd = -INFINITY;
+  if (active && key < L) {
+    const float* kp = g.qkv + (row0 + key) * g.ldq + g.koff + head * kHD + 32 * hh;
+    const float* vp = g.qkv + (row0 + key) * g.ldq + g.voff + head * kHD + 32 * hh;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 x = ld4(kp + 4 * j), y = ld4(vp + 4 * j);
+      kf[4 * j] = x.x * 0.125f; kf[4 * j + 1] = x.y * 0.125f; kf[4 * j + 2] = x.z * 0.125f; kf[4 * j + 3] = x.w * 0.125f;
+      vf[4 * j] = y.x; vf[4 * j + 1] = y.y; vf[4 * j + 2] = y.z; vf[4 * j + 3] = y.w;
+    }
+    kadd = nr_mask_at(g.mask, g.mdt, row0 + key) ? 0.f : kNegMax;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 32; ++j) kf[j] = vf[j] = 0.f;
+  }
+  f32x16 dk0, dk1, dv0, dv1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dk0[r] = dk1[r] = dv0[r] = dv1[r] = 0.f;
+  const int nqb = (L + 31) / 32;
+  for (int qb = 0; qb < nqb; ++qb) {
+    __syncthreads();
+    for (int f = threadIdx.x; f < 512; f += blockDim.x) {   // Q and dctx rows of the query tile
+      const int r = f >> 4, cc = (f & 15) * 4;
+      const int j = qb * 32 + r;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if (j < L) {
+        a = ld4(g.qkv + (row0 + j) * g.ldq + head * kHD + cc);
+        b = ld4(g.dctx + (row0 + j) * g.ldd + head * kHD + cc);
+      }
+      st4(&Qs[r][cc], a);
+      st4(&Os[r][cc], b);
+    }
+    if (threadIdx.x < 32) {
+      const int j = qb * 32 + threadIdx.x;
+      if (j < L) {
+        const float* mp = g.ml + ((row0 + j) * g.heads + head) * 2;
+        qm[threadIdx.x] = mp[0];
+        qi[threadIdx.x] = mp[1];
+        qd[threadIdx.x] = g.Dq[(row0 + j) * g.heads + head];
+      } else {
+        qm[threadIdx.x] = INFINITY;   // exp(s - inf) = 0: no such query
+        qi[threadIdx.x] = 0.f;
+        qd[threadIdx.x] = 0.f;
+      }
+    }
+    __syncthreads();
+    if (!active) continue;
+    f32x16 s, dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 a = ld4(&Qs[c][32 * hh + 4 * j]);
+      const float4 b = ld4(&Os[c][32 * hh + 4 * j]);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, kf[4 * j], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, kf[4 * j + 1], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, kf[4 * j + 2], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, kf[4 * j + 3], s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(b.x, vf[4 * j], dp, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(b.y, vf[4 * j + 1], dp, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(b.z, vf[4 * j + 2], dp, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(b.w, vf[4 * j + 3], dp, 0, 0, 0);
+    }
+    // S rows = queries crow(r, hh) of the tile, column = this lane's key
+    float pd[16], ds[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qr = crow(r, hh);
+      const float pr = __expf(s[r] + kadd - qm[qr]) * qi[qr];
+      float d = dp[r];
+      float pdr = pr;
+      if (DROP) {
+        const uint32_t e = (uint32_t)(qb * 32 + qr) * (uint32_t)L + (uint32_t)key;
+        const bool kp = nr_dropout_keep(dkey, e, g.thresh);
+        d = kp ? d * g.pscale : 0.f;
+        pdr = kp ? pr * g.pscale : 0.f;
+      }
+      pd[r] = pdr;
+      ds[r] = pr * (d - qd[qr]);
+    }
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int qr = crow(st, hh);
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x2f32(Os[qr][c], pd[st], dv0, 0, 0, 0);
+      dv1 = __builtin_amdgcn_mfma_f32_32x32x2f32(Os[qr][32 + c], pd[st], dv1, 0, 0, 0);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x2f32(Qs[qr][c], ds[st], dk0, 0, 0, 0);
+      dk1 = __builtin_amdgcn_mfma_f32_32x32x2f32(Qs[qr][32 + c], ds[st], dk1, 0, 0, 0);
+    }
+  }
+  if (!active || key >= L) return;
+  float* kp = g.dqkv + (row0 + key) * g.lddq + g.koff + head * kHD;
+  float* vp = g.dqkv + (row0 + key) * g.lddq + g.voff + head * kHD;
+#pragma unroll
+  for (int gq = 0; gq < 4; ++gq) {
+    const int d = 8 * gq + 4 * hh;
+    st4(kp + d, make_float4(dk0[4 * gq] * 0.125f, dk0[4 * gq + 1] * 0.125f, dk0[4 * gq + 2] * 0.125f,
+                            dk0[4 * gq + 3] * 0.125f));
+    st4(kp + 32 + d, make_float4(dk1[4 * gq] * 0.125f, dk1[4 * gq + 1] * 0.125f, dk1[4 * gq + 2] * 0.125f,
+                                 dk1[4 * gq + 3] * 0.125f));
+    st4(vp + d, make_float4(dv0[4 * gq], dv0[4 * gq + 1], dv0[4 * gq + 2], dv0[4 * gq + 3]));
+    st4(vp + 32 + d, make_float4(dv1[4 * gq], dv1[4 * gq + 1], dv1[4 * gq + 2], dv1[4 * gq + 3]));
+  }
+}
+
+// dQ: a wave owns 32 queries; key tiles staged in LDS; scores transposed (query on the lane).
+template <bool DROP>
+__global__ void __launch_bounds__(256) attn_bwd_q_kernel(AttnArgs g) {
+  __shared__ float Ks[32][kLS];
+  __shared__ float Vs[32][kLS];
+  __shared__ float kadd[32];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, hh = lane >> 5;
+  const int nw = blockDim.x >> 6;
+  int64_t bid = blockIdx.x;
+  const int qc = (int)(bid % g.chunks);
+  bid /= g.chunks;
+  const int head = (int)(bid % g.heads);
+  const int64_t seq = bid / g.heads;
+  const int L = g.L;
+  const int64_t row0 = seq * L;
+  const int q0 = (qc * nw + wave) * 32;
+  const bool active = q0 < L;
+  const int q = q0 + c;
+  const uint32_t dkey = DROP ? attn_key(g, seq, head) : 0u;
+
+  float qf[32], df[32];
+  float mq = INFINITY, iq = 0.f, dq = 0.f;
+  if (active && q < L) {
+    const float* qp = g.qkv + (row0 + q) * g.ldq + head * kHD + 32 * hh;
+    const float* op = g.dctx + (row0 + q) * g.ldd + head * kHD + 32 * hh;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 x = ld4(qp + 4 * j), y = ld4(op + 4 * j);
+      qf[4 * j] = x.x * 0.125f; qf[4 * j + 1] = x.y * 0.125f; qf[4 * j + 2] = x.z * 0.125f; qf[4 * j + 3] = x.w * 0.125f;
+      df[4 * j] = y.x; df[4 * j + 1] = y.y; df[4 * j + 2] = y.z; df[4 * j + 3] = y.w;
+    }
+    const float* mp = g.ml + ((row0 + q) * g.heads + head) * 2;
+    mq = mp[0];
+    iq = mp[1];
+    dq = g.Dq[(row0 + q) * g.heads + head];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 32; ++j) qf[j] = df[j] = 0.f;
+  }
+  f32x16 a0, a1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) a0[r] = a1[r] = 0.f;
+  const int nkb = (L + 31) / 32;
+  for (int kb = 0; kb < nkb; ++kb) {
+    __syncthreads();
+    stage2(Ks, Vs, g.qkv, g.ldq, row0, kb * 32, L, g.koff + head * kHD, g.voff + head * kHD);
+    if (threadIdx.x < 32) {
+      const int j = kb * 32 + threadIdx.x;
+      kadd[threadIdx.x] = j >= L ? -INFINITY : (nr_mask_at(g.mask, g.mdt, row0 + j) ? 0.f : kNegMax);
+    }
+    __syncthreads();
+    if (!active) continue;
+    f32x16 s, dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 a = ld4(&Ks[c][32 * hh + 4 * j]);
+      const float4 b = ld4(&Vs[c][32 * hh + 4 * j]);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, qf[4 * j], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, qf[4 * j + 1], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, qf[4 * j + 2], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, qf[4 * j + 3], s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(b.x, df[4 * j], dp, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(b.y, df[4 * j + 1], dp, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(b.z, df[4 * j + 2], dp, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x2f32(b.w, df[4 * j + 3], dp, 0, 0, 0);
+    }
+    float ds[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kr = crow(r, hh);
+      const float pr = __expf(s[r] + kadd[kr] - mq) * iq;
+      float d = dp[r];
+      if (DROP) {
+        const uint32_t e = (uint32_t)q * (uint32_t)L + (uint32_t)(kb * 32 + kr);
+        d = nr_dropout_keep(dkey, e, g.thresh) ? d * g.pscale : 0.f;
+      }
+      ds[r] = pr * (d - dq);
+    }
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int kr = crow(st, hh);
+      a0 = __builtin_amdgcn_mfma_f32_32x32x2f32(Ks[kr][c], ds[st], a0, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f32_32x32x2f32(Ks[kr][32 + c], ds[st], a1, 0, 0, 0);
+    }
+  }
+  if (!active || q >= L) return;
+  float* op = g.dqkv + (row0 + q) * g.lddq + head * kHD;
+#pragma unroll
+  for (int gq = 0; gq < 4; ++gq) {
+    const int d = 8 * gq + 4 * hh;
+    st4(op + d, make_float4(a0[4 * gq] * 0.125f, a0[4 * gq + 1] * 0.125f, a0[4 * gq + 2] * 0.125f,
+                            a0[4 * gq + 3] * 0.125f));
+    st4(op + 32 + d, make_float4(a1[4 * gq] * 0.125f, a1[4 * gq + 1] * 0.125f, a1[4 * gq + 2] * 0.125f,
+                                 a1[4 * gq + 3] * 0.125f));
+  }
+}
+
+__global__ void __launch_bounds__(256) tanh_bwd_kernel(const float* y, int64_t ldy, const float* dy, int64_t lddy,
+                                                       int64_t rows, int cols, float* dx, int64_t lddx) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * cols) return;
+  const int64_t r = i / cols;
+  const int c = (int)(i - r * cols);
+  const float v = y[r * ldy + c];
+  dx[r * lddx + c] = dy[r * lddy + c] * (1.f - v * v);
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int attn_setup(AttnArgs& g, const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
+               int32_t mdt, int64_t nseq, int32_t L, int32_t heads, float p, uint64_t seed, uint64_t offset,
+               const uint64_t* rng, float* ml) {
+  if (nseq < 0 || L <= 0 || heads <= 0) return NR_EINVAL(0);
+  if (!qkv || !mask || !ml) return NR_EINVAL(1);
+  if (!al16(qkv) || (ldq & 3) || (koff & 3) || (voff & 3)) return NR_EINVAL(2);
+  if (p < 0.f || p >= 1.f) return NR_EINVAL(3);
+  g.qkv = qkv; g.ldq = ldq; g.koff = koff; g.voff = voff; g.mask = mask; g.mdt = mdt;
+  g.nseq = nseq; g.L = L; g.heads = heads;
+  g.p = p; g.pscale = p > 0.f ? 1.f / (1.f - p) : 1.f; g.thresh = nr_dropout_threshold(p);
+  g.key = nr_dropout_key(seed, offset); g.rng = rng; g.offset = offset; g.ml = ml;
+  return NR_OK;
+}
+
+// waves per workgroup: enough to cover L with 32-row waves, at most 4
+int attn_waves(int L) {
+  const int w = (L + 31) / 32;
+  return w < 4 ? w : 4;
+}
+
+}  // namespace
+
+// ==================================================================================== C ABI
+
+extern "C" int nr_bert_embed_fwd(const float* word, int64_t V, const float* pos, int64_t P, const float* type0,
+                                 const int64_t* ids, int64_t nseq, int32_t L, int32_t H, const float* gamma,
+                                 const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset,
+                                 const uint64_t* rng, float* out, int64_t ldo, float* stats, int32_t* status,
+                                 hipStream_t stream) {
+  if (nseq < 0 || L <= 0 || H <= 0 || (H & 3) || H > 1024) return NR_EINVAL(0);
+  if (L > P) return NR_EINVAL(3);
+  if (!word || !pos || !type0 || !ids || !gamma || !beta || !out || !stats) return NR_EINVAL(1);
+  if (!al16(word) || !al16(pos) || !al16(type0) || !al16(out) || (ldo & 3)) return NR_EINVAL(2);
+  LnArgs g{};
+  g.word = word; g.V = V; g.pos = pos; g.type0 = type0; g.ids = ids; g.L = L;
+  g.T = nseq * L; g.H = H; g.gamma = gamma; g.beta = beta; g.eps = eps;
+  set_drop(g, p_drop, seed, offset, rng);
+  g.out = out; g.ldo = ldo; g.stats = stats; g.status = status;
+  return launch_ln<true, false>(g, stream);
+}
+
+extern "C" int nr_bert_embed_bwd(const float* word, int64_t V, const float* pos, const float* type0,
+                                 const int64_t* ids, int64_t nseq, int32_t L, int32_t H, const float* gamma,
+                                 float p_drop, uint64_t seed, uint64_t offset, const uint64_t* rng,
+                                 const float* stats, const float* dout, int64_t ldd, float* ds, int64_t ldds,
+                                 float* dgamma, float* dbeta, hipStream_t stream) {
+  if (nseq < 0 || L <= 0 || H <= 0 || (H & 3) || H > 1024) return NR_EINVAL(0);
+  if (!word || !pos || !type0 || !ids || !gamma || !stats || !dout || !ds || !dgamma || !dbeta) return NR_EINVAL(1);
+  if (!al16(dout) || !al16(ds) || (ldd & 3) || (ldds & 3)) return NR_EINVAL(2);
+  LnArgs g{};
+  g.word = word; g.V = V; g.pos = pos; g.type0 = type0; g.ids = ids; g.L = L;
+  g.T = nseq * L; g.H = H; g.gamma = gamma;
+  set_drop(g, p_drop, seed, offset, rng);
+  g.stats = const_cast<float*>(stats); g.dout = dout; g.ldd = ldd; g.ds = ds; g.ldds = ldds; g.dgamma = dgamma; g.dbeta = dbeta;
+  return launch_ln<true, true>(g, stream);
+}
+
+extern "C" int nr_bert_add_ln_fwd(const float* x, int64_t ldx, const float* res, int64_t ldr, int64_t T, int32_t H,
+                                  const float* gamma, const float* beta, float eps, float p_drop, uint64_t seed,
+                                  uint64_t offset, const uint64_t* rng, float* out, int64_t ldo, float* stats,
+                                  hipStream_t stream) {
+  if (T < 0 || H <= 0 || (H & 3) || H > 1024) return NR_EINVAL(0);
+  if (!x || !res || !gamma || !beta || !out || !stats) return NR_EINVAL(1);
+  if (!al16(x) || !al16(res) || !al16(out) || (ldx & 3) || (ldr & 3) || (ldo & 3)) return NR_EINVAL(2);
+  LnArgs g{};
+  g.x = x; g.ldx = ldx; g.res = res; g.ldr = ldr; g.T = T; g.H = H; g.gamma = gamma; g.beta = beta; g.eps = eps;
+  set_drop(g, p_drop, seed, offset, rng);
+  g.out = out; g.ldo = ldo; g.stats = stats;
+  return launch_ln<false, false>(g, stream);
+}
+
+extern "C" int nr_bert_add_ln_bwd(const float* x, int64_t ldx, const float* res, int64_t ldr, int64_t T, int32_t H,
+                                  const float* gamma, float p_drop, uint64_t seed, uint64_t offset,
+                                  const uint64_t* rng, const float* stats, const float* dout, int64_t ldd,
+                                  float* dres, int64_t lddr, float* dx, int64_t lddx, float* dgamma, float* dbeta,
+                                  hipStream_t stream) {
+  if (T < 0 || H <= 0 || (H & 3) || H > 1024) return NR_EINVAL(0);
+  if (!x || !res || !gamma || !stats || !dout || !dres || !dx || !dgamma || !dbeta) return NR_EINVAL(1);
+  if (!al16(x) || !al16(res) || !al16(dout) || !al16(dres) || !al16(dx) || ((ldx | ldr | ldd | lddr | lddx) & 3))
+    return NR_EINVAL(2);
+  LnArgs g{};
+  g.x = x; g.ldx = ldx; g.res = res; g.ldr = ldr; g.T = T; g.H = H; g.gamma = gamma;
+  set_drop(g, p_drop, seed, offset, rng);
+  g.stats = const_cast<float*>(stats); g.dout = dout; g.ldd = ldd; g.ds = dres; g.ldds = lddr; g.dx = dx; g.lddx = lddx;
+  g.dgamma = dgamma; g.dbeta = dbeta;
+  return launch_ln<false, true>(g, stream);
+}
+
+extern "C" int nr_bert_attn_fwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
+                                int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, float p_drop,
+                                uint64_t seed, uint64_t offset, const uint64_t* rng, float* ctx, int64_t ldc,
+                                float* ml, hipStream_t stream) {
+  AttnArgs g{};
+  int rc = attn_setup(g, qkv, ldq, koff, voff, mask, mask_dtype, nseq, L, heads, p_drop, seed, offset, rng, ml);
+  if (rc) return rc;
+  if (!ctx || !al16(ctx) || (ldc & 3)) return NR_EINVAL(4);
+  if (nseq == 0) return NR_OK;
+  g.ctx = ctx; g.ldc = ldc;
+  const int nw = attn_waves(L);
+  g.chunks = (L + 32 * nw - 1) / (32 * nw);
+  const dim3 grid((unsigned)(nseq * heads * g.chunks));
+  if (p_drop > 0.f) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(64 * nw), 0, stream, g);
+  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(64 * nw), 0, stream, g);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int64_t nr_bert_attn_bwd_workspace(int64_t nseq, int32_t L, int32_t heads) {
+  return nseq * (int64_t)L * heads * (int64_t)sizeof(float);
+}
+
+extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
+                                int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, float p_drop,
+                                uint64_t seed, uint64_t offset, const uint64_t* rng, const float* ctx, int64_t ldc,
+                                const float* ml, const float* dctx, int64_t ldd, float* work, float* dqkv,
+                                int64_t lddq, hipStream_t stream) {
+  AttnArgs g{};
+  int rc = attn_setup(g, qkv, ldq, koff, voff, mask, mask_dtype, nseq, L, heads, p_drop, seed, offset, rng,
+                      const_cast<float*>(ml));
+  if (rc) return rc;
+  if (!ctx || !dctx || !work || !dqkv) return NR_EINVAL(4);
+  if (!al16(ctx) || !al16(dctx) || !al16(dqkv) || ((ldc | ldd | lddq) & 3)) return NR_EINVAL(5);
+  if (nseq == 0) return NR_OK;
+  const int64_t T = nseq * L;
+  hipLaunchKernelGGL(attn_dsum_kernel, dim3((unsigned)((T * heads + 255) / 256)), dim3(256), 0, stream, dctx, ldd, ctx,
+                     ldc, T, heads, work);
+  NR_LAUNCH_CHECK();
+  g.dctx = dctx; g.ldd = ldd; g.Dq = work; g.dqkv = dqkv; g.lddq = lddq;
+  const int nw = attn_waves(L);
+  g.chunks = (L + 32 * nw - 1) / (32 * nw);
+  const dim3 grid((unsigned)(nseq * heads * g.chunks));
+  if (p_drop > 0.f) {
+    hipLaunchKernelGGL(attn_bwd_kv_kernel<true>, grid, dim3(64 * nw), 0, stream, g);
+    hipLaunchKernelGGL(attn_bwd_q_kernel<true>, grid, dim3(64 * nw), 0, stream, g);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_kv_kernel<false>, grid, dim3(64 * nw), 0, stream, g);
+    hipLaunchKernelGGL(attn_bwd_q_kernel<false>, grid, dim3(64 * nw), 0, stream, g);
+  }
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_tanh_bwd(const float* y, int64_t ldy, const float* dy, int64_t lddy, int64_t rows, int32_t cols,
+                           float* dx, int64_t lddx, hipStream_t stream) {
+  if (rows < 0 || cols < 0) return NR_EINVAL(0);
+  if (!y || !dy || !dx) return NR_EINVAL(1);
+  if (rows * cols == 0) return NR_OK;
+  hipLaunchKernelGGL(tanh_bwd_kernel, dim3((unsigned)((rows * cols + 255) / 256)), dim3(256), 0, stream, y, ldy, dy,
+                     lddy, rows, cols, dx, lddx);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}

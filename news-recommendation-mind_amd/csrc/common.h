@@ -107,3 +107,10 @@ __device__ __forceinline__ uint32_t nr_hash32(uint32_t x) {
 __device__ __forceinline__ bool nr_dropout_keep(uint32_t key, uint32_t elem, uint32_t thresh) {
   return nr_hash32(key + elem * 0x9E3779B1u) >= thresh;
 }
+
+// Exact (erf) GELU of transformers' "gelu" activation (BertIntermediate) and its derivative.
+__device__ __forceinline__ float nr_gelu(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float nr_gelu_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  return cdf + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}

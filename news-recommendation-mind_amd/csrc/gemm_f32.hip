@@ -214,7 +214,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(Args g) {
       const int64_t col = n0 + wn + 32 * j + (lane & 31);
       if (col >= g.N) continue;
       const float bcol = (g.bias && (g.epi == NR_EPI_STORE || g.epi == NR_EPI_STORE_RELU ||
-                                     g.epi == NR_EPI_STORE_TANH || g.epi == NR_EPI_ACCUM)) ? g.bias[col] : 0.f;
+                                     g.epi == NR_EPI_STORE_TANH || g.epi == NR_EPI_ACCUM ||
+                                     g.epi == NR_EPI_STORE_GELU)) ? g.bias[col] : 0.f;
       int sj = 0;
       int64_t scol = col;
       if (g.epi == NR_EPI_SCATTER && g.Cm.map == NR_ROWS_CONV3) {
@@ -237,6 +238,12 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(Args g) {
           g.C[o] = g.Cm.base[row * g.Cm.ld + col] > 0.f ? g.C[o] + v : 0.f;
         } else if (g.epi == NR_EPI_ACCUM) {
           g.C[row * g.ldc + col] += v + bcol;
+        } else if (g.epi == NR_EPI_STORE_GELU) {
+          const float x = v + bcol;
+          const_cast<float*>(g.Cm.base)[row * g.Cm.ld + col] = x;
+          g.C[row * g.ldc + col] = nr_gelu(x);
+        } else if (g.epi == NR_EPI_GELU_GRAD) {
+          g.C[row * g.ldc + col] = v * nr_gelu_grad(g.Cm.base[row * g.Cm.ld + col]);
         } else if (g.epi == NR_EPI_ATOMIC) {
           atomicAdd(&g.C[row * g.ldc + col], v);
         } else {  // NR_EPI_SCATTER
@@ -313,7 +320,9 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
     return NR_EINVAL(2);   // gathered tables must be float4-addressable
   if (epilogue == NR_EPI_SCATTER && (!c_rows || (c_rows->map != NR_ROWS_PLAIN && !c_rows->rows)))
     return NR_EINVAL(4);
-  if (epilogue == NR_EPI_ACCUM_GATE && (!c_rows || !c_rows->data)) return NR_EINVAL(4);
+  if ((epilogue == NR_EPI_ACCUM_GATE || epilogue == NR_EPI_STORE_GELU || epilogue == NR_EPI_GELU_GRAD) &&
+      (!c_rows || !c_rows->data))
+    return NR_EINVAL(4);
   if (split_k < 1) split_k = 1;
   if (split_k > 1 && epilogue != NR_EPI_ATOMIC && epilogue != NR_EPI_SCATTER) return NR_EINVAL(5);
   if (M == 0 || N == 0) return NR_OK;
@@ -369,7 +378,9 @@ extern "C" int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand
   if ((A->ld & 3) || (B->ld & 3)) return NR_EINVAL(2);
   if (epilogue == NR_EPI_SCATTER && (!c_rows || (c_rows->map != NR_ROWS_PLAIN && !c_rows->rows)))
     return NR_EINVAL(4);
-  if (epilogue == NR_EPI_ACCUM_GATE && (!c_rows || !c_rows->data)) return NR_EINVAL(4);
+  if ((epilogue == NR_EPI_ACCUM_GATE || epilogue == NR_EPI_STORE_GELU || epilogue == NR_EPI_GELU_GRAD) &&
+      (!c_rows || !c_rows->data))
+    return NR_EINVAL(4);
   if (epilogue == NR_EPI_SCATTER_STORE && (!c_rows || c_rows->map != NR_ROWS_GATHER || !c_rows->rows))
     return NR_EINVAL(4);
   if (split_k < 1) split_k = 1;

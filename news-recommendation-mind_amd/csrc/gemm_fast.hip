@@ -203,6 +203,11 @@ __device__ __forceinline__ float4 epi_combine(const Args& g, float4 v, float4 b,
     const float4 o = *reinterpret_cast<const float4*>(crow + n);
     return make_float4(o.x + v.x + b.x, o.y + v.y + b.y, o.z + v.z + b.z, o.w + v.w + b.w);
   }
+  if (EPI == NR_EPI_GELU_GRAD) {
+    const float4 a = *reinterpret_cast<const float4*>(arow + n);
+    return make_float4(v.x * nr_gelu_grad(a.x), v.y * nr_gelu_grad(a.y), v.z * nr_gelu_grad(a.z),
+                       v.w * nr_gelu_grad(a.w));
+  }
   // NR_EPI_ACCUM_GATE
   const float4 o = *reinterpret_cast<const float4*>(crow + n);
   const float4 a = *reinterpret_cast<const float4*>(arow + n);
@@ -217,6 +222,7 @@ __device__ __forceinline__ float epi_combine1(const Args& g, float v, float b, c
   if (EPI == NR_EPI_STORE_RELU) return fmaxf(v + b, 0.f);
   if (EPI == NR_EPI_STORE_TANH) return tanhf(v + b);
   if (EPI == NR_EPI_ACCUM) return crow[n] + v + b;
+  if (EPI == NR_EPI_GELU_GRAD) return v * nr_gelu_grad(arow[n]);
   return arow[n] > 0.f ? crow[n] + v : 0.f;
 }
 
@@ -224,7 +230,7 @@ template <int EPI, int TI, int TJ>
 __device__ __forceinline__ void epilogue_t(const Args& g, f32x16 (&acc)[TI][TJ], int64_t m0, int64_t n0, int wm,
                                            int wn, int h, int c, bool vec) {
   const bool has_bias = g.bias && (EPI == NR_EPI_STORE || EPI == NR_EPI_STORE_RELU || EPI == NR_EPI_STORE_TANH ||
-                                   EPI == NR_EPI_ACCUM);
+                                   EPI == NR_EPI_ACCUM || EPI == NR_EPI_STORE_GELU);
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
     const int64_t row = m0 + wm + 32 * i + c;
@@ -235,7 +241,9 @@ __device__ __forceinline__ void epilogue_t(const Args& g, f32x16 (&acc)[TI][TJ],
       if (tok == g.pad_row) continue;
       crow = g.C + tok * g.ldc;
     }
-    const float* arow = EPI == NR_EPI_ACCUM_GATE ? g.Cm.base + row * g.Cm.ld : nullptr;
+    const float* arow =
+        (EPI == NR_EPI_ACCUM_GATE || EPI == NR_EPI_GELU_GRAD || EPI == NR_EPI_STORE_GELU) ? g.Cm.base + row * g.Cm.ld
+                                                                                          : nullptr;
     int64_t tok = 0, nbase = 0;
     int tpos = 0;
     if (EPI == NR_EPI_SCATTER) {
@@ -283,6 +291,23 @@ __device__ __forceinline__ void epilogue_t(const Args& g, f32x16 (&acc)[TI][TJ],
 #pragma unroll
             for (int u = 0; u < 4; ++u)
               if (n + u < g.N) crow[n + u] = e[u];
+          }
+        } else if (EPI == NR_EPI_STORE_GELU) {   // pre-activation to aux, GELU to C
+          float* xrow = const_cast<float*>(arow);
+          const float e[4] = {v.x, v.y, v.z, v.w};
+          if (vec && n + 3 < g.N) {
+            const float4 b = has_bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 x = make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
+            *reinterpret_cast<float4*>(xrow + n) = x;
+            *reinterpret_cast<float4*>(crow + n) = make_float4(nr_gelu(x.x), nr_gelu(x.y), nr_gelu(x.z), nr_gelu(x.w));
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (n + u < g.N) {
+                const float x = e[u] + (has_bias ? g.bias[n + u] : 0.f);
+                xrow[n + u] = x;
+                crow[n + u] = nr_gelu(x);
+              }
           }
         } else if (vec && n + 3 < g.N) {
           const float4 b = has_bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -361,6 +386,8 @@ __device__ __forceinline__ void epilogue(const Args& g, f32x16 (&acc)[TI][TJ], i
     case NR_EPI_STORE_TANH: epilogue_t<NR_EPI_STORE_TANH, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
     case NR_EPI_ACCUM: epilogue_t<NR_EPI_ACCUM, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
     case NR_EPI_ACCUM_GATE: epilogue_t<NR_EPI_ACCUM_GATE, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_STORE_GELU: epilogue_t<NR_EPI_STORE_GELU, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_GELU_GRAD: epilogue_t<NR_EPI_GELU_GRAD, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
     case NR_EPI_ATOMIC: epilogue_t<NR_EPI_ATOMIC, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
     case NR_EPI_SCATTER_STORE: epilogue_t<NR_EPI_SCATTER_STORE, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
     default: epilogue_t<NR_EPI_SCATTER, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
@@ -692,7 +719,8 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   {
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     bool v = N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!bias || al16(bias));
-    if (epilogue == NR_EPI_ACCUM_GATE) v = v && c_rows && c_rows->ld % 4 == 0 && al16(c_rows->data);
+    if (epilogue == NR_EPI_ACCUM_GATE || epilogue == NR_EPI_STORE_GELU || epilogue == NR_EPI_GELU_GRAD)
+      v = v && c_rows && c_rows->ld % 4 == 0 && al16(c_rows->data);
     g.vec = v ? 1 : 0;
   }
   g.kchunk = (K + split_k - 1) / split_k;

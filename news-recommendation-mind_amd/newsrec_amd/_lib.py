@@ -26,6 +26,7 @@ KCONTIG, MNCONTIG = 0, 1
 EPI_STORE, EPI_STORE_RELU, EPI_ATOMIC, EPI_SCATTER = 0, 1, 2, 3
 MASK_U8, MASK_I64, MASK_F64, MASK_F32 = 0, 1, 2, 3
 EPI_STORE_TANH, EPI_ACCUM_GATE, EPI_ACCUM, EPI_SCATTER_STORE = 4, 5, 6, 7
+EPI_STORE_GELU, EPI_GELU_GRAD = 8, 9
 CELL_LSTM, CELL_GRU = 0, 1
 SCORE_RAW, SCORE_LOG_SOFTMAX, SCORE_SIGMOID = 0, 1, 2
 
@@ -80,9 +81,23 @@ _SIGS = {
     "nr_score_ragged": [c_ptr, c_i64, c_i64, c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i32, c_i32, c_ptr,
                         c_ptr, c_ptr],
     "nr_impression_metrics": [c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i32, c_ptr, c_ptr, c_ptr],
+    "nr_bert_embed_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i32, c_i32, c_ptr, c_ptr, c_f32,
+                          c_f32, c_u64, c_u64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr],
+    "nr_bert_embed_bwd": [c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_i32, c_i32, c_ptr, c_f32, c_u64, c_u64,
+                          c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr],
+    "nr_bert_add_ln_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_ptr, c_f32, c_f32, c_u64, c_u64,
+                           c_ptr, c_ptr, c_i64, c_ptr, c_ptr],
+    "nr_bert_add_ln_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_f32, c_u64, c_u64, c_ptr, c_ptr,
+                           c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr],
+    "nr_bert_attn_fwd": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_u64, c_u64,
+                         c_ptr, c_ptr, c_i64, c_ptr, c_ptr],
+    "nr_bert_attn_bwd_workspace": [c_i64, c_i32, c_i32],
+    "nr_bert_attn_bwd": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_u64, c_u64,
+                         c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr],
+    "nr_tanh_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr],
 }
 
-_RESTYPES = {"nr_segment_rows_sum_workspace": c_i64}
+_RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64}
 
 # enum nr_batch_flags / nr_metric_flags
 BATCH_REVERSE_HISTORY, BATCH_SHUFFLE_POS = 1, 2

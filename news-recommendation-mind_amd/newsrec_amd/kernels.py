@@ -396,3 +396,132 @@ def mha_pool_bwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, stats, p
            L.ptr(dz), dz.stride(0) if dz is not None else 0, L.ptr(o), o.stride(0) if o is not None else 0,
            L.ptr(dob), dob.stride(0) if dob is not None else 0, L.ptr(dy), dy.stride(0), L.ptr(dbias), L.ptr(dq),
            L.ptr(dgamma), L.ptr(dbeta), L.stream_ptr(y))
+
+
+# ---------------------------------------------------------------------- BERT towers
+
+def _al(t, name):
+    if t.dim() != 2 or t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
+        raise L.HipError("%s: 2-D row-major, ld %% 4 == 0, 16-B aligned required" % name)
+
+
+def _drop(p, seed, offset, rng):
+    _rng_ok(rng)
+    return float(p), int(seed), int(offset), L.ptr(rng)
+
+
+def bert_embed_fwd(word, pos, type0, ids, nseq, seq_len, gamma, beta, eps, out, stats, p_drop=0.0, seed=0,
+                   offset=0, rng=None, status=None):
+    """BertEmbeddings: out = Dropout(LN(word[ids] + pos[l] + type0)), stats [T, 2]."""
+    _f32(word, pos, type0, gamma, beta, out, stats)
+    _check_rows(ids, None, "ids")
+    V, H = word.shape
+    T = nseq * seq_len
+    if ids.numel() != T or pos.shape[1] != H or type0.numel() < H or not word.is_contiguous():
+        raise L.HipError("bert_embed_fwd: shape mismatch")
+    if pos.shape[0] < seq_len:
+        raise L.HipError("bert_embed_fwd: %d positions < sequence length %d" % (pos.shape[0], seq_len))
+    _al(out, "bert_embed_fwd out")
+    _rows_ok(out, T, H, "out")
+    if stats.numel() < 2 * T:
+        raise L.HipError("bert_embed_fwd: stats too small")
+    p, s, o, r = _drop(p_drop, seed, offset, rng)
+    L.call("nr_bert_embed_fwd", L.ptr(word), V, L.ptr(pos), pos.shape[0], L.ptr(type0), L.ptr(ids), nseq,
+           seq_len, H, L.ptr(gamma), L.ptr(beta), float(eps), p, s, o, r, L.ptr(out), out.stride(0), L.ptr(stats),
+           L.ptr(status), L.stream_ptr(word))
+
+
+def bert_embed_bwd(word, pos, type0, ids, nseq, seq_len, gamma, stats, dout, ds, dgamma, dbeta, p_drop=0.0,
+                   seed=0, offset=0, rng=None):
+    _f32(word, pos, type0, gamma, stats, dout, ds, dgamma, dbeta)
+    _check_rows(ids, None, "ids")
+    V, H = word.shape
+    T = nseq * seq_len
+    if ids.numel() != T:
+        raise L.HipError("bert_embed_bwd: shape mismatch")
+    _al(dout, "dout")
+    _al(ds, "ds")
+    _rows_ok(dout, T, H, "dout")
+    _rows_ok(ds, T, H, "ds")
+    p, s, o, r = _drop(p_drop, seed, offset, rng)
+    L.call("nr_bert_embed_bwd", L.ptr(word), V, L.ptr(pos), L.ptr(type0), L.ptr(ids), nseq, seq_len, H,
+           L.ptr(gamma), p, s, o, r, L.ptr(stats), L.ptr(dout), dout.stride(0), L.ptr(ds), ds.stride(0),
+           L.ptr(dgamma), L.ptr(dbeta), L.stream_ptr(word))
+
+
+def bert_add_ln_fwd(x, res, gamma, beta, eps, out, stats, p_drop=0.0, seed=0, offset=0, rng=None):
+    """out = LayerNorm(Dropout(x) + res)."""
+    _f32(x, res, gamma, beta, out, stats)
+    T, H = x.shape
+    for t, n in ((x, "x"), (res, "res"), (out, "out")):
+        _al(t, n)
+        _rows_ok(t, T, H, n)
+    if stats.numel() < 2 * T or gamma.numel() < H:
+        raise L.HipError("bert_add_ln_fwd: shape mismatch")
+    p, s, o, r = _drop(p_drop, seed, offset, rng)
+    L.call("nr_bert_add_ln_fwd", L.ptr(x), x.stride(0), L.ptr(res), res.stride(0), T, H, L.ptr(gamma), L.ptr(beta),
+           float(eps), p, s, o, r, L.ptr(out), out.stride(0), L.ptr(stats), L.stream_ptr(x))
+
+
+def bert_add_ln_bwd(x, res, gamma, stats, dout, dres, dx, dgamma, dbeta, p_drop=0.0, seed=0, offset=0, rng=None):
+    _f32(x, res, gamma, stats, dout, dres, dx, dgamma, dbeta)
+    T, H = x.shape
+    for t, n in ((x, "x"), (res, "res"), (dout, "dout"), (dres, "dres"), (dx, "dx")):
+        _al(t, n)
+        _rows_ok(t, T, H, n)
+    p, s, o, r = _drop(p_drop, seed, offset, rng)
+    L.call("nr_bert_add_ln_bwd", L.ptr(x), x.stride(0), L.ptr(res), res.stride(0), T, H, L.ptr(gamma), p, s, o, r,
+           L.ptr(stats), L.ptr(dout), dout.stride(0), L.ptr(dres), dres.stride(0), L.ptr(dx), dx.stride(0),
+           L.ptr(dgamma), L.ptr(dbeta), L.stream_ptr(x))
+
+
+def _attn_check(qkv, heads, koff, voff, mask, nseq, seq_len):
+    _f32(qkv)
+    _al(qkv, "qkv")
+    T = nseq * seq_len
+    _rows_ok(qkv, T, max(koff, voff) + heads * 64, "qkv")
+    return mask_arg(mask, T)
+
+
+def bert_attn_fwd(qkv, heads, mask, nseq, seq_len, ctx, ml, koff=None, voff=None, p_drop=0.0, seed=0, offset=0,
+                  rng=None):
+    """BertSelfAttention core on a fused [T, 3*heads*64] (Q | K | V) projection."""
+    koff = heads * 64 if koff is None else koff
+    voff = 2 * heads * 64 if voff is None else voff
+    mp, mdt = _attn_check(qkv, heads, koff, voff, mask, nseq, seq_len)
+    _f32(ctx, ml)
+    _al(ctx, "ctx")
+    T = nseq * seq_len
+    _rows_ok(ctx, T, heads * 64, "ctx")
+    if ml.numel() < 2 * T * heads:
+        raise L.HipError("bert_attn_fwd: ml too small")
+    p, s, o, r = _drop(p_drop, seed, offset, rng)
+    L.call("nr_bert_attn_fwd", L.ptr(qkv), qkv.stride(0), koff, voff, mp, mdt, nseq, seq_len, heads, p, s, o, r,
+           L.ptr(ctx), ctx.stride(0), L.ptr(ml), L.stream_ptr(qkv))
+
+
+def bert_attn_bwd(qkv, heads, mask, nseq, seq_len, ctx, ml, dctx, dqkv, koff=None, voff=None, p_drop=0.0, seed=0,
+                  offset=0, rng=None):
+    koff = heads * 64 if koff is None else koff
+    voff = 2 * heads * 64 if voff is None else voff
+    mp, mdt = _attn_check(qkv, heads, koff, voff, mask, nseq, seq_len)
+    _f32(ctx, ml, dctx, dqkv)
+    T = nseq * seq_len
+    for t, n, w in ((ctx, "ctx", heads * 64), (dctx, "dctx", heads * 64), (dqkv, "dqkv", max(koff, voff) + heads * 64)):
+        _al(t, n)
+        _rows_ok(t, T, w, n)
+    nbytes = L.load().nr_bert_attn_bwd_workspace(nseq, seq_len, heads)
+    work = torch.empty(max(1, nbytes // 4), device=qkv.device, dtype=torch.float32)
+    p, s, o, r = _drop(p_drop, seed, offset, rng)
+    L.call("nr_bert_attn_bwd", L.ptr(qkv), qkv.stride(0), koff, voff, mp, mdt, nseq, seq_len, heads, p, s, o, r,
+           L.ptr(ctx), ctx.stride(0), L.ptr(ml), L.ptr(dctx), dctx.stride(0), L.ptr(work), L.ptr(dqkv),
+           dqkv.stride(0), L.stream_ptr(qkv))
+
+
+def tanh_bwd(y, dy, dx):
+    _f32(y, dy, dx)
+    rows, cols = y.shape
+    _rows_ok(dy, rows, cols, "dy")
+    _rows_ok(dx, rows, cols, "dx")
+    L.call("nr_tanh_bwd", L.ptr(y), y.stride(0), L.ptr(dy), dy.stride(0), rows, cols, L.ptr(dx), dx.stride(0),
+           L.stream_ptr(y))
