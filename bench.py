@@ -37,6 +37,7 @@ USERS_LARGE, NEWS_LARGE_DEV, NEWS_LARGE_TRAIN = 876956, 72023, 101527
 DEV_IMPR_LARGE = 376471            # MIND-large dev impressions
 TRAIN_IMPR_SYNTH = 262144          # train impressions resident for the synthetic split (a subset of 2.23 M)
 FP32_MFMA_PEAK_TF = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = f32 vector peak
+BF16_MFMA_PEAK_TF = 2500.0         # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -203,6 +204,51 @@ def fast_eval_leg(model, dev, world, rank, n_impr):
             "metrics_random_model": res}
 
 
+def xformer_leg(dev, steps=5, warmup=2, b=B):
+    """configs[4] beside the headline: XFormer (bert-base news encoder + 501-token user sequence,
+    12 layers, dropout 0.1, Adam) train steps and eval forwards on synthetic MIND-shaped batches,
+    one GPU, eager.  FLOPs are algorithmic (dense layers + attention + pooler, train = 3x fwd)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_bert as BB
+    from newsrec_amd.manager import get_optim
+    model = BB.build("xformer", 12, dev)
+    opt = get_optim(model)
+    gen = torch.Generator().manual_seed(3)
+    x = {k: v.to(dev) for k, v in BB.synth(gen, b).items()}
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        logits, _ = model(x)
+        torch.nn.functional.nll_loss(logits, x["label"]).backward()
+        opt.step()
+    model.train()
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    model.eval()
+    with torch.no_grad():
+        model(x)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            model(x)
+        torch.cuda.synchronize()
+        ev = (time.perf_counter() - t1) / steps
+    f = BB.flops_per_impression("xformer", 12) * b
+    del model, opt
+    torch.cuda.empty_cache()
+    return {"workload": "XFormer train step: bert-base (12 layers, 768, 12 heads) over 5x30-token candidates + "
+                        "501-token user sequence, dropout 0.1, Adam; synthetic batches, random init",
+            "per_gpu_batch": b, "impressions_per_s": round(b / el, 1), "ms_per_step": round(el * 1e3, 2),
+            "train_tflops": round(3 * f / el / 1e12, 1), "eval_impressions_per_s": round(b / ev, 1),
+            "eval_tflops": round(f / ev / 1e12, 1)}
+
+
 def cpu_baseline(seconds=20.0):
     """The oracle (oracle/restatement.py, torch fp32 CPU) on the same NRMS step, timed on this
     host's cores over a bounded sample (steps of B=32 until ~`seconds` elapse)."""
@@ -237,6 +283,8 @@ def main():
                     help="device: form each batch on the GPU from a resident MIND split; resident: pre-formed")
     ap.add_argument("--eval-impr", type=int, default=DEV_IMPR_LARGE,
                     help="dev impressions of the fast-eval leg (0 skips it)")
+    ap.add_argument("--xformer-steps", type=int, default=5,
+                    help="timed XFormer (configs[4]) train steps reported beside the headline (0 skips; N=1 only)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the train step as a HIP graph (auto: single GPU)")
     a = ap.parse_args()
@@ -325,6 +373,7 @@ def main():
     del evb
     # eval (b): the fast-eval pipeline over a MIND-large-shaped dev split
     fast = fast_eval_leg(model, dev, world, rank, a.eval_impr) if a.eval_impr > 0 else None
+    xf = xformer_leg(dev, a.xformer_steps) if (a.xformer_steps > 0 and world == 1) else None
 
     if rank == 0:
         ms = el / a.steps * 1e3
@@ -335,6 +384,10 @@ def main():
         gemm_rows = probe.get("proj_fwd_rows", float(B * (C + NH) * L))
         gemm_flops = 2.0 * gemm_rows * E * (E + H)
         achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms else None
+        from newsrec_amd import _lib as Lb, kernels as Kn
+        split = Kn.get_gemm_precision() == Lb.GEMM_BF16X6
+        # bf16x6: six bf16 MFMAs per fp32 multiply-add -> fp32-equivalent peak = bf16 dense peak / 6
+        peak = BF16_MFMA_PEAK_TF / 6 if split else FP32_MFMA_PEAK_TF
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_proj_fwd.json")
         if os.path.exists(pmc):
@@ -344,6 +397,9 @@ def main():
             "value": round(value, 1), "unit": "impressions/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (MIND-large-shaped, random-init weights)",
+            "gemm_arithmetic": ("bf16x6: fp32 operands split into 3 bf16 terms, 6 products on the bf16 MFMA, "
+                                "fp32 accumulate (measured as accurate as the f32 MFMA)") if split else
+                               "f32 MFMA (exact fp32 products)",
             "config": {"workload": "NRMS train step: MHA news encoder + MHA user encoder, H=384, 12 heads, "
                                    "V=30522 word table (trainable), dropout 0.2, Adam",
                        "launch": "hipGraph replay of the whole step" if use_graph else "eager",
@@ -355,13 +411,18 @@ def main():
             "eval": dict(fast or {}, forward={"candidates_per_s": round(world * B * C * ne / el_eval, 1),
                                               "impressions_per_s": round(world * B * ne / el_eval, 1),
                                               "mode": "model(x) in eval mode (sigmoid) on train-shaped batches"}),
-            "roofline": {"kernel": "gemm_f32 gather+key/value projection (fwd)", "bound": "mfma",
-                         "achieved": round(achieved, 2) if achieved else None, "peak": FP32_MFMA_PEAK_TF,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TF, 4) if achieved else None,
+            "roofline": {"kernel": "gemm gather+key/value projection (fwd)", "bound": "mfma",
+                         "achieved": round(achieved, 2) if achieved else None, "peak": round(peak, 1),
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
+                         "peak_basis": ("fp32-equivalent: 2.5 PF bf16 dense MFMA / 6 (bf16x6 split arithmetic)"
+                                        if split else "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
+                         "frac_of_fp32_peak": round(achieved / FP32_MFMA_PEAK_TF, 4) if achieved else None,
                          "traffic": traffic, "launch_ms": round(gemm_ms, 4) if gemm_ms else None,
                          "flops_per_launch": gemm_flops, "rows_per_launch": gemm_rows,
                          "tokens_per_launch": B * (C + NH) * L},
         }
+        if xf is not None:
+            out["xformer"] = xf
         if not a.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(out), flush=True)

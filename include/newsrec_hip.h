@@ -70,6 +70,19 @@ enum nr_epilogue {
                             the dgrad of the intermediate dense through its GELU               */
 };
 
+/* GEMM arithmetic of every nr_gemm_f32 / nr_gemm_f32_dyn call in the process.
+ *   NR_GEMM_F32     v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation.
+ *   NR_GEMM_BF16X6  each fp32 operand split into three bf16 terms (x = h + m + l to 2^-24 |x|) and
+ *                   the six products of order >= 2^-16 (hh, hm, mh, hl, mm, lh) accumulated in fp32 on
+ *                   v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA rate): fp32-class accuracy (dropped
+ *                   terms <= 3 * 2^-24 |a b|), 6 bf16 MFMAs per f32-equivalent.  128x128-tile fast
+ *                   path only (CONV3 operands along N and small problems stay on f32).
+ * The initial mode comes from the environment variable NR_GEMM_PREC ("bf16x6", the default, | "f32").
+ * nr_gemm_set_precision returns the previous mode (or -1000 on an invalid one). */
+enum nr_gemm_precision { NR_GEMM_F32 = 0, NR_GEMM_BF16X6 = 1 };
+int nr_gemm_set_precision(int32_t mode);
+int nr_gemm_get_precision(void);
+
 /* C (op)= A(m,k) * B(k,n) over k in [0,K), fp32 on the f32-input MFMA.
  * Replaces: nn.Linear / F.linear of models/Modules/Attention.py:107-108 (keyProject,
  * valueProject), CNN.py:23 (wordQueryProject is done in nr_attn_pool), the Conv1d of

@@ -22,8 +22,44 @@
 #include "gemm_fast.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// GEMM arithmetic for the whole process (nr_gemm_set_precision; initial value from NR_GEMM_PREC =
+// "bf16x6" (default) | "f32").  bf16x6 is measured at least as accurate as the f32 MFMA
+// (tools/split_probe.py: max / mean |C - C_fp64| 1.6e-4 / 8.1e-6 vs 1.9e-4 / 9.6e-6 at K = 768).
+static int g_gemm_prec = [] {
+  const char* e = getenv("NR_GEMM_PREC");
+  return (e && e[0] == 'f') ? NR_GEMM_F32 : NR_GEMM_BF16X6;
+}();
 
 namespace nrfast {
+
+// ---- bf16x6 arithmetic: fp32 operands as three bf16 terms (x = h + m + l to 2^-24 |x|) and six
+// products a_h b_h + a_h b_m + a_m b_h + a_h b_l + a_m b_m + a_l b_h on v_mfma_f32_32x32x16_bf16
+// (16x the f32 MFMA rate); the dropped terms are O(2^-24) of |a b|, like the f32 MFMA rounding.
+__device__ __forceinline__ uint32_t bf_rne(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float bf_f(uint32_t b) { return __uint_as_float(b << 16); }
+__device__ __forceinline__ void split1(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = bf_rne(x);
+  const float r = x - bf_f(h);   // exact
+  m = bf_rne(r);
+  l = bf_rne(r - bf_f(m));
+}
+__device__ __forceinline__ void split4(float a, float b, float c, float d, uint2& p0, uint2& p1, uint2& p2) {
+  uint32_t h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
+  split1(a, h0, m0, l0);
+  split1(b, h1, m1, l1);
+  split1(c, h2, m2, l2);
+  split1(d, h3, m3, l3);
+  p0 = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+  p1 = make_uint2(m0 | (m1 << 16), m2 | (m3 << 16));
+  p2 = make_uint2(l0 | (l1 << 16), l2 | (l3 << 16));
+}
+constexpr int SROW = 40;          // split LDS image: [plane][row][k] bf16, 32 k + 8 pad (80-B rows)
+constexpr int SPL = 128 * SROW;   // one plane of a 128-row operand tile
 
 // operand modes
 enum { KC_PLAIN = 0, KC_GATHER = 1, KC_CONV3 = 2, MN_PLAIN = 3, MN_GATHER = 4, MN_CONV3 = 5 };
@@ -179,11 +215,80 @@ struct Loader {
     }
   }
 
+  // bf16x6 image (K-contiguous operands only): the float4 of 4 k of one row -> 3 planes
+  __device__ __forceinline__ void store_split(uint16_t* lds, int tid) const {
+    if constexpr (KC) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int f = tid + 256 * i;
+        uint2 p0, p1, p2;
+        split4(v[i].x, v[i].y, v[i].z, v[i].w, p0, p1, p2);
+        uint16_t* q = lds + (f >> 3) * SROW + 4 * (f & 7);
+        *reinterpret_cast<uint2*>(q) = p0;
+        *reinterpret_cast<uint2*>(q + SPL) = p1;
+        *reinterpret_cast<uint2*>(q + 2 * SPL) = p2;
+      }
+    }
+  }
+
   // the 4 operand values of k-steps 4q..4q+3 for tile row `row` (lane half h)
   __device__ __forceinline__ float4 frag(const float* lds, int row, int h, int q) const {
     if (KC) return *reinterpret_cast<const float4*>(&lds[row * 36 + 16 * h + 4 * q]);
     const int k = 16 * h + 4 * q;
     return make_float4(lds[k * S + row], lds[(k + 1) * S + row], lds[(k + 2) * S + row], lds[(k + 3) * S + row]);
+  }
+};
+
+// bf16x6 loader of an MN-contiguous 128-row operand (stored rows = k): thread (kg = tid & 7,
+// cg = tid >> 3) loads the 4x4 block k0+4kg.., columns r0+4cg.. as 4 float4 (8 lanes cover 128
+// contiguous bytes of a stored row), transposes it in registers and writes each column's 4
+// consecutive k to the [row][k] planes (b64 stores, 2-way bank aliasing).
+template <int MODE>
+struct MNBlk {
+  static_assert(MODE == MN_PLAIN || MODE == MN_GATHER, "MNBlk: plain or gathered rows");
+  float4 v[4];
+  int64_t kid[4];   // MN_GATHER: stored-row ids of the next tile (prefetched)
+
+  __device__ __forceinline__ void init(const Op&, int64_t, int64_t, int) {}
+
+  __device__ __forceinline__ void load(const Op& d, int64_t r0, int64_t rlim, int64_t k0, int tid) {
+    const int kg = tid & 7, cg = tid >> 3;
+    int64_t col = r0 + 4 * cg;
+    const int64_t cmax = ((rlim + 3) & ~int64_t(3)) - 4;
+    col = col < cmax ? col : cmax;   // clamp inside the padded row; rows >= M are discarded
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = MODE == MN_PLAIN ? k0 + 4 * kg + u : kid[u];
+      v[u] = *reinterpret_cast<const float4*>(d.base + row * d.ld + col);
+    }
+  }
+
+  __device__ __forceinline__ void prefetch_idx(const Op& d, int64_t k0, int64_t K, int tid) {
+    if (MODE == MN_GATHER) {
+      const int kg = tid & 7;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t k = k0 + 4 * kg + u;
+        kid[u] = d.idx[k < K ? k : K - 1];
+      }
+    }
+  }
+
+  __device__ __forceinline__ void put(uint16_t* q, float a, float b, float c, float e) const {
+    uint2 p0, p1, p2;
+    split4(a, b, c, e, p0, p1, p2);
+    *reinterpret_cast<uint2*>(q) = p0;
+    *reinterpret_cast<uint2*>(q + SPL) = p1;
+    *reinterpret_cast<uint2*>(q + 2 * SPL) = p2;
+  }
+
+  __device__ __forceinline__ void store_split(uint16_t* lds, int tid) const {
+    const int kg = tid & 7, cg = tid >> 3;
+    uint16_t* q = lds + (4 * cg) * SROW + 4 * kg;
+    put(q, v[0].x, v[1].x, v[2].x, v[3].x);
+    put(q + SROW, v[0].y, v[1].y, v[2].y, v[3].y);
+    put(q + 2 * SROW, v[0].z, v[1].z, v[2].z, v[3].z);
+    put(q + 3 * SROW, v[0].w, v[1].w, v[2].w, v[3].w);
   }
 };
 
@@ -609,6 +714,179 @@ __global__ __launch_bounds__(256, 2) void gemm_fast_kernel(Args g) {
   epilogue_any<TR, TI, TJ>(g, acc, cp.u.m0, cp.u.n0, wm, wn, h, c);
 }
 
+// bf16x6 form of gemm_fast_kernel (128x128 tiles, the same persistent two-deep pipeline and
+// epilogues): the loaders split each fp32 element into three bf16 planes as they publish a
+// k-tile to LDS (K-contiguous operands as loaded, MN-contiguous ones through a 4x4 register
+// transpose), and each 16-deep k-step runs six v_mfma_f32_32x32x16_bf16 per 32x32 output tile,
+// smallest terms first.  The accumulators have the f32 MFMA's C/D layout, so the epilogues are
+// shared.  One LDS image (60 KiB) so two workgroups share a CU: tile P+1 waits in registers while
+// P computes, is published between two barriers, and P+2's loads go out right behind it.
+template <int AM, int BMODE, bool TR>
+__global__ __launch_bounds__(256, 2) void gemm_split_kernel(Args g) {
+  using LA = typename std::conditional<is_kc(AM), Loader<128, AM>, MNBlk<AM>>::type;
+  using LB = typename std::conditional<is_kc(BMODE), Loader<128, BMODE>, MNBlk<BMODE>>::type;
+  constexpr int BM = 128, BN = 128;
+  __shared__ __attribute__((aligned(16))) uint16_t As[3 * SPL];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[3 * SPL];
+  constexpr bool IDX_AHEAD = AM == MN_GATHER || BMODE == MN_GATHER;
+
+  if (g.mdyn) {
+    const int64_t m = *g.mdyn;
+    g.M = m < g.M ? (m > 0 ? m : 0) : g.M;
+  }
+  if (g.kdyn) {
+    const int64_t k = *g.kdyn;
+    g.K = k < g.K ? (k > 0 ? k : 0) : g.K;
+    const int64_t kc = (g.K + g.splits - 1) / g.splits;
+    g.kchunk = kc > 0 ? (kc + 31) / 32 * 32 : 32;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int gn = (int)((g.N + BN - 1) / BN);
+  const int ntiles = (int)((g.M + BM - 1) / BM) * gn;
+  const int units = ntiles * g.splits;
+  const int G = gridDim.x;
+
+  auto skip_empty = [&](int id, Unit& u) -> int {
+    for (; id < units; id += G) {
+      u = decode_unit(g, id, units, ntiles, gn, BM, BN);
+      if (u.nt > 0) return id;
+    }
+    return units;
+  };
+  auto advance = [&](Cursor& p) -> bool {
+    if (p.kt + 1 < p.u.nt) { ++p.kt; return true; }
+    Unit u;
+    const int nid = skip_empty(p.id + G, u);
+    if (nid >= units) return false;
+    p.id = nid;
+    p.kt = 0;
+    p.u = u;
+    return true;
+  };
+  auto kof = [](const Cursor& p) -> int64_t { return p.u.kbeg + (int64_t)p.kt * 32; };
+  auto peek_k = [&](const Cursor& p) -> int64_t {
+    if (p.kt + 1 < p.u.nt) return kof(p) + 32;
+    Unit u;
+    return skip_empty(p.id + G, u) < units ? u.kbeg : -1;
+  };
+
+  Cursor cp;
+  cp.kt = 0;
+  cp.id = skip_empty(blockIdx.x, cp.u);
+  if (cp.id >= units) return;
+
+  constexpr int TI = 2, TJ = 2;
+  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  LA la;
+  LB lb;
+  Cursor lp = cp;
+  la.init(g.A, lp.u.m0, g.M, tid);
+  lb.init(g.B, lp.u.n0, g.N, tid);
+  auto issue = [&](const Cursor& p) {
+    const int64_t k = kof(p);
+    la.load(g.A, p.u.m0, g.M, k, tid);
+    lb.load(g.B, p.u.n0, g.N, k, tid);
+    if (IDX_AHEAD) {
+      const int64_t pk = peek_k(p);
+      if (pk >= 0) {
+        la.prefetch_idx(g.A, pk, g.K, tid);
+        lb.prefetch_idx(g.B, pk, g.K, tid);
+      }
+    }
+  };
+  auto step_load = [&]() -> bool {
+    const int old = lp.id;
+    if (!advance(lp)) return false;
+    if (lp.id != old) {
+      la.init(g.A, lp.u.m0, g.M, tid);
+      lb.init(g.B, lp.u.n0, g.N, tid);
+    }
+    issue(lp);
+    return true;
+  };
+
+  if (IDX_AHEAD) {
+    la.prefetch_idx(g.A, kof(lp), g.K, tid);
+    lb.prefetch_idx(g.B, kof(lp), g.K, tid);
+  }
+  issue(lp);
+  la.store_split(As, tid);
+  lb.store_split(Bs, tid);
+  bool staged = step_load();
+  __syncthreads();
+
+  bool pending = false;
+  int64_t pm0 = 0, pn0 = 0;
+  for (;;) {
+    if (pending) {
+      epilogue_any<TR, TI, TJ>(g, acc, pm0, pn0, wm, wn, h, c);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      pending = false;
+    }
+    const uint16_t* a_s = As;
+    const uint16_t* b_s = Bs;
+    const bool had_staged = staged;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 a[TI][3], b[TJ][3];
+      const int ko = 16 * s + 8 * h;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          a[i][p] = *reinterpret_cast<const bf16x8*>(a_s + p * SPL + (wm + 32 * i + c) * SROW + ko);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          b[j][p] = *reinterpret_cast<const bf16x8*>(b_s + p * SPL + (wn + 32 * j + c) * SROW + ko);
+#define NR_MF(X, Y)                                                                              \
+  acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][Y], a[i][X], acc[i][j], 0, 0, 0) \
+                 : __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][X], b[j][Y], acc[i][j], 0, 0, 0)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          NR_MF(2, 0);
+          NR_MF(1, 1);
+          NR_MF(0, 2);
+          NR_MF(1, 0);
+          NR_MF(0, 1);
+          NR_MF(0, 0);
+        }
+#undef NR_MF
+    }
+    __syncthreads();                // every wave is done reading P
+    const int old = cp.id;
+    const int64_t om0 = cp.u.m0, on0 = cp.u.n0;
+    if (!had_staged) break;
+    la.store_split(As, tid);        // publish P+1 (its loads landed during P's MFMAs)
+    lb.store_split(Bs, tid);
+    staged = step_load();           // and start P+2
+    __syncthreads();
+    advance(cp);
+    if (cp.id != old) {
+      pending = true;
+      pm0 = om0;
+      pn0 = on0;
+    }
+  }
+  epilogue_any<TR, TI, TJ>(g, acc, cp.u.m0, cp.u.n0, wm, wn, h, c);
+}
+
 // Resident-block slots for a kernel instantiation (CUs x occupancy), cached per device.
 template <typename Kern>
 int resident_slots(Kern k) {
@@ -651,8 +929,46 @@ int launch(const Args& g, int splits, hipStream_t s) {
   return NR_OK;
 }
 
+template <int AM, int BMODE, bool TR>
+int launch_split(const Args& g, int splits, hipStream_t s) {
+  const int64_t gm = (g.M + 127) / 128, gn = (g.N + 127) / 128;
+  const int64_t units = gm * gn * splits;
+  if (units <= 0) return NR_OK;
+  if (units > 0x7fffffff) return NR_EINVAL(0);
+  int grid = (int)units;
+  if (!persistent_disabled()) {
+    const int slots = resident_slots(gemm_split_kernel<AM, BMODE, TR>);
+    if (slots > 0 && slots < grid) grid = slots;
+  }
+  Args a = g;
+  a.splits = splits;
+  hipLaunchKernelGGL((gemm_split_kernel<AM, BMODE, TR>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+// bf16x6 operand-mode combinations (CONV3 taps along N stay on the f32 kernel); -1 = none
+int launch_split_modes(const Args& g, int am, int bm, int splits, hipStream_t s) {
+  const bool atomic_epi = g.epi == NR_EPI_ATOMIC || g.epi == NR_EPI_SCATTER;
+#define NR_SAB(A_, B_, TR_) \
+  if (am == A_ && bm == B_ && atomic_epi == !TR_) return launch_split<A_, B_, TR_>(g, splits, s);
+  NR_SAB(KC_GATHER, KC_PLAIN, true)
+  NR_SAB(KC_CONV3, KC_PLAIN, true)
+  NR_SAB(KC_PLAIN, KC_PLAIN, true)
+  NR_SAB(KC_PLAIN, MN_PLAIN, true)
+  NR_SAB(KC_PLAIN, MN_PLAIN, false)
+  NR_SAB(MN_PLAIN, MN_GATHER, false)
+  NR_SAB(MN_PLAIN, MN_PLAIN, false)
+#undef NR_SAB
+  return -1;
+}
+
 template <int BM, int BN>
 int launch_modes(const Args& g, int am, int bm, int splits, hipStream_t s) {
+  if (BM == 128 && BN == 128 && g_gemm_prec == NR_GEMM_BF16X6) {
+    const int rc = launch_split_modes(g, am, bm, splits, s);
+    if (rc != -1) return rc;
+  }
 #define NR_AB(A_, B_, TR_) \
   if (am == A_ && bm == B_ && atomic_epi == !TR_) return launch<BM, BN, A_, B_, TR_>(g, splits, s);
   // transposed accumulators (float4 stores) for store epilogues, C-major for atomic ones
@@ -731,3 +1047,12 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   if (bm == 64 && bn == 64) return launch_modes<64, 64>(g, am, bmode, splits, stream);
   return -1;
 }
+
+extern "C" int nr_gemm_set_precision(int32_t mode) {
+  if (mode != NR_GEMM_F32 && mode != NR_GEMM_BF16X6) return NR_EINVAL(0);
+  const int old = g_gemm_prec;
+  g_gemm_prec = mode;
+  return old;
+}
+
+extern "C" int nr_gemm_get_precision(void) { return g_gemm_prec; }

@@ -27,6 +27,7 @@ EPI_STORE, EPI_STORE_RELU, EPI_ATOMIC, EPI_SCATTER = 0, 1, 2, 3
 MASK_U8, MASK_I64, MASK_F64, MASK_F32 = 0, 1, 2, 3
 EPI_STORE_TANH, EPI_ACCUM_GATE, EPI_ACCUM, EPI_SCATTER_STORE = 4, 5, 6, 7
 EPI_STORE_GELU, EPI_GELU_GRAD = 8, 9
+GEMM_F32, GEMM_BF16X6 = 0, 1
 CELL_LSTM, CELL_GRU = 0, 1
 SCORE_RAW, SCORE_LOG_SOFTMAX, SCORE_SIGMOID = 0, 1, 2
 
@@ -95,6 +96,8 @@ _SIGS = {
     "nr_bert_attn_bwd": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_u64, c_u64,
                          c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr],
     "nr_tanh_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr],
+    "nr_gemm_set_precision": [c_i32],
+    "nr_gemm_get_precision": [],
 }
 
 _RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64}

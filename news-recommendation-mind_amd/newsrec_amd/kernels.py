@@ -20,6 +20,19 @@ def _check_rows(rows, limit, name):
             raise L.HipError("%s: row table must be a contiguous int64 CUDA tensor" % name)
 
 
+def set_gemm_precision(mode):
+    """nr_gemm_set_precision: L.GEMM_F32 (exact f32 MFMA) or L.GEMM_BF16X6 (fp32 operands as three bf16
+    terms on the bf16 matrix cores).  Returns the previous mode."""
+    rc = L.load().nr_gemm_set_precision(int(mode))
+    if rc < 0:
+        raise L.HipError("nr_gemm_set_precision: invalid mode %r" % (mode,))
+    return rc
+
+
+def get_gemm_precision():
+    return L.load().nr_gemm_get_precision()
+
+
 def gemm(M, N, K, A, B, C, ldc=None, bias=None, epilogue=L.EPI_STORE, c_rows=None,
          pad_row=-1, split_k=1):
     """C (op)= A(m,k) B(k,n); A, B, c_rows are nr_operand structs built by ``operand``."""

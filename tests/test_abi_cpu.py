@@ -21,7 +21,7 @@ def declared_arity():
     txt = open(HEADER).read()
     out = {}
     for m in re.finditer(r"^(?:int|int64_t)\s+(nr_\w+)\s*\(([^)]*)\)\s*;", txt, flags=re.M):
-        params = [p for p in m.group(2).replace("\n", " ").split(",") if p.strip()]
+        params = [p for p in m.group(2).replace("\n", " ").split(",") if p.strip() and p.strip() != "void"]
         out[m.group(1)] = len(params)
     return out
 

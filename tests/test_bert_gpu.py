@@ -154,8 +154,16 @@ def _oracle_fwd(g, P, x, training):
     return R.plm_forward(P, x, g.encU, training, g.heads)
 
 
+@pytest.fixture(params=["bf16x6", "f32"])
+def gemm_prec(request):
+    from newsrec_amd import _lib as Lb, kernels as Kn
+    old = Kn.set_gemm_precision(Lb.GEMM_BF16X6 if request.param == "bf16x6" else Lb.GEMM_F32)
+    yield request.param
+    Kn.set_gemm_precision(old)
+
+
 @pytest.mark.parametrize("cfg", list(BERT_CONFIGS))
-def test_bert_models_forward_parity(cfg):
+def test_bert_models_forward_parity(cfg, gemm_prec):
     g = Golden(cfg)
     model = build_bert_model(g)
     x = g.inputs("cuda")
@@ -174,7 +182,7 @@ def test_bert_models_forward_parity(cfg):
 
 
 @pytest.mark.parametrize("cfg", list(BERT_CONFIGS))
-def test_bert_models_grad_parity(cfg):
+def test_bert_models_grad_parity(cfg, gemm_prec):
     g = Golden(cfg)
     model = build_bert_model(g)
     x = g.inputs("cuda")
@@ -192,7 +200,7 @@ def test_bert_models_grad_parity(cfg):
         np.testing.assert_allclose(got, want, rtol=0, atol=max(1e-3 * scale, 2e-6), err_msg=n)
 
 
-def test_xformer_bert_base_width_vs_oracle():
+def test_xformer_bert_base_width_vs_oracle(gemm_prec):
     """BERT-base width (768, 12 heads, 3072) with 2 layers on the full 501-token user sequence
     and 30-token titles, against the fp32 CPU oracle (logits and a few gradients)."""
     from newsrec_amd.bert import BertConfig

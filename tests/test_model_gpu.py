@@ -24,8 +24,17 @@ def _setup(cfg):
     return g, model, g.inputs("cuda")
 
 
+@pytest.fixture(params=["bf16x6", "f32"])
+def gemm_prec(request):
+    """Both GEMM arithmetics (nr_gemm_set_precision) are held to the same parity bars."""
+    from newsrec_amd import _lib as Lb, kernels as Kn
+    old = Kn.set_gemm_precision(Lb.GEMM_BF16X6 if request.param == "bf16x6" else Lb.GEMM_F32)
+    yield request.param
+    Kn.set_gemm_precision(old)
+
+
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_forward_parity(cfg):
+def test_forward_parity(cfg, gemm_prec):
     g, model, x = _setup(cfg)
     model.eval()
     with torch.no_grad():
@@ -42,7 +51,7 @@ def test_forward_parity(cfg):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS)
-def test_grad_parity(cfg):
+def test_grad_parity(cfg, gemm_prec):
     g, model, x = _setup(cfg)
     model.train()
     logits, _ = model(x)
