@@ -42,12 +42,26 @@ __device__ __forceinline__ uint32_t bf_rne(float x) {
   return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
 }
 __device__ __forceinline__ float bf_f(uint32_t b) { return __uint_as_float(b << 16); }
+#ifndef NR_SPLIT_MANUAL_RNE
+// hardware conversions: the compiler pairs the casts into v_cvt_pk_bf16_f32 (round to nearest even)
+__device__ __forceinline__ uint32_t bf_bits(__bf16 v) { return (uint32_t)__builtin_bit_cast(uint16_t, v); }
+__device__ __forceinline__ void split1(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
+  const __bf16 hb = (__bf16)x;
+  const float r = x - (float)hb;   // exact
+  const __bf16 mb = (__bf16)r;
+  const __bf16 lb = (__bf16)(r - (float)mb);
+  h = bf_bits(hb);
+  m = bf_bits(mb);
+  l = bf_bits(lb);
+}
+#else
 __device__ __forceinline__ void split1(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
   h = bf_rne(x);
   const float r = x - bf_f(h);   // exact
   m = bf_rne(r);
   l = bf_rne(r - bf_f(m));
 }
+#endif
 __device__ __forceinline__ void split4(float a, float b, float c, float d, uint2& p0, uint2& p1, uint2& p2) {
   uint32_t h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
   split1(a, h0, m0, l0);

@@ -61,38 +61,93 @@ class Partition_Sampler:
 
 
 class GradSync:
-    """All-reduce-SUM of every gradient over the group; ``__call__`` (after backward) returns the
-    1/world factor for ``FusedAdam.step(grad_scale=...)``.
+    """The DDP all-reduce-mean of every gradient; ``__call__`` (after backward) returns the 1/world
+    factor for ``FusedAdam.step(grad_scale=...)``.
 
-    overlap_tables: install the word-table gradient hook so the table's all-reduce starts inside
-    the backward (the Function then hands the table its gradient directly)."""
+    * word table (dense [30522, 768] gradient, produced last in the backward): its all-reduce is
+      started from INSIDE the news-tower backward (TABLE_GRAD_HOOK) and overlaps the remaining
+      weight-gradient GEMMs;
+    * row-sparse tables (LSTUR's 876,957-row user table, SPARSE_GRAD_HOOK): an exact row-sparse
+      exchange -- all-gather of the step's (row id, gradient row) pairs, then every rank adds all
+      ranks' rows into a zero dense gradient in rank order (the same sum DDP's dense all-reduce
+      forms, at B rows per rank instead of 526 MB);
+    * every other gradient: flattened into buckets of <= ``bucket_mb`` MB, one all-reduce per
+      bucket (a few large collectives over xGMI instead of one per parameter).
+    """
 
-    def __init__(self, model, group=None, overlap_tables=True):
+    def __init__(self, model, group=None, overlap_tables=True, sparse_tables=True, bucket_mb=128):
         self.model = model
         self.group = group
         self.world = dist.get_world_size(group)
         self.pending = []
+        self.sparse = []
+        self.bucket_elems = int(bucket_mb * (1 << 20) // 4)
         self.overlap = overlap_tables and self.world > 1
+        self.use_sparse = sparse_tables and self.world > 1
         if self.overlap:
             functions.TABLE_GRAD_HOOK.set(self._table_hook)
+        if self.use_sparse:
+            functions.SPARSE_GRAD_HOOK.set(self._sparse_hook)
 
     def _table_hook(self, table, dtable):
         work = dist.all_reduce(dtable, group=self.group, async_op=True)
         self.pending.append((table, dtable, work))
         return True
 
+    def _sparse_hook(self, table, rows, grads):
+        rows = rows.reshape(-1).contiguous()
+        grads = grads.reshape(rows.numel(), -1).contiguous()
+        ids = [torch.empty_like(rows) for _ in range(self.world)]
+        gs = [torch.empty_like(grads) for _ in range(self.world)]
+        w1 = dist.all_gather(ids, rows, group=self.group, async_op=True)
+        w2 = dist.all_gather(gs, grads, group=self.group, async_op=True)
+        self.sparse.append((table, ids, gs, w1, w2))
+        return True
+
     def close(self):
         if self.overlap:
             functions.TABLE_GRAD_HOOK.set(None)
+        if self.use_sparse:
+            functions.SPARSE_GRAD_HOOK.set(None)
+
+    def _buckets(self, params):
+        out, cur, n = [], [], 0
+        for p in params:
+            if cur and n + p.grad.numel() > self.bucket_elems:
+                out.append(cur)
+                cur, n = [], 0
+            cur.append(p)
+            n += p.grad.numel()
+        if cur:
+            out.append(cur)
+        return out
 
     def __call__(self):
         if self.world == 1:
             return 1.0
-        hooked = {id(t) for t, _, _ in self.pending}
-        works = [dist.all_reduce(p.grad, group=self.group, async_op=True)
-                 for p in self.model.parameters() if p.grad is not None and id(p) not in hooked]
-        for w in works:
+        hooked = {id(t) for t, _, _ in self.pending} | {id(t) for t, *_ in self.sparse}
+        dense = [p for p in self.model.parameters() if p.grad is not None and id(p) not in hooked]
+        flights = []
+        for bucket in self._buckets(dense):
+            inplace = len(bucket) == 1 and bucket[0].grad.is_contiguous()
+            flat = bucket[0].grad.view(-1) if inplace else torch.cat([p.grad.reshape(-1) for p in bucket])
+            flights.append((bucket, flat, inplace, dist.all_reduce(flat, group=self.group, async_op=True)))
+        for table, ids, gs, w1, w2 in self.sparse:
+            w1.wait()
+            w2.wait()
+            g = torch.zeros_like(table)
+            for r in range(self.world):      # rank order: every rank forms the same sum
+                g.index_add_(0, ids[r], gs[r])
+            table.grad = g if table.grad is None else table.grad.add_(g)
+        self.sparse = []
+        for bucket, flat, inplace, w in flights:
             w.wait()
+            if not inplace:
+                off = 0
+                for p in bucket:
+                    n = p.grad.numel()
+                    p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                    off += n
         for table, dtable, w in self.pending:
             w.wait()
             if table.grad is None:

@@ -113,6 +113,25 @@ class _TableGradHook:
 TABLE_GRAD_HOOK = _TableGradHook()
 
 
+class _SparseGradHook:
+    """Optional callback ``hook(table_param, rows [n] int64, grads [n, E]) -> bool`` for tables whose
+    step gradient touches only a few rows (LSTUR's user table: B rows of 876,957).  Returning True
+    means the callback owns the gradient (e.g. an exact row-sparse exchange across ranks) and the
+    Function returns None for the table instead of a dense [V, E] gradient."""
+
+    def __init__(self):
+        self.fn = None
+
+    def set(self, fn):
+        self.fn = fn
+
+    def __call__(self, table, rows, grads):
+        return bool(self.fn(table, rows, grads)) if self.fn is not None else False
+
+
+SPARSE_GRAD_HOOK = _SparseGradHook()
+
+
 # ---------------------------------------------------------------------- MHA news encoder
 
 class MHANewsFn(torch.autograd.Function):
@@ -385,6 +404,7 @@ class RNNUserFn(torch.autograd.Function):
                   h0=user_table if user_table is not None else None, h0_idx=h0_idx, mask=mask, reverse=reverse)
         ctx.save_for_backward(x, w_ih, w_hh, gates, hprev, cprev, mask, h0_idx, user_table)
         ctx.cfg = (cell, B, N, reverse)
+        ctx.table_ref = user_table
         return hout
 
     @staticmethod
@@ -410,8 +430,9 @@ class RNNUserFn(torch.autograd.Function):
         _proj_wgrad(dgh_, K.operand(hprev, L.MNCONTIG), dw_hh, db_hh, B * N)
         dtab = None
         if user_table is not None and ctx.needs_input_grad[5]:
-            dtab = torch.zeros_like(user_table)
-            K.embedding_bwd(dh0, h0_idx, dtab, padding_idx=None)
+            if not SPARSE_GRAD_HOOK(ctx.table_ref, h0_idx, dh0):
+                dtab = torch.zeros_like(user_table)
+                K.embedding_bwd(dh0, h0_idx, dtab, padding_idx=None)
         return dx, dw_ih, dw_hh, db_ih, db_hh, dtab, None, None, None, None, None, None
 
 

@@ -26,7 +26,9 @@ class Tiny(torch.nn.Module):
         super().__init__()
         torch.manual_seed(0)
         self.table = torch.nn.Parameter(torch.randn(10, 4))
+        self.users = torch.nn.Parameter(torch.randn(50, 4))
         self.lin = torch.nn.Linear(4, 3)
+        self.lin2 = torch.nn.Linear(3, 2)
 
 
 def _grads(model, x, use_hook):
@@ -45,8 +47,22 @@ def _grads(model, x, use_hook):
             if use_hook and F.TABLE_GRAD_HOOK(ctx.table_ref, dt):
                 dt = None
             return dt, None
+    class UserRows(torch.autograd.Function):   # LSTUR's h0 = userEmbedding[u] (RNNUserFn)
+        @staticmethod
+        def forward(ctx, table, idx):
+            ctx.save_for_backward(idx)
+            ctx.table_ref = table
+            return table[idx]
+
+        @staticmethod
+        def backward(ctx, g):
+            (idx,) = ctx.saved_tensors
+            if use_hook and F.SPARSE_GRAD_HOOK(ctx.table_ref, idx, g):
+                return None, None
+            return torch.zeros_like(ctx.table_ref).index_add_(0, idx, g), None
     model.zero_grad(set_to_none=True)
-    out = model.lin(Gather.apply(model.table, x))
+    u = torch.tensor([int(x[0]) * 7 % 50, 3, 3])    # a repeated user row, a rank-dependent one
+    out = model.lin2(model.lin(Gather.apply(model.table, x) + UserRows.apply(model.users, u)))
     (out ** 2).sum().backward()
 
 
@@ -56,7 +72,7 @@ def _worker(rank, world, port, q):
     D.setup(rank, world, backend="gloo", master_port=str(port))
     model = Tiny()
     x = torch.tensor([rank, rank + 3, 7])
-    sync = D.GradSync(model)
+    sync = D.GradSync(model, bucket_mb=1e-4)   # tiny buckets: several collectives
     _grads(model, x, use_hook=True)
     scale = sync()
     sync.close()
