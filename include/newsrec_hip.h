@@ -270,6 +270,23 @@ int nr_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, 
             float lr, float beta1, float beta2, float eps, float weight_decay, int64_t step,
             const int64_t* step_dev, float grad_scale, hipStream_t stream);
 
+/* One torch.optim.Adam step over many tensors in as few launches as possible (<= 40 tensors per
+ * launch, descriptors passed by value: graph-capturable).  Per tensor: contiguous fp32 param /
+ * grad / exp_avg / exp_avg_sq of n elements, its group's lr, and the step count after increment
+ * (host `step`, or `step_dev` on the device).  Same arithmetic as nr_adam. */
+typedef struct nr_adam_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t n;
+  float lr;
+  int64_t step;
+  const int64_t* step_dev;
+} nr_adam_tensor;
+int nr_adam_multi(const nr_adam_tensor* tensors, int32_t count, float beta1, float beta2, float eps,
+                  float weight_decay, float grad_scale, hipStream_t stream);
+
 /* out[i] = table[idx[i]] rows of E floats (E % 4 == 0).  BERT_Embedding.forward, BERT.py:39. */
 int nr_embedding_fwd(const float* table, int64_t V, int64_t E, const int64_t* idx, int64_t n,
                      float* out, hipStream_t stream);

@@ -229,6 +229,27 @@ struct Loader {
     }
   }
 
+  // bf16x6, split ahead of the publish (the VALU work overlaps the current tile's MFMAs)
+  uint2 sp[KC ? NV : 1][3];
+  __device__ __forceinline__ void presplit() {
+    if constexpr (KC) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) split4(v[i].x, v[i].y, v[i].z, v[i].w, sp[i][0], sp[i][1], sp[i][2]);
+    }
+  }
+  __device__ __forceinline__ void store_presplit(uint16_t* lds, int tid) const {
+    if constexpr (KC) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int f = tid + 256 * i;
+        uint16_t* q = lds + (f >> 3) * SROW + 4 * (f & 7);
+        *reinterpret_cast<uint2*>(q) = sp[i][0];
+        *reinterpret_cast<uint2*>(q + SPL) = sp[i][1];
+        *reinterpret_cast<uint2*>(q + 2 * SPL) = sp[i][2];
+      }
+    }
+  }
+
   // bf16x6 image (K-contiguous operands only): the float4 of 4 k of one row -> 3 planes
   __device__ __forceinline__ void store_split(uint16_t* lds, int tid) const {
     if constexpr (KC) {
@@ -294,6 +315,24 @@ struct MNBlk {
     *reinterpret_cast<uint2*>(q) = p0;
     *reinterpret_cast<uint2*>(q + SPL) = p1;
     *reinterpret_cast<uint2*>(q + 2 * SPL) = p2;
+  }
+
+  uint2 sp[4][3];
+  __device__ __forceinline__ void presplit() {
+    split4(v[0].x, v[1].x, v[2].x, v[3].x, sp[0][0], sp[0][1], sp[0][2]);
+    split4(v[0].y, v[1].y, v[2].y, v[3].y, sp[1][0], sp[1][1], sp[1][2]);
+    split4(v[0].z, v[1].z, v[2].z, v[3].z, sp[2][0], sp[2][1], sp[2][2]);
+    split4(v[0].w, v[1].w, v[2].w, v[3].w, sp[3][0], sp[3][1], sp[3][2]);
+  }
+  __device__ __forceinline__ void store_presplit(uint16_t* lds, int tid) const {
+    const int kg = tid & 7, cg = tid >> 3;
+    uint16_t* q = lds + (4 * cg) * SROW + 4 * kg;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      *reinterpret_cast<uint2*>(q + u * SROW) = sp[u][0];
+      *reinterpret_cast<uint2*>(q + u * SROW + SPL) = sp[u][1];
+      *reinterpret_cast<uint2*>(q + u * SROW + 2 * SPL) = sp[u][2];
+    }
   }
 
   __device__ __forceinline__ void store_split(uint16_t* lds, int tid) const {
@@ -870,6 +909,9 @@ __global__ __launch_bounds__(256, 2) void gemm_split_kernel(Args g) {
 #define NR_MF(X, Y)                                                                              \
   acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][Y], a[i][X], acc[i][j], 0, 0, 0) \
                  : __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][X], b[j][Y], acc[i][j], 0, 0, 0)
+#ifdef NR_SPLIT_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -881,14 +923,28 @@ __global__ __launch_bounds__(256, 2) void gemm_split_kernel(Args g) {
           NR_MF(0, 1);
           NR_MF(0, 0);
         }
+#ifdef NR_SPLIT_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
 #undef NR_MF
+#ifdef NR_SPLIT_EARLY
+      if (s == 0 && had_staged) {   // split P+1 while P's second k-step runs on the matrix cores
+        la.presplit();
+        lb.presplit();
+      }
+#endif
     }
     __syncthreads();                // every wave is done reading P
     const int old = cp.id;
     const int64_t om0 = cp.u.m0, on0 = cp.u.n0;
     if (!had_staged) break;
+#ifdef NR_SPLIT_EARLY
+    la.store_presplit(As, tid);     // publish P+1 (split during P's MFMAs)
+    lb.store_presplit(Bs, tid);
+#else
     la.store_split(As, tid);        // publish P+1 (its loads landed during P's MFMAs)
     lb.store_split(Bs, tid);
+#endif
     staged = step_load();           // and start P+2
     __syncthreads();
     advance(cp);

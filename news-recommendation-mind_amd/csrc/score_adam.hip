@@ -138,6 +138,79 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 #undef NR_ADAM1
 }
 
+// ---- multi-tensor Adam: up to kAdamMulti tensors per launch, their descriptors passed by value
+// (graph-capturable: no device-side pointer table), blocks assigned to tensors by a prefix sum
+constexpr int kAdamMulti = 40;
+constexpr int kAdamChunk = 4096;   // elements per block (256 threads x 4 float4)
+
+struct AdamEntry {
+  float* p; const float* g; float* m; float* v;
+  int64_t n;
+  const int64_t* step_dev;   // device step count (graph replays) or null
+  float step_size;           // lr / (1 - beta1^t) when step_dev is null
+  float bc2_sqrt;            // sqrt(1 - beta2^t) when step_dev is null
+  float lr;
+};
+
+struct AdamMulti {
+  AdamEntry e[kAdamMulti];
+  int32_t blk_off[kAdamMulti + 1];
+  int count;
+  float b1, b2, eps, wd, gscale;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float b1, float b2, float eps,
+                                          float wd, float gscale, float step, float bc2_sqrt) {
+  float gc = g * gscale;
+  if (wd != 0.f) gc = fmaf(wd, p, gc);
+  m = fmaf(1.f - b1, gc - m, m);
+  v = fmaf(v, b2, (1.f - b2) * gc * gc);
+  const float den = sqrtf(v) / bc2_sqrt + eps;
+  p = fmaf(-step, m / den, p);
+}
+
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
+  const int b = blockIdx.x;
+  int t = 0;
+  while (t + 1 < a.count && b >= a.blk_off[t + 1]) ++t;
+  const AdamEntry& e = a.e[t];
+  float step = e.step_size, bc2_sqrt = e.bc2_sqrt;
+  if (e.step_dev) {
+    const double st = (double)*e.step_dev;
+    step = (float)((double)e.lr / (1.0 - pow((double)a.b1, st)));
+    bc2_sqrt = (float)sqrt(1.0 - pow((double)a.b2, st));
+  }
+  const int64_t base = (int64_t)(b - a.blk_off[t]) * kAdamChunk;
+  const int64_t end = base + kAdamChunk < e.n ? base + kAdamChunk : e.n;
+  const bool vec = ((reinterpret_cast<uintptr_t>(e.p) | reinterpret_cast<uintptr_t>(e.g) |
+                     reinterpret_cast<uintptr_t>(e.m) | reinterpret_cast<uintptr_t>(e.v)) & 15) == 0;
+  if (vec && end - base == kAdamChunk) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = base / 4 + u * 256 + threadIdx.x;
+      float4 pp = reinterpret_cast<float4*>(e.p)[i];
+      const float4 gg = reinterpret_cast<const float4*>(e.g)[i];
+      float4 mm = reinterpret_cast<float4*>(e.m)[i];
+      float4 vv = reinterpret_cast<float4*>(e.v)[i];
+      adam_elem(pp.x, gg.x, mm.x, vv.x, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
+      adam_elem(pp.y, gg.y, mm.y, vv.y, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
+      adam_elem(pp.z, gg.z, mm.z, vv.z, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
+      adam_elem(pp.w, gg.w, mm.w, vv.w, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
+      reinterpret_cast<float4*>(e.p)[i] = pp;
+      reinterpret_cast<float4*>(e.m)[i] = mm;
+      reinterpret_cast<float4*>(e.v)[i] = vv;
+    }
+  } else {
+    for (int64_t i = base + threadIdx.x; i < end; i += 256) {
+      float pp = e.p[i], mm = e.m[i], vv = e.v[i];
+      adam_elem(pp, e.g[i], mm, vv, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
+      e.p[i] = pp;
+      e.m[i] = mm;
+      e.v[i] = vv;
+    }
+  }
+}
+
 // one wave per output row, float4 along E
 __global__ __launch_bounds__(256) void embedding_fwd_kernel(const float* table, int64_t E, const int64_t* idx,
                                                             int64_t n, float* out) {
@@ -165,9 +238,17 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* x, int64_t ldx
   if (c >= cols) return;
   const int64_t r0 = (int64_t)blockIdx.y * chunk;
   const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
-  float acc = 0.f;
-  for (int64_t r = r0; r < r1; ++r) acc += x[r * ldx + c];
-  atomicAdd(&out[c], acc);
+  // eight independent partial sums: eight loads in flight per thread (the loop is latency-bound
+  // with one)
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int64_t r = r0;
+  const float* p = x + r0 * ldx + c;
+  for (; r + 8 <= r1; r += 8, p += 8 * ldx) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += p[u * ldx];
+  }
+  for (; r < r1; ++r, p += ldx) a[0] += *p;
+  atomicAdd(&out[c], ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])));
 }
 
 }  // namespace
@@ -248,7 +329,7 @@ extern "C" int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols
   if (!x || !out) return NR_EINVAL(1);
   if (rows == 0 || cols == 0) return NR_OK;
   const int64_t cb = (cols + 255) / 256;
-  int64_t chunks = (512 + cb - 1) / cb;
+  int64_t chunks = (1024 + cb - 1) / cb;
   if (chunks > rows) chunks = rows;
   const int64_t chunk = (rows + chunks - 1) / chunks;
   chunks = (rows + chunk - 1) / chunk;
@@ -256,4 +337,50 @@ extern "C" int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols
                      cols, chunk, out);
   NR_LAUNCH_CHECK();
   return NR_OK;
+}
+
+namespace {
+int adam_multi_launch(AdamMulti& a, int64_t blocks, hipStream_t stream) {
+  if (a.count == 0) return NR_OK;
+  a.blk_off[a.count] = (int32_t)blocks;
+  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+}  // namespace
+
+extern "C" int nr_adam_multi(const nr_adam_tensor* tensors, int32_t count, float beta1, float beta2, float eps,
+                             float weight_decay, float grad_scale, hipStream_t stream) {
+  if (count < 0 || (count > 0 && !tensors)) return NR_EINVAL(0);
+  for (int32_t t = 0; t < count; ++t) {   // validate everything before the first launch
+    const nr_adam_tensor& d = tensors[t];
+    if (d.n < 0 || (d.step < 1 && !d.step_dev)) return NR_EINVAL(1);
+    if (d.n > 0 && (!d.param || !d.grad || !d.exp_avg || !d.exp_avg_sq)) return NR_EINVAL(2);
+    if ((d.n + kAdamChunk - 1) / kAdamChunk > 0x3fffffff) return NR_EINVAL(3);
+  }
+  AdamMulti a;
+  a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.wd = weight_decay; a.gscale = grad_scale;
+  a.count = 0;
+  int64_t blocks = 0;
+  for (int32_t t = 0; t < count; ++t) {
+    const nr_adam_tensor& d = tensors[t];
+    if (d.n == 0) continue;
+    const int64_t nb = (d.n + kAdamChunk - 1) / kAdamChunk;
+    if (a.count == kAdamMulti || blocks + nb > 0x7fffffff) {
+      const int rc = adam_multi_launch(a, blocks, stream);
+      if (rc) return rc;
+      a.count = 0;
+      blocks = 0;
+    }
+    AdamEntry& e = a.e[a.count];
+    e.p = d.param; e.g = d.grad; e.m = d.exp_avg; e.v = d.exp_avg_sq; e.n = d.n;
+    e.step_dev = d.step_dev; e.lr = d.lr;
+    const double st = (double)(d.step < 1 ? 1 : d.step);   // bias corrections in double, as torch's Python floats
+    e.step_size = (float)((double)d.lr / (1.0 - pow((double)beta1, st)));
+    e.bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, st));
+    a.blk_off[a.count] = (int32_t)blocks;
+    blocks += nb;
+    ++a.count;
+  }
+  return adam_multi_launch(a, blocks, stream);
 }

@@ -37,6 +37,12 @@ class nr_operand(ctypes.Structure):
                 ("map", c_i32), ("seq_len", c_i32), ("seg", c_i32), ("layout", c_i32)]
 
 
+class nr_adam_tensor(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("n", c_i64), ("lr", c_f32), ("step", c_i64),
+                ("step_dev", ctypes.c_void_p)]
+
+
 # name -> argtypes (restype int32 unless listed in _RESTYPES)
 _SIGS = {
     "nr_gemm_f32": [c_i64, c_i64, c_i64, ctypes.POINTER(nr_operand), ctypes.POINTER(nr_operand),
@@ -97,6 +103,7 @@ _SIGS = {
                          c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr],
     "nr_tanh_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr],
     "nr_gemm_set_precision": [c_i32],
+    "nr_adam_multi": [ctypes.POINTER(nr_adam_tensor), c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_ptr],
     "nr_gemm_get_precision": [],
 }
 

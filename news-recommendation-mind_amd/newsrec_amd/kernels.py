@@ -324,6 +324,28 @@ def adam(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, 
            weight_decay, step, L.ptr(step_dev), grad_scale, L.stream_ptr(param))
 
 
+def adam_multi(entries, beta1, beta2, eps, weight_decay, grad_scale=1.0):
+    """entries: [(param, grad, exp_avg, exp_avg_sq, lr, step)] with ``step`` an int or an int64 CUDA
+    scalar; one nr_adam_multi call (a launch per <= 40 tensors)."""
+    if not entries:
+        return
+    arr = (L.nr_adam_tensor * len(entries))()
+    for i, (p, g, m, v, lr, step) in enumerate(entries):
+        _f32(p, g, m, v)
+        n = p.numel()
+        for t in (p, g, m, v):
+            if not t.is_contiguous() or t.numel() != n:
+                raise L.HipError("adam_multi: tensors must be contiguous with equal numel")
+        sd = 0
+        if torch.is_tensor(step):
+            if step.dtype != torch.int64 or not step.is_cuda:
+                raise L.HipError("adam_multi: a device step count must be an int64 CUDA tensor")
+            sd, step = step.data_ptr(), 0
+        arr[i] = L.nr_adam_tensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, float(lr), int(step), sd)
+    L.call("nr_adam_multi", arr, len(entries), beta1, beta2, eps, weight_decay, grad_scale,
+           L.stream_ptr(entries[0][0]))
+
+
 def embedding_fwd(table, idx, out):
     _f32(table, out)
     _check_rows(idx, None, "idx")

@@ -38,11 +38,15 @@ class FusedAdam(torch.optim.Optimizer):
             steps = [st["step"] for _, _, st in todo]
             if steps:
                 torch._foreach_add_(steps, 1)
+        # one nr_adam_multi call per (betas, eps, weight_decay) combination: every tensor of the
+        # step in a few launches instead of one launch per parameter
+        batches = {}
         for group, p, st in todo:
-            b1, b2 = group["betas"]
             if not self.capturable:
                 st["step"] += 1
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-            K.adam(p, g, st["exp_avg"], st["exp_avg_sq"], group["lr"], b1, b2, group["eps"],
-                   group["weight_decay"], st["step"], grad_scale)
+            key = (tuple(group["betas"]), group["eps"], group["weight_decay"])
+            batches.setdefault(key, []).append((p, g, st["exp_avg"], st["exp_avg_sq"], group["lr"], st["step"]))
+        for (betas, eps, wd), entries in batches.items():
+            K.adam_multi(entries, betas[0], betas[1], eps, wd, grad_scale)
         return loss

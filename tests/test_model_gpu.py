@@ -110,6 +110,29 @@ def test_fused_adam_kernel_matches_torch_adam():
         torch.testing.assert_close(q.detach().cpu(), p.detach(), rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("capturable", [False, True])
+def test_adam_multi_many_tensors(capturable):
+    """nr_adam_multi over 90 tensors (three launches of <= 40), ragged sizes, two param groups,
+    host and device step counts, against torch.optim.Adam."""
+    from newsrec_amd.optim import FusedAdam
+    g = torch.Generator().manual_seed(1)
+    shapes = [(int(n),) for n in torch.randint(1, 9000, (88,), generator=g)] + [(4096,), (30522 * 3,)]
+    ps = [torch.randn(s, generator=g) for s in shapes]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    mine = [p.clone().cuda().requires_grad_(True) for p in ps]
+    o1 = torch.optim.Adam([{"params": ref[:50], "lr": 1e-3}, {"params": ref[50:], "lr": 6e-6}])
+    o2 = FusedAdam([{"params": mine[:50], "lr": 1e-3}, {"params": mine[50:], "lr": 6e-6}], capturable=capturable)
+    for step in range(3):
+        for p, q in zip(ref, mine):
+            gg = torch.randn(p.shape, generator=g)
+            p.grad = gg.clone()
+            q.grad = gg.cuda()
+        o1.step()
+        o2.step()
+    for p, q in zip(ref, mine):
+        torch.testing.assert_close(q.detach().cpu(), p.detach(), rtol=0, atol=1e-6)
+
+
 def test_unfused_composition_matches_fused():
     """encoderN(embedding(tokens), mask) (the reference composition) == the fused path."""
     g, model, x = _setup("nrms")
