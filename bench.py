@@ -249,6 +249,34 @@ def xformer_leg(dev, steps=5, warmup=2, b=B):
             "eval_tflops": round(f / ev / 1e12, 1)}
 
 
+def config_legs(dev, steps=10, warmup=3):
+    """The other two-tower configurations of BASELINE.json (configs[1], configs[3] and the GRU
+    variant) beside the headline: train steps (fwd + NLL + bwd + Adam) on pre-formed synthetic
+    MIND-shaped batches of B = 32, one GPU, eager.  H = 150 (Manager.py:61)."""
+    from newsrec_amd.manager import build_model, get_optim
+    gen = torch.Generator().manual_seed(11)
+    batches = [synth_batch(gen, dev) for _ in range(2)]
+    out = {}
+    for name, encN, encU in (("cnn_attn", "cnn", "attn"), ("cnn_lstur", "cnn", "lstur"), ("cnn_gru", "cnn", "gru")):
+        torch.manual_seed(42)
+        model = build_model(encN, encU, 150, vocab=V, device=dev, user_num=USERS_LARGE)
+        model.train()
+        opt = get_optim(model)
+        for i in range(warmup + steps):
+            if i == warmup:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            train_step(model, opt, batches[i % 2], None)
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / steps
+        out[name] = {"impressions_per_s": round(B / el, 1), "ms_per_step": round(el * 1e3, 3)}
+        del model, opt
+    torch.cuda.empty_cache()
+    out["note"] = ("eager train steps, B=32, H=150, V=30522 trainable table, MIND-large user table for LSTUR "
+                   "(876,957 rows); lstur = the reference's LSTUR_User_Encoder (LSTM, RNN.py:76-104)")
+    return out
+
+
 def cpu_baseline(seconds=20.0):
     """The oracle (oracle/restatement.py, torch fp32 CPU) on the same NRMS step, timed on this
     host's cores over a bounded sample (steps of B=32 until ~`seconds` elapse)."""
@@ -283,6 +311,7 @@ def main():
                     help="device: form each batch on the GPU from a resident MIND split; resident: pre-formed")
     ap.add_argument("--eval-impr", type=int, default=DEV_IMPR_LARGE,
                     help="dev impressions of the fast-eval leg (0 skips it)")
+    ap.add_argument("--config-legs", type=int, default=1, help="1: time configs[1]/[3] beside the headline (N=1)")
     ap.add_argument("--xformer-steps", type=int, default=5,
                     help="timed XFormer (configs[4]) train steps reported beside the headline (0 skips; N=1 only)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
@@ -374,6 +403,7 @@ def main():
     # eval (b): the fast-eval pipeline over a MIND-large-shaped dev split
     fast = fast_eval_leg(model, dev, world, rank, a.eval_impr) if a.eval_impr > 0 else None
     xf = xformer_leg(dev, a.xformer_steps) if (a.xformer_steps > 0 and world == 1) else None
+    legs = config_legs(dev) if (a.config_legs and world == 1) else None
 
     if rank == 0:
         ms = el / a.steps * 1e3
@@ -423,6 +453,8 @@ def main():
         }
         if xf is not None:
             out["xformer"] = xf
+        if legs is not None:
+            out["other_configs"] = legs
         if not a.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -119,6 +119,19 @@ class MINDStore:
         np.savez(path, meta=meta, **{k: getattr(self, k).cpu().numpy() for k in keys})
 
     @classmethod
+    def from_reference_cache(cls, news_pkl, behaviors_pkl, mode, device="cuda", seed=None, **opts):
+        """A store from the caches the reference's MIND dataset writes:
+        ``news.pkl`` = {"encoded_news": i64 [N+1, 512], "attn_mask": i64 [N+1, 512]}
+        (utils/MIND.py:144-151) and the split's ``behaviors.pkl`` (:199-207 train, dev/test
+        below it).  These are pickles: load only caches your own reference run wrote."""
+        import pickle
+        with open(news_pkl, "rb") as f:
+            news = pickle.load(f)
+        with open(behaviors_pkl, "rb") as f:
+            behaviors = pickle.load(f)
+        return cls(news, behaviors, mode, device=device, seed=seed, **opts)
+
+    @classmethod
     def load(cls, path, device="cuda", seed=None):
         with np.load(path, allow_pickle=False) as z:
             meta = z["meta"]
@@ -381,3 +394,15 @@ def synthetic_arrays(mode, n_news, n_impr, his_len=(50, 100), neg_len=(4, 60), c
             lab[off[full] + (first[full] - off[full] + 1) % (off[full + 1] - off[full])] = 0
             a["cand_labels"] = lab
     return a
+
+
+def write_reference_cache(news_pkl, behaviors_pkl, encoded_news, attn_mask, behaviors):
+    """Write caches in the reference's on-disk format (utils/MIND.py:144-151 and :199-207) so the
+    reference's own Manager / MIND dataset can run on them offline (the tokenizer is skipped when
+    the caches exist).  ``behaviors`` is the split's dict ("imprs", "histories", "negatives" for
+    train, "uindexes")."""
+    import pickle
+    with open(news_pkl, "wb") as f:
+        pickle.dump({"encoded_news": np.asarray(encoded_news), "attn_mask": np.asarray(attn_mask)}, f)
+    with open(behaviors_pkl, "wb") as f:
+        pickle.dump(behaviors, f)

@@ -236,3 +236,27 @@ def test_eval_gathers_gloo():
     assert out[0][0] == list(range(12)) and out[1][0] is None
     for r in range(world):
         assert out[r][1] == [0.0] * 4 + [1.0] * 4 + [2.0] * 2
+
+
+def test_reference_cache_round_trip(tmp_path):
+    """news.pkl / behaviors.pkl in the reference's format (MIND.py:144-151, :199-207) -> MINDStore:
+    the token table is truncated to L with [SEP] forced (MIND.py:103-108), CSR arrays match."""
+    import numpy as np
+    from newsrec_amd.mind import MINDStore, write_reference_cache
+    rng = np.random.default_rng(0)
+    enc = rng.integers(1000, 30000, (7, 512))
+    enc[:, 0] = 101
+    msk = np.ones((7, 512), np.int64)
+    enc[0, 2:] = 0
+    msk[0, 2:] = 0
+    beh = {"imprs": [(0, 3), (1, 5)], "histories": [[1, 2], []], "negatives": [[4, 6], [1]], "uindexes": [7, 9]}
+    write_reference_cache(tmp_path / "news.pkl", tmp_path / "behaviors.pkl", enc, msk, beh)
+    st = MINDStore.from_reference_cache(tmp_path / "news.pkl", tmp_path / "behaviors.pkl", "train", device="cpu",
+                                        signal_length=30)
+    tok = st.tok.numpy()
+    assert tok.shape == (7, 30)
+    assert (tok[1:, -1] == 102).all() and tok[0, -1] == 0
+    assert (tok[1:, :-1] == enc[1:, :29]).all()
+    assert st.his_off.tolist() == [0, 2, 2] and st.his_ids.tolist() == [1, 2]
+    assert st.neg_off.tolist() == [0, 2, 3] and st.neg_ids.tolist() == [4, 6, 1]
+    assert st.imprs.tolist() == [[0, 3], [1, 5]] and st.uindex.tolist() == [7, 9]
