@@ -11,6 +11,8 @@
 // coalesced layout.  The forward saves the activated gates and h_{t-1} (and c_{t-1}) of every
 // step, so the backward is exact BPTT without recomputation, and the weight gradients become
 // two more GEMMs: dW_ih = dGIᵀ X, dW_hh = dGHᵀ H_prev.
+#include <stdlib.h>
+
 #include "common.h"
 #include "../../include/newsrec_hip.h"
 
@@ -199,7 +201,206 @@ __global__ __launch_bounds__(256) void rnn_bwd_kernel(RnnArgs g) {
     for (int u = tid; u < H; u += blockDim.x) g.dh0[b * g.lddh0 + u] = dh[u];
 }
 
+// ---- weights-stationary forms for H = 150 (Manager.py:61): W_hh lives in registers for the whole
+// sequence (one gate row per thread in the forward, 150 weights of one column per thread in the
+// backward), so a step costs 150 FMAs against LDS-broadcast h (or dg) instead of 150 (or 600)
+// dependent L2 loads.  One workgroup per sequence, G*H threads (LSTM 600, GRU 450).
+// KR weights of each row in registers, the other H - KR in LDS as [k][row] (a wave reads 64
+// consecutive floats: conflict-free): 600 LSTM rows at 3 waves/SIMD leave ~168 VGPRs per lane.
+template <int H, int G, int KR>
+__global__ __launch_bounds__(((G * H + 63) / 64) * 64) void rnn_fwd_reg_kernel(RnnArgs g) {
+  constexpr int GH = G * H;
+  constexpr int KL = H - KR;
+  __shared__ __attribute__((aligned(16))) float h[H + 2];
+  __shared__ float c[H];
+  __shared__ float gh[GH];
+  __shared__ float wl[KL > 0 ? KL * GH : 1];
+  __shared__ int red;
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  float w[KR];
+  float bias = 0.f;
+  if (tid < GH) {
+#pragma unroll
+    for (int k = 0; k < KR; ++k) w[k] = g.whh[(int64_t)k * GH + tid];   // W_hhᵀ [H][GH]: row tid of W_hh
+    for (int k = KR; k < H; ++k) wl[(k - KR) * GH + tid] = g.whh[(int64_t)k * GH + tid];
+    bias = g.bhh ? g.bhh[tid] : 0.f;
+  }
+  if (tid == 0) red = 0;
+  if (tid < H) {
+    float h0 = 0.f;
+    if (g.h0) {
+      const int64_t r = g.h0_idx ? g.h0_idx[b] : b;
+      h0 = g.h0[r * g.ldh0 + tid];
+    }
+    h[tid] = h0;
+    c[tid] = 0.f;
+  }
+  if (tid < 2) h[H + tid] = 0.f;
+  __syncthreads();
+  const int len = seq_len(g, b, &red);
+  for (int t = 0; t < g.N; ++t) {
+    const int tt = g.reverse ? g.N - 1 - t : t;
+    const int64_t row = b * g.N + tt;
+    if (t >= len) {   // padded steps: zero what the backward GEMMs read
+      for (int r = tid; r < 4 * H; r += blockDim.x) g.gates[row * 4 * H + r] = 0.f;
+      if (tid < H) {
+        g.hprev[row * H + tid] = 0.f;
+        if (g.cprev) g.cprev[row * H + tid] = 0.f;
+      }
+      continue;
+    }
+    if (tid < GH) {
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+      for (int k = 0; k < KR; k += 4) {   // h is padded to a multiple of 4 with zeros
+        const float4 hv = *reinterpret_cast<const float4*>(&h[k]);
+        a0 = fmaf(w[k], hv.x, a0);
+        if (k + 1 < KR) a1 = fmaf(w[k + 1], hv.y, a1);
+        if (k + 2 < KR) a2 = fmaf(w[k + 2], hv.z, a2);
+        if (k + 3 < KR) a3 = fmaf(w[k + 3], hv.w, a3);
+        if ((k & 15) == 12) __builtin_amdgcn_sched_barrier(0);   // keep the h reads from all hoisting
+      }
+#pragma unroll 10
+      for (int k = KR; k < H; ++k) a0 = fmaf(wl[(k - KR) * GH + tid], h[k], a0);
+      gh[tid] = bias + ((a0 + a1) + (a2 + a3));
+    }
+    __syncthreads();
+    float hn = 0.f, cn = 0.f;
+    if (tid < H) {
+      const int u = tid;
+      const float* xs = g.gx + row * g.ldgx;
+      float* gs = g.gates + row * 4 * H;
+      g.hprev[row * H + u] = h[u];
+      if (G == 4) {
+        const float ig = sigm(xs[u] + gh[u]);
+        const float fg = sigm(xs[H + u] + gh[H + u]);
+        const float gg = tanhf(xs[2 * H + u] + gh[2 * H + u]);
+        const float og = sigm(xs[3 * H + u] + gh[3 * H + u]);
+        const float cc = fmaf(fg, c[u], ig * gg);
+        g.cprev[row * H + u] = c[u];
+        gs[u] = ig; gs[H + u] = fg; gs[2 * H + u] = gg; gs[3 * H + u] = og;
+        cn = cc;
+        hn = og * tanhf(cc);
+      } else {
+        const float rg = sigm(xs[u] + gh[u]);
+        const float zg = sigm(xs[H + u] + gh[H + u]);
+        const float ng = tanhf(fmaf(rg, gh[2 * H + u], xs[2 * H + u]));
+        gs[u] = rg; gs[H + u] = zg; gs[2 * H + u] = ng; gs[3 * H + u] = gh[2 * H + u];
+        hn = fmaf(zg, h[u] - ng, ng);
+      }
+    }
+    __syncthreads();
+    if (tid < H) {
+      h[tid] = hn;
+      c[tid] = cn;
+      if (t == len - 1) g.hout[b * g.ldho + tid] = hn;
+    }
+    __syncthreads();
+  }
+}
+
+template <int H, int G>
+__global__ __launch_bounds__(((G * H + 63) / 64) * 64) void rnn_bwd_reg_kernel(RnnArgs g) {
+  constexpr int GH = G * H;
+  __shared__ float dh[H];
+  __shared__ float dc[H];
+  __shared__ __attribute__((aligned(16))) float dg[GH + 4];
+  __shared__ float ps[G][H];
+  __shared__ int red;
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int kcol = tid % H, part = tid / H;   // thread: column kcol of W_hh rows part*H .. part*H+H-1
+  float w[H];
+  if (tid < GH) {
+#pragma unroll
+    for (int i = 0; i < H; ++i) w[i] = g.whh[(int64_t)(part * H + i) * H + kcol];   // W_hh [GH][H]
+  }
+  if (tid == 0) red = 0;
+  if (tid < H) {
+    dh[tid] = g.dhout[b * g.lddho + tid];
+    dc[tid] = 0.f;
+  }
+  if (tid < 4) dg[GH + tid] = 0.f;
+  __syncthreads();
+  const int len = seq_len(g, b, &red);
+  for (int t = len; t < g.N; ++t) {
+    const int tt = g.reverse ? g.N - 1 - t : t;
+    const int64_t row = b * g.N + tt;
+    for (int r = tid; r < GH; r += blockDim.x) {
+      g.dgi[row * g.lddg + r] = 0.f;
+      if (g.dgh) g.dgh[row * g.lddg + r] = 0.f;
+    }
+  }
+  for (int t = len - 1; t >= 0; --t) {
+    const int tt = g.reverse ? g.N - 1 - t : t;
+    const int64_t row = b * g.N + tt;
+    if (tid < H) {
+      const int u = tid;
+      const float* gs = g.gates + row * 4 * H;
+      float* dgi = g.dgi + row * g.lddg;
+      float* dgh = g.dgh ? g.dgh + row * g.lddg : nullptr;
+      if (G == 4) {
+        const float ig = gs[u], fg = gs[H + u], gg = gs[2 * H + u], og = gs[3 * H + u];
+        const float cp = g.cprev[row * H + u];
+        const float cc = fmaf(fg, cp, ig * gg);
+        const float tc = tanhf(cc);
+        const float dcc = dc[u] + dh[u] * og * (1.f - tc * tc);
+        const float di = dcc * gg * ig * (1.f - ig);
+        const float df = dcc * cp * fg * (1.f - fg);
+        const float dgg = dcc * ig * (1.f - gg * gg);
+        const float dog = dh[u] * tc * og * (1.f - og);
+        dgi[u] = di; dgi[H + u] = df; dgi[2 * H + u] = dgg; dgi[3 * H + u] = dog;
+        if (dgh) { dgh[u] = di; dgh[H + u] = df; dgh[2 * H + u] = dgg; dgh[3 * H + u] = dog; }
+        dg[u] = di; dg[H + u] = df; dg[2 * H + u] = dgg; dg[3 * H + u] = dog;
+        dc[u] = dcc * fg;
+      } else {
+        const float rg = gs[u], zg = gs[H + u], ng = gs[2 * H + u], ghn = gs[3 * H + u];
+        const float hp = g.hprev[row * H + u];
+        const float dn = dh[u] * (1.f - zg) * (1.f - ng * ng);
+        const float dz = dh[u] * (hp - ng) * zg * (1.f - zg);
+        const float dr = dn * ghn * rg * (1.f - rg);
+        dgi[u] = dr; dgi[H + u] = dz; dgi[2 * H + u] = dn;
+        dgh[u] = dr; dgh[H + u] = dz; dgh[2 * H + u] = dn * rg;
+        dg[u] = dr; dg[H + u] = dz; dg[2 * H + u] = dn * rg;
+        dc[u] = dh[u] * zg;
+      }
+    }
+    __syncthreads();
+    if (tid < GH) {
+      float a0 = 0.f, a1 = 0.f;
+      const float* d = dg + part * H;
+#pragma unroll
+      for (int i = 0; i < H; i += 2) {
+        a0 = fmaf(d[i], w[i], a0);
+        if (i + 1 < H) a1 = fmaf(d[i + 1], w[i + 1], a1);
+        if ((i & 15) == 14) __builtin_amdgcn_sched_barrier(0);
+      }
+      ps[part][kcol] = a0 + a1;
+    }
+    __syncthreads();
+    if (tid < H) {
+      float acc = G == 3 ? dc[tid] : 0.f;
+#pragma unroll
+      for (int p = 0; p < G; ++p) acc += ps[p][tid];
+      dh[tid] = acc;
+      if (G == 3) dc[tid] = 0.f;
+    }
+    __syncthreads();
+  }
+  if (g.dh0 && tid < H) g.dh0[b * g.lddh0 + tid] = dh[tid];
+}
+
 size_t rnn_smem(int cell, int H) { return (size_t)(2 * H + (cell == NR_CELL_LSTM ? 4 : 3) * H + 4) * sizeof(float); }
+
+bool reg_disabled() {   // NR_RNN_STREAM=1: the L2-streaming kernels (A/B, any H)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NR_RNN_STREAM");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
 
 }  // namespace
 
@@ -214,6 +415,12 @@ extern "C" int nr_rnn_fwd(int32_t cell, const float* gx, int64_t ldgx, const flo
   g.cell = cell; g.gx = gx; g.ldgx = ldgx; g.whh = whh_t; g.bhh = bhh; g.h0 = h0; g.ldh0 = ldh0;
   g.h0_idx = h0_idx; g.mask = mask; g.mask_dt = mask_dtype; g.reverse = reverse; g.B = B; g.N = N; g.H = H;
   g.gates = gates; g.hprev = hprev; g.cprev = cprev; g.hout = hout; g.ldho = ldho;
+  if (H == 150 && !reg_disabled()) {
+    if (cell == NR_CELL_LSTM) hipLaunchKernelGGL((rnn_fwd_reg_kernel<150, 4, 88>), dim3((unsigned)B), dim3(640), 0, stream, g);
+    else hipLaunchKernelGGL((rnn_fwd_reg_kernel<150, 3, 150>), dim3((unsigned)B), dim3(512), 0, stream, g);
+    NR_LAUNCH_CHECK();
+    return NR_OK;
+  }
   hipLaunchKernelGGL(rnn_fwd_kernel, dim3((unsigned)B), dim3(256), rnn_smem(cell, H), stream, g);
   NR_LAUNCH_CHECK();
   return NR_OK;
@@ -233,6 +440,12 @@ extern "C" int nr_rnn_bwd(int32_t cell, const float* whh, const float* gates, co
   g.cprev = const_cast<float*>(cprev); g.mask = mask; g.mask_dt = mask_dtype; g.reverse = reverse; g.B = B;
   g.N = N; g.H = H; g.dhout = dhout; g.lddho = lddho; g.dgi = dgi; g.dgh = dgh; g.lddg = lddg; g.dh0 = dh0;
   g.lddh0 = lddh0;
+  if (H == 150 && !reg_disabled()) {
+    if (cell == NR_CELL_LSTM) hipLaunchKernelGGL((rnn_bwd_reg_kernel<150, 4>), dim3((unsigned)B), dim3(640), 0, stream, g);
+    else hipLaunchKernelGGL((rnn_bwd_reg_kernel<150, 3>), dim3((unsigned)B), dim3(512), 0, stream, g);
+    NR_LAUNCH_CHECK();
+    return NR_OK;
+  }
   hipLaunchKernelGGL(rnn_bwd_kernel, dim3((unsigned)B), dim3(256), rnn_smem(cell, H), stream, g);
   NR_LAUNCH_CHECK();
   return NR_OK;
