@@ -280,7 +280,7 @@ struct Loader {
 // consecutive k to the [row][k] planes (b64 stores, 2-way bank aliasing).
 template <int MODE>
 struct MNBlk {
-  static_assert(MODE == MN_PLAIN || MODE == MN_GATHER, "MNBlk: plain or gathered rows");
+  static_assert(MODE == MN_PLAIN || MODE == MN_GATHER || MODE == MN_CONV3, "MNBlk: plain, gathered or conv3 rows");
   float4 v[4];
   int64_t kid[4];   // MN_GATHER: stored-row ids of the next tile (prefetched)
 
@@ -291,6 +291,21 @@ struct MNBlk {
     int64_t col = r0 + 4 * cg;
     const int64_t cmax = ((rlim + 3) & ~int64_t(3)) - 4;
     col = col < cmax ? col : cmax;   // clamp inside the padded row; rows >= M are discarded
+    if (MODE == MN_CONV3) {   // stored rows = tokens, columns = tap * seg + e (the tile is within one tap)
+      const int j = (int)(r0 / d.seg);
+      const int64_t ecol = col - (int64_t)j * d.seg;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t kk = k0 + 4 * kg + u;
+        const int64_t n = kk / d.L;
+        const int t2 = (int)(kk - n * d.L) + j - 1;
+        const bool ok = t2 >= 0 && t2 < d.L;
+        const int64_t tok = ok ? d.idx[n * d.L + t2] : 0;
+        v[u] = *reinterpret_cast<const float4*>(d.base + tok * d.ld + ecol);
+        if (!ok) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t row = MODE == MN_PLAIN ? k0 + 4 * kg + u : kid[u];
@@ -1029,6 +1044,8 @@ int launch_split_modes(const Args& g, int am, int bm, int splits, hipStream_t s)
   NR_SAB(KC_PLAIN, MN_PLAIN, false)
   NR_SAB(MN_PLAIN, MN_GATHER, false)
   NR_SAB(MN_PLAIN, MN_PLAIN, false)
+  if (am == MN_PLAIN && bm == MN_CONV3 && atomic_epi && g.B.seg % 128 == 0)
+    return launch_split<MN_PLAIN, MN_CONV3, false>(g, splits, s);
 #undef NR_SAB
   return -1;
 }

@@ -285,7 +285,11 @@ class CNNNewsFn(torch.autograd.Function):
         H = w3.shape[0]
         dev = table.device
         dnews = dnews.contiguous()
-        dC = _empty(T, H, table)
+        # dC with its columns padded to a multiple of 32 (zeros): the table dgrad below contracts
+        # over H and takes the fast GEMM path only for K % 32 == 0
+        Hp = (H + 31) // 32 * 32
+        dC_full = torch.zeros(T, Hp, device=dev)
+        dC = dC_full[:, :H]
         dKq = _empty(T, H, table)
         dq = torch.zeros(H, device=dev)
         K.attn_pool_bwd(C, query, mask, n, seq_len, probs, dnews, dC, dq, key=Kq, dk=dKq, key_tanh=True,
@@ -303,7 +307,8 @@ class CNNNewsFn(torch.autograd.Function):
         dtable = None
         if ctx.needs_input_grad[0]:
             dtable = torch.zeros(V, E, device=dev)
-            K.gemm(T, 3 * E, H, K.operand(dC, L.KCONTIG), K.operand(w3, L.MNCONTIG), dtable,
+            w3p = w3 if Hp == H else torch.cat([w3, w3.new_zeros(Hp - H, 3 * E)], 0)
+            K.gemm(T, 3 * E, Hp, K.operand(dC_full, L.KCONTIG), K.operand(w3p, L.MNCONTIG), dtable,
                    epilogue=L.EPI_SCATTER, c_rows=K.rows_map(ids, L.ROWS_CONV3, seq_len=seq_len, seg=E),
                    pad_row=pad_row)
             if TABLE_GRAD_HOOK(ctx.table_ref, dtable):

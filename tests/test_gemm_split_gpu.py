@@ -146,3 +146,29 @@ def test_split_gelu_and_conv3():
         return Y
     r32, r6 = _run_both(conv)
     _check(r32, r6, wantc, _tol(table, W3, 3 * E))
+
+
+def test_split_conv3_wgrad():
+    """dW3 = dCᵀ conv3(table[tok]) (MN_CONV3 B operand, split-K atomics): CNN_Encoder's conv wgrad."""
+    from newsrec_amd import functions as F
+    g = torch.Generator().manual_seed(4)
+    V, E, n, Lq, H = 400, 256, 64, 30, 150
+    table = torch.randn(V, E, generator=g)
+    tok = torch.randint(0, V, (n * Lq,), generator=g)
+    dC = torch.randn(n * Lq, H, generator=g)
+    x = table[tok].view(n, Lq, E).double()
+    xp = torch.nn.functional.pad(x, (0, 0, 1, 1))
+    cols = torch.cat([xp[:, 0:Lq], xp[:, 1:Lq + 1], xp[:, 2:Lq + 2]], -1).reshape(n * Lq, 3 * E)
+    want = dC.double().t() @ cols
+    tc, tokc = table.cuda(), tok.cuda()
+    dCc = torch.zeros(n * Lq, 152, device="cuda")
+    dCc[:, :H] = dC.cuda()
+
+    def fn():
+        dw = torch.zeros(H, 3 * E, device="cuda")
+        K.gemm_dyn(H, 3 * E, n * Lq, K.operand(dCc[:, :H], L.MNCONTIG),
+                   K.operand(tc, L.MNCONTIG, rows=tokc, mapping=L.ROWS_CONV3, seq_len=Lq, seg=E), dw,
+                   epilogue=L.EPI_ATOMIC, split_k=F._split_k(H, 3 * E, n * Lq))
+        return dw
+    r32, r6 = _run_both(fn)
+    _check(r32, r6, want, _tol(dC, table, n * Lq))
