@@ -1,0 +1,615 @@
+// Shared device code of the fast GEMM kernels (gemm_fast.hip: exact f32 MFMA; gemm_split.hip:
+// bf16x6): operand loaders, LDS images, epilogues, the persistent tile scheduler.  Internal.
+#pragma once
+#include <stdlib.h>
+
+#include "common.h"
+#include "../../include/newsrec_hip.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+namespace nrfast {
+
+// ---- bf16x6 arithmetic: fp32 operands as three bf16 terms (x = h + m + l to 2^-24 |x|) and six
+// products a_h b_h + a_h b_m + a_m b_h + a_h b_l + a_m b_m + a_l b_h on v_mfma_f32_32x32x16_bf16
+// (16x the f32 MFMA rate); the dropped terms are O(2^-24) of |a b|, like the f32 MFMA rounding.
+__device__ __forceinline__ uint32_t bf_rne(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float bf_f(uint32_t b) { return __uint_as_float(b << 16); }
+#ifndef NR_SPLIT_MANUAL_RNE
+// hardware conversions: the compiler pairs the casts into v_cvt_pk_bf16_f32 (round to nearest even)
+__device__ __forceinline__ uint32_t bf_bits(__bf16 v) { return (uint32_t)__builtin_bit_cast(uint16_t, v); }
+__device__ __forceinline__ void split1(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
+  const __bf16 hb = (__bf16)x;
+  const float r = x - (float)hb;   // exact
+  const __bf16 mb = (__bf16)r;
+  const __bf16 lb = (__bf16)(r - (float)mb);
+  h = bf_bits(hb);
+  m = bf_bits(mb);
+  l = bf_bits(lb);
+}
+#else
+__device__ __forceinline__ void split1(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = bf_rne(x);
+  const float r = x - bf_f(h);   // exact
+  m = bf_rne(r);
+  l = bf_rne(r - bf_f(m));
+}
+#endif
+__device__ __forceinline__ void split4(float a, float b, float c, float d, uint2& p0, uint2& p1, uint2& p2) {
+  uint32_t h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
+  split1(a, h0, m0, l0);
+  split1(b, h1, m1, l1);
+  split1(c, h2, m2, l2);
+  split1(d, h3, m3, l3);
+  p0 = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+  p1 = make_uint2(m0 | (m1 << 16), m2 | (m3 << 16));
+  p2 = make_uint2(l0 | (l1 << 16), l2 | (l3 << 16));
+}
+constexpr int SROW = 40;          // split LDS image: [plane][row][k] bf16, 32 k + 8 pad (80-B rows)
+constexpr int SPL = 128 * SROW;   // one plane of a 128-row operand tile
+
+// operand modes
+enum { KC_PLAIN = 0, KC_GATHER = 1, KC_CONV3 = 2, MN_PLAIN = 3, MN_GATHER = 4, MN_CONV3 = 5 };
+
+constexpr bool is_kc(int m) { return m <= KC_CONV3; }
+
+struct Op {
+  const float* base;
+  int64_t ld;
+  const int64_t* idx;
+  int L;
+  int seg;
+};
+
+struct Args {
+  int64_t M, N, K;
+  Op A, B, Cm;
+  float* C;
+  int64_t ldc;
+  const float* bias;
+  int epi;
+  int64_t pad_row;
+  int64_t kchunk;
+  int vec;   // float4 epilogue: N, ldc (and aux ld) % 4 == 0, C (and aux) 16-B aligned
+  int splits;
+  const int32_t* mdyn;   // device-resident M (<= M), or null
+  const int32_t* kdyn;   // device-resident K (<= K), or null
+  int dbg;   // NR_GEMM_DEBUG bits (timing experiments only): 1 = skip the output stores
+};
+
+// Register-staged tile loader for an operand of R rows (the M or N extent) x 32 k.
+template <int R, int MODE>
+struct Loader {
+  static constexpr bool KC = is_kc(MODE);
+  static constexpr int NV = R / 32;              // float4 per thread
+  static constexpr int S = KC ? 36 : R + 4;      // LDS stride
+  static constexpr int LDS_FLOATS = KC ? R * 36 : 32 * (R + 4);
+  float4 v[NV];
+  // K-contiguous: per-thread row bases (hoisted); conv3: the three tap token ids
+  const float* rowp[NV];
+  int64_t nbase[NV];     // conv3: first token row of the row's news
+  int tpos[NV];          // conv3: position in the news
+  uint32_t okbits;       // conv3: rows whose tap t+j-1 exists
+  int curj;              // conv3: tap the row pointers are set up for
+  int64_t kcol[NV];      // MN_GATHER: token ids of the next tile's rows (prefetched)
+
+  __device__ __forceinline__ void init(const Op& d, int64_t r0, int64_t rlim, int tid) {
+    if (KC) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int f = tid + 256 * i;
+        int64_t row = r0 + (f >> 3);
+        row = row < rlim ? row : rlim - 1;                  // clamp: rows >= M are discarded
+        if (MODE == KC_PLAIN) rowp[i] = d.base + row * d.ld;
+        if (MODE == KC_GATHER) rowp[i] = d.base + d.idx[row] * d.ld;
+        if (MODE == KC_CONV3) {
+          const int64_t n = row / d.L;
+          nbase[i] = n * d.L;
+          tpos[i] = (int)(row - n * d.L);
+        }
+      }
+      curj = -1;
+      okbits = 0;
+    }
+  }
+
+  // conv3: point every row at tap j (token t+j-1 of its news; offset so that column k maps
+  // to k - j*seg).  Runs when the k-tile crosses into a new tap: 3 times per block.
+  __device__ __forceinline__ void set_tap(const Op& d, int j) {
+    okbits = 0;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int t2 = tpos[i] + j - 1;
+      const bool ok = t2 >= 0 && t2 < d.L;
+      const int64_t tok = ok ? d.idx[nbase[i] + t2] : 0;
+      rowp[i] = d.base + tok * d.ld - (int64_t)j * d.seg;
+      okbits |= (ok ? 1u : 0u) << i;
+    }
+    curj = j;
+  }
+
+  // column offset (k) within the row for K-contiguous; r0 = tile's first row/col
+  // Full 32-deep tiles only (the dispatcher requires K % 32 == 0): no per-element branches,
+  // so hipcc keeps every load in flight across the MFMAs of the current tile.
+  __device__ __forceinline__ void load(const Op& d, int64_t r0, int64_t rlim, int64_t k0, int tid) {
+    if (MODE == KC_CONV3) {
+      const int j = (int)(k0 / d.seg);
+      if (j != curj) set_tap(d, j);
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int f = tid + 256 * i;
+      if (KC) {
+        const int kq = f & 7;
+        const int64_t k = k0 + 4 * kq;
+        const float* p = rowp[i] + k;
+        const bool ok = MODE != KC_CONV3 || ((okbits >> i) & 1u);
+        float4 x = *reinterpret_cast<const float4*>(p);
+        if (MODE == KC_CONV3 && !ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
+        v[i] = x;
+      } else {
+        constexpr int CPR = R / 4;
+        const int kr = f / CPR, c4 = f % CPR;
+        const int64_t k = k0 + kr;
+        int64_t col = r0 + 4 * c4;
+        const int64_t cmax = ((rlim + 3) & ~int64_t(3)) - 4;
+        col = col < cmax ? col : cmax;                      // clamp inside the padded row
+        const int64_t kk = k;
+        const float* p;
+        bool ok = true;
+        if (MODE == MN_PLAIN) {
+          p = d.base + kk * d.ld + col;
+        } else if (MODE == MN_GATHER) {
+          p = d.base + kcol[i] * d.ld + col;
+        } else {   // MN_CONV3: rows = tokens, columns = tap*seg + e
+          const int j = (int)(r0 / d.seg);
+          const int64_t n = kk / d.L;
+          const int t2 = (int)(kk - n * d.L) + j - 1;
+          ok = t2 >= 0 && t2 < d.L;
+          const int64_t tok = ok ? d.idx[n * d.L + t2] : 0;
+          p = d.base + tok * d.ld + (col - (int64_t)j * d.seg);
+        }
+        float4 x = *reinterpret_cast<const float4*>(p);
+        if (!ok) x = make_float4(0.f, 0.f, 0.f, 0.f);
+        v[i] = x;
+      }
+    }
+  }
+
+  // MN_GATHER: fetch the token ids of tile k0's rows (one tile ahead of its data loads)
+  __device__ __forceinline__ void prefetch_idx(const Op& d, int64_t k0, int64_t K, int tid) {
+    if (MODE == MN_GATHER) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int f = tid + 256 * i;
+        constexpr int CPR = R / 4;
+        const int64_t k = k0 + f / CPR;
+        kcol[i] = d.idx[k < K ? k : K - 1];
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(float* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int f = tid + 256 * i;
+      if (KC) {
+        *reinterpret_cast<float4*>(&lds[(f >> 3) * 36 + 4 * (f & 7)]) = v[i];
+      } else {
+        constexpr int CPR = R / 4;
+        *reinterpret_cast<float4*>(&lds[(f / CPR) * S + 4 * (f % CPR)]) = v[i];
+      }
+    }
+  }
+
+  // bf16x6, split ahead of the publish (the VALU work overlaps the current tile's MFMAs)
+  uint2 sp[KC ? NV : 1][3];
+  __device__ __forceinline__ void presplit() {
+    if constexpr (KC) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) split4(v[i].x, v[i].y, v[i].z, v[i].w, sp[i][0], sp[i][1], sp[i][2]);
+    }
+  }
+  __device__ __forceinline__ void store_presplit(uint16_t* lds, int tid) const {
+    if constexpr (KC) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int f = tid + 256 * i;
+        uint16_t* q = lds + (f >> 3) * SROW + 4 * (f & 7);
+        *reinterpret_cast<uint2*>(q) = sp[i][0];
+        *reinterpret_cast<uint2*>(q + SPL) = sp[i][1];
+        *reinterpret_cast<uint2*>(q + 2 * SPL) = sp[i][2];
+      }
+    }
+  }
+
+  // bf16x6 image (K-contiguous operands only): the float4 of 4 k of one row -> 3 planes
+  __device__ __forceinline__ void store_split(uint16_t* lds, int tid) const {
+    if constexpr (KC) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int f = tid + 256 * i;
+        uint2 p0, p1, p2;
+        split4(v[i].x, v[i].y, v[i].z, v[i].w, p0, p1, p2);
+        uint16_t* q = lds + (f >> 3) * SROW + 4 * (f & 7);
+        *reinterpret_cast<uint2*>(q) = p0;
+        *reinterpret_cast<uint2*>(q + SPL) = p1;
+        *reinterpret_cast<uint2*>(q + 2 * SPL) = p2;
+      }
+    }
+  }
+
+  // the 4 operand values of k-steps 4q..4q+3 for tile row `row` (lane half h)
+  __device__ __forceinline__ float4 frag(const float* lds, int row, int h, int q) const {
+    if (KC) return *reinterpret_cast<const float4*>(&lds[row * 36 + 16 * h + 4 * q]);
+    const int k = 16 * h + 4 * q;
+    return make_float4(lds[k * S + row], lds[(k + 1) * S + row], lds[(k + 2) * S + row], lds[(k + 3) * S + row]);
+  }
+};
+
+// bf16x6 loader of an MN-contiguous 128-row operand (stored rows = k): thread (kg = tid & 7,
+// cg = tid >> 3) loads the 4x4 block k0+4kg.., columns r0+4cg.. as 4 float4 (8 lanes cover 128
+// contiguous bytes of a stored row), transposes it in registers and writes each column's 4
+// consecutive k to the [row][k] planes (b64 stores, 2-way bank aliasing).
+template <int MODE>
+struct MNBlk {
+  static_assert(MODE == MN_PLAIN || MODE == MN_GATHER || MODE == MN_CONV3, "MNBlk: plain, gathered or conv3 rows");
+  float4 v[4];
+  int64_t kid[4];   // MN_GATHER: stored-row ids of the next tile (prefetched)
+
+  __device__ __forceinline__ void init(const Op&, int64_t, int64_t, int) {}
+
+  __device__ __forceinline__ void load(const Op& d, int64_t r0, int64_t rlim, int64_t k0, int tid) {
+    const int kg = tid & 7, cg = tid >> 3;
+    int64_t col = r0 + 4 * cg;
+    const int64_t cmax = ((rlim + 3) & ~int64_t(3)) - 4;
+    col = col < cmax ? col : cmax;   // clamp inside the padded row; rows >= M are discarded
+    if (MODE == MN_CONV3) {   // stored rows = tokens, columns = tap * seg + e (the tile is within one tap)
+      const int j = (int)(r0 / d.seg);
+      const int64_t ecol = col - (int64_t)j * d.seg;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t kk = k0 + 4 * kg + u;
+        const int64_t n = kk / d.L;
+        const int t2 = (int)(kk - n * d.L) + j - 1;
+        const bool ok = t2 >= 0 && t2 < d.L;
+        const int64_t tok = ok ? d.idx[n * d.L + t2] : 0;
+        v[u] = *reinterpret_cast<const float4*>(d.base + tok * d.ld + ecol);
+        if (!ok) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      return;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = MODE == MN_PLAIN ? k0 + 4 * kg + u : kid[u];
+      v[u] = *reinterpret_cast<const float4*>(d.base + row * d.ld + col);
+    }
+  }
+
+  __device__ __forceinline__ void prefetch_idx(const Op& d, int64_t k0, int64_t K, int tid) {
+    if (MODE == MN_GATHER) {
+      const int kg = tid & 7;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t k = k0 + 4 * kg + u;
+        kid[u] = d.idx[k < K ? k : K - 1];
+      }
+    }
+  }
+
+  __device__ __forceinline__ void put(uint16_t* q, float a, float b, float c, float e) const {
+    uint2 p0, p1, p2;
+    split4(a, b, c, e, p0, p1, p2);
+    *reinterpret_cast<uint2*>(q) = p0;
+    *reinterpret_cast<uint2*>(q + SPL) = p1;
+    *reinterpret_cast<uint2*>(q + 2 * SPL) = p2;
+  }
+
+  uint2 sp[4][3];
+  __device__ __forceinline__ void presplit() {
+    split4(v[0].x, v[1].x, v[2].x, v[3].x, sp[0][0], sp[0][1], sp[0][2]);
+    split4(v[0].y, v[1].y, v[2].y, v[3].y, sp[1][0], sp[1][1], sp[1][2]);
+    split4(v[0].z, v[1].z, v[2].z, v[3].z, sp[2][0], sp[2][1], sp[2][2]);
+    split4(v[0].w, v[1].w, v[2].w, v[3].w, sp[3][0], sp[3][1], sp[3][2]);
+  }
+  __device__ __forceinline__ void store_presplit(uint16_t* lds, int tid) const {
+    const int kg = tid & 7, cg = tid >> 3;
+    uint16_t* q = lds + (4 * cg) * SROW + 4 * kg;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      *reinterpret_cast<uint2*>(q + u * SROW) = sp[u][0];
+      *reinterpret_cast<uint2*>(q + u * SROW + SPL) = sp[u][1];
+      *reinterpret_cast<uint2*>(q + u * SROW + 2 * SPL) = sp[u][2];
+    }
+  }
+
+  __device__ __forceinline__ void store_split(uint16_t* lds, int tid) const {
+    const int kg = tid & 7, cg = tid >> 3;
+    uint16_t* q = lds + (4 * cg) * SROW + 4 * kg;
+    put(q, v[0].x, v[1].x, v[2].x, v[3].x);
+    put(q + SROW, v[0].y, v[1].y, v[2].y, v[3].y);
+    put(q + 2 * SROW, v[0].z, v[1].z, v[2].z, v[3].z);
+    put(q + 3 * SROW, v[0].w, v[1].w, v[2].w, v[3].w);
+  }
+};
+
+// Output-tile epilogue.  The MFMAs run with the operands swapped (B tile as the "A" operand),
+// so each accumulator holds a Cᵀ tile: lane (c, h) owns output row m = c of the 32x32 tile
+// and, in register group q = r >> 2, the four consecutive columns n = 8q + 4h .. +3 — one
+// float4 per group.  Per wave: TI*TJ*4 vector stores (vs 64 scalar stores in the C-major
+// layout), one bias float4 per group, one token-id lookup per row for the scatter.
+template <int EPI>
+__device__ __forceinline__ float4 epi_combine(const Args& g, float4 v, float4 b, const float* crow, const float* arow,
+                                              int64_t n) {
+  if (EPI == NR_EPI_STORE) return make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
+  if (EPI == NR_EPI_STORE_RELU)
+    return make_float4(fmaxf(v.x + b.x, 0.f), fmaxf(v.y + b.y, 0.f), fmaxf(v.z + b.z, 0.f), fmaxf(v.w + b.w, 0.f));
+  if (EPI == NR_EPI_STORE_TANH) return make_float4(tanhf(v.x + b.x), tanhf(v.y + b.y), tanhf(v.z + b.z), tanhf(v.w + b.w));
+  if (EPI == NR_EPI_ACCUM) {
+    const float4 o = *reinterpret_cast<const float4*>(crow + n);
+    return make_float4(o.x + v.x + b.x, o.y + v.y + b.y, o.z + v.z + b.z, o.w + v.w + b.w);
+  }
+  if (EPI == NR_EPI_GELU_GRAD) {
+    const float4 a = *reinterpret_cast<const float4*>(arow + n);
+    return make_float4(v.x * nr_gelu_grad(a.x), v.y * nr_gelu_grad(a.y), v.z * nr_gelu_grad(a.z),
+                       v.w * nr_gelu_grad(a.w));
+  }
+  // NR_EPI_ACCUM_GATE
+  const float4 o = *reinterpret_cast<const float4*>(crow + n);
+  const float4 a = *reinterpret_cast<const float4*>(arow + n);
+  return make_float4(a.x > 0.f ? o.x + v.x : 0.f, a.y > 0.f ? o.y + v.y : 0.f, a.z > 0.f ? o.z + v.z : 0.f,
+                     a.w > 0.f ? o.w + v.w : 0.f);
+}
+
+template <int EPI>
+__device__ __forceinline__ float epi_combine1(const Args& g, float v, float b, const float* crow, const float* arow,
+                                              int64_t n) {
+  if (EPI == NR_EPI_STORE) return v + b;
+  if (EPI == NR_EPI_STORE_RELU) return fmaxf(v + b, 0.f);
+  if (EPI == NR_EPI_STORE_TANH) return tanhf(v + b);
+  if (EPI == NR_EPI_ACCUM) return crow[n] + v + b;
+  if (EPI == NR_EPI_GELU_GRAD) return v * nr_gelu_grad(arow[n]);
+  return arow[n] > 0.f ? crow[n] + v : 0.f;
+}
+
+template <int EPI, int TI, int TJ>
+__device__ __forceinline__ void epilogue_t(const Args& g, f32x16 (&acc)[TI][TJ], int64_t m0, int64_t n0, int wm,
+                                           int wn, int h, int c, bool vec) {
+  const bool has_bias = g.bias && (EPI == NR_EPI_STORE || EPI == NR_EPI_STORE_RELU || EPI == NR_EPI_STORE_TANH ||
+                                   EPI == NR_EPI_ACCUM || EPI == NR_EPI_STORE_GELU);
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int64_t row = m0 + wm + 32 * i + c;
+    if (row >= g.M) continue;
+    float* crow = g.C + row * g.ldc;
+    if (EPI == NR_EPI_SCATTER_STORE) {   // distinct destination rows: plain stores
+      const int64_t tok = g.Cm.idx[row];
+      if (tok == g.pad_row) continue;
+      crow = g.C + tok * g.ldc;
+    }
+    const float* arow =
+        (EPI == NR_EPI_ACCUM_GATE || EPI == NR_EPI_GELU_GRAD || EPI == NR_EPI_STORE_GELU) ? g.Cm.base + row * g.Cm.ld
+                                                                                          : nullptr;
+    int64_t tok = 0, nbase = 0;
+    int tpos = 0;
+    if (EPI == NR_EPI_SCATTER) {
+      if (g.Cm.L == 1) {
+        tok = g.Cm.idx[row];
+      } else {
+        nbase = row / g.Cm.L;
+        tpos = (int)(row - nbase * g.Cm.L);
+        nbase *= g.Cm.L;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t n = n0 + wn + 32 * j + 8 * q + 4 * h;
+        if (n >= g.N) continue;
+        const float4 v = make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+        if (EPI == NR_EPI_ATOMIC || EPI == NR_EPI_SCATTER) {
+          float* dst;
+          int64_t t = tok;
+          int64_t sn = n;
+          if (EPI == NR_EPI_ATOMIC) {
+            dst = crow;
+          } else {
+            if (g.Cm.L != 1) {   // conv3 row map: column tap sj of token t + sj - 1
+              const int sj = (int)(n / g.Cm.seg);
+              sn = n - (int64_t)sj * g.Cm.seg;
+              const int t2 = tpos + sj - 1;
+              if (t2 < 0 || t2 >= g.Cm.L) continue;
+              t = g.Cm.idx[nbase + t2];
+            }
+            if (t == g.pad_row) continue;
+            dst = g.C + t * g.ldc;
+          }
+          const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (n + u < g.N) atomicAdd(dst + sn + u, e[u]);
+        } else if (EPI == NR_EPI_SCATTER_STORE) {
+          if (vec && n + 3 < g.N) {
+            *reinterpret_cast<float4*>(crow + n) = v;
+          } else {
+            const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (n + u < g.N) crow[n + u] = e[u];
+          }
+        } else if (EPI == NR_EPI_STORE_GELU) {   // pre-activation to aux, GELU to C
+          float* xrow = const_cast<float*>(arow);
+          const float e[4] = {v.x, v.y, v.z, v.w};
+          if (vec && n + 3 < g.N) {
+            const float4 b = has_bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 x = make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
+            *reinterpret_cast<float4*>(xrow + n) = x;
+            *reinterpret_cast<float4*>(crow + n) = make_float4(nr_gelu(x.x), nr_gelu(x.y), nr_gelu(x.z), nr_gelu(x.w));
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (n + u < g.N) {
+                const float x = e[u] + (has_bias ? g.bias[n + u] : 0.f);
+                xrow[n + u] = x;
+                crow[n + u] = nr_gelu(x);
+              }
+          }
+        } else if (vec && n + 3 < g.N) {
+          const float4 b = has_bias ? *reinterpret_cast<const float4*>(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+          *reinterpret_cast<float4*>(crow + n) = epi_combine<EPI>(g, v, b, crow, arow, n);
+        } else {
+          const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (n + u < g.N) crow[n + u] = epi_combine1<EPI>(g, e[u], has_bias ? g.bias[n + u] : 0.f, crow, arow, n + u);
+        }
+      }
+  }
+}
+
+// Atomic epilogues in the C-major accumulator layout (operands not swapped): lane c owns
+// column n = c, register r row (r & 3) + 8 (r >> 2) + 4h — each atomic instruction covers 32
+// consecutive columns of two rows (two cache lines), 16x fewer line transactions than the
+// transposed layout would issue.
+template <int EPI, int TI, int TJ>
+__device__ __forceinline__ void epilogue_cmajor(const Args& g, f32x16 (&acc)[TI][TJ], int64_t m0, int64_t n0, int wm,
+                                                int wn, int h, int c) {
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int64_t col = n0 + wn + 32 * j + c;
+      if (col >= g.N) continue;
+      int sj = 0;
+      int64_t scol = col;
+      if (EPI == NR_EPI_SCATTER && g.Cm.L != 1) {
+        sj = (int)(col / g.Cm.seg);
+        scol = col - (int64_t)sj * g.Cm.seg;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= g.M) continue;
+        const float v = acc[i][j][r];
+        if (EPI == NR_EPI_ATOMIC) {
+          atomicAdd(&g.C[row * g.ldc + col], v);
+        } else {
+          int64_t tok;
+          if (g.Cm.L == 1) {
+            tok = g.Cm.idx[row];
+          } else {
+            const int64_t n = row / g.Cm.L;
+            const int t2 = (int)(row - n * g.Cm.L) + sj - 1;
+            if (t2 < 0 || t2 >= g.Cm.L) continue;
+            tok = g.Cm.idx[n * g.Cm.L + t2];
+          }
+          if (tok == g.pad_row) continue;
+          atomicAdd(&g.C[tok * g.ldc + scol], v);
+        }
+      }
+    }
+}
+
+template <int TI, int TJ>
+__device__ __forceinline__ void epilogue(const Args& g, f32x16 (&acc)[TI][TJ], int64_t m0, int64_t n0, int wm,
+                                         int wn, int h, int c) {
+  if (g.dbg & 1) {   // timing experiment: keep the accumulators live, store nothing
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s += acc[i][j][r];
+    if (s == 1234.5678f) g.C[0] = s;
+    return;
+  }
+  const bool vec = g.vec;
+  switch (g.epi) {
+    case NR_EPI_STORE: epilogue_t<NR_EPI_STORE, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_STORE_RELU: epilogue_t<NR_EPI_STORE_RELU, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_STORE_TANH: epilogue_t<NR_EPI_STORE_TANH, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_ACCUM: epilogue_t<NR_EPI_ACCUM, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_ACCUM_GATE: epilogue_t<NR_EPI_ACCUM_GATE, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_STORE_GELU: epilogue_t<NR_EPI_STORE_GELU, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_GELU_GRAD: epilogue_t<NR_EPI_GELU_GRAD, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_ATOMIC: epilogue_t<NR_EPI_ATOMIC, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    case NR_EPI_SCATTER_STORE: epilogue_t<NR_EPI_SCATTER_STORE, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+    default: epilogue_t<NR_EPI_SCATTER, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
+  }
+}
+
+template <bool TR, int TI, int TJ>
+__device__ __forceinline__ void epilogue_any(const Args& g, f32x16 (&acc)[TI][TJ], int64_t m0, int64_t n0, int wm,
+                                             int wn, int h, int c) {
+  if (TR) {
+    epilogue<TI, TJ>(g, acc, m0, n0, wm, wn, h, c);
+  } else if (g.epi == NR_EPI_ATOMIC) {
+    epilogue_cmajor<NR_EPI_ATOMIC, TI, TJ>(g, acc, m0, n0, wm, wn, h, c);
+  } else {
+    epilogue_cmajor<NR_EPI_SCATTER, TI, TJ>(g, acc, m0, n0, wm, wn, h, c);
+  }
+}
+
+// A work unit = one BM x BN output tile x one K split.
+struct Unit {
+  int64_t m0, n0, kbeg;
+  int nt;   // 32-deep k-tiles
+};
+
+// Virtual block id -> unit.  Ids congruent mod 8 run on the same XCD (the hardware deals
+// workgroups round-robin over the 8 XCDs); each XCD gets a contiguous run of units, n fastest,
+// so the blocks resident on one XCD at a time share A row panels (and all of B) in its L2.
+__device__ __forceinline__ Unit decode_unit(const Args& g, int id, int units, int ntiles, int gn, int BM, int BN) {
+  const int xcd = id & 7, q8 = units >> 3, rr = units & 7;
+  const int u = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (id >> 3);
+  const int tile = u % ntiles, split = u / ntiles;
+  Unit r;
+  r.m0 = (int64_t)(tile / gn) * BM;
+  r.n0 = (int64_t)(tile % gn) * BN;
+  r.kbeg = (int64_t)split * g.kchunk;
+  const int64_t kend = r.kbeg + g.kchunk < g.K ? r.kbeg + g.kchunk : g.K;
+  r.nt = kend > r.kbeg ? (int)((kend - r.kbeg + 31) / 32) : 0;
+  return r;
+}
+
+// Position in a block's flattened (unit, k-tile) sequence.
+struct Cursor {
+  int id;   // virtual block id (units of this block: blockIdx.x + j * gridDim.x)
+  int kt;   // k-tile within the unit
+  Unit u;
+};
+
+// Resident-block slots for a kernel instantiation (CUs x occupancy), cached per device.
+template <typename Kern>
+int resident_slots(Kern k) {
+  static int cache[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  if (cache[dev] == 0) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 256, 0) != hipSuccess) return 0;
+    cache[dev] = cus * per;
+  }
+  return cache[dev];
+}
+
+inline bool persistent_disabled() {   // NR_GEMM_NOPERSIST=1: one unit per block (A/B testing)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("NR_GEMM_NOPERSIST");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
+// bf16x6 launch of the 128x128 fast-path operand combinations (gemm_split.hip); -1 = not covered
+int launch_split_modes(const Args& g, int am, int bm, int splits, hipStream_t s);
+
+}  // namespace nrfast
