@@ -340,9 +340,9 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
     return NR_EINVAL(4);
   if (!getenv_generic()) {
     const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128) * splits;
-    // bf16x6 runs on 128x128 tiles only: take them for every shape in that mode, so one
-    // contraction gets one arithmetic whatever its size (e.g. token-wise vs distinct-row rows)
-    const int fb = (t128 >= 400 || nr_gemm_get_precision() == NR_GEMM_BF16X6) ? 128 : 64;
+    // small problems (< 400 tiles of 128x128) take 64x64 tiles, which only the exact-f32 kernel
+    // has: they are latency-bound, and 128x128 bf16x6 tiles would leave most CUs idle
+    const int fb = t128 >= 400 ? 128 : 64;
     const int rc =
         nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, fb, fb, nullptr, nullptr, stream);
     if (rc != -1) return rc;

@@ -185,6 +185,10 @@ def test_mha_news_dedup_vs_tokenwise(monkeypatch):
         (news * torch.linspace(-1, 1, H, device="cuda")).sum().backward()
         res.append([news.detach().clone()] + [t.grad.clone() for t in (table, w, b, gamma, beta, q)])
     torch.cuda.synchronize()
-    assert torch.equal(res[0][0], res[1][0])   # forward: identical rows, identical arithmetic
+    from newsrec_amd import _lib as Lb
+    if K.get_gemm_precision() == Lb.GEMM_F32:
+        assert torch.equal(res[0][0], res[1][0])   # forward: identical rows, identical arithmetic
+    else:   # bf16x6: the small token-wise GEMM runs on the f32 64x64 kernel, the distinct-row one on bf16x6
+        torch.testing.assert_close(res[1][0], res[0][0], rtol=1e-5, atol=1e-5)
     for a, c in zip(res[0][1:], res[1][1:]):   # backward: same sums, different fp32 order
         torch.testing.assert_close(c, a, rtol=1e-4, atol=5e-5)
