@@ -28,6 +28,18 @@ def _empty(rows, cols, like, ld=None):
     return buf[:, :cols]
 
 
+def _zeros_views(dev, *shapes):
+    """Views of ONE zero-filled buffer (one fill launch instead of one per gradient), each
+    starting 16-B aligned."""
+    sizes = [int(torch.Size(sh).numel()) for sh in shapes]
+    offs, tot = [], 0
+    for n in sizes:
+        offs.append(tot)
+        tot += _pad4(n)
+    buf = torch.zeros(max(tot, 1), device=dev)
+    return [buf[o:o + n].view(sh) for o, n, sh in zip(offs, sizes, shapes)]
+
+
 def _split_k(m, n, k, slots=512):
     """Split-K factor for a wgrad GEMM: fill the 256 CUs x 2 resident 128x128 blocks in ONE
     wave (a 1.16-wave grid runs as two), keeping >= 512 k per split."""
@@ -200,12 +212,9 @@ class MHANewsFn(torch.autograd.Function):
         NQ = heads * dk
         NY = NQ + H
         dnews = dnews.contiguous()
-        dq = torch.zeros(H, device=table.device)
-        dgamma = torch.zeros(H, device=table.device)
-        dbeta = torch.zeros(H, device=table.device)
+        dq, dgamma, dbeta, db, dw = _zeros_views(table.device, (H,), (H,), (H,), (NY,), (NY, E))
         dY = _empty(T, NY, table)
         dz = dtok.contiguous() if dtok is not None else None
-        db = torch.zeros(NY, device=table.device)
         ur = ctx.ur
         if fused:
             dob = _empty(T, H, table) if O is not None else None
@@ -220,7 +229,6 @@ class MHANewsFn(torch.autograd.Function):
             K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
             K.colsum(dY, T, NY, db)
         dtable = None
-        dw = torch.zeros(NY, E, device=table.device)
         if ur is not None:
             # per-distinct-row gradient, then the two GEMMs over U rows instead of T tokens
             dYu = _empty(ur.cap, NY, table)
@@ -295,13 +303,10 @@ class CNNNewsFn(torch.autograd.Function):
         K.attn_pool_bwd(C, query, mask, n, seq_len, probs, dnews, dC, dq, key=Kq, dk=dKq, key_tanh=True,
                         dz=dC_out.contiguous() if dC_out is not None else None)
         # key projection: dWq = dKqᵀ C, dbq = colsum(dKq); dC += dKq Wq, then ReLU'(C)
-        dwq = torch.zeros(H, H, device=dev)
-        dbq = torch.zeros(H, device=dev)
+        dwq, dbq, dconv_b, dw3 = _zeros_views(dev, (H, H), (H,), (H,), (H, 3 * E))
         _proj_wgrad(dKq, K.operand(C, L.MNCONTIG), dwq, dbq, T)
         K.gemm(T, H, H, K.operand(dKq, L.KCONTIG), K.operand(wq, L.MNCONTIG), dC, epilogue=L.EPI_ACCUM_GATE,
                c_rows=K.aux_operand(C))
-        dconv_b = torch.zeros(H, device=dev)
-        dw3 = torch.zeros(H, 3 * E, device=dev)
         _proj_wgrad(dC, K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_CONV3, seq_len=seq_len, seg=E),
                     dw3, dconv_b, T)
         dtable = None
@@ -380,8 +385,7 @@ class MHAFn(torch.autograd.Function):
         K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, nseq, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
         dx = _empty(rows, D, x)
         K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx)
-        dw = torch.zeros(NY, D, device=dev)
-        db = torch.zeros(NY, device=dev)
+        dw, db = _zeros_views(dev, (NY, D), (NY,))
         _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows)
         return dx, None, dw, db, None, None, None, None, None
 
@@ -427,11 +431,8 @@ class RNNUserFn(torch.autograd.Function):
         dgh_ = dgi if dgh is None else dgh
         dx = _empty(B * N, H, x)
         K.gemm(B * N, H, G * H, K.operand(dgi, L.KCONTIG), K.operand(w_ih, L.MNCONTIG), dx)
-        dw_ih = torch.zeros(G * H, H, device=dev)
-        db_ih = torch.zeros(G * H, device=dev)
+        dw_ih, db_ih, dw_hh, db_hh = _zeros_views(dev, (G * H, H), (G * H,), (G * H, H), (G * H,))
         _proj_wgrad(dgi, K.operand(x, L.MNCONTIG), dw_ih, db_ih, B * N)
-        dw_hh = torch.zeros(G * H, H, device=dev)
-        db_hh = torch.zeros(G * H, device=dev)
         _proj_wgrad(dgh_, K.operand(hprev, L.MNCONTIG), dw_hh, db_hh, B * N)
         dtab = None
         if user_table is not None and ctx.needs_input_grad[5]:
