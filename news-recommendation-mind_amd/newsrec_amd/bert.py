@@ -27,7 +27,7 @@ from torch import nn
 
 from . import _lib as L
 from . import kernels as K
-from .functions import _empty, _proj_wgrad
+from .functions import _empty, _proj_wgrad, _zeros_views
 
 
 class BertConfig:
@@ -252,7 +252,10 @@ class BertFn(torch.autograd.Function):
         for li in reversed(range(nl)):
             x, wqkv, qkv, cx, ml, a, st1, h1, U, G, o, st2 = saved[12 * li: 12 * (li + 1)]
             wq, bq, wk, bk, wv, bv, wo, bo, l1w, l1b, wi, bi, wo2, bo2, l2w, l2b = lp[li]
-            g = [z(t) for t in lp[li]]
+            # one fill for all 16 gradients of the layer; Q/K/V weight and bias grads are slices of the
+            # fused [3H, H] / [3H] wgrad outputs
+            dwqkv, dbqkv, *grest = _zeros_views(dev, (3 * H, H), (3 * H,), *[tuple(t.shape) for t in lp[li][6:]])
+            g = [dwqkv[:H], dbqkv[:H], dwqkv[H:2 * H], dbqkv[H:2 * H], dwqkv[2 * H:], dbqkv[2 * H:]] + grest
             dh1 = _empty(T, H, word)
             do = _empty(T, H, word)
             K.bert_add_ln_bwd(o, h1, l2w, st2, dh, dh1, do, g[14], g[15], **dsite_seg(3 + 3 * li, p_h, 0))
@@ -275,23 +278,20 @@ class BertFn(torch.autograd.Function):
                                 ml[r0 * heads * 2:(r0 + n) * heads * 2], dcx[r0:r0 + n], dqkv[r0:r0 + n],
                                 **dsite_seg(1 + 3 * li, p_a, r0))
             K.gemm(T, H, 3 * H, K.operand(dqkv, L.KCONTIG), K.operand(wqkv, L.MNCONTIG), dx, epilogue=L.EPI_ACCUM)
-            dwqkv = torch.zeros(3 * H, H, device=dev)
-            dbqkv = torch.zeros(3 * H, device=dev)
             _proj_wgrad(dqkv, K.operand(x, L.MNCONTIG), dwqkv, dbqkv, T)
-            g[0], g[2], g[4] = dwqkv[:H], dwqkv[H:2 * H], dwqkv[2 * H:]
-            g[1], g[3], g[5] = dbqkv[:H], dbqkv[H:2 * H], dbqkv[2 * H:]
             for k in range(16):
                 grads[5 + 16 * li + k] = g[k]
             dh = dx
         ds = _empty(T, H, word)
-        delw, delb = z(elw), z(elb)
+        delw, delb, dpos, dtyp = _zeros_views(dev, tuple(elw.shape), tuple(elb.shape), tuple(pos.shape),
+                                              tuple(typ.shape))
         ids_all = []
         for s, r0 in zip(segs, r0s):
             n = s.nseq * s.L
             K.bert_embed_bwd(word, pos, typ[0], s.ids, s.nseq, s.L, elw, st_e[r0:r0 + n], dh[r0:r0 + n],
                              ds[r0:r0 + n], delw, delb, **dsite_seg(0, p_h, r0 * H))
             ids_all.append(s.ids)
-        dword, dpos, dtyp = z(word), z(pos), z(typ)
+        dword = z(word)
         K.embedding_bwd(ds, torch.cat(ids_all) if len(ids_all) > 1 else ids_all[0], dword,
                         padding_idx=c.pad_token_id)
         for s, r0 in zip(segs, r0s):
