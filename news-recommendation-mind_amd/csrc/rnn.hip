@@ -70,6 +70,10 @@ __global__ __launch_bounds__(256) void rnn_fwd_kernel(RnnArgs g) {
   }
   __syncthreads();
   const int len = seq_len(g, b, red);
+  // an all-zero mask row (len 0; pack_padded_sequence raises, MIND forces his_mask[0] = 1):
+  // defined output h0, and the backward passes dh straight to dh0
+  if (len == 0)
+    for (int u = tid; u < H; u += blockDim.x) g.hout[b * g.ldho + u] = h[u];
   for (int t = 0; t < g.N; ++t) {
     const int tt = g.reverse ? g.N - 1 - t : t;
     const int64_t row = b * g.N + tt;
@@ -239,6 +243,7 @@ __global__ __launch_bounds__(((G * H + 63) / 64) * 64) void rnn_fwd_reg_kernel(R
   if (tid < 2) h[H + tid] = 0.f;
   __syncthreads();
   const int len = seq_len(g, b, &red);
+  if (len == 0 && tid < H) g.hout[b * g.ldho + tid] = h[tid];   // all-zero mask row: h0
   for (int t = 0; t < g.N; ++t) {
     const int tt = g.reverse ? g.N - 1 - t : t;
     const int64_t row = b * g.N + tt;

@@ -69,8 +69,9 @@ class GradSync:
       weight-gradient GEMMs;
     * row-sparse tables (LSTUR's 876,957-row user table, SPARSE_GRAD_HOOK): an exact row-sparse
       exchange -- all-gather of the step's (row id, gradient row) pairs, then every rank adds all
-      ranks' rows into a zero dense gradient in rank order (the same sum DDP's dense all-reduce
-      forms, at B rows per rank instead of 526 MB);
+      ranks' rows in rank order into a dense gradient buffer that persists across steps (only the
+      previous step's rows are re-zeroed) -- the same sum DDP's dense all-reduce forms, at B rows
+      per rank instead of 526 MB;
     * every other gradient: flattened into buckets of <= ``bucket_mb`` MB, one all-reduce per
       bucket (a few large collectives over xGMI instead of one per parameter).
     """
@@ -81,6 +82,7 @@ class GradSync:
         self.world = dist.get_world_size(group)
         self.pending = []
         self.sparse = []
+        self._dense, self._touched = {}, {}
         self.bucket_elems = int(bucket_mb * (1 << 20) // 4)
         self.overlap = overlap_tables and self.world > 1
         self.use_sparse = sparse_tables and self.world > 1
@@ -103,6 +105,19 @@ class GradSync:
         w2 = dist.all_gather(gs, grads, group=self.group, async_op=True)
         self.sparse.append((table, ids, gs, w1, w2))
         return True
+
+    def _sparse_buffer(self, table):
+        """The dense gradient of a row-sparse table, allocated and zeroed ONCE: each step only
+        re-zeroes the rows the previous step wrote (B * world rows instead of a 526 MB fill)."""
+        buf = self._dense.get(id(table))
+        if buf is None:
+            buf = torch.zeros_like(table)
+            self._dense[id(table)] = buf
+        else:
+            prev = self._touched.get(id(table))
+            if prev is not None:
+                buf.index_fill_(0, prev, 0.0)
+        return buf
 
     def close(self):
         if self.overlap:
@@ -135,10 +150,14 @@ class GradSync:
         for table, ids, gs, w1, w2 in self.sparse:
             w1.wait()
             w2.wait()
-            g = torch.zeros_like(table)
+            g = self._sparse_buffer(table)
             for r in range(self.world):      # rank order: every rank forms the same sum
                 g.index_add_(0, ids[r], gs[r])
-            table.grad = g if table.grad is None else table.grad.add_(g)
+            self._touched[id(table)] = torch.cat(ids)
+            if table.grad is None:
+                table.grad = g
+            elif table.grad.data_ptr() != g.data_ptr():
+                table.grad.add_(g)
         self.sparse = []
         for bucket, flat, inplace, w in flights:
             w.wait()

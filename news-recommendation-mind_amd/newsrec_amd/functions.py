@@ -119,7 +119,15 @@ class _TableGradHook:
         self.fn = fn
 
     def __call__(self, table, dtable):
-        return bool(self.fn(table, dtable)) if self.fn is not None else False
+        # only a leaf parameter's gradient may be taken over: a non-leaf "table" (an activation,
+        # e.g. encoderN(embedding(tokens)) on the unfused path) must flow back through autograd
+        if self.fn is None or not _is_param_leaf(table):
+            return False
+        return bool(self.fn(table, dtable))
+
+
+def _is_param_leaf(t):
+    return t is not None and t.is_leaf and t.requires_grad
 
 
 TABLE_GRAD_HOOK = _TableGradHook()
@@ -138,7 +146,9 @@ class _SparseGradHook:
         self.fn = fn
 
     def __call__(self, table, rows, grads):
-        return bool(self.fn(table, rows, grads)) if self.fn is not None else False
+        if self.fn is None or not _is_param_leaf(table):
+            return False
+        return bool(self.fn(table, rows, grads))
 
 
 SPARSE_GRAD_HOOK = _SparseGradHook()
