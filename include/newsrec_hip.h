@@ -25,6 +25,10 @@ extern "C" {
 
 typedef struct ihipStream_t* hipStream_t;
 
+/* Hash of the sources this library was built from (build.py source_hash: csrc, include, flags);
+ * the Python binding refuses a library whose hash differs from the tree next to it. */
+const char* nr_build_hash(void);
+
 /* ------------------------------------------------------------------ GEMM operands */
 
 /* How the stored row index of an operand is found. */
@@ -70,27 +74,28 @@ enum nr_epilogue {
                             the dgrad of the intermediate dense through its GELU               */
 };
 
-/* GEMM arithmetic of every nr_gemm_f32 / nr_gemm_f32_dyn call in the process.
+/* GEMM arithmetic, chosen PER CALL (the `prec` argument of nr_gemm_f32 / nr_gemm_f32_dyn; the
+ * library holds no precision state, so calls are re-entrant across threads and streams):
  *   NR_GEMM_F32     v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation.
  *   NR_GEMM_BF16X6  each fp32 operand split into three bf16 terms (x = h + m + l to 2^-24 |x|) and
  *                   the six products of order >= 2^-16 (hh, hm, mh, hl, mm, lh) accumulated in fp32 on
  *                   v_mfma_f32_32x32x16_bf16 (16x the f32 MFMA rate): fp32-class accuracy (dropped
  *                   terms <= 3 * 2^-24 |a b|), 6 bf16 MFMAs per f32-equivalent.  128x128-tile fast
- *                   path only (CONV3 operands along N and small problems stay on f32).
- * The initial mode comes from the environment variable NR_GEMM_PREC ("bf16x6", the default, | "f32").
- * nr_gemm_set_precision returns the previous mode (or -1000 on an invalid one). */
-enum nr_gemm_precision { NR_GEMM_F32 = 0, NR_GEMM_BF16X6 = 1 };
-int nr_gemm_set_precision(int32_t mode);
-int nr_gemm_get_precision(void);
+ *                   path (problems under 400 such tiles and ineligible operands run NR_GEMM_F32).
+ *   NR_GEMM_BF16    bf16 arithmetic (autocast-style): fp32 operands rounded to bf16 (RNE) on their way
+ *                   to LDS, ONE v_mfma_f32_32x32x16_bf16 product per tile and k-step, fp32
+ *                   accumulation and fp32 outputs.  Ineligible operands run NR_GEMM_F32.
+ * Storage stays fp32 in every mode (fp32 master weights). */
+enum nr_gemm_precision { NR_GEMM_F32 = 0, NR_GEMM_BF16X6 = 1, NR_GEMM_BF16 = 2 };
 
-/* C (op)= A(m,k) * B(k,n) over k in [0,K), fp32 on the f32-input MFMA.
+/* C (op)= A(m,k) * B(k,n) over k in [0,K) in the arithmetic `prec` (enum nr_gemm_precision).
  * Replaces: nn.Linear / F.linear of models/Modules/Attention.py:107-108 (keyProject,
  * valueProject), CNN.py:23 (wordQueryProject is done in nr_attn_pool), the Conv1d of
  * CNN.py:12-17 (as a K = 3E GEMM over CONV3 rows) and their autograd backward.
  * split_k > 1 requires NR_EPI_ATOMIC or NR_EPI_SCATTER. */
 int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B,
                 float* C, int64_t ldc, const float* bias, int32_t epilogue,
-                const nr_operand* c_rows, int64_t pad_row, int32_t split_k,
+                const nr_operand* c_rows, int64_t pad_row, int32_t split_k, int32_t prec,
                 hipStream_t stream);
 
 /* nr_gemm_f32 with device-resident extents: M and K are host upper bounds (grid sizing) and
@@ -100,7 +105,8 @@ int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_o
 int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B,
                     float* C, int64_t ldc, const float* bias, int32_t epilogue,
                     const nr_operand* c_rows, int64_t pad_row, int32_t split_k,
-                    const int32_t* m_dev, const int32_t* k_dev, hipStream_t stream);
+                    const int32_t* m_dev, const int32_t* k_dev, int32_t prec,
+                    hipStream_t stream);
 
 /* ------------------------------------------------------------------ distinct token rows */
 
@@ -132,6 +138,25 @@ int nr_segment_rows_sum(const float* src, int64_t lds, int64_t width, int64_t T,
                         const int32_t* seg_off, const int32_t* seg_tok, const int32_t* seg_of,
                         const int32_t* counts, int64_t rows_max, float* work, float* dst,
                         int64_t ldd, hipStream_t stream);
+
+/* The CNN encoder's k = 3 convolution per distinct row (CNN.py:41, Conv1d(E -> H, k = 3, pad = 1)).
+ * nr_segment_rows_sum_conv3: dst[u][tap*tap_width + c] = sum over the CSR tokens t of distinct row u
+ * of src[t + 1 - tap][c] for tap in {0, 1, 2}, zero when t + 1 - tap leaves t's title of L tokens
+ * (the CSR must hold every token: nr_unique_rows with grad_mask NULL).  The per-distinct-row input of
+ * both the table dgrad (dtable[u] = dst[u] . W3) and the conv wgrad (dW3 = dstᵀ table[uids]).
+ * Workspace: nr_segment_rows_sum_workspace(T, 3 * tap_width).  Same alignment rules as above. */
+int nr_segment_rows_sum_conv3(const float* src, int64_t lds, int64_t tap_width, int32_t L, int64_t T,
+                              const int32_t* seg_off, const int32_t* seg_tok, const int32_t* seg_of,
+                              const int32_t* counts, int64_t rows_max, float* work, float* dst,
+                              int64_t ldd, hipStream_t stream);
+
+/* out[t][h] = act(bias[h] + sum_{tap} P[inv[t + tap - 1]][tap*tap_width + h]) for h < H (taps outside
+ * t's title of L tokens skipped; act = ReLU when relu != 0), out[t][h] = 0 for H <= h < tap_width.
+ * P = the per-distinct-row tap projections [U][3 * tap_width] (one GEMM over distinct rows).
+ * tap_width, ldp, ldo multiples of 4; P, out 16-B aligned. */
+int nr_conv3_rows_fwd(const float* P, int64_t ldp, int32_t tap_width, int32_t H, const int64_t* inv,
+                      int64_t T, int32_t L, const float* bias, int32_t relu, float* out, int64_t ldo,
+                      hipStream_t stream);
 
 /* ------------------------------------------------------------------ attention */
 

@@ -1,0 +1,64 @@
+// Distinct-row k = 3 convolution of the CNN news encoder (models/Encoders/CNN.py:12-17,41-42).
+//
+// Conv1d(E -> H, k = 3, pad = 1) over gathered word rows is linear in each tap, so it commutes with
+// the gather: with P[u] = [W_0 table[u] | W_1 table[u] | W_2 table[u]] computed ONCE per distinct
+// word row u of the batch (one GEMM over U rows instead of a K = 3E GEMM over T tokens),
+//   C[t] = ReLU(b + sum_j P[inv[t + j - 1]][tap j])     (zero taps outside the title)
+// is a three-row gather-add per token.  The backward mirrors it (nr_segment_rows_sum_conv3 sums
+// the shifted dC rows per distinct row; the table dgrad and the conv wgrad are then GEMMs over U).
+#include "common.h"
+#include "../../include/newsrec_hip.h"
+
+namespace {
+
+// one thread per (token, float4 column); consecutive threads walk one token's columns
+__global__ __launch_bounds__(256) void conv3_rows_fwd_kernel(const float* __restrict__ P, int64_t ldp, int tw4,
+                                                             int H, const int64_t* __restrict__ inv, int64_t T, int L,
+                                                             const float* __restrict__ bias, int relu,
+                                                             float* __restrict__ out, int64_t ldo) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= T * tw4) return;
+  const int64_t t = g / tw4;
+  const int c4 = (int)(g - t * tw4);
+  const int pos = (int)(t % L);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int p2 = pos + j - 1;
+    if (p2 < 0 || p2 >= L) continue;
+    const int64_t r = inv[t + j - 1];
+    const float4 v = reinterpret_cast<const float4*>(P + r * ldp)[j * tw4 + c4];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const int h = 4 * c4;
+  float e[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    if (h + u < H) {
+      float x = e[u] + (bias ? bias[h + u] : 0.f);
+      e[u] = relu ? fmaxf(x, 0.f) : x;
+    } else {
+      e[u] = 0.f;   // padded columns: exact zeros (the next GEMM contracts over them)
+    }
+  }
+  reinterpret_cast<float4*>(out + t * ldo)[c4] = make_float4(e[0], e[1], e[2], e[3]);
+}
+
+}  // namespace
+
+extern "C" int nr_conv3_rows_fwd(const float* P, int64_t ldp, int32_t tap_width, int32_t H, const int64_t* inv,
+                                 int64_t T, int32_t L, const float* bias, int32_t relu, float* out, int64_t ldo,
+                                 hipStream_t stream) {
+  if (tap_width < 4 || (tap_width & 3) || H < 1 || H > tap_width || L < 1 || T < 0 || (T % L) || (ldp & 3) ||
+      (ldo & 3) || ldp < 3 * tap_width || ldo < tap_width)
+    return NR_EINVAL(0);
+  if (!P || !inv || !out) return NR_EINVAL(1);
+  if ((reinterpret_cast<uintptr_t>(P) & 15) || (reinterpret_cast<uintptr_t>(out) & 15)) return NR_EINVAL(2);
+  if (T == 0) return NR_OK;
+  const int tw4 = tap_width / 4;
+  const int64_t n = T * tw4;
+  hipLaunchKernelGGL(conv3_rows_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, P, ldp, tw4, H,
+                     inv, T, L, bias, relu, out, ldo);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}

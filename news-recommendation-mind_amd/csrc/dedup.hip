@@ -236,7 +236,12 @@ __global__ __launch_bounds__(CNT_THREADS) void fill_kernel(const int64_t* __rest
 // first piece, slot 1: a later one) for pass 2.  A table in LDS marks each piece's last
 // position and destination; one thread per float4 column streams the range 8 rows at a time
 // (8 independent loads in flight), flushing at piece ends (block-uniform branches).
+// TAPS (the k = 3 convolution's per-distinct-row sums, nr_segment_rows_sum_conv3): output column
+// block `tap` (wt4 float4 wide) of token t's contribution is src row t + 1 - tap of the same title
+// of L tokens, zero when that row is outside the title.
+template <bool TAPS>
 __global__ __launch_bounds__(1024) void segsum_pieces_kernel(const float* __restrict__ src, int64_t lds, int64_t w4,
+                                                             int64_t wt4, int L,
                                                              const int32_t* __restrict__ seg_off,
                                                              const int32_t* __restrict__ seg_tok,
                                                              const int32_t* __restrict__ seg_of,
@@ -249,11 +254,17 @@ __global__ __launch_bounds__(1024) void segsum_pieces_kernel(const float* __rest
   const int64_t p1 = p0 + SEG_RANGE < T ? p0 + SEG_RANGE : T;
   const int n = (int)(p1 - p0);
   __shared__ int32_t s_tok[SEG_RANGE], s_seg[SEG_RANGE + 1];
+  __shared__ uint8_t s_ok[TAPS ? SEG_RANGE : 1];   // TAPS: bit j = src row t + 1 - j inside the title
   __shared__ int64_t s_dst[SEG_RANGE];   // at a piece's last position: its float4 destination
   const int tid = threadIdx.x;
   if (tid < n) {
-    s_tok[tid] = seg_tok[p0 + tid];
+    const int32_t t = seg_tok[p0 + tid];
+    s_tok[tid] = t;
     s_seg[tid] = seg_of[p0 + tid];
+    if (TAPS) {
+      const int pos = t % L;
+      s_ok[tid] = (uint8_t)((pos + 1 < L ? 1 : 0) | 2 | (pos > 0 ? 4 : 0));
+    }
   }
   if (tid == 0) s_seg[n] = -1;
   __syncthreads();
@@ -268,13 +279,26 @@ __global__ __launch_bounds__(1024) void segsum_pieces_kernel(const float* __rest
   __syncthreads();
   float4* dst4 = reinterpret_cast<float4*>(dst);
   for (int64_t j = tid; j < w4; j += blockDim.x) {
+    int tap = 0;
+    int64_t jc = j;
+    if (TAPS) {
+      tap = (int)(j / wt4);
+      jc = j - tap * wt4;
+    }
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int i0 = 0; i0 < n; i0 += 8) {
       float4 x[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int i = i0 + k < n ? i0 + k : n - 1;
-        x[k] = reinterpret_cast<const float4*>(src + (int64_t)s_tok[i] * lds)[j];
+        if (TAPS) {
+          const bool ok = (s_ok[i] >> tap) & 1;
+          const int64_t r = ok ? (int64_t)s_tok[i] + 1 - tap : (int64_t)s_tok[i];
+          const float4 v = reinterpret_cast<const float4*>(src + r * lds)[jc];
+          x[k] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          x[k] = reinterpret_cast<const float4*>(src + (int64_t)s_tok[i] * lds)[j];
+        }
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -439,24 +463,51 @@ extern "C" int64_t nr_segment_rows_sum_workspace(int64_t T, int64_t width) {
   return ((T + SEG_RANGE - 1) / SEG_RANGE) * 2 * width * (int64_t)sizeof(float);
 }
 
-extern "C" int nr_segment_rows_sum(const float* src, int64_t lds, int64_t width, int64_t T, const int32_t* seg_off,
-                                   const int32_t* seg_tok, const int32_t* seg_of, const int32_t* counts,
-                                   int64_t rows_max, float* work, float* dst, int64_t ldd, hipStream_t stream) {
-  if (width < 0 || (width & 3) || (lds & 3) || (ldd & 3) || rows_max < 0 || T < 0) return NR_EINVAL(0);
-  if (!src || !seg_off || !seg_tok || !seg_of || !counts || !dst || (T > 0 && !work)) return NR_EINVAL(1);
-  if ((reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 15) ||
-      (reinterpret_cast<uintptr_t>(work) & 15))
-    return NR_EINVAL(2);
+namespace {
+int segsum_launch(bool taps, const float* src, int64_t lds, int64_t width, int64_t wt4, int L, int64_t T,
+                  const int32_t* seg_off, const int32_t* seg_tok, const int32_t* seg_of, const int32_t* counts,
+                  int64_t rows_max, float* work, float* dst, int64_t ldd, hipStream_t stream) {
   if (rows_max == 0 || width == 0) return NR_OK;
   const int64_t w4 = width / 4;
-  if (T > 0)
-    hipLaunchKernelGGL(segsum_pieces_kernel, dim3((unsigned)((T + SEG_RANGE - 1) / SEG_RANGE)),
-                       dim3((unsigned)(w4 >= 1024 ? 1024 : (w4 < SEG_RANGE ? SEG_RANGE : (w4 + 63) / 64 * 64))), 0,
-                       stream, src, lds, w4, seg_off, seg_tok, seg_of, counts, reinterpret_cast<float4*>(work), dst,
-                       ldd);
+  if (T > 0) {
+    const dim3 grid((unsigned)((T + SEG_RANGE - 1) / SEG_RANGE));
+    const dim3 block((unsigned)(w4 >= 1024 ? 1024 : (w4 < SEG_RANGE ? SEG_RANGE : (w4 + 63) / 64 * 64)));
+    if (taps)
+      hipLaunchKernelGGL(segsum_pieces_kernel<true>, grid, block, 0, stream, src, lds, w4, wt4, L, seg_off, seg_tok,
+                         seg_of, counts, reinterpret_cast<float4*>(work), dst, ldd);
+    else
+      hipLaunchKernelGGL(segsum_pieces_kernel<false>, grid, block, 0, stream, src, lds, w4, wt4, L, seg_off, seg_tok,
+                         seg_of, counts, reinterpret_cast<float4*>(work), dst, ldd);
+  }
   const int64_t fb = (rows_max + FIX_THREADS - 1) / FIX_THREADS;
   hipLaunchKernelGGL(segsum_fix_kernel, dim3((unsigned)(fb < FIX_BLOCKS ? fb : FIX_BLOCKS)), dim3(FIX_THREADS), 0,
                      stream, w4, seg_off, counts, reinterpret_cast<const float4*>(work), dst, ldd);
   NR_LAUNCH_CHECK();
   return NR_OK;
+}
+
+bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) != 0; }
+}  // namespace
+
+extern "C" int nr_segment_rows_sum(const float* src, int64_t lds, int64_t width, int64_t T, const int32_t* seg_off,
+                                   const int32_t* seg_tok, const int32_t* seg_of, const int32_t* counts,
+                                   int64_t rows_max, float* work, float* dst, int64_t ldd, hipStream_t stream) {
+  if (width < 0 || (width & 3) || (lds & 3) || (ldd & 3) || rows_max < 0 || T < 0) return NR_EINVAL(0);
+  if (!src || !seg_off || !seg_tok || !seg_of || !counts || !dst || (T > 0 && !work)) return NR_EINVAL(1);
+  if (misaligned(src) || misaligned(dst) || misaligned(work)) return NR_EINVAL(2);
+  return segsum_launch(false, src, lds, width, 0, 1, T, seg_off, seg_tok, seg_of, counts, rows_max, work, dst, ldd,
+                       stream);
+}
+
+extern "C" int nr_segment_rows_sum_conv3(const float* src, int64_t lds, int64_t tap_width, int32_t L, int64_t T,
+                                         const int32_t* seg_off, const int32_t* seg_tok, const int32_t* seg_of,
+                                         const int32_t* counts, int64_t rows_max, float* work, float* dst,
+                                         int64_t ldd, hipStream_t stream) {
+  if (tap_width < 0 || (tap_width & 3) || (lds & 3) || (ldd & 3) || rows_max < 0 || T < 0 || L < 1 ||
+      (T % L) || ldd < 3 * tap_width || lds < tap_width)
+    return NR_EINVAL(0);
+  if (!src || !seg_off || !seg_tok || !seg_of || !counts || !dst || (T > 0 && !work)) return NR_EINVAL(1);
+  if (misaligned(src) || misaligned(dst) || misaligned(work)) return NR_EINVAL(2);
+  return segsum_launch(true, src, lds, 3 * tap_width, tap_width / 4, L, T, seg_off, seg_tok, seg_of, counts, rows_max,
+                       work, dst, ldd, stream);
 }

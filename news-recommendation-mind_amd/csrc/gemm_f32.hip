@@ -313,8 +313,9 @@ int pick_tile(int64_t n) {  // 64 or 128: least padding, ties -> 128
 extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
                            const nr_operand* B, float* C, int64_t ldc, const float* bias,
                            int32_t epilogue, const nr_operand* c_rows, int64_t pad_row,
-                           int32_t split_k, hipStream_t stream) {
+                           int32_t split_k, int32_t prec, hipStream_t stream) {
   if (M < 0 || N < 0 || K < 0) return NR_EINVAL(0);
+  if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(12);
   if (!A || !B || !C || !A->data || !B->data) return NR_EINVAL(1);
   if (((A->map != NR_ROWS_PLAIN) && (A->ld & 3)) || ((B->map != NR_ROWS_PLAIN) && (B->ld & 3)))
     return NR_EINVAL(2);   // gathered tables must be float4-addressable
@@ -340,11 +341,12 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
     return NR_EINVAL(4);
   if (!getenv_generic()) {
     const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128) * splits;
-    // small problems (< 400 tiles of 128x128) take 64x64 tiles, which only the exact-f32 kernel
-    // has: they are latency-bound, and 128x128 bf16x6 tiles would leave most CUs idle
-    const int fb = t128 >= 400 ? 128 : 64;
-    const int rc =
-        nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, fb, fb, nullptr, nullptr, stream);
+    // bf16x6: small problems (< 400 tiles of 128x128) take 64x64 tiles, which only the exact-f32
+    // kernel has (they are latency-bound, and 128x128 bf16x6 tiles would leave most CUs idle).
+    // bf16: every eligible shape runs on the bf16 kernel (one product per tile is cheap).
+    const int fb = (prec == NR_GEMM_BF16 || (prec == NR_GEMM_BF16X6 && t128 >= 400)) ? 128 : 64;
+    const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, fb, fb, nullptr,
+                                nullptr, prec, stream);
     if (rc != -1) return rc;
   }
   if (epilogue == NR_EPI_SCATTER_STORE) g.epi = NR_EPI_SCATTER;   // generic kernel: same sums via atomics
@@ -374,8 +376,9 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
 extern "C" int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B,
                                float* C, int64_t ldc, const float* bias, int32_t epilogue,
                                const nr_operand* c_rows, int64_t pad_row, int32_t split_k, const int32_t* m_dev,
-                               const int32_t* k_dev, hipStream_t stream) {
+                               const int32_t* k_dev, int32_t prec, hipStream_t stream) {
   if (M < 0 || N < 0 || K < 0 || (K % 32)) return NR_EINVAL(0);
+  if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(14);
   if (!A || !B || !C || !A->data || !B->data) return NR_EINVAL(1);
   if ((A->ld & 3) || (B->ld & 3)) return NR_EINVAL(2);
   if (epilogue == NR_EPI_SCATTER && (!c_rows || (c_rows->map != NR_ROWS_PLAIN && !c_rows->rows)))
@@ -389,6 +392,6 @@ extern "C" int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand
   if (split_k > 1 && epilogue != NR_EPI_ATOMIC && epilogue != NR_EPI_SCATTER) return NR_EINVAL(5);
   if (M == 0 || N == 0 || K == 0) return NR_OK;
   const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, 128, 128, m_dev,
-                              k_dev, stream);
+                              k_dev, prec, stream);
   return rc == -1 ? NR_EINVAL(7) : rc;
 }

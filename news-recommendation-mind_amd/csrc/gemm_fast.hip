@@ -21,14 +21,6 @@
 
 #include "gemm_fast_impl.h"
 
-// GEMM arithmetic for the whole process (nr_gemm_set_precision; initial value from NR_GEMM_PREC =
-// "bf16x6" (default) | "f32").  bf16x6 is measured at least as accurate as the f32 MFMA
-// (tools/split_probe.py: max / mean |C - C_fp64| 1.6e-4 / 8.1e-6 vs 1.9e-4 / 9.6e-6 at K = 768).
-static int g_gemm_prec = [] {
-  const char* e = getenv("NR_GEMM_PREC");
-  return (e && e[0] == 'f') ? NR_GEMM_F32 : NR_GEMM_BF16X6;
-}();
-
 namespace nrfast {
 int launch_modes64(const Args& g, int am, int bm, int splits, hipStream_t s);   // gemm_fast64.hip
 }  // namespace nrfast
@@ -37,7 +29,8 @@ int launch_modes64(const Args& g, int am, int bm, int splits, hipStream_t s);   
 // Returns -1 if the shape/operands are not eligible (the caller falls back), else a status.
 int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B, float* C,
                  int64_t ldc, const float* bias, int32_t epilogue, const nr_operand* c_rows, int64_t pad_row,
-                 int32_t split_k, int bm, int bn, const int32_t* m_dev, const int32_t* k_dev, hipStream_t stream) {
+                 int32_t split_k, int bm, int bn, const int32_t* m_dev, const int32_t* k_dev, int32_t prec,
+                 hipStream_t stream) {
   using namespace nrfast;
   if (K <= 0) return -1;
   auto aligned = [](const nr_operand* o) {
@@ -90,16 +83,7 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   g.kchunk = (g.kchunk + 31) / 32 * 32;
   if (g.kchunk == 0) g.kchunk = 32;
   const int splits = (int)((K + g.kchunk - 1) / g.kchunk) > 0 ? (int)((K + g.kchunk - 1) / g.kchunk) : 1;
-  if (bm == 128 && bn == 128) return launch_modes<128, 128>(g, am, bmode, splits, stream);
+  if (bm == 128 && bn == 128) return launch_modes<128, 128>(g, am, bmode, splits, prec, stream);
   if (bm == 64 && bn == 64) return launch_modes64(g, am, bmode, splits, stream);
   return -1;
 }
-
-extern "C" int nr_gemm_set_precision(int32_t mode) {
-  if (mode != NR_GEMM_F32 && mode != NR_GEMM_BF16X6) return NR_EINVAL(0);
-  const int old = g_gemm_prec;
-  g_gemm_prec = mode;
-  return old;
-}
-
-extern "C" int nr_gemm_get_precision(void) { return g_gemm_prec; }

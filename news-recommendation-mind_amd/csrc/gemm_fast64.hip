@@ -5,7 +5,7 @@
 namespace nrfast {
 
 int launch_modes64(const Args& g, int am, int bm, int splits, hipStream_t s) {
-  return launch_modes<64, 64>(g, am, bm, splits, s);
+  return launch_modes<64, 64>(g, am, bm, splits, NR_GEMM_F32, s);
 }
 
 }  // namespace nrfast

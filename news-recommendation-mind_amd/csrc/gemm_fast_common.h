@@ -19,7 +19,6 @@ __device__ __forceinline__ uint32_t bf_rne(float x) {
   return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
 }
 __device__ __forceinline__ float bf_f(uint32_t b) { return __uint_as_float(b << 16); }
-#ifndef NR_SPLIT_MANUAL_RNE
 // hardware conversions: the compiler pairs the casts into v_cvt_pk_bf16_f32 (round to nearest even)
 __device__ __forceinline__ uint32_t bf_bits(__bf16 v) { return (uint32_t)__builtin_bit_cast(uint16_t, v); }
 __device__ __forceinline__ void split1(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
@@ -31,14 +30,6 @@ __device__ __forceinline__ void split1(float x, uint32_t& h, uint32_t& m, uint32
   m = bf_bits(mb);
   l = bf_bits(lb);
 }
-#else
-__device__ __forceinline__ void split1(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
-  h = bf_rne(x);
-  const float r = x - bf_f(h);   // exact
-  m = bf_rne(r);
-  l = bf_rne(r - bf_f(m));
-}
-#endif
 __device__ __forceinline__ void split4(float a, float b, float c, float d, uint2& p0, uint2& p1, uint2& p2) {
   uint32_t h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
   split1(a, h0, m0, l0);
@@ -48,6 +39,10 @@ __device__ __forceinline__ void split4(float a, float b, float c, float d, uint2
   p0 = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
   p1 = make_uint2(m0 | (m1 << 16), m2 | (m3 << 16));
   p2 = make_uint2(l0 | (l1 << 16), l2 | (l3 << 16));
+}
+// bf16 arithmetic (one product): the four values rounded to bf16 (RNE), packed
+__device__ __forceinline__ uint2 hi4(float a, float b, float c, float d) {
+  return make_uint2(bf_bits((__bf16)a) | (bf_bits((__bf16)b) << 16), bf_bits((__bf16)c) | (bf_bits((__bf16)d) << 16));
 }
 constexpr int SROW = 40;          // split LDS image: [plane][row][k] bf16, 32 k + 8 pad (80-B rows)
 constexpr int SPL = 128 * SROW;   // one plane of a 128-row operand tile
@@ -206,39 +201,24 @@ struct Loader {
     }
   }
 
-  // bf16x6, split ahead of the publish (the VALU work overlaps the current tile's MFMAs)
-  uint2 sp[KC ? NV : 1][3];
-  __device__ __forceinline__ void presplit() {
-    if constexpr (KC) {
-#pragma unroll
-      for (int i = 0; i < NV; ++i) split4(v[i].x, v[i].y, v[i].z, v[i].w, sp[i][0], sp[i][1], sp[i][2]);
-    }
-  }
-  __device__ __forceinline__ void store_presplit(uint16_t* lds, int tid) const {
-    if constexpr (KC) {
-#pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int f = tid + 256 * i;
-        uint16_t* q = lds + (f >> 3) * SROW + 4 * (f & 7);
-        *reinterpret_cast<uint2*>(q) = sp[i][0];
-        *reinterpret_cast<uint2*>(q + SPL) = sp[i][1];
-        *reinterpret_cast<uint2*>(q + 2 * SPL) = sp[i][2];
-      }
-    }
-  }
-
-  // bf16x6 image (K-contiguous operands only): the float4 of 4 k of one row -> 3 planes
+  // split LDS image (K-contiguous operands only): the float4 of 4 k of one row -> NP planes
+  // (NP = 3: bf16x6 terms h, m, l; NP = 1: bf16 arithmetic, the value rounded to bf16)
+  template <int NP>
   __device__ __forceinline__ void store_split(uint16_t* lds, int tid) const {
     if constexpr (KC) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         const int f = tid + 256 * i;
-        uint2 p0, p1, p2;
-        split4(v[i].x, v[i].y, v[i].z, v[i].w, p0, p1, p2);
         uint16_t* q = lds + (f >> 3) * SROW + 4 * (f & 7);
-        *reinterpret_cast<uint2*>(q) = p0;
-        *reinterpret_cast<uint2*>(q + SPL) = p1;
-        *reinterpret_cast<uint2*>(q + 2 * SPL) = p2;
+        if constexpr (NP == 1) {
+          *reinterpret_cast<uint2*>(q) = hi4(v[i].x, v[i].y, v[i].z, v[i].w);
+        } else {
+          uint2 p0, p1, p2;
+          split4(v[i].x, v[i].y, v[i].z, v[i].w, p0, p1, p2);
+          *reinterpret_cast<uint2*>(q) = p0;
+          *reinterpret_cast<uint2*>(q + SPL) = p1;
+          *reinterpret_cast<uint2*>(q + 2 * SPL) = p2;
+        }
       }
     }
   }
@@ -301,39 +281,27 @@ struct MNBlk {
     }
   }
 
+  template <int NP>
   __device__ __forceinline__ void put(uint16_t* q, float a, float b, float c, float e) const {
-    uint2 p0, p1, p2;
-    split4(a, b, c, e, p0, p1, p2);
-    *reinterpret_cast<uint2*>(q) = p0;
-    *reinterpret_cast<uint2*>(q + SPL) = p1;
-    *reinterpret_cast<uint2*>(q + 2 * SPL) = p2;
-  }
-
-  uint2 sp[4][3];
-  __device__ __forceinline__ void presplit() {
-    split4(v[0].x, v[1].x, v[2].x, v[3].x, sp[0][0], sp[0][1], sp[0][2]);
-    split4(v[0].y, v[1].y, v[2].y, v[3].y, sp[1][0], sp[1][1], sp[1][2]);
-    split4(v[0].z, v[1].z, v[2].z, v[3].z, sp[2][0], sp[2][1], sp[2][2]);
-    split4(v[0].w, v[1].w, v[2].w, v[3].w, sp[3][0], sp[3][1], sp[3][2]);
-  }
-  __device__ __forceinline__ void store_presplit(uint16_t* lds, int tid) const {
-    const int kg = tid & 7, cg = tid >> 3;
-    uint16_t* q = lds + (4 * cg) * SROW + 4 * kg;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      *reinterpret_cast<uint2*>(q + u * SROW) = sp[u][0];
-      *reinterpret_cast<uint2*>(q + u * SROW + SPL) = sp[u][1];
-      *reinterpret_cast<uint2*>(q + u * SROW + 2 * SPL) = sp[u][2];
+    if constexpr (NP == 1) {
+      *reinterpret_cast<uint2*>(q) = hi4(a, b, c, e);
+    } else {
+      uint2 p0, p1, p2;
+      split4(a, b, c, e, p0, p1, p2);
+      *reinterpret_cast<uint2*>(q) = p0;
+      *reinterpret_cast<uint2*>(q + SPL) = p1;
+      *reinterpret_cast<uint2*>(q + 2 * SPL) = p2;
     }
   }
 
+  template <int NP>
   __device__ __forceinline__ void store_split(uint16_t* lds, int tid) const {
     const int kg = tid & 7, cg = tid >> 3;
     uint16_t* q = lds + (4 * cg) * SROW + 4 * kg;
-    put(q, v[0].x, v[1].x, v[2].x, v[3].x);
-    put(q + SROW, v[0].y, v[1].y, v[2].y, v[3].y);
-    put(q + 2 * SROW, v[0].z, v[1].z, v[2].z, v[3].z);
-    put(q + 3 * SROW, v[0].w, v[1].w, v[2].w, v[3].w);
+    put<NP>(q, v[0].x, v[1].x, v[2].x, v[3].x);
+    put<NP>(q + SROW, v[0].y, v[1].y, v[2].y, v[3].y);
+    put<NP>(q + 2 * SROW, v[0].z, v[1].z, v[2].z, v[3].z);
+    put<NP>(q + 3 * SROW, v[0].w, v[1].w, v[2].w, v[3].w);
   }
 };
 
@@ -609,7 +577,8 @@ inline bool persistent_disabled() {   // NR_GEMM_NOPERSIST=1: one unit per block
   return v == 1;
 }
 
-// bf16x6 launch of the 128x128 fast-path operand combinations (gemm_split.hip); -1 = not covered
-int launch_split_modes(const Args& g, int am, int bm, int splits, hipStream_t s);
+// bf16 launches of the 128x128 fast-path operand combinations (gemm_split_*.hip), np = 3 (bf16x6)
+// or 1 (bf16); -1 = not covered
+int launch_split_modes(const Args& g, int am, int bm, int splits, int np, hipStream_t s);
 
 }  // namespace nrfast

@@ -4,8 +4,6 @@
 #pragma once
 #include "gemm_fast_common.h"
 
-int nr_gemm_get_precision(void);   // newsrec_hip.h (C ABI)
-
 namespace nrfast {
 
 
@@ -202,9 +200,9 @@ int launch(const Args& g, int splits, hipStream_t s) {
 }
 
 template <int BM, int BN>
-int launch_modes(const Args& g, int am, int bm, int splits, hipStream_t s) {
-  if (BM == 128 && BN == 128 && nr_gemm_get_precision() == NR_GEMM_BF16X6) {
-    const int rc = launch_split_modes(g, am, bm, splits, s);
+int launch_modes(const Args& g, int am, int bm, int splits, int prec, hipStream_t s) {
+  if (BM == 128 && BN == 128 && prec != NR_GEMM_F32) {
+    const int rc = launch_split_modes(g, am, bm, splits, prec == NR_GEMM_BF16 ? 1 : 3, s);
     if (rc != -1) return rc;
   }
 #define NR_AB(A_, B_, TR_) \

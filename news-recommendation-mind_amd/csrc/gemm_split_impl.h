@@ -1,5 +1,6 @@
-// bf16x6 GEMM kernel (nr_gemm_set_precision(NR_GEMM_BF16X6)), included by gemm_split_kc.hip and
-// gemm_split_mn.hip so its instantiations compile in parallel.  Shared code: gemm_fast_common.h.
+// bf16 matrix-core GEMM kernels (NR_GEMM_BF16X6: NP = 3 planes, six products; NR_GEMM_BF16: NP = 1,
+// one product), included by the gemm_split_*.hip translation units so the instantiations compile in
+// parallel.  Shared code: gemm_fast_common.h.
 #pragma once
 #include <type_traits>
 
@@ -14,13 +15,15 @@ namespace nrfast {
 // smallest terms first.  The accumulators have the f32 MFMA's C/D layout, so the epilogues are
 // shared.  One LDS image (60 KiB) so two workgroups share a CU: tile P+1 waits in registers while
 // P computes, is published between two barriers, and P+2's loads go out right behind it.
-template <int AM, int BMODE, bool TR>
+// NP = 1 (bf16 arithmetic): the same pipeline with one plane per operand and one MFMA per
+// 32x32 tile and k-step (fp32 operands rounded to bf16 on the way to LDS, fp32 accumulation).
+template <int AM, int BMODE, bool TR, int NP>
 __global__ __launch_bounds__(256, 2) void gemm_split_kernel(Args g) {
   using LA = typename std::conditional<is_kc(AM), Loader<128, AM>, MNBlk<AM>>::type;
   using LB = typename std::conditional<is_kc(BMODE), Loader<128, BMODE>, MNBlk<BMODE>>::type;
   constexpr int BM = 128, BN = 128;
-  __shared__ __attribute__((aligned(16))) uint16_t As[3 * SPL];
-  __shared__ __attribute__((aligned(16))) uint16_t Bs[3 * SPL];
+  __shared__ __attribute__((aligned(16))) uint16_t As[NP * SPL];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[NP * SPL];
   constexpr bool IDX_AHEAD = AM == MN_GATHER || BMODE == MN_GATHER;
 
   if (g.mdyn) {
@@ -111,8 +114,8 @@ __global__ __launch_bounds__(256, 2) void gemm_split_kernel(Args g) {
     lb.prefetch_idx(g.B, kof(lp), g.K, tid);
   }
   issue(lp);
-  la.store_split(As, tid);
-  lb.store_split(Bs, tid);
+  la.template store_split<NP>(As, tid);
+  lb.template store_split<NP>(Bs, tid);
   bool staged = step_load();
   __syncthreads();
 
@@ -134,57 +137,42 @@ __global__ __launch_bounds__(256, 2) void gemm_split_kernel(Args g) {
     const bool had_staged = staged;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8 a[TI][3], b[TJ][3];
+      bf16x8 a[TI][NP], b[TJ][NP];
       const int ko = 16 * s + 8 * h;
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
           a[i][p] = *reinterpret_cast<const bf16x8*>(a_s + p * SPL + (wm + 32 * i + c) * SROW + ko);
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
           b[j][p] = *reinterpret_cast<const bf16x8*>(b_s + p * SPL + (wn + 32 * j + c) * SROW + ko);
 #define NR_MF(X, Y)                                                                              \
   acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][Y], a[i][X], acc[i][j], 0, 0, 0) \
                  : __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][X], b[j][Y], acc[i][j], 0, 0, 0)
-#ifdef NR_SPLIT_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
-          NR_MF(2, 0);
-          NR_MF(1, 1);
-          NR_MF(0, 2);
-          NR_MF(1, 0);
-          NR_MF(0, 1);
+          if constexpr (NP == 3) {   // smallest terms first
+            NR_MF(2, 0);
+            NR_MF(1, 1);
+            NR_MF(0, 2);
+            NR_MF(1, 0);
+            NR_MF(0, 1);
+          }
           NR_MF(0, 0);
         }
-#ifdef NR_SPLIT_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
 #undef NR_MF
-#ifdef NR_SPLIT_EARLY
-      if (s == 0 && had_staged) {   // split P+1 while P's second k-step runs on the matrix cores
-        la.presplit();
-        lb.presplit();
-      }
-#endif
     }
     __syncthreads();                // every wave is done reading P
     const int old = cp.id;
     const int64_t om0 = cp.u.m0, on0 = cp.u.n0;
     if (!had_staged) break;
-#ifdef NR_SPLIT_EARLY
-    la.store_presplit(As, tid);     // publish P+1 (split during P's MFMAs)
-    lb.store_presplit(Bs, tid);
-#else
-    la.store_split(As, tid);        // publish P+1 (its loads landed during P's MFMAs)
-    lb.store_split(Bs, tid);
-#endif
+    la.template store_split<NP>(As, tid);   // publish P+1 (its loads landed during P's MFMAs)
+    lb.template store_split<NP>(Bs, tid);
     staged = step_load();           // and start P+2
     __syncthreads();
     advance(cp);
@@ -197,7 +185,7 @@ __global__ __launch_bounds__(256, 2) void gemm_split_kernel(Args g) {
   epilogue_any<TR, TI, TJ>(g, acc, cp.u.m0, cp.u.n0, wm, wn, h, c);
 }
 
-template <int AM, int BMODE, bool TR>
+template <int AM, int BMODE, bool TR, int NP>
 int launch_split(const Args& g, int splits, hipStream_t s) {
   const int64_t gm = (g.M + 127) / 128, gn = (g.N + 127) / 128;
   const int64_t units = gm * gn * splits;
@@ -205,14 +193,46 @@ int launch_split(const Args& g, int splits, hipStream_t s) {
   if (units > 0x7fffffff) return NR_EINVAL(0);
   int grid = (int)units;
   if (!persistent_disabled()) {
-    const int slots = resident_slots(gemm_split_kernel<AM, BMODE, TR>);
+    const int slots = resident_slots(gemm_split_kernel<AM, BMODE, TR, NP>);
     if (slots > 0 && slots < grid) grid = slots;
   }
   Args a = g;
   a.splits = splits;
-  hipLaunchKernelGGL((gemm_split_kernel<AM, BMODE, TR>), dim3((unsigned)grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((gemm_split_kernel<AM, BMODE, TR, NP>), dim3((unsigned)grid), dim3(256), 0, s, a);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
+
+// K-contiguous A operand (projections, dgrads)
+template <int NP>
+int launch_split_kc(const Args& g, int am, int bm, int splits, hipStream_t s) {
+  const bool atomic_epi = g.epi == NR_EPI_ATOMIC || g.epi == NR_EPI_SCATTER;
+#define NR_SAB(A_, B_, TR_) \
+  if (am == A_ && bm == B_ && atomic_epi == !TR_) return launch_split<A_, B_, TR_, NP>(g, splits, s);
+  NR_SAB(KC_GATHER, KC_PLAIN, true)
+  NR_SAB(KC_CONV3, KC_PLAIN, true)
+  NR_SAB(KC_PLAIN, KC_PLAIN, true)
+  NR_SAB(KC_PLAIN, MN_PLAIN, true)
+  NR_SAB(KC_PLAIN, MN_PLAIN, false)
+#undef NR_SAB
+  return -1;
+}
+
+// MN-contiguous A operand (weight gradients)
+template <int NP>
+int launch_split_mn(const Args& g, int am, int bm, int splits, hipStream_t s) {
+  const bool atomic_epi = g.epi == NR_EPI_ATOMIC || g.epi == NR_EPI_SCATTER;
+  if (!atomic_epi || am != MN_PLAIN) return -1;
+  if (bm == MN_GATHER) return launch_split<MN_PLAIN, MN_GATHER, false, NP>(g, splits, s);
+  if (bm == MN_PLAIN) return launch_split<MN_PLAIN, MN_PLAIN, false, NP>(g, splits, s);
+  if (bm == MN_CONV3 && g.B.seg % 128 == 0) return launch_split<MN_PLAIN, MN_CONV3, false, NP>(g, splits, s);
+  return -1;
+}
+
+// one translation unit per (operand family, plane count): gemm_split_{kc,mn}{1,3}.hip
+int launch_split_kc1(const Args& g, int am, int bm, int splits, hipStream_t s);
+int launch_split_kc3(const Args& g, int am, int bm, int splits, hipStream_t s);
+int launch_split_mn1(const Args& g, int am, int bm, int splits, hipStream_t s);
+int launch_split_mn3(const Args& g, int am, int bm, int splits, hipStream_t s);
 
 }  // namespace nrfast

@@ -27,7 +27,7 @@ EPI_STORE, EPI_STORE_RELU, EPI_ATOMIC, EPI_SCATTER = 0, 1, 2, 3
 MASK_U8, MASK_I64, MASK_F64, MASK_F32 = 0, 1, 2, 3
 EPI_STORE_TANH, EPI_ACCUM_GATE, EPI_ACCUM, EPI_SCATTER_STORE = 4, 5, 6, 7
 EPI_STORE_GELU, EPI_GELU_GRAD = 8, 9
-GEMM_F32, GEMM_BF16X6 = 0, 1
+GEMM_F32, GEMM_BF16X6, GEMM_BF16 = 0, 1, 2
 CELL_LSTM, CELL_GRU = 0, 1
 SCORE_RAW, SCORE_LOG_SOFTMAX, SCORE_SIGMOID = 0, 1, 2
 
@@ -46,14 +46,18 @@ class nr_adam_tensor(ctypes.Structure):
 # name -> argtypes (restype int32 unless listed in _RESTYPES)
 _SIGS = {
     "nr_gemm_f32": [c_i64, c_i64, c_i64, ctypes.POINTER(nr_operand), ctypes.POINTER(nr_operand),
-                    c_ptr, c_i64, c_ptr, c_i32, ctypes.POINTER(nr_operand), c_i64, c_i32, c_ptr],
+                    c_ptr, c_i64, c_ptr, c_i32, ctypes.POINTER(nr_operand), c_i64, c_i32, c_i32, c_ptr],
     "nr_gemm_f32_dyn": [c_i64, c_i64, c_i64, ctypes.POINTER(nr_operand), ctypes.POINTER(nr_operand),
-                        c_ptr, c_i64, c_ptr, c_i32, ctypes.POINTER(nr_operand), c_i64, c_i32, c_ptr, c_ptr, c_ptr],
+                        c_ptr, c_i64, c_ptr, c_i32, ctypes.POINTER(nr_operand), c_i64, c_i32, c_ptr, c_ptr, c_i32,
+                        c_ptr],
     "nr_unique_rows": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                        c_ptr],
     "nr_segment_rows_sum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
                             c_ptr],
     "nr_segment_rows_sum_workspace": [c_i64, c_i64],
+    "nr_segment_rows_sum_conv3": [c_ptr, c_i64, c_i64, c_i32, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr,
+                                  c_i64, c_ptr],
+    "nr_conv3_rows_fwd": [c_ptr, c_i64, c_i32, c_i32, c_ptr, c_i64, c_i32, c_ptr, c_i32, c_ptr, c_i64, c_ptr],
     "nr_mha_attn_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
                         c_f32, c_ptr, c_i64, c_ptr],
     "nr_mha_attn_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
@@ -102,12 +106,12 @@ _SIGS = {
     "nr_bert_attn_bwd": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_u64, c_u64,
                          c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr],
     "nr_tanh_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr],
-    "nr_gemm_set_precision": [c_i32],
     "nr_adam_multi": [ctypes.POINTER(nr_adam_tensor), c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_ptr],
-    "nr_gemm_get_precision": [],
+    "nr_build_hash": [],
 }
 
-_RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64}
+_RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64,
+             "nr_build_hash": ctypes.c_char_p}
 
 # enum nr_batch_flags / nr_metric_flags
 BATCH_REVERSE_HISTORY, BATCH_SHUFFLE_POS = 1, 2
@@ -120,13 +124,36 @@ class HipError(RuntimeError):
     pass
 
 
+def _expected_hash():
+    """Hash of the sources next to the package (build.py's source_hash), or None when the tree
+    carries no sources (an installed library) or NR_LIB_PATH points at another build."""
+    if os.environ.get("NR_LIB_PATH"):
+        return None
+    build_py = os.path.join(os.path.dirname(_HERE), "build.py")
+    if not os.path.exists(build_py):
+        return None
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_newsrec_build", build_py)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.source_hash()
+
+
 def load():
-    """Load (once) and return the ctypes library.  Raises if it is missing."""
+    """Load (once) and return the ctypes library.  Raises if it is missing or was built from
+    other sources than the ones in this tree (build provenance, see build.py)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise HipError("libnewsrec_hip.so not built (%s): run __graft_entry__.build()" % LIB_PATH)
         lib = ctypes.CDLL(LIB_PATH)
+        lib.nr_build_hash.restype = ctypes.c_char_p
+        lib.nr_build_hash.argtypes = []
+        built = lib.nr_build_hash().decode()
+        want = _expected_hash()
+        if want is not None and built != want:
+            raise HipError("libnewsrec_hip.so was built from other sources (hash %s, tree %s): run "
+                           "__graft_entry__.build()" % (built, want))
         for name, argtypes in _SIGS.items():
             fn = getattr(lib, name)
             fn.argtypes = argtypes

@@ -27,7 +27,7 @@ from torch import nn
 
 from . import _lib as L
 from . import kernels as K
-from .functions import _empty, _proj_wgrad, _zeros_views
+from .functions import _empty, _gemm_backward, _proj_wgrad, _zeros_views
 
 
 class BertConfig:
@@ -137,6 +137,7 @@ class BertFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, cfg, segs, drop, *params):
+        ctx.prec = K.get_gemm_precision()
         c = cfg
         H, heads, I = c.hidden_size, c.num_attention_heads, c.intermediate_size
         nl = c.num_hidden_layers
@@ -215,6 +216,7 @@ class BertFn(torch.autograd.Function):
         return x, pooled
 
     @staticmethod
+    @_gemm_backward
     def backward(ctx, dhid, dpooled):
         c = ctx.cfg
         H, heads, I = c.hidden_size, c.num_attention_heads, c.intermediate_size

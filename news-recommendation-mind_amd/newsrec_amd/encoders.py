@@ -14,7 +14,8 @@ from torch import nn
 
 from . import _lib as L
 from .attention import MultiheadAttention
-from .functions import AttnPoolFn, CNNNewsFn, MHAFn, MHANewsFn, RNNUserFn
+from . import functions as F
+from .functions import AttnPoolFn, CNNNewsFn, CNNNewsRowsFn, MHAFn, MHANewsFn, RNNUserFn
 
 
 def _identity_rows(n, device):
@@ -69,11 +70,27 @@ class CNN_Encoder(nn.Module):
         # Conv1d weight [H, E, 3] -> [H][tap*E + e] (the K = 3E GEMM operand)
         return self.cnn.weight.permute(0, 2, 1).reshape(self.hidden_dim, 3 * self.embedding_dim)
 
+    def _rows_operands(self):
+        """The distinct-row path's operands: the conv weight as [3*Hp, E] (row tap*Hp + h =
+        weight[h, :, tap]) and the key projection zero-padded to Hp = ceil32(H) (K % 32 == 0)."""
+        H = self.hidden_dim
+        Hp = (H + 31) // 32 * 32
+        w3t = torch.nn.functional.pad(self.cnn.weight.permute(2, 0, 1), (0, 0, 0, Hp - H))
+        w3t = w3t.reshape(3 * Hp, self.embedding_dim)
+        wq = torch.nn.functional.pad(self.wordQueryProject.weight, (0, Hp - H, 0, Hp - H))
+        bq = torch.nn.functional.pad(self.wordQueryProject.bias, (0, Hp - H))
+        return w3t, wq, bq
+
     def encode_tokens(self, table, token_ids, attn_mask, pad_row=0):
         lead = token_ids.shape[:-1]
         seq_len = token_ids.shape[-1]
         T = token_ids.numel()
         ids = token_ids.reshape(T)
+        if F.DEDUP_ROWS:
+            w3t, wq, bq = self._rows_operands()
+            news, tok = CNNNewsRowsFn.apply(table, ids, _mask_rows(attn_mask, T), w3t, self.cnn.bias, wq, bq,
+                                            self.query_words, seq_len, pad_row, self.hidden_dim)
+            return tok.reshape(*lead, seq_len, self.hidden_dim), news.reshape(*lead, self.hidden_dim)
         news, tok = CNNNewsFn.apply(table, ids, _mask_rows(attn_mask, T), self._w3().contiguous(), self.cnn.bias,
                                     self.wordQueryProject.weight, self.wordQueryProject.bias, self.query_words,
                                     seq_len, pad_row)

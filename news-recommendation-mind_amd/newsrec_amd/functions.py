@@ -9,12 +9,23 @@ operand loader) and scatter the table gradient straight out of the dgrad GEMM, s
 [T, 768] embedding activations are never materialised.  A standalone ``encoderN(emb, mask)``
 call uses the same functions with the embeddings as the "table" and identity row ids.
 """
+import functools
 import os
 
 import torch
 
 from . import _lib as L
 from . import kernels as K
+
+
+def _gemm_backward(fn):
+    """Run a Function's backward under the GEMM arithmetic its forward recorded in ``ctx.prec``
+    (the autograd engine runs CUDA backwards on its own thread, which has its own default)."""
+    @functools.wraps(fn)
+    def wrapper(ctx, *grads):
+        with K.gemm_precision(ctx.prec):
+            return fn(ctx, *grads)
+    return wrapper
 
 
 def _pad4(n):
@@ -164,6 +175,7 @@ class MHANewsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, table, ids, mask, w_cat, b_cat, gamma, beta, query, heads, dk, dv, seq_len,
                 pad_row, p_drop, seed, offset, want_tokens, rng=None):
+        ctx.prec = K.get_gemm_precision()
         T = ids.numel()
         n = T // seq_len
         V, E = table.shape
@@ -212,6 +224,7 @@ class MHANewsFn(torch.autograd.Function):
         return news, tok
 
     @staticmethod
+    @_gemm_backward
     def backward(ctx, dnews, dtok):
         table, ids, mask, w_cat, gamma, beta, query, Y, O, probs, stats = ctx.saved_tensors
         heads, dk, dv, seq_len, pad_row, p_drop, seed, offset, fused = ctx.cfg
@@ -276,6 +289,7 @@ class CNNNewsFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, table, ids, mask, w3, conv_b, wq, bq, query, seq_len, pad_row):
+        ctx.prec = K.get_gemm_precision()
         T = ids.numel()
         n = T // seq_len
         E = table.shape[1]
@@ -294,6 +308,7 @@ class CNNNewsFn(torch.autograd.Function):
         return news, C
 
     @staticmethod
+    @_gemm_backward
     def backward(ctx, dnews, dC_out):
         table, ids, mask, w3, wq, query, C, Kq, probs = ctx.saved_tensors
         seq_len, pad_row = ctx.cfg
@@ -329,6 +344,84 @@ class CNNNewsFn(torch.autograd.Function):
             if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
                 dtable = None
         return dtable, None, None, dw3, dconv_b, dwq, dbq, dq.view_as(query), None, None
+
+
+class CNNNewsRowsFn(torch.autograd.Function):
+    """CNN_Encoder.forward (models/Encoders/CNN.py:30-50) over DISTINCT word rows.
+
+    The k = 3 Conv1d is linear per tap and the embedding lookup (BERT.py:39) is a row gather, so
+    they commute: P = table[uids] · [W_0 | W_1 | W_2]ᵀ is ONE GEMM over the U distinct ids of the
+    batch (U ≈ 24.6 k of T = 52.8 k tokens on uniform ids), and C[t] = ReLU(b + Σ_j P[inv[t+j-1]][j])
+    is a three-row gather-add (nr_conv3_rows_fwd).  The backward sums the shifted dC rows per
+    distinct id once (S = nr_segment_rows_sum_conv3), after which the table gradient
+    (S · W3 -> plain stores into the distinct rows, no atomics) and the conv weight gradient
+    (Sᵀ · table[uids]) are GEMMs over U rows instead of T tokens.
+
+    w3t: [3*Hp, E] with row tap*Hp + h = Conv1d.weight[h, :, tap] (rows h >= H zero); wq, bq: the
+    key projection zero-padded to [Hp, Hp] / [Hp] so every contraction has K % 32 == 0.
+    Returns (news [n, H], C [T, H] view)."""
+
+    @staticmethod
+    def forward(ctx, table, ids, mask, w3t, conv_b, wq, bq, query, seq_len, pad_row, H):
+        ctx.prec = K.get_gemm_precision()
+        T = ids.numel()
+        n = T // seq_len
+        V, E = table.shape
+        Hp = w3t.shape[0] // 3
+        ur = K.UniqueRows(ids, V, fill_row=pad_row if 0 <= pad_row < V else 0)
+        P = _empty(ur.cap, 3 * Hp, table)
+        ev0 = PROBE.record()
+        K.gemm_dyn(ur.cap, 3 * Hp, E, K.operand(table, L.KCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER),
+                   K.operand(w3t, L.KCONTIG), P, m_dev=ur.u_pad)
+        PROBE.add("conv_fwd", ev0, PROBE.record(), ur)
+        C = _empty(T, Hp, table)
+        K.conv3_rows_fwd(P, Hp, H, ur.inv, seq_len, conv_b, C, relu=True)
+        Kq = _empty(T, Hp, table)
+        K.gemm(T, Hp, Hp, K.operand(C, L.KCONTIG), K.operand(wq, L.KCONTIG), Kq, bias=bq, epilogue=L.EPI_STORE_TANH)
+        news = _empty(n, H, table)
+        probs = torch.empty(T, device=table.device)
+        K.attn_pool_fwd(C, query, mask, n, seq_len, news, probs, key=Kq)
+        ctx.save_for_backward(table, ids, mask, w3t, wq, query, C, Kq, probs)
+        ctx.cfg = (seq_len, pad_row, H)
+        ctx.table_ref = table
+        ctx.ur = ur
+        return news, C[:, :H]
+
+    @staticmethod
+    @_gemm_backward
+    def backward(ctx, dnews, dC_out):
+        table, ids, mask, w3t, wq, query, C, Kq, probs = ctx.saved_tensors
+        seq_len, pad_row, H = ctx.cfg
+        ur = ctx.ur
+        T = ids.numel()
+        n = T // seq_len
+        V, E = table.shape
+        Hp = w3t.shape[0] // 3
+        dev = table.device
+        dC = _empty(T, Hp, table)
+        dwq, dbq, dconv_b, dw3t, dq, dKq = _zeros_views(dev, (Hp, Hp), (Hp,), (H,), (3 * Hp, E), (H,), (T, Hp))
+        K.attn_pool_bwd(C, query, mask, n, seq_len, probs, dnews.contiguous(), dC, dq, key=Kq, dk=dKq, key_tanh=True,
+                        dz=dC_out.contiguous() if dC_out is not None else None)
+        # key projection: dWq = dKqᵀ C, dbq = colsum(dKq); dC = ReLU'(C) ⊙ (dC + dKq Wq) (padded
+        # columns of C are zero, so the gate also zeroes dC's padding)
+        _proj_wgrad(dKq, K.operand(C, L.MNCONTIG), dwq, dbq, T)
+        K.gemm(T, Hp, Hp, K.operand(dKq, L.KCONTIG), K.operand(wq, L.MNCONTIG), dC, epilogue=L.EPI_ACCUM_GATE,
+               c_rows=K.aux_operand(C))
+        K.colsum(dC, T, H, dconv_b)
+        S = _empty(ur.cap, 3 * Hp, table)
+        ur.segment_sum_conv3(dC, S, Hp, seq_len)
+        dtable = None
+        if ctx.needs_input_grad[0]:
+            dtable = torch.zeros(V, E, device=dev)
+            K.gemm_dyn(ur.cap, E, 3 * Hp, K.operand(S, L.KCONTIG), K.operand(w3t, L.MNCONTIG), dtable,
+                       m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_STORE, c_rows=K.rows_map(ur.uids, L.ROWS_GATHER),
+                       pad_row=pad_row)
+            if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
+                dtable = None
+        K.gemm_dyn(3 * Hp, E, ur.cap, K.operand(S, L.MNCONTIG),
+                   K.operand(table, L.MNCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER), dw3t, k_dev=ur.u_pad,
+                   epilogue=L.EPI_ATOMIC, split_k=_split_k(3 * Hp, E, ur.cap))
+        return (dtable, None, None, dw3t, dconv_b, dwq, dbq, dq.view_as(query), None, None, None)
 
 
 # ---------------------------------------------------------------------- pooling user encoder
@@ -368,6 +461,7 @@ class MHAFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, mask, w_cat, b_cat, nseq, seq_len, heads, dk, dv):
+        ctx.prec = K.get_gemm_precision()
         D = x.shape[1]
         NQ = heads * dk
         NY = w_cat.shape[0]
@@ -381,6 +475,7 @@ class MHAFn(torch.autograd.Function):
         return O
 
     @staticmethod
+    @_gemm_backward
     def backward(ctx, dO):
         x, mask, w_cat, Y = ctx.saved_tensors
         nseq, seq_len, heads, dk, dv = ctx.cfg
@@ -409,6 +504,7 @@ class RNNUserFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, user_table, cell, mask, B, N, reverse, h0_idx):
+        ctx.prec = K.get_gemm_precision()
         H = x.shape[1]
         G = 4 if cell == L.CELL_LSTM else 3
         dev = x.device
@@ -427,6 +523,7 @@ class RNNUserFn(torch.autograd.Function):
         return hout
 
     @staticmethod
+    @_gemm_backward
     def backward(ctx, dh):
         x, w_ih, w_hh, gates, hprev, cprev, mask, h0_idx, user_table = ctx.saved_tensors
         cell, B, N, reverse = ctx.cfg

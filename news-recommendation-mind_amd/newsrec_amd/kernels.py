@@ -3,6 +3,10 @@
 Each wrapper validates shapes/dtypes on the host BEFORE launching (a wrong shape on the
 device is a memory fault, not an exception), then calls the kernel on the current stream.
 """
+import contextlib
+import os
+import threading
+
 import torch
 
 from . import _lib as L
@@ -20,31 +24,62 @@ def _check_rows(rows, limit, name):
             raise L.HipError("%s: row table must be a contiguous int64 CUDA tensor" % name)
 
 
-def set_gemm_precision(mode):
-    """nr_gemm_set_precision: L.GEMM_F32 (exact f32 MFMA) or L.GEMM_BF16X6 (fp32 operands as three bf16
-    terms on the bf16 matrix cores).  Returns the previous mode."""
-    rc = L.load().nr_gemm_set_precision(int(mode))
-    if rc < 0:
-        raise L.HipError("nr_gemm_set_precision: invalid mode %r" % (mode,))
-    return rc
+_PREC_NAMES = {"f32": L.GEMM_F32, "bf16x6": L.GEMM_BF16X6, "bf16": L.GEMM_BF16}
+_prec_state = threading.local()
+
+
+def _env_precision():
+    e = os.environ.get("NR_GEMM_PREC", "bf16x6")
+    if e not in _PREC_NAMES:
+        raise L.HipError("NR_GEMM_PREC must be one of %s, got %r" % (sorted(_PREC_NAMES), e))
+    return _PREC_NAMES[e]
 
 
 def get_gemm_precision():
-    return L.load().nr_gemm_get_precision()
+    """The calling thread's default GEMM arithmetic (L.GEMM_F32 / GEMM_BF16X6 / GEMM_BF16); the
+    process default comes from NR_GEMM_PREC ("bf16x6").  The library itself is stateless: every
+    nr_gemm_f32 call carries its arithmetic."""
+    p = getattr(_prec_state, "mode", None)
+    return _env_precision() if p is None else p
+
+
+def set_gemm_precision(mode):
+    """Set the calling thread's default GEMM arithmetic; returns the previous one."""
+    if mode not in _PREC_NAMES.values():
+        raise L.HipError("invalid GEMM precision %r" % (mode,))
+    old = get_gemm_precision()
+    _prec_state.mode = int(mode)
+    return old
+
+
+@contextlib.contextmanager
+def gemm_precision(mode):
+    """``with gemm_precision(L.GEMM_BF16): ...`` — the arithmetic of the GEMMs launched inside
+    (autograd Functions record it at forward time, so their backward uses the same)."""
+    old = set_gemm_precision(mode)
+    try:
+        yield
+    finally:
+        _prec_state.mode = old
+
+
+def _prec(prec):
+    return get_gemm_precision() if prec is None else int(prec)
 
 
 def gemm(M, N, K, A, B, C, ldc=None, bias=None, epilogue=L.EPI_STORE, c_rows=None,
-         pad_row=-1, split_k=1):
-    """C (op)= A(m,k) B(k,n); A, B, c_rows are nr_operand structs built by ``operand``."""
+         pad_row=-1, split_k=1, prec=None):
+    """C (op)= A(m,k) B(k,n); A, B, c_rows are nr_operand structs built by ``operand``; ``prec``:
+    the GEMM arithmetic (None: the thread default, ``get_gemm_precision``)."""
     _f32(C, bias)
     if bias is not None and bias.numel() < N:
         raise L.HipError("gemm: bias has %d < N=%d entries" % (bias.numel(), N))
     L.call("nr_gemm_f32", M, N, K, A, B, L.ptr(C), ldc if ldc is not None else C.stride(0),
-           L.ptr(bias), epilogue, c_rows, pad_row, split_k, L.stream_ptr(C))
+           L.ptr(bias), epilogue, c_rows, pad_row, split_k, _prec(prec), L.stream_ptr(C))
 
 
 def gemm_dyn(M, N, K, A, B, C, m_dev=None, k_dev=None, ldc=None, bias=None, epilogue=L.EPI_STORE,
-             c_rows=None, pad_row=-1, split_k=1):
+             c_rows=None, pad_row=-1, split_k=1, prec=None):
     """``gemm`` with device-resident extents: M, K are upper bounds, the kernel reads the actual
     M / K from the int32 CUDA scalars ``m_dev`` / ``k_dev`` (e.g. ``UniqueRows.counts[1:2]``)."""
     _f32(C, bias)
@@ -56,7 +91,8 @@ def gemm_dyn(M, N, K, A, B, C, m_dev=None, k_dev=None, ldc=None, bias=None, epil
     if K % 32:
         raise L.HipError("gemm_dyn: K must be a multiple of 32")
     L.call("nr_gemm_f32_dyn", M, N, K, A, B, L.ptr(C), ldc if ldc is not None else C.stride(0),
-           L.ptr(bias), epilogue, c_rows, pad_row, split_k, L.ptr(m_dev), L.ptr(k_dev), L.stream_ptr(C))
+           L.ptr(bias), epilogue, c_rows, pad_row, split_k, L.ptr(m_dev), L.ptr(k_dev), _prec(prec),
+           L.stream_ptr(C))
 
 
 def _ceil32(n):
@@ -86,6 +122,7 @@ class UniqueRows:
         self.seg_of = torch.empty(max(T, 1), **i32)
         self.counts = torch.empty(4, **i32)
         mp, mdt = mask_arg(grad_mask, T) if grad_mask is not None else (None, 0)
+        self.all_tokens = grad_mask is None
         L.call("nr_unique_rows", L.ptr(ids), T, vocab, fill_row, mp, mdt, L.ptr(work), L.ptr(self.uids),
                L.ptr(self.inv), L.ptr(self.seg_off), L.ptr(self.seg_tok), L.ptr(self.seg_of), L.ptr(self.counts),
                L.stream_ptr(ids))
@@ -103,6 +140,38 @@ class UniqueRows:
         L.call("nr_segment_rows_sum", L.ptr(src), src.stride(0), width, self.T, L.ptr(self.seg_off),
                L.ptr(self.seg_tok), L.ptr(self.seg_of), L.ptr(self.counts), self.cap, L.ptr(work), L.ptr(dst),
                dst.stride(0), L.stream_ptr(src))
+
+
+    def segment_sum_conv3(self, src, dst, tap_width, seq_len):
+        """dst[u][tap*tap_width + c] = Σ src[t + 1 - tap][c] over the tokens t of distinct row u (taps
+        outside t's title skipped): the CNN encoder's per-distinct-row conv gradient input.  The CSR
+        must hold every token (grad_mask None)."""
+        _f32(src, dst)
+        _rows_ok(src, self.T, tap_width, "segment_sum_conv3 src")
+        _rows_ok(dst, self.cap, 3 * tap_width, "segment_sum_conv3 dst")
+        if not self.all_tokens:
+            raise L.HipError("segment_sum_conv3 needs the CSR of every token (grad_mask=None)")
+        nbytes = L.load().nr_segment_rows_sum_workspace(self.T, 3 * tap_width)
+        work = torch.empty(max(1, nbytes // 4), device=src.device, dtype=torch.float32)
+        L.call("nr_segment_rows_sum_conv3", L.ptr(src), src.stride(0), tap_width, seq_len, self.T,
+               L.ptr(self.seg_off), L.ptr(self.seg_tok), L.ptr(self.seg_of), L.ptr(self.counts), self.cap,
+               L.ptr(work), L.ptr(dst), dst.stride(0), L.stream_ptr(src))
+
+
+def conv3_rows_fwd(P, tap_width, H, inv, seq_len, bias, out, relu=True):
+    """out[t][:H] = act(bias + Σ_tap P[inv[t + tap - 1]][tap block]) (taps inside the title), out[t][H:
+    tap_width] = 0.  P [U, >= 3*tap_width], inv [T] int64, out [T, >= tap_width]."""
+    _f32(P, bias, out)
+    _check_rows(inv, None, "inv")
+    T = inv.numel()
+    _al(P, "conv3_rows P")
+    _al(out, "conv3_rows out")
+    _rows_ok(P, 1, 3 * tap_width, "conv3_rows P")
+    _rows_ok(out, T, tap_width, "conv3_rows out")
+    if bias is not None and bias.numel() < H:
+        raise L.HipError("conv3_rows: bias has %d < %d entries" % (bias.numel(), H))
+    L.call("nr_conv3_rows_fwd", L.ptr(P), P.stride(0), tap_width, H, L.ptr(inv), T, seq_len, L.ptr(bias),
+           int(relu), L.ptr(out), out.stride(0), L.stream_ptr(P))
 
 
 def operand(t, layout, rows=None, mapping=L.ROWS_PLAIN, seq_len=1, seg=1, ld=None):

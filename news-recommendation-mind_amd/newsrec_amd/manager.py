@@ -31,9 +31,14 @@ class ManagerConfig:
         return NEWS_NUM[self.scale]
 
 
-def build_model(encN, encU, hidden, vocab=30522, device="cuda", user_num=40, dropout_p=0.0, cfg=None):
+PRECISIONS = {"f32": 0, "bf16x6": 1, "bf16": 2}   # enum nr_gemm_precision
+
+
+def build_model(encN, encU, hidden, vocab=30522, device="cuda", user_num=40, dropout_p=0.0, cfg=None,
+                precision=None):
     """twotower.py:17-47 dispatch (incl. the 'lstur' choice whose import is broken in the
-    reference, twotower.py:44 / SURVEY Appendix A.2)."""
+    reference, twotower.py:44 / SURVEY Appendix A.2).  ``precision``: the model's GEMM arithmetic
+    ("f32", "bf16x6" or "bf16"; None = NR_GEMM_PREC, default bf16x6)."""
     from .embedding import BERT_Embedding
     from . import encoders as E
     from .twotower import TwoTower
@@ -42,7 +47,10 @@ def build_model(encN, encU, hidden, vocab=30522, device="cuda", user_num=40, dro
     en = E.CNN_Encoder(m) if encN == "cnn" else E.MHA_Encoder(m)
     eu = {"attn": E.Attention_Pooling, "avg": E.Average_Pooling, "lstm": E.RNN_User_Encoder,
           "gru": E.RNN_User_Encoder, "lstur": E.LSTUR_User_Encoder, "mha": E.MHA_User_Encoder}[encU](m)
-    return TwoTower(m, emb, en, eu).to(device)
+    model = TwoTower(m, emb, en, eu).to(device)
+    if precision is not None:
+        model.gemm_prec = PRECISIONS[precision]
+    return model
 
 
 def get_optim(model, lr=1e-4, bert_lr=6e-6, capturable=False):

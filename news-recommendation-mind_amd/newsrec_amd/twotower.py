@@ -6,12 +6,14 @@ titles are concatenated into ONE token batch, the gather is fused into the encod
 GEMM, and the scorer + head is one kernel.  Otherwise the reference composition
 ``encoderN(embedding(tokens), mask)`` runs (still on the HIP kernels).
 """
+import contextlib
 import math
 
 import torch
 from torch import nn
 
 from . import _lib as L
+from . import kernels as K
 from .functions import ScoreFn
 
 
@@ -31,6 +33,12 @@ class TwoTowerBaseModel(nn.Module):
         self.device = manager.device
         self.hidden_dim = manager.bert_dim
         self.news_reprs = None
+        # GEMM arithmetic of this model's forward AND backward (the autograd Functions record it):
+        # None = the thread default (NR_GEMM_PREC, bf16x6); L.GEMM_BF16 = the bf16 configuration
+        self.gemm_prec = None
+
+    def arithmetic(self):
+        return K.gemm_precision(self.gemm_prec) if self.gemm_prec is not None else contextlib.nullcontext()
 
     def init_encoding(self):
         self.encoding = True
@@ -63,9 +71,10 @@ class TwoTowerBaseModel(nn.Module):
 
     def forward(self, x):
         """TwoTowerBaseModel.py:65-75: (log_softmax logits when training, sigmoid otherwise, kid)."""
-        cdd_repr, user_repr, kid = self._encode_both(x)
-        mode = L.SCORE_LOG_SOFTMAX if self.training else L.SCORE_SIGMOID
-        return self.compute_score(cdd_repr, user_repr, mode), kid
+        with self.arithmetic():
+            cdd_repr, user_repr, kid = self._encode_both(x)
+            mode = L.SCORE_LOG_SOFTMAX if self.training else L.SCORE_SIGMOID
+            return self.compute_score(cdd_repr, user_repr, mode), kid
 
     def _encode_both(self, x):
         cdd_repr = self.encode_news(x)
@@ -75,7 +84,8 @@ class TwoTowerBaseModel(nn.Module):
     def predict_fast(self, x):
         """TwoTowerBaseModel.py:78-83: candidates gathered from the news table inside the
         scorer kernel, the user encoded in full."""
-        user_repr, _ = self.encode_user(x)
+        with self.arithmetic():
+            user_repr, _ = self.encode_user(x)
         cdd_id = x["cdd_id"].to(user_repr.device)
         if cdd_id.dim() == 1:
             cdd_id = cdd_id.unsqueeze(0)
@@ -119,7 +129,8 @@ class TwoTower(TwoTowerBaseModel):
 
     def encode_news(self, x):
         """TwoTower.py:21-33."""
-        return self._news(x["cdd_encoded_index"], x["cdd_attn_mask"])
+        with self.arithmetic():
+            return self._news(x["cdd_encoded_index"], x["cdd_attn_mask"])
 
     def _user_from_his(self, his_news_repr, x):
         dev = his_news_repr.device
@@ -127,8 +138,9 @@ class TwoTower(TwoTowerBaseModel):
 
     def encode_user(self, x):
         """TwoTower.py:36-49."""
-        his = self._news(x["his_encoded_index"], x["his_attn_mask"])
-        return self._user_from_his(his, x), None
+        with self.arithmetic():
+            his = self._news(x["his_encoded_index"], x["his_attn_mask"])
+            return self._user_from_his(his, x), None
 
     def _encode_both(self, x):
         if not self._fused():

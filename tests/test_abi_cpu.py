@@ -13,14 +13,14 @@ HEADER = os.path.join(ROOT, "include", "newsrec_hip.h")
 
 def declared():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|int64_t)\s+(nr_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(nr_\w+)\s*\(", txt, flags=re.M)))
 
 
 def declared_arity():
     """name -> number of parameters, from the prototypes in the header."""
     txt = open(HEADER).read()
     out = {}
-    for m in re.finditer(r"^(?:int|int64_t)\s+(nr_\w+)\s*\(([^)]*)\)\s*;", txt, flags=re.M):
+    for m in re.finditer(r"^(?:int|int64_t|const char\*)\s+(nr_\w+)\s*\(([^)]*)\)\s*;", txt, flags=re.M):
         params = [p for p in m.group(2).replace("\n", " ").split(",") if p.strip() and p.strip() != "void"]
         out[m.group(1)] = len(params)
     return out
@@ -57,3 +57,18 @@ def test_product_path_fails_loudly_without_gpu():
     t = torch.zeros(4, 4)
     with pytest.raises(_lib.HipError):
         kernels.colsum(t, 4, 4, torch.zeros(4))
+
+
+def test_library_built_from_this_tree():
+    """Build provenance: the hash embedded in the library equals the hash of csrc/ + include/."""
+    import importlib.util
+    from newsrec_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built (run __graft_entry__.build())")
+    spec = importlib.util.spec_from_file_location("nr_build", os.path.join(ROOT, "news-recommendation-mind_amd",
+                                                                           "build.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    lib.nr_build_hash.restype = ctypes.c_char_p
+    assert lib.nr_build_hash().decode() == b.source_hash()
