@@ -132,21 +132,23 @@ class GraphedStep:
 
     def __init__(self, model, opt, feed, sync, warmup):
         self.feed = feed
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):   # warm-up off the default stream (allocator, lazy init)
-            for i in range(max(2, warmup)):
-                feed.feed(i)
-                train_step(model, opt, feed.form(), sync)
-        torch.cuda.current_stream().wait_stream(s)
+        self.opt = opt
+        # warm-up as ordinary eager steps on the current stream (allocator, lazy init, optimizer
+        # state); the capture then runs on torch.cuda.graph's own stream
+        for i in range(max(2, warmup)):
+            feed.feed(i)
+            train_step(model, opt, feed.form(), sync)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.loss = train_step(model, opt, feed.form(), sync)
+            # detached: the captured loss must not keep the capture's autograd graph (and its
+            # AccumulateGrad nodes, bound to the capture stream) alive
+            self.loss = train_step(model, opt, feed.form(), sync).detach()
         torch.cuda.synchronize()
 
     def __call__(self, i):
         self.feed.feed(i)
+        self.opt.sync_lr()   # a scheduler's lr changes reach the captured Adam
         self.graph.replay()
 
 
@@ -246,42 +248,122 @@ def xformer_leg(dev, steps=5, warmup=2, b=B):
                         "501-token user sequence, dropout 0.1, Adam; synthetic batches, random init",
             "per_gpu_batch": b, "impressions_per_s": round(b / el, 1), "ms_per_step": round(el * 1e3, 2),
             "train_tflops": round(3 * f / el / 1e12, 1), "eval_impressions_per_s": round(b / ev, 1),
-            "eval_tflops": round(f / ev / 1e12, 1)}
+            "eval_tflops": round(f / ev / 1e12, 1),
+            "roofline": {"bound": "mfma", "peak_tflops": round(BF16_MFMA_PEAK_TF / 6, 1),
+                         "peak_basis": "fp32-equivalent bf16x6 (2.5 PF bf16 dense / 6)",
+                         "frac": round(3 * f / el / 1e12 / (BF16_MFMA_PEAK_TF / 6), 4)}}
 
 
-def config_legs(dev, steps=10, warmup=3):
-    """The other two-tower configurations of BASELINE.json (configs[1], configs[3] and the GRU
-    variant) beside the headline: train steps (fwd + NLL + bwd + Adam) on pre-formed synthetic
-    MIND-shaped batches of B = 32, one GPU, eager.  H = 150 (Manager.py:61)."""
+# algorithmic train FLOPs per impression (token-wise count, fwd x 3) and the
+# parameter count of the dense Adam per configuration (H = 150, V = 30522)
+LEG_FLOPS = {"cnn_attn": 3.65e9, "cnn_attn_bf16": 3.65e9, "cnn_lstur": 3.70e9, "cnn_gru": 3.60e9}
+
+
+def _leg_floor(name, model, ms):
+    """Roofline of one config leg: the step's floor = max(algorithmic FLOPs / MFMA peak, HBM bytes /
+    HBM peak) with bytes = the dense Adam's 28 B per parameter + the dense word-table gradient's zero
+    fill and store (2 x 4 B x V x E); frac = floor / measured."""
+    bf16 = name.endswith("bf16")
+    peak_tf = BF16_MFMA_PEAK_TF if bf16 else BF16_MFMA_PEAK_TF / 6
+    n_params = sum(p.numel() for p in model.parameters())
+    flops = LEG_FLOPS[name] * B
+    bytes_ = 28 * n_params + 2 * 4 * V * E
+    t_mfma = flops / (peak_tf * 1e12) * 1e3
+    t_hbm = bytes_ / (HBM_PEAK_GBS * 1e9) * 1e3
+    floor = max(t_mfma, t_hbm)
+    return {"bound": "mfma" if t_mfma >= t_hbm else "hbm", "floor_ms": round(floor, 4),
+            "frac": round(floor / ms, 4), "achieved_tflops": round(flops / (ms * 1e-3) / 1e12, 1),
+            "peak_tflops": round(peak_tf, 1), "adam_params": n_params, "hbm_bytes_floor": bytes_,
+            "gemm_arithmetic": "bf16 (operands rounded to bf16, fp32 accumulate)" if bf16 else "bf16x6 (fp32-class)"}
+
+
+def config_legs(dev, feed, steps=20, warmup=3, only=None):
+    """The other two-tower configurations of BASELINE.json beside the headline: configs[1] CNN news +
+    additive-attention user (fp32-class and the bf16 configuration), configs[3] LSTUR (CNN news +
+    LSTM with user embedding, MIND-large user table) and the GRU variant.  Train steps (batch
+    formation on the device, fwd, NLL, bwd, Adam) of B = 32, H = 150, V = 30522, one GPU, each leg's
+    whole step replayed as a HIP graph like the headline."""
     from newsrec_amd.manager import build_model, get_optim
-    gen = torch.Generator().manual_seed(11)
-    batches = [synth_batch(gen, dev) for _ in range(2)]
     out = {}
-    for name, encN, encU in (("cnn_attn", "cnn", "attn"), ("cnn_lstur", "cnn", "lstur"), ("cnn_gru", "cnn", "gru")):
+    for name, encN, encU, prec in (("cnn_attn", "cnn", "attn", None), ("cnn_attn_bf16", "cnn", "attn", "bf16"),
+                                   ("cnn_lstur", "cnn", "lstur", None), ("cnn_gru", "cnn", "gru", None)):
+        if only is not None and name not in only:
+            continue
         torch.manual_seed(42)
-        model = build_model(encN, encU, 150, vocab=V, device=dev, user_num=USERS_LARGE)
+        model = build_model(encN, encU, 150, vocab=V, device=dev, user_num=USERS_LARGE, precision=prec)
         model.train()
-        opt = get_optim(model)
-        for i in range(warmup + steps):
-            if i == warmup:
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-            train_step(model, opt, batches[i % 2], None)
+        opt = get_optim(model, capturable=True)
+        step = GraphedStep(model, opt, feed, None, warmup)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(i)
         torch.cuda.synchronize()
         el = (time.perf_counter() - t0) / steps
-        out[name] = {"impressions_per_s": round(B / el, 1), "ms_per_step": round(el * 1e3, 3)}
-        del model, opt
-    torch.cuda.empty_cache()
-    out["note"] = ("eager train steps, B=32, H=150, V=30522 trainable table, MIND-large user table for LSTUR "
-                   "(876,957 rows); lstur = the reference's LSTUR_User_Encoder (LSTM, RNN.py:76-104)")
+        ms = el * 1e3
+        out[name] = {"impressions_per_s": round(B / el, 1), "ms_per_step": round(ms, 3),
+                     "roofline": _leg_floor(name, model, ms)}
+        del step, model, opt
+        torch.cuda.empty_cache()
+    out["note"] = ("hipGraph replay of the whole train step (device batch formation, fwd, NLL, bwd, Adam), B=32, "
+                   "H=150, V=30522 trainable table, MIND-large user table for LSTUR (876,957 rows); cnn_attn_bf16 = "
+                   "configs[1]'s bf16 configuration (GEMM operands rounded to bf16, fp32 accumulation, fp32 master "
+                   "weights); lstur = the reference's LSTUR_User_Encoder (LSTM, RNN.py:76-104)")
     return out
+
+
+def gather_probe(dev, reps=20):
+    """BERT_Embedding.forward (BERT.py:39) as the standalone gather (nr_embedding_fwd, the unfused
+    contract): the step's T = 52,800 token rows of the 30522 x 768 fp32 table, read + write bytes ÷
+    time (HIP events on the launch stream)."""
+    from newsrec_amd import kernels as Kn
+    g = torch.Generator().manual_seed(3)
+    table = torch.randn(V, E, device=dev)
+    ids = torch.randint(0, V, (B * (C + NH) * L,), generator=g).to(dev)
+    out = torch.empty(ids.numel(), E, device=dev)
+    for _ in range(3):
+        Kn.embedding_fwd(table, ids, out)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        Kn.embedding_fwd(table, ids, out)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    nbytes = 2 * ids.numel() * E * 4 + ids.numel() * 8
+    return {"kernel": "nr_embedding_fwd (standalone gather)", "rows": ids.numel(), "ms": round(ms, 4),
+            "achieved_gbs": round(nbytes / (ms * 1e-3) / 1e9, 1), "peak_gbs": HBM_PEAK_GBS,
+            "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "bytes": nbytes}
+
+
+def host_cores():
+    """The cores this process may actually use: len(sched_getaffinity(0)), capped by
+    the cgroup CPU quota when one is set (a GPU box exposes every core of the machine to affinity
+    but grants a 16-core share; more threads than that only oversubscribe it)."""
+    n = len(os.sched_getaffinity(0))
+    try:   # cgroup v2
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        try:   # cgroup v1
+            quota = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if quota > 0:
+                n = min(n, max(1, quota // period))
+        except (OSError, ValueError):
+            pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:   # the box's own share (16 on the GPU pool)
+        n = min(n, int(omp))
+    return n
 
 
 def cpu_baseline(seconds=20.0):
     """The oracle (oracle/restatement.py, torch fp32 CPU) on the same NRMS step, timed on this
     host's cores over a bounded sample (steps of B=32 until ~`seconds` elapse)."""
     from oracle import restatement as R
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = host_cores()
     torch.set_num_threads(threads)
     model = build("cpu")
     P = {n: p.detach().clone().requires_grad_(True) for n, p in model.named_parameters()}
@@ -296,8 +378,21 @@ def cpu_baseline(seconds=20.0):
         el = time.perf_counter() - t0
         if el >= seconds or steps >= 50:
             break
+    # eval: the forward in eval mode (sigmoid), candidates scored per second
+    with torch.no_grad():
+        Pn = {n: p.detach() for n, p in P.items()}
+        R.forward(Pn, x, "mha", "mha", False)
+        ne, t1 = 0, time.perf_counter()
+        while True:
+            R.forward(Pn, x, "mha", "mha", False)
+            ne += 1
+            el_e = time.perf_counter() - t1
+            if el_e >= seconds / 4 or ne >= 50:
+                break
     return {"value": round(steps * B / el, 2), "unit": "impressions/s", "cores": threads, "kind": "port",
-            "sample": "%d NRMS train steps of B=32 (fwd+bwd+Adam, fp32) after 1 warm-up, oracle/restatement.py" % steps}
+            "sample": "%d NRMS train steps of B=32 (fwd+bwd+Adam, fp32) after 1 warm-up, oracle/restatement.py" % steps,
+            "eval_candidates_per_s": round(ne * B * C / el_e, 1),
+            "eval_sample": "%d eval-mode forwards of B=32 x 5 candidates (sigmoid), oracle/restatement.py" % ne}
 
 
 def main():
@@ -403,7 +498,8 @@ def main():
     # eval (b): the fast-eval pipeline over a MIND-large-shaped dev split
     fast = fast_eval_leg(model, dev, world, rank, a.eval_impr) if a.eval_impr > 0 else None
     xf = xformer_leg(dev, a.xformer_steps) if (a.xformer_steps > 0 and world == 1) else None
-    legs = config_legs(dev) if (a.config_legs and world == 1) else None
+    legs = config_legs(dev, feed) if (a.config_legs and world == 1 and a.data == "device") else None
+    gather = gather_probe(dev) if world == 1 else None
 
     if rank == 0:
         ms = el / a.steps * 1e3
@@ -455,6 +551,8 @@ def main():
             out["xformer"] = xf
         if legs is not None:
             out["other_configs"] = legs
+        if gather is not None:
+            out["gather"] = gather
         if not a.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
         print(json.dumps(out), flush=True)

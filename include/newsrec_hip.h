@@ -297,8 +297,9 @@ int nr_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, 
 
 /* One torch.optim.Adam step over many tensors in as few launches as possible (<= 40 tensors per
  * launch, descriptors passed by value: graph-capturable).  Per tensor: contiguous fp32 param /
- * grad / exp_avg / exp_avg_sq of n elements, its group's lr, and the step count after increment
- * (host `step`, or `step_dev` on the device).  Same arithmetic as nr_adam. */
+ * grad / exp_avg / exp_avg_sq of n elements, its group's lr (host `lr`, or `lr_dev` read on the
+ * device: a replayed graph follows a learning-rate scheduler, Manager.py:415-420), and the step
+ * count after increment (host `step`, or `step_dev` on the device).  Same arithmetic as nr_adam. */
 typedef struct nr_adam_tensor {
   float* param;
   const float* grad;
@@ -308,6 +309,7 @@ typedef struct nr_adam_tensor {
   float lr;
   int64_t step;
   const int64_t* step_dev;
+  const float* lr_dev;
 } nr_adam_tensor;
 int nr_adam_multi(const nr_adam_tensor* tensors, int32_t count, float beta1, float beta2, float eps,
                   float weight_decay, float grad_scale, hipStream_t stream);
@@ -321,8 +323,10 @@ int nr_embedding_fwd(const float* table, int64_t V, int64_t E, const int64_t* id
 int nr_embedding_bwd(const float* dout, int64_t V, int64_t E, const int64_t* idx, int64_t n,
                      int64_t padding_idx, float* dtable, hipStream_t stream);
 
-/* out[c] += Σ_r x[r][c]  (bias gradients; out pre-zeroed or accumulated). */
-int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out,
+/* out[c] += Σ_r x[r][c]  (bias gradients; out pre-zeroed or accumulated).  Deterministic two-pass
+ * reduction (no atomics) through `work` of nr_colsum_workspace(rows, cols) bytes. */
+int64_t nr_colsum_workspace(int64_t rows, int64_t cols);
+int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out, float* work,
               hipStream_t stream);
 
 /* ---------------------------------------------------------------- device-side MIND data path

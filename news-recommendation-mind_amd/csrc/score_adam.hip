@@ -147,9 +147,11 @@ struct AdamEntry {
   float* p; const float* g; float* m; float* v;
   int64_t n;
   const int64_t* step_dev;   // device step count (graph replays) or null
-  float step_size;           // lr / (1 - beta1^t) when step_dev is null
+  const float* lr_dev;       // device learning rate (a scheduler updates it between replays) or null
+  float step_size;           // lr / (1 - beta1^t) when neither is on the device
   float bc2_sqrt;            // sqrt(1 - beta2^t) when step_dev is null
   float lr;
+  int64_t step;              // host step count
 };
 
 struct AdamMulti {
@@ -175,9 +177,10 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
   while (t + 1 < a.count && b >= a.blk_off[t + 1]) ++t;
   const AdamEntry& e = a.e[t];
   float step = e.step_size, bc2_sqrt = e.bc2_sqrt;
-  if (e.step_dev) {
-    const double st = (double)*e.step_dev;
-    step = (float)((double)e.lr / (1.0 - pow((double)a.b1, st)));
+  if (e.step_dev || e.lr_dev) {
+    const double st = e.step_dev ? (double)*e.step_dev : (double)e.step;
+    const double lr = e.lr_dev ? (double)*e.lr_dev : (double)e.lr;
+    step = (float)(lr / (1.0 - pow((double)a.b1, st)));
     bc2_sqrt = (float)sqrt(1.0 - pow((double)a.b2, st));
   }
   const int64_t base = (int64_t)(b - a.blk_off[t]) * kAdamChunk;
@@ -232,23 +235,57 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const float* dout, i
   for (int64_t c = lane; c < E; c += 64) atomicAdd(&dtable[t * E + c], dout[row * E + c]);
 }
 
-__global__ __launch_bounds__(256) void colsum_kernel(const float* x, int64_t ldx, int64_t rows, int64_t cols,
-                                                     int64_t chunk, float* out) {
+// Column sums, deterministic two-pass: pass 1 = one block per (64-column chunk, row block), each of
+// its 4 waves strides the block's rows with its 64 lanes on 64 consecutive columns (256-B row
+// segments, 8 loads in flight), the waves combine in LDS and store the block's partial row; pass 2
+// sums the partials per column in row-block order.  No atomics: a few thousand blocks adding into
+// the same H addresses serialise on the L2 (the old one-pass form ran at ~1 TB/s on [52800, 150]).
+constexpr int kColsumBlocks = 2048;
+
+__global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows,
+                                                          int64_t cols, int64_t rb_rows, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t r0 = (int64_t)blockIdx.y * rb_rows;
+  const int64_t r1 = r0 + rb_rows < rows ? r0 + rb_rows : rows;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    int64_t r = r0 + w;
+    const float* p = x + r * ldx + c;
+    for (; r + 28 < r1; r += 32, p += 32 * ldx) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += p[4 * u * ldx];
+    }
+    for (; r < r1; r += 4, p += 4 * ldx) a[0] += *p;
+  }
+  red[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (w == 0 && c < cols) part[(int64_t)blockIdx.y * cols + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int64_t nrb, int64_t cols,
+                                                           float* __restrict__ out) {
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (c >= cols) return;
-  const int64_t r0 = (int64_t)blockIdx.y * chunk;
-  const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
-  // eight independent partial sums: eight loads in flight per thread (the loop is latency-bound
-  // with one)
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int64_t r = r0;
-  const float* p = x + r0 * ldx + c;
-  for (; r + 8 <= r1; r += 8, p += 8 * ldx) {
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  int64_t b = 0;
+  for (; b + 4 <= nrb; b += 4) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) a[u] += p[u * ldx];
+    for (int u = 0; u < 4; ++u) a[u] += part[(b + u) * cols + c];
   }
-  for (; r < r1; ++r, p += ldx) a[0] += *p;
-  atomicAdd(&out[c], ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7])));
+  for (; b < nrb; ++b) a[0] += part[b * cols + c];
+  out[c] += (a[0] + a[1]) + (a[2] + a[3]);
+}
+
+void colsum_grid(int64_t rows, int64_t cols, int64_t* nrb, int64_t* rb_rows) {
+  const int64_t cc = (cols + 63) / 64;
+  int64_t n = kColsumBlocks / cc;
+  const int64_t by_rows = (rows + 31) / 32;   // at least 32 rows per block
+  if (n > by_rows) n = by_rows;
+  if (n < 1) n = 1;
+  *rb_rows = (rows + n - 1) / n;
+  *nrb = (rows + *rb_rows - 1) / *rb_rows;
 }
 
 }  // namespace
@@ -323,18 +360,24 @@ extern "C" int nr_embedding_bwd(const float* dout, int64_t V, int64_t E, const i
   return NR_OK;
 }
 
-extern "C" int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out,
+extern "C" int64_t nr_colsum_workspace(int64_t rows, int64_t cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  int64_t nrb, rb_rows;
+  colsum_grid(rows, cols, &nrb, &rb_rows);
+  return nrb * cols * (int64_t)sizeof(float);
+}
+
+extern "C" int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out, float* work,
                          hipStream_t stream) {
-  if (rows < 0 || cols < 0) return NR_EINVAL(0);
-  if (!x || !out) return NR_EINVAL(1);
+  if (rows < 0 || cols < 0 || ldx < cols) return NR_EINVAL(0);
+  if (!x || !out || (rows > 0 && cols > 0 && !work)) return NR_EINVAL(1);
   if (rows == 0 || cols == 0) return NR_OK;
-  const int64_t cb = (cols + 255) / 256;
-  int64_t chunks = (1024 + cb - 1) / cb;
-  if (chunks > rows) chunks = rows;
-  const int64_t chunk = (rows + chunks - 1) / chunks;
-  chunks = (rows + chunk - 1) / chunk;
-  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)cb, (unsigned)chunks), dim3(256), 0, stream, x, ldx, rows,
-                     cols, chunk, out);
+  int64_t nrb, rb_rows;
+  colsum_grid(rows, cols, &nrb, &rb_rows);
+  hipLaunchKernelGGL(colsum_part_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)nrb), dim3(256), 0, stream, x,
+                     ldx, rows, cols, rb_rows, work);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, stream, work, nrb, cols,
+                     out);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
@@ -374,8 +417,9 @@ extern "C" int nr_adam_multi(const nr_adam_tensor* tensors, int32_t count, float
     }
     AdamEntry& e = a.e[a.count];
     e.p = d.param; e.g = d.grad; e.m = d.exp_avg; e.v = d.exp_avg_sq; e.n = d.n;
-    e.step_dev = d.step_dev; e.lr = d.lr;
+    e.step_dev = d.step_dev; e.lr_dev = d.lr_dev; e.lr = d.lr;
     const double st = (double)(d.step < 1 ? 1 : d.step);   // bias corrections in double, as torch's Python floats
+    e.step = (int64_t)st;
     e.step_size = (float)((double)d.lr / (1.0 - pow((double)beta1, st)));
     e.bc2_sqrt = (float)sqrt(1.0 - pow((double)beta2, st));
     a.blk_off[a.count] = (int32_t)blocks;

@@ -40,7 +40,7 @@ class nr_operand(ctypes.Structure):
 class nr_adam_tensor(ctypes.Structure):
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
                 ("exp_avg_sq", ctypes.c_void_p), ("n", c_i64), ("lr", c_f32), ("step", c_i64),
-                ("step_dev", ctypes.c_void_p)]
+                ("step_dev", ctypes.c_void_p), ("lr_dev", ctypes.c_void_p)]
 
 
 # name -> argtypes (restype int32 unless listed in _RESTYPES)
@@ -77,7 +77,8 @@ _SIGS = {
     "nr_adam": [c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i64, c_ptr, c_f32, c_ptr],
     "nr_embedding_fwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr],
     "nr_embedding_bwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_ptr],
-    "nr_colsum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr],
+    "nr_colsum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr],
+    "nr_colsum_workspace": [c_i64, c_i64],
     "nr_mha_pool_fwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_f32,
                         c_u64, c_u64, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr],
     "nr_mha_pool_bwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_u64,
@@ -111,6 +112,7 @@ _SIGS = {
 }
 
 _RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64,
+             "nr_colsum_workspace": c_i64,
              "nr_build_hash": ctypes.c_char_p}
 
 # enum nr_batch_flags / nr_metric_flags

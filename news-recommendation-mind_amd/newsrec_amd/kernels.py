@@ -395,7 +395,8 @@ def adam(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, 
 
 def adam_multi(entries, beta1, beta2, eps, weight_decay, grad_scale=1.0):
     """entries: [(param, grad, exp_avg, exp_avg_sq, lr, step)] with ``step`` an int or an int64 CUDA
-    scalar; one nr_adam_multi call (a launch per <= 40 tensors)."""
+    scalar and ``lr`` a float or a float32 CUDA scalar (read on the device); one nr_adam_multi call
+    (a launch per <= 40 tensors)."""
     if not entries:
         return
     arr = (L.nr_adam_tensor * len(entries))()
@@ -405,12 +406,17 @@ def adam_multi(entries, beta1, beta2, eps, weight_decay, grad_scale=1.0):
         for t in (p, g, m, v):
             if not t.is_contiguous() or t.numel() != n:
                 raise L.HipError("adam_multi: tensors must be contiguous with equal numel")
-        sd = 0
+        sd, ld = 0, 0
         if torch.is_tensor(step):
             if step.dtype != torch.int64 or not step.is_cuda:
                 raise L.HipError("adam_multi: a device step count must be an int64 CUDA tensor")
             sd, step = step.data_ptr(), 0
-        arr[i] = L.nr_adam_tensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, float(lr), int(step), sd)
+        if torch.is_tensor(lr):
+            if lr.dtype != torch.float32 or not lr.is_cuda or lr.numel() != 1:
+                raise L.HipError("adam_multi: a device learning rate must be a float32 CUDA scalar")
+            ld, lr = lr.data_ptr(), 0.0
+        arr[i] = L.nr_adam_tensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, float(lr), int(step), sd,
+                                  ld)
     L.call("nr_adam_multi", arr, len(entries), beta1, beta2, eps, weight_decay, grad_scale,
            L.stream_ptr(entries[0][0]))
 
@@ -439,7 +445,9 @@ def colsum(x, rows, cols, out):
     _rows_ok(x, rows, cols, "x")
     if out.numel() < cols:
         raise L.HipError("colsum: out too small")
-    L.call("nr_colsum", L.ptr(x), x.stride(0), rows, cols, L.ptr(out), L.stream_ptr(x))
+    nbytes = L.load().nr_colsum_workspace(rows, cols)
+    work = torch.empty(max(1, nbytes // 4), device=x.device, dtype=torch.float32)
+    L.call("nr_colsum", L.ptr(x), x.stride(0), rows, cols, L.ptr(out), L.ptr(work), L.stream_ptr(x))
 
 
 MHA_POOL_SHAPES = {(64, 32, 384), (64, 64, 768), (64, 32, 256), (32, 32, 384)}

@@ -14,6 +14,25 @@ class FusedAdam(torch.optim.Optimizer):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self.capturable = capturable
+        # capturable: each group's lr lives on the device too (read by the kernel), so a graph
+        # replay follows group["lr"] changes (a warmup scheduler, Manager.py:415-420) once
+        # sync_lr() has copied them over -- step() does it when not capturing, GraphedStep before
+        # every replay
+        self._lr_dev, self._lr_host = {}, {}
+
+    def sync_lr(self):
+        """Copy every group's host lr into its device scalar (only the ones that changed)."""
+        for i, group in enumerate(self.param_groups):
+            t = self._lr_dev.get(i)
+            if t is None:
+                dev = next((p.device for p in group["params"]), None)
+                if dev is None:
+                    continue
+                t = self._lr_dev[i] = torch.empty((), dtype=torch.float32, device=dev)
+                self._lr_host[i] = None
+            if self._lr_host[i] != group["lr"]:
+                t.fill_(float(group["lr"]))
+                self._lr_host[i] = group["lr"]
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale=1.0):
@@ -24,7 +43,9 @@ class FusedAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         todo = []
-        for group in self.param_groups:
+        if self.capturable and not torch.cuda.is_current_stream_capturing():
+            self.sync_lr()
+        for gi, group in enumerate(self.param_groups):
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -33,20 +54,21 @@ class FusedAdam(torch.optim.Optimizer):
                     st["step"] = (torch.zeros((), dtype=torch.int64, device=p.device) if self.capturable else 0)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                todo.append((group, p, st))
+                todo.append((gi, group, p, st))
         if self.capturable:
-            steps = [st["step"] for _, _, st in todo]
+            steps = [st["step"] for _, _, _, st in todo]
             if steps:
                 torch._foreach_add_(steps, 1)
         # one nr_adam_multi call per (betas, eps, weight_decay) combination: every tensor of the
         # step in a few launches instead of one launch per parameter
         batches = {}
-        for group, p, st in todo:
+        for gi, group, p, st in todo:
             if not self.capturable:
                 st["step"] += 1
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
             key = (tuple(group["betas"]), group["eps"], group["weight_decay"])
-            batches.setdefault(key, []).append((p, g, st["exp_avg"], st["exp_avg_sq"], group["lr"], st["step"]))
+            lr = self._lr_dev[gi] if self.capturable else group["lr"]
+            batches.setdefault(key, []).append((p, g, st["exp_avg"], st["exp_avg_sq"], lr, st["step"]))
         for (betas, eps, wd), entries in batches.items():
             K.adam_multi(entries, betas[0], betas[1], eps, wd, grad_scale)
         return loss

@@ -1,0 +1,184 @@
+"""End-to-end parity at the BENCHMARKED configuration (BASELINE configs[2], bench.py's headline):
+one NRMS train step at B = 32 impressions, V = 30522, H = 384, 12 heads, 5 candidates, 50-click
+history, 30-token titles — the bench's exact kernels (128x128 bf16x6 GEMMs over the distinct-row
+projection, the fused attention kernels, the split backward, Adam) — against the fp32 CPU oracle
+(oracle/restatement.py, which tests/test_oracle_golden.py pins to the reference's goldens):
+
+* logits within the north star's 1e-3 (models/TwoTowerBaseModel.py:65-75), the loss;
+* the word-table, projection and every other gradient within 1e-3 of each one's max magnitude;
+* every parameter after one Adam step (Manager.py:404-413,647);
+* the same step replayed as a HIP graph (bench.GraphedStep) against eager steps;
+* XFormer at BERT-base width with enough rows (B = 16, 2 layers: 10,416 token rows, QKV = 1,476
+  tiles of 128x128) that its GEMMs run the bf16x6 kernel, against the oracle.
+Dropout is 0 (the oracle cannot replay the device RNG's masks; dropout itself is covered by the
+kernel tests with recovered keep masks)."""
+import copy
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+pytestmark = pytest.mark.gpu
+
+from oracle import restatement as R
+
+B, C, NH, L, V, H = 32, 5, 50, 30, 30522, 384
+
+
+def _nrms(dev):
+    from newsrec_amd.manager import build_model
+    torch.manual_seed(42)
+    m = build_model("mha", "mha", H, vocab=V, device=dev, user_num=876956, dropout_p=0.0)
+    with torch.no_grad():   # spread the candidate scores (reference init gives near-equal logits)
+        m.embedding.bert_word_embedding.weight.normal_(0, 0.5)
+        m.encoderN.query_words.normal_(0, 1.0)
+        m.encoderU.query_news.normal_(0, 1.0)
+    return m
+
+
+def _batch(seed):
+    """bench.synth_batch with ragged titles (lengths U[5, 30]) and ragged / empty histories (the
+    reference forces his_mask[0] = 1 for an empty history, MIND.py:330-337)."""
+    import bench
+    gen = torch.Generator().manual_seed(seed)
+    x = bench.synth_batch(gen, "cpu", full=False)
+    lens = torch.randint(0, NH + 1, (B,), generator=gen)
+    lens[:4] = 0
+    his = (torch.arange(NH)[None] < lens[:, None]).double()
+    his[:, 0] = 1.0
+    x["his_mask"] = his.unsqueeze(-1)
+    return x
+
+
+def _oracle_params(model):
+    return {n: p.detach().cpu().clone().requires_grad_(True) for n, p in model.named_parameters()}
+
+
+def _close_grads(model, P, names=None, rel=1e-3):
+    ps = dict(model.named_parameters())
+    for n in (names or list(P)):
+        want = P[n].grad
+        assert want is not None, n
+        got = ps[n].grad
+        assert got is not None, n
+        scale = max(want.abs().max().item(), 1e-8)
+        err = (got.detach().cpu() - want).abs().max().item()
+        assert err <= rel * scale, (n, err, scale)
+
+
+def test_nrms_fullsize_step_vs_oracle():
+    from newsrec_amd.manager import get_optim
+    dev = torch.device("cuda", 0)
+    model = _nrms(dev)
+    model.train()
+    x = _batch(1)
+    xg = {k: v.to(dev) for k, v in x.items()}
+    P = _oracle_params(model)
+    opt = get_optim(model)
+    opt.zero_grad(set_to_none=True)
+    logits, _ = model(xg)
+    loss = F.nll_loss(logits, xg["label"])
+    loss.backward()
+    opt.step()
+    torch.cuda.synchronize()
+    want_loss, want_logits, _ = R.train_step(P, x, "mha", "mha")
+    assert want_logits.std().item() > 0.05   # the comparison is not between constants
+    err = (logits.detach().cpu() - want_logits).abs().max().item()
+    print("NRMS full size: max |logit err| %.3e, loss %.6f vs %.6f" % (err, loss.item(), want_loss.item()))
+    assert err <= 1e-3
+    assert abs(loss.item() - want_loss.item()) <= 1e-4
+    _close_grads(model, P)
+    # parameters after Adam: torch.optim.Adam on the oracle's gradients vs nr_adam_multi on ours.
+    # Adam's first step moves every element by lr * g / |g|, so an element whose gradient is at the
+    # rounding level may flip sign (a 2 lr difference): every element within 2 lr, all but
+    # max(2, 1e-3 of) the elements that received a gradient within 1e-3 lr.
+    worst = 0.0
+    for n, p in model.named_parameters():
+        d = (p.detach().cpu() - P[n].detach()).abs()
+        lr = 6e-6 if "bert" in n else 1e-4
+        assert d.max().item() <= 2 * lr + 1e-7, n
+        moved = P[n].grad != 0
+        off = int((d[moved] > 1e-3 * lr).sum().item())
+        worst = max(worst, off / max(1, int(moved.sum().item())))
+        assert off <= max(2, 1e-3 * int(moved.sum().item())), (n, off)
+    print("NRMS full size: worst fraction of updated elements off by > 1e-3 lr: %.2e" % worst)
+
+
+def test_nrms_fullsize_graph_replay_matches_eager():
+    """bench.GraphedStep at the benchmark's size: 2 eager warm-up steps + 2 replays vs 4 eager steps."""
+    import bench
+    from newsrec_amd.manager import get_optim
+    dev = torch.device("cuda", 0)
+    m_eager = _nrms(dev)
+    m_graph = copy.deepcopy(m_eager)
+    batches = [{k: v.to(dev) for k, v in _batch(10 + i).items()} for i in range(4)]
+    o_eager = get_optim(m_eager)
+    o_graph = get_optim(m_graph, capturable=True)
+    m_eager.train()
+    m_graph.train()
+    for i in range(2):
+        bench.train_step(m_eager, o_eager, batches[i], None)
+    g = bench.GraphedStep(m_graph, o_graph, bench.ResidentFeed(batches), None, 2)
+    for i in range(2, 4):
+        bench.train_step(m_eager, o_eager, batches[i], None)
+        g(i)
+    torch.cuda.synchronize()
+    for (n, a), (_, b) in zip(m_eager.named_parameters(), m_graph.named_parameters()):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=2e-5, msg=n)
+
+
+def test_xformer_bf16x6_gemms_vs_oracle():
+    """XFormer at BERT-base width, B = 16, 2 layers: 16*5*30 + 16*501 = 10,416 token rows, so the
+    dense layers take the 128x128 bf16x6 kernel (>= 400 tiles), against the fp32 oracle."""
+    from newsrec_amd import _lib as Lb, kernels as Kn
+    from newsrec_amd.bert import BertConfig
+    from newsrec_amd.manager import ManagerConfig
+    from newsrec_amd.xformer import XFormer
+    assert Kn.get_gemm_precision() == Lb.GEMM_BF16X6
+    torch.manual_seed(7)
+    Bx, Cx, N, Lt = 16, 5, 50, 30
+    bc = BertConfig(num_hidden_layers=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    m = ManagerConfig("bert", "xformer", 768, bert_dim=768)
+    model = XFormer(m, bert_config=bc).cuda()
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            if p.dim() == 2 and "embeddings" not in n:
+                p.normal_(0, 1.5 / math.sqrt(p.shape[1]))
+    gen = torch.Generator().manual_seed(0)
+
+    def titles(n):
+        t = torch.randint(1000, V, (n, Lt), generator=gen)
+        lens = torch.randint(3, Lt + 1, (n,), generator=gen)
+        msk = (torch.arange(Lt)[None] < lens[:, None]).long()
+        t = t * msk
+        t[:, 0] = 101
+        return t, msk
+    ct, cm = titles(Bx * Cx)
+    ht, hm = titles(Bx * N)
+    x = {"cdd_encoded_index": ct.view(Bx, Cx, Lt), "cdd_attn_mask": cm.view(Bx, Cx, Lt),
+         "his_encoded_index": ht.view(Bx, N, Lt), "his_attn_mask": hm.view(Bx, N, Lt),
+         "label": torch.zeros(Bx, dtype=torch.long)}
+    xg = {k: v.cuda() for k, v in x.items()}
+    model.train()
+    logits, _ = model(xg)
+    F.nll_loss(logits, xg["label"]).backward()
+    P = {n: p.detach().cpu().clone().requires_grad_() for n, p in model.named_parameters()}
+    want = R.xformer_forward(P, x, True, 12)
+    err = (logits.detach().cpu() - want.detach()).abs().max().item()
+    print("XFormer B=16 bf16x6: max |logit err| %.3e" % err)
+    assert want.detach().std().item() > 0.05
+    assert err <= 1e-3
+    R.nll_loss(want, x["label"]).backward()
+    _close_grads(model, P, ["bert.embeddings.word_embeddings.weight",
+                            "bert.encoder.layer.0.attention.self.query.weight",
+                            "bert.encoder.layer.0.attention.output.dense.weight",
+                            "bert.encoder.layer.1.intermediate.dense.weight",
+                            "bert.encoder.layer.1.output.dense.weight", "bert.pooler.dense.weight", "userBias"],
+                 rel=5e-3)

@@ -59,3 +59,29 @@ def test_graph_replay_matches_eager():
         torch.testing.assert_close(b, a, rtol=1e-4, atol=2e-5, msg=n)
     # the replays really trained: parameters moved away from the post-warm-up state
     assert m_graph.encoderN.query_words.abs().sum() > 0
+
+
+def test_graph_replay_follows_lr_schedule():
+    """A captured step replays with the CURRENT group["lr"] (device learning rates, synced before each
+    replay), as the reference's linear-warmup scheduler changes it (Manager.py:415-420)."""
+    import bench
+    from newsrec_amd.manager import get_optim
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator().manual_seed(5)
+    batches = [_batch(gen, dev) for _ in range(5)]
+    m_eager = _small_model(dev)
+    m_graph = copy.deepcopy(m_eager)
+    o_eager = get_optim(m_eager, capturable=False)
+    o_graph = get_optim(m_graph, capturable=True)
+    for i in range(2):
+        bench.train_step(m_eager, o_eager, batches[i], None)
+    g = bench.GraphedStep(m_graph, o_graph, bench.ResidentFeed(batches), None, 2)
+    for i, scale in zip(range(2, 5), (0.25, 3.0, 0.5)):
+        for o in (o_eager, o_graph):
+            for grp, base in zip(o.param_groups, (1e-4, 6e-6)):
+                grp["lr"] = base * scale
+        bench.train_step(m_eager, o_eager, batches[i], None)
+        g(i)
+    torch.cuda.synchronize()
+    for (n, a), (_, b) in zip(m_eager.named_parameters(), m_graph.named_parameters()):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=2e-5, msg=n)
