@@ -128,11 +128,19 @@ class GraphedStep:
     HIP graph and replayed: the ~80 kernels of a step launch back to back with no host work
     between them.  Each step first feeds its sampler indices (or resident batch) into the
     captured input buffers; dropout draws, negative sampling and Adam step counts advance on the
-    device, so replays are real training steps."""
+    device, so replays are real training steps.
+
+    Data parallel (``sync`` = a GradSync, N > 1): two graphs per step -- forward/backward (ending in
+    GradSync.prepare: bucket packing) and the optimizer (starting with GradSync.unpack) -- with the
+    step's RCCL collectives issued eagerly between them (GradSync.exchange), so no collective is
+    ever captured."""
 
     def __init__(self, model, opt, feed, sync, warmup):
         self.feed = feed
         self.opt = opt
+        self.sync = sync
+        if sync is not None:
+            sync.deferred = True
         # warm-up as ordinary eager steps on the current stream (allocator, lazy init, optimizer
         # state); the capture then runs on torch.cuda.graph's own stream
         for i in range(max(2, warmup)):
@@ -140,25 +148,44 @@ class GraphedStep:
             train_step(model, opt, feed.form(), sync)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            # detached: the captured loss must not keep the capture's autograd graph (and its
-            # AccumulateGrad nodes, bound to the capture stream) alive
-            self.loss = train_step(model, opt, feed.form(), sync).detach()
+        if sync is None:
+            with torch.cuda.graph(self.graph):
+                # detached: the captured loss must not keep the capture's autograd graph (and its
+                # AccumulateGrad nodes, bound to the capture stream) alive
+                self.loss = train_step(model, opt, feed.form(), sync).detach()
+            self.opt_graph = None
+        else:
+            pool = torch.cuda.graph_pool_handle()   # both graphs share one memory pool
+            with torch.cuda.graph(self.graph, pool=pool):
+                self.loss = forward_backward(model, opt, feed.form()).detach()
+                self.packed, self.rec = sync.prepare()
+            self.opt_graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.opt_graph, pool=pool):
+                sync.unpack(self.packed)
+                opt.step(grad_scale=sync.scale)
         torch.cuda.synchronize()
 
     def __call__(self, i):
         self.feed.feed(i)
         self.opt.sync_lr()   # a scheduler's lr changes reach the captured Adam
         self.graph.replay()
+        if self.opt_graph is not None:
+            self.sync.exchange(self.packed, self.rec)
+            self.opt_graph.replay()
+
+
+def forward_backward(model, opt, x):
+    opt.zero_grad(set_to_none=True)
+    logits, _ = model(x)
+    loss = torch.nn.functional.nll_loss(logits, x["label"])
+    loss.backward()
+    return loss
 
 
 def train_step(model, opt, x, sync):
     """utils/Manager.py:636-647 with the DDP gradient mean (GradSync: the word-table gradient's
     all-reduce starts inside the backward; 1/world folded into Adam)."""
-    opt.zero_grad(set_to_none=True)
-    logits, _ = model(x)
-    loss = torch.nn.functional.nll_loss(logits, x["label"])
-    loss.backward()
+    loss = forward_backward(model, opt, x)
     scale = sync() if sync is not None else 1.0
     opt.step(grad_scale=scale)
     return loss
@@ -410,7 +437,8 @@ def main():
     ap.add_argument("--xformer-steps", type=int, default=5,
                     help="timed XFormer (configs[4]) train steps reported beside the headline (0 skips; N=1 only)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
-                    help="replay the train step as a HIP graph (auto: single GPU)")
+                    help="replay the train step as HIP graphs (auto = on; N > 1: forward/backward and "
+                         "optimizer graphs with the RCCL collectives between them)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -435,7 +463,7 @@ def main():
         with torch.no_grad():
             for p in model.parameters():
                 dist.broadcast(p, 0)
-    use_graph = a.graph == "on" or (a.graph == "auto" and world == 1)
+    use_graph = a.graph in ("on", "auto")
     opt = make_optim(model, capturable=use_graph)
     sync = GradSync(model) if world > 1 else None
     gen = torch.Generator().manual_seed(1234 + rank)

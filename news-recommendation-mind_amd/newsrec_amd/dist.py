@@ -73,10 +73,20 @@ class GradSync:
       previous step's rows are re-zeroed) -- the same sum DDP's dense all-reduce forms, at B rows
       per rank instead of 526 MB;
     * every other gradient: flattened into buckets of <= ``bucket_mb`` MB, one all-reduce per
-      bucket (a few large collectives over xGMI instead of one per parameter).
+      bucket (a few large collectives over xGMI instead of one per parameter); a gradient of
+      >= ``inplace_mb`` MB is all-reduced in place, never copied into a bucket.
+
+    ``deferred`` (a train step replayed as HIP graphs, bench.GraphedStep at N > 1): the collectives
+    run between two graphs instead of inside the backward.  ``prepare()`` (captured at the end of
+    the forward/backward graph) packs the dense buckets and installs the sparse tables' persistent
+    gradient buffers, ``exchange(packed, records)`` (eager, between the graphs) runs every
+    collective, and ``unpack(packed)`` (captured at the head of the optimizer graph) copies the
+    reduced buckets back.  No RCCL call is ever captured, and the gradient tensors keep the graph
+    pool's static addresses.
     """
 
-    def __init__(self, model, group=None, overlap_tables=True, sparse_tables=True, bucket_mb=128):
+    def __init__(self, model, group=None, overlap_tables=True, sparse_tables=True, bucket_mb=128, inplace_mb=16,
+                 deferred=False):
         self.model = model
         self.group = group
         self.world = dist.get_world_size(group)
@@ -84,14 +94,23 @@ class GradSync:
         self.sparse = []
         self._dense, self._touched = {}, {}
         self.bucket_elems = int(bucket_mb * (1 << 20) // 4)
+        self.inplace_elems = int(inplace_mb * (1 << 20) // 4)
         self.overlap = overlap_tables and self.world > 1
         self.use_sparse = sparse_tables and self.world > 1
+        self.deferred = deferred
+        self._rec = []
         if self.overlap:
             functions.TABLE_GRAD_HOOK.set(self._table_hook)
         if self.use_sparse:
             functions.SPARSE_GRAD_HOOK.set(self._sparse_hook)
 
+    @property
+    def scale(self):
+        return 1.0 / self.world
+
     def _table_hook(self, table, dtable):
+        if self.deferred:          # an ordinary gradient: all-reduced in exchange()
+            return False
         work = dist.all_reduce(dtable, group=self.group, async_op=True)
         self.pending.append((table, dtable, work))
         return True
@@ -99,6 +118,9 @@ class GradSync:
     def _sparse_hook(self, table, rows, grads):
         rows = rows.reshape(-1).contiguous()
         grads = grads.reshape(rows.numel(), -1).contiguous()
+        if self.deferred:          # recorded; exchanged between the graphs
+            self._rec.append((table, rows, grads))
+            return True
         ids = [torch.empty_like(rows) for _ in range(self.world)]
         gs = [torch.empty_like(grads) for _ in range(self.world)]
         w1 = dist.all_gather(ids, rows, group=self.group, async_op=True)
@@ -119,6 +141,13 @@ class GradSync:
                 buf.index_fill_(0, prev, 0.0)
         return buf
 
+    def _sparse_reduce(self, table, ids, gs):
+        g = self._sparse_buffer(table)
+        for r in range(self.world):      # rank order: every rank forms the same sum
+            g.index_add_(0, ids[r], gs[r])
+        self._touched[id(table)] = torch.cat(ids)
+        return g
+
     def close(self):
         if self.overlap:
             functions.TABLE_GRAD_HOOK.set(None)
@@ -126,34 +155,87 @@ class GradSync:
             functions.SPARSE_GRAD_HOOK.set(None)
 
     def _buckets(self, params):
+        """-> [(params, inplace)]: big gradients alone and in place, the rest in flat buckets."""
         out, cur, n = [], [], 0
         for p in params:
+            if p.grad.numel() >= self.inplace_elems and p.grad.is_contiguous():
+                out.append(([p], True))
+                continue
             if cur and n + p.grad.numel() > self.bucket_elems:
-                out.append(cur)
+                out.append((cur, False))
                 cur, n = [], 0
             cur.append(p)
             n += p.grad.numel()
         if cur:
-            out.append(cur)
+            out.append((cur, len(cur) == 1 and cur[0].grad.is_contiguous()))
         return out
+
+    def _dense_params(self, skip):
+        return [p for p in self.model.parameters() if p.grad is not None and id(p) not in skip]
+
+    # ---- deferred (graph) mode
+    def prepare(self):
+        """End of the forward/backward (graph): takes the step's sparse records, gives each sparse
+        table its persistent gradient buffer as .grad (the optimizer reads it) and packs the dense
+        gradients into flat buckets.  -> (packed, records) for exchange() / unpack()."""
+        rec, self._rec = self._rec, []
+        for table, _, _ in rec:
+            table.grad = self._sparse_buffer_noreset(table)
+        skip = {id(t) for t, _, _ in rec}
+        packed = []
+        for bucket, inplace in self._buckets(self._dense_params(skip)):
+            flat = bucket[0].grad.view(-1) if inplace else torch.cat([p.grad.reshape(-1) for p in bucket])
+            packed.append((bucket, flat, inplace))
+        return packed, rec
+
+    def _sparse_buffer_noreset(self, table):
+        buf = self._dense.get(id(table))
+        if buf is None:
+            buf = torch.zeros_like(table)
+            self._dense[id(table)] = buf
+        return buf
+
+    def exchange(self, packed, rec):
+        """Eager, between the graphs: every collective of the step."""
+        works = [dist.all_reduce(flat, group=self.group, async_op=True) for _, flat, _ in packed]
+        for table, rows, grads in rec:
+            ids = [torch.empty_like(rows) for _ in range(self.world)]
+            gs = [torch.empty_like(grads) for _ in range(self.world)]
+            dist.all_gather(ids, rows, group=self.group)
+            dist.all_gather(gs, grads, group=self.group)
+            self._sparse_reduce(table, ids, gs)
+        for w in works:
+            w.wait()
+
+    @staticmethod
+    def unpack(packed):
+        """Head of the optimizer (graph): copy the reduced buckets back into the gradients."""
+        for bucket, flat, inplace in packed:
+            if inplace:
+                continue
+            off = 0
+            for p in bucket:
+                n = p.grad.numel()
+                p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                off += n
 
     def __call__(self):
         if self.world == 1:
             return 1.0
+        if self.deferred:
+            packed, rec = self.prepare()
+            self.exchange(packed, rec)
+            self.unpack(packed)
+            return self.scale
         hooked = {id(t) for t, _, _ in self.pending} | {id(t) for t, *_ in self.sparse}
-        dense = [p for p in self.model.parameters() if p.grad is not None and id(p) not in hooked]
         flights = []
-        for bucket in self._buckets(dense):
-            inplace = len(bucket) == 1 and bucket[0].grad.is_contiguous()
+        for bucket, inplace in self._buckets(self._dense_params(hooked)):
             flat = bucket[0].grad.view(-1) if inplace else torch.cat([p.grad.reshape(-1) for p in bucket])
             flights.append((bucket, flat, inplace, dist.all_reduce(flat, group=self.group, async_op=True)))
         for table, ids, gs, w1, w2 in self.sparse:
             w1.wait()
             w2.wait()
-            g = self._sparse_buffer(table)
-            for r in range(self.world):      # rank order: every rank forms the same sum
-                g.index_add_(0, ids[r], gs[r])
-            self._touched[id(table)] = torch.cat(ids)
+            g = self._sparse_reduce(table, ids, gs)
             if table.grad is None:
                 table.grad = g
             elif table.grad.data_ptr() != g.data_ptr():
@@ -174,4 +256,4 @@ class GradSync:
             else:
                 table.grad.add_(dtable)
         self.pending = []
-        return 1.0 / self.world
+        return self.scale

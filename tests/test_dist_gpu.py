@@ -1,0 +1,145 @@
+"""Data parallelism of the REAL models on the GPU (utils/Manager.py:167,211-213; twotower.py:49-50):
+two ranks, spawned as fresh processes on the one leased GPU, each train on half of a batch through
+GradSync and must reproduce one process training on the whole batch (DDP's gradient mean).
+
+This exercises the production hook sites: the word-table gradient handed over inside the news
+tower backward (functions.py MHANewsFn / CNNNewsRowsFn, TABLE_GRAD_HOOK), LSTUR's row-sparse
+user-table exchange (RNNUserFn, SPARSE_GRAD_HOOK), the bucketed dense all-reduce, and the
+two-graph data-parallel step (bench.GraphedStep: forward/backward graph, collectives, optimizer
+graph).  The collectives run over gloo on device tensors (RCCL cannot put two ranks on one GPU);
+GradSync's code path is the same for both backends."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+CASES = {"nrms": ("mha", "mha", 384), "lstur": ("cnn", "lstur", 150)}
+V, USERS, BT, C, NH, L = 2000, 40, 8, 5, 10, 30
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model(case, dev):
+    from newsrec_amd.manager import build_model
+    encN, encU, H = CASES[case]
+    torch.manual_seed(11)
+    m = build_model(encN, encU, H, vocab=V, device=dev, user_num=USERS, dropout_p=0.0)
+    with torch.no_grad():
+        m.embedding.bert_word_embedding.weight.normal_(0, 0.5)
+    return m
+
+
+def _batch(seed, dev):
+    g = torch.Generator().manual_seed(seed)
+
+    def titles(n):
+        tok = torch.randint(1000, V, (n, L), generator=g)
+        lens = torch.randint(5, L + 1, (n,), generator=g)
+        mask = (torch.arange(L)[None] < lens[:, None]).long()
+        return tok * mask, mask
+    ct, cm = titles(BT * C)
+    ht, hm = titles(BT * NH)
+    his = (torch.arange(NH)[None] < torch.randint(1, NH + 1, (BT, 1), generator=g)).double().unsqueeze(-1)
+    x = {"cdd_encoded_index": ct.view(BT, C, L), "cdd_attn_mask": cm.view(BT, C, L),
+         "his_encoded_index": ht.view(BT, NH, L), "his_attn_mask": hm.view(BT, NH, L), "his_mask": his,
+         "user_id": torch.randint(1, USERS, (BT,), generator=g), "label": torch.zeros(BT, dtype=torch.long)}
+    x["user_id"][0] = x["user_id"][BT // 2]    # one user row on both ranks: the sparse sum adds
+    return {k: v.to(dev) for k, v in x.items()}
+
+
+def _half(x, rank, world):
+    n = BT // world
+    return {k: v[rank * n:(rank + 1) * n].contiguous() for k, v in x.items()}
+
+
+def _set_keep(model, case, keep):
+    if case == "lstur":
+        model.encoderU.keep_override = keep
+
+
+def _worker(rank, world, port, case, mode, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        sys.path.insert(0, os.path.join(ROOT, "news-recommendation-mind_amd"))
+        sys.path.insert(0, ROOT)
+        import torch.distributed as dist
+        import bench
+        from newsrec_amd.dist import GradSync
+        from newsrec_amd.manager import get_optim
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        steps = 4
+        batches = [_batch(100 + i, dev) for i in range(steps)]
+        keep = torch.ones(BT, dtype=torch.long, device=dev)   # device-resident: read inside the captured graph
+        keep[1] = 0
+        # reference: one process, whole batches, eager
+        ref = _model(case, dev)
+        _set_keep(ref, case, keep)
+        o_ref = get_optim(ref)
+        ref.train()
+        for x in batches:
+            bench.train_step(ref, o_ref, x, None)
+        # this rank: half of every batch, gradients averaged over the two ranks
+        m = _model(case, dev)
+        _set_keep(m, case, keep[rank * BT // world:(rank + 1) * BT // world])
+        m.train()
+        sync = GradSync(m, bucket_mb=0.5)   # several dense buckets
+        halves = [_half(x, rank, world) for x in batches]
+        if mode == "eager":
+            opt = get_optim(m)
+            for x in halves:
+                bench.train_step(m, opt, x, sync)
+        else:   # two-graph step: 2 eager warm-up steps, capture, 2 replays
+            opt = get_optim(m, capturable=True)
+            g = bench.GraphedStep(m, opt, bench.ResidentFeed(halves), sync, 2)
+            for i in range(2, steps):
+                g(i)
+        torch.cuda.synchronize()
+        sync.close()
+        diffs = {}
+        for (n, a), (_, b) in zip(ref.named_parameters(), m.named_parameters()):
+            d = (b.detach() - a.detach()).abs()
+            diffs[n] = (d.max().item(), int((d > 1e-7).sum().item()), d.numel())
+        q.put((rank, None, diffs))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:   # report instead of hanging the parent
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e), None))
+
+
+@pytest.mark.parametrize("mode", ["eager", "graphs"])
+@pytest.mark.parametrize("case", list(CASES))
+def test_data_parallel_real_model_world2(case, mode):
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, case, mode, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, err, diffs in res:
+        assert err is None, err
+        for n, (dmax, n_off, n_all) in diffs.items():
+            # 4 Adam steps from identical state.  Adam moves each element by ~lr * g / |g|, so an
+            # element whose gradient sits at the rounding level (the two ranks' half-batch means vs
+            # one whole-batch mean) may differ by up to 2 lr per step; every other element agrees to
+            # 1e-3 lr.  A missing or wrong exchange moves most elements off.
+            assert dmax <= 4 * 2 * 1e-4 + 1e-6, (rank, n, dmax)
+            assert n_off <= max(4, 1e-3 * n_all), (rank, n, n_off, n_all)
