@@ -1,0 +1,311 @@
+// Large-tile bf16 matrix-core GEMM (bf16x6: NP = 3 planes, six products; bf16: NP = 1), included by
+// the gemm_big_*.hip translation units.  Same operand modes, epilogues, persistent XCD-aware unit
+// order and C ABI semantics as the 128x128 kernel (gemm_split_impl.h); built for the big
+// contractions of the step (the news-tower projection and its dgrad / wgrad, the BERT dense layers).
+//
+// Why a second kernel: at 128x128 every fp32 element loaded feeds 2x fewer MFMAs, and the per-tile
+// split (fp32 -> three bf16 terms) costs ~10 VALU per MFMA; with two workgroups per CU phase-locked
+// on two barriers per k-step the VALU and the matrix cores barely overlap (MFMA busy 0.37,
+// profiles/pmc_proj_fwd.json).  Here:
+//   * 256 x BN tile (BN = 256 or 128), 8 waves (512 threads), wave tile 128x64 or 64x64: each loaded
+//     element feeds twice the MFMAs, halving the split work per MFMA;
+//   * 16-deep k-tiles, LDS DOUBLE-buffered ([stage][plane][row][24] bf16, 48-B rows: ds_read_b128
+//     fragments conflict-free), ONE barrier per k-tile: while the waves run k-tile P's MFMAs from
+//     one stage, the same waves split k-tile P+1 (already in registers) into the other stage and
+//     issue the global loads of P+2, so the VALU / LDS-store / load work is interleaved with the
+//     MFMA stream of the same wave instead of being serialised between barriers;
+//   * one workgroup per CU (147 KiB of LDS at BN = 256), persistent over the (tile, k-split) units.
+#pragma once
+#include <type_traits>
+
+#include "gemm_fast_common.h"
+
+namespace nrfast {
+
+constexpr int BIG_BM = 256;
+constexpr int BIG_BK = 16;
+constexpr int BIG_SR = 24;   // bf16 per LDS row: 16 k + 8 pad (48 B: odd multiple of 16 B)
+
+// K-contiguous operand, R rows x 16 k: 512 threads x (R / 128) float4 (row f >> 2, k quad f & 3)
+template <int R, int MODE>
+struct BigKC {
+  static constexpr int NV = R / 128;
+  float4 v[2][NV];   // two register sets: k-tile t lives in set t % 2 (loads issued 3 tiles ahead)
+  const float* rowp[NV];
+  __device__ __forceinline__ void init(const Op& d, int64_t r0, int64_t rlim, int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int f = tid + 512 * i;
+      int64_t row = r0 + (f >> 2);
+      row = row < rlim ? row : rlim - 1;   // clamp: rows >= M are computed and discarded
+      rowp[i] = MODE == KC_GATHER ? d.base + d.idx[row] * d.ld : d.base + row * d.ld;
+    }
+  }
+  template <int S>
+  __device__ __forceinline__ void prefetch_idx(const Op&, int64_t, int64_t, int) {}
+  template <int S>
+  __device__ __forceinline__ void load(const Op& d, int64_t, int64_t, int64_t k0, int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int f = tid + 512 * i;
+      v[S][i] = *reinterpret_cast<const float4*>(rowp[i] + k0 + 4 * (f & 3));
+    }
+  }
+  template <int S, int NP>
+  __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
+    constexpr int PL = R * BIG_SR;   // one plane
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int f = tid + 512 * i;
+      uint16_t* q = lds + (f >> 2) * BIG_SR + 4 * (f & 3);
+      const float4 x = v[S][i];
+      if constexpr (NP == 1) {
+        *reinterpret_cast<uint2*>(q) = hi4(x.x, x.y, x.z, x.w);
+      } else {
+        uint2 p0, p1, p2;
+        split4(x.x, x.y, x.z, x.w, p0, p1, p2);
+        *reinterpret_cast<uint2*>(q) = p0;
+        *reinterpret_cast<uint2*>(q + PL) = p1;
+        *reinterpret_cast<uint2*>(q + 2 * PL) = p2;
+      }
+    }
+  }
+};
+
+// MN-contiguous operand (stored rows = k), R rows x 16 k: thread t < 2R loads the 2 (k) x 4 (row)
+// block k = k0 + 2 (t & 7) + {0, 1}, rows r0 + 4 (t >> 3) .. + 3 as two float4 and writes each row's
+// two consecutive k as one 32-bit word per plane.
+template <int R, int MODE>
+struct BigMN {
+  static_assert(MODE == MN_PLAIN || MODE == MN_GATHER, "BigMN: plain or gathered stored rows");
+  float4 v[2][2];     // [register set][k of the pair]
+  int64_t kid[2][2];  // MN_GATHER: stored-row ids of a set's next tile (prefetched one load ahead)
+  __device__ __forceinline__ void init(const Op&, int64_t, int64_t, int) {}
+  template <int S>
+  __device__ __forceinline__ void prefetch_idx(const Op& d, int64_t k0, int64_t K, int tid) {
+    if (MODE == MN_GATHER && tid < 2 * R) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t k = k0 + 2 * (tid & 7) + u;
+        kid[S][u] = d.idx[k < K ? k : K - 1];
+      }
+    }
+  }
+  template <int S>
+  __device__ __forceinline__ void load(const Op& d, int64_t r0, int64_t rlim, int64_t k0, int tid) {
+    if (tid >= 2 * R) return;
+    int64_t col = r0 + 4 * (tid >> 3);
+    const int64_t cmax = ((rlim + 3) & ~int64_t(3)) - 4;
+    col = col < cmax ? col : cmax;   // clamp inside the padded row; rows >= M are discarded
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t row = MODE == MN_PLAIN ? k0 + 2 * (tid & 7) + u : kid[S][u];
+      v[S][u] = *reinterpret_cast<const float4*>(d.base + row * d.ld + col);
+    }
+  }
+  template <int NP>
+  __device__ __forceinline__ void put(uint16_t* q, float a, float b) const {
+    constexpr int PL = R * BIG_SR;
+    if constexpr (NP == 1) {
+      *reinterpret_cast<uint32_t*>(q) = pk_bf16(a, b);
+    } else {
+      uint32_t hh, mm, ll;
+      split2(a, b, hh, mm, ll);
+      *reinterpret_cast<uint32_t*>(q) = hh;
+      *reinterpret_cast<uint32_t*>(q + PL) = mm;
+      *reinterpret_cast<uint32_t*>(q + 2 * PL) = ll;
+    }
+  }
+  template <int S, int NP>
+  __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
+    if (tid >= 2 * R) return;
+    uint16_t* q = lds + (4 * (tid >> 3)) * BIG_SR + 2 * (tid & 7);
+    put<NP>(q, v[S][0].x, v[S][1].x);
+    put<NP>(q + BIG_SR, v[S][0].y, v[S][1].y);
+    put<NP>(q + 2 * BIG_SR, v[S][0].z, v[S][1].z);
+    put<NP>(q + 3 * BIG_SR, v[S][0].w, v[S][1].w);
+  }
+};
+
+template <int R, int MODE>
+using BigLoader = typename std::conditional<is_kc(MODE), BigKC<R, MODE>, BigMN<R, MODE>>::type;
+
+template <int AM, int BMODE, bool TR, int NP, int BN>
+__global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
+  constexpr int BM = BIG_BM;
+  using LA = BigLoader<BM, AM>;
+  using LB = BigLoader<BN, BMODE>;
+  constexpr int PA = BM * BIG_SR, PB = BN * BIG_SR;   // one plane
+  __shared__ __attribute__((aligned(16))) uint16_t As[2 * NP * PA];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2 * NP * PB];
+  constexpr bool IDX_AHEAD = AM == MN_GATHER || BMODE == MN_GATHER;
+
+  if (g.mdyn) {
+    const int64_t m = *g.mdyn;
+    g.M = m < g.M ? (m > 0 ? m : 0) : g.M;
+  }
+  if (g.kdyn) {
+    const int64_t k = *g.kdyn;
+    g.K = k < g.K ? (k > 0 ? k : 0) : g.K;
+    const int64_t kc = (g.K + g.splits - 1) / g.splits;
+    g.kchunk = kc > 0 ? (kc + 31) / 32 * 32 : 32;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
+  const int gn = (int)((g.N + BN - 1) / BN);
+  const int ntiles = (int)((g.M + BM - 1) / BM) * gn;
+  const int units = ntiles * g.splits;
+
+  // wave grid: BN = 256 -> 2 (M) x 4 (N) waves of 128x64; BN = 128 -> 4 x 2 waves of 64x64
+  constexpr int WN = BN == 256 ? 4 : 2;
+  constexpr int TI = (BM / (8 / WN)) / 32, TJ = (BN / WN) / 32;
+  const int wm = (w / WN) * (BM / (8 / WN)), wn = (w % WN) * (BN / WN);
+  f32x16 acc[TI][TJ];
+  LA la;
+  LB lb;
+
+  // persistent over this block's units (virtual ids blockIdx.x + j * gridDim.x); each unit runs its
+  // own two-deep pipeline, so the k-loop carries no unit bookkeeping (a pipeline refill per unit
+  // costs one load latency against ~48 k-tiles of MFMAs)
+  for (int id = blockIdx.x; id < units; id += gridDim.x) {
+    const Unit u = decode_unit(g, id, units, ntiles, gn, BM, BN);
+    if (u.nt <= 0) continue;   // a k-split past a device-resident K
+    const int64_t kend = u.kbeg + g.kchunk < g.K ? u.kbeg + g.kchunk : g.K;
+    const int nt = (int)((kend - u.kbeg + BIG_BK - 1) / BIG_BK);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    la.init(g.A, u.m0, g.M, tid);
+    lb.init(g.B, u.n0, g.N, tid);
+    // k-tile t is loaded into register set t % 2, three tiles ahead of its MFMAs: tile kt+3's loads
+    // are issued during k-tile kt and stored to LDS during kt+2 (two MFMA phases of latency cover:
+    // the gathered rows come from the Infinity Cache / HBM)
+    auto issue = [&](auto set, int kt) {
+      constexpr int S = decltype(set)::value;
+      const int64_t k = u.kbeg + (int64_t)kt * BIG_BK;
+      la.template load<S>(g.A, u.m0, g.M, k, tid);
+      lb.template load<S>(g.B, u.n0, g.N, k, tid);
+      if (IDX_AHEAD && kt + 2 < nt) {   // ids of the set's next tile (kt + 2)
+        la.template prefetch_idx<S>(g.A, k + 2 * BIG_BK, g.K, tid);
+        lb.template prefetch_idx<S>(g.B, k + 2 * BIG_BK, g.K, tid);
+      }
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    if (IDX_AHEAD) {
+      la.template prefetch_idx<0>(g.A, u.kbeg, g.K, tid);
+      lb.template prefetch_idx<0>(g.B, u.kbeg, g.K, tid);
+      la.template prefetch_idx<1>(g.A, u.kbeg + BIG_BK, g.K, tid);
+      lb.template prefetch_idx<1>(g.B, u.kbeg + BIG_BK, g.K, tid);
+    }
+    __syncthreads();   // the previous unit's last stage reads are done before stage 0 is rewritten
+    issue(S0{}, 0);
+    if (nt > 1) issue(S1{}, 1);
+    la.template store<0, NP>(As, tid);
+    lb.template store<0, NP>(Bs, tid);
+    if (nt > 2) issue(S0{}, 2);
+    __syncthreads();
+    // one k-tile: MFMAs from stage st; behind row blocks 0 / 1 the wave splits k-tile kt+1 (set
+    // (kt+1) % 2 = NS) into the other stage, then reuses that set for k-tile kt+3's loads
+    auto ktile = [&](auto nset, int kt, int st) {
+      constexpr int NS = decltype(nset)::value;
+      const bool stage_next = kt + 1 < nt;
+      const uint16_t* a_s = As + st * NP * PA;
+      const uint16_t* b_s = Bs + st * NP * PB;
+      bf16x8 b[TJ][NP];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          b[j][p] = *reinterpret_cast<const bf16x8*>(b_s + p * PB + (wn + 32 * j + c) * BIG_SR + 8 * h);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        bf16x8 a[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          a[p] = *reinterpret_cast<const bf16x8*>(a_s + p * PA + (wm + 32 * i + c) * BIG_SR + 8 * h);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+#define NR_MF(X, Y)                                                                                    \
+  acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][Y], a[X], acc[i][j], 0, 0, 0) \
+                 : __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[X], b[j][Y], acc[i][j], 0, 0, 0)
+          if constexpr (NP == 3) {   // smallest terms first
+            NR_MF(2, 0);
+            NR_MF(1, 1);
+            NR_MF(0, 2);
+            NR_MF(1, 0);
+            NR_MF(0, 1);
+          }
+          NR_MF(0, 0);
+#undef NR_MF
+        }
+        // (g.dbg bits 2 / 4: timing experiments only -- skip the split-stores / the loads)
+        if (i == 0 && stage_next && !(g.dbg & 2)) la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid);
+        if (i == 1 && stage_next) {
+          if (!(g.dbg & 2)) lb.template store<NS, NP>(Bs + (st ^ 1) * NP * PB, tid);
+          if (kt + 3 < nt && !(g.dbg & 4)) issue(nset, kt + 3);
+        }
+      }
+      __syncthreads();   // stage st fully read; stage st^1 fully written
+    };
+    for (int kt = 0; kt < nt; kt += 2) {   // unrolled by two: the register sets alternate statically
+      ktile(S1{}, kt, 0);
+      if (kt + 1 < nt) ktile(S0{}, kt + 1, 1);
+    }
+    epilogue_any<TR, TI, TJ>(g, acc, u.m0, u.n0, wm, wn, h, c);
+  }
+}
+
+template <typename Kern>
+int resident_slots_512(Kern k) {
+  static int cache[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  if (cache[dev] == 0) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 512, 0) != hipSuccess) return 0;
+    cache[dev] = cus * per;
+  }
+  return cache[dev];
+}
+
+template <int AM, int BMODE, bool TR, int NP, int BN>
+int launch_big(const Args& g, int splits, hipStream_t s) {
+  const int64_t gm = (g.M + BIG_BM - 1) / BIG_BM, gn = (g.N + BN - 1) / BN;
+  const int64_t units = gm * gn * splits;
+  if (units <= 0) return NR_OK;
+  if (units > 0x7fffffff) return NR_EINVAL(0);
+  int grid = (int)units;
+  const int slots = resident_slots_512(gemm_big_kernel<AM, BMODE, TR, NP, BN>);
+  if (slots > 0 && slots < grid) grid = slots;
+  Args a = g;
+  a.splits = splits;
+  hipLaunchKernelGGL((gemm_big_kernel<AM, BMODE, TR, NP, BN>), dim3((unsigned)grid), dim3(512), 0, s, a);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+// operand-mode dispatch of one (NP, BN); -1 = combination not instantiated
+template <int NP, int BN>
+int launch_big_modes(const Args& g, int am, int bm, int splits, hipStream_t s) {
+  const bool atomic_epi = g.epi == NR_EPI_ATOMIC || g.epi == NR_EPI_SCATTER;
+#define NR_BIG(A_, B_, TR_) \
+  if (am == A_ && bm == B_ && atomic_epi == !TR_) return launch_big<A_, B_, TR_, NP, BN>(g, splits, s);
+  NR_BIG(KC_GATHER, KC_PLAIN, true)    // gathered projection (fwd)
+  NR_BIG(KC_PLAIN, KC_PLAIN, true)     // y = x Wᵀ
+  NR_BIG(KC_PLAIN, MN_PLAIN, true)     // dgrad (store / scatter-store epilogues)
+  NR_BIG(MN_PLAIN, MN_GATHER, false)   // wgrad over gathered rows
+  NR_BIG(MN_PLAIN, MN_PLAIN, false)    // wgrad
+#undef NR_BIG
+  return -1;
+}
+
+int launch_big_1_256(const Args& g, int am, int bm, int splits, hipStream_t s);   // gemm_big_*.hip
+int launch_big_3_256(const Args& g, int am, int bm, int splits, hipStream_t s);
+int launch_big_1_128(const Args& g, int am, int bm, int splits, hipStream_t s);
+int launch_big_3_128(const Args& g, int am, int bm, int splits, hipStream_t s);
+
+}  // namespace nrfast

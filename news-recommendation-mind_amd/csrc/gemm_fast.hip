@@ -23,6 +23,26 @@
 
 namespace nrfast {
 int launch_modes64(const Args& g, int am, int bm, int splits, hipStream_t s);   // gemm_fast64.hip
+int launch_big_1_256(const Args& g, int am, int bm, int splits, hipStream_t s);   // gemm_big_*.hip
+int launch_big_3_256(const Args& g, int am, int bm, int splits, hipStream_t s);
+int launch_big_1_128(const Args& g, int am, int bm, int splits, hipStream_t s);
+int launch_big_3_128(const Args& g, int am, int bm, int splits, hipStream_t s);
+
+// Large-tile (256 x BN) bf16 kernel choice: 0 = stay on the 128x128 kernel.  NR_GEMM_BIG = 0 disables
+// it, 128 / 256 forces BN where eligible (A/B timing); auto: enough 256-row tiles to fill the chip,
+// BN = 256 when N fills 256-wide tiles well (N % 256 == 0 or N >= 1024), else 128.
+int big_bn(int64_t M, int64_t N, int splits) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("NR_GEMM_BIG");
+    mode = e ? atoi(e) : 1;
+  }
+  if (mode == 0 || N < 128) return 0;
+  const int64_t gm = (M + 255) / 256;
+  if (gm * splits < 8) return 0;
+  if (mode == 128 || mode == 256) return mode;
+  return (N % 256 == 0 || N >= 1024) ? 256 : 128;
+}
 }  // namespace nrfast
 
 
@@ -83,6 +103,27 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   g.kchunk = (g.kchunk + 31) / 32 * 32;
   if (g.kchunk == 0) g.kchunk = 32;
   const int splits = (int)((K + g.kchunk - 1) / g.kchunk) > 0 ? (int)((K + g.kchunk - 1) / g.kchunk) : 1;
+  if (bm == 128 && bn == 128 && prec != NR_GEMM_F32) {
+    const int BN = big_bn(M, N, splits);
+    if (BN) {
+      Args gb = g;
+      int sp = splits;
+      if (split_k > 1 && (epilogue == NR_EPI_ATOMIC || epilogue == NR_EPI_SCATTER)) {
+        // re-split for 256 x BN tiles: one wave of units over the 256 CUs, >= 512 k per split
+        const int64_t tiles = ((M + 255) / 256) * ((N + BN - 1) / BN);
+        int64_t want = 256 / (tiles > 0 ? tiles : 1);
+        if (want > K / 512) want = K / 512;
+        if (want > 64) want = 64;
+        if (want < 1) want = 1;
+        gb.kchunk = ((K + want - 1) / want + 31) / 32 * 32;
+        sp = (int)((K + gb.kchunk - 1) / gb.kchunk);
+      }
+      const int np = prec == NR_GEMM_BF16 ? 1 : 3;
+      const int rc = BN == 256 ? (np == 1 ? launch_big_1_256(gb, am, bmode, sp, stream) : launch_big_3_256(gb, am, bmode, sp, stream))
+                               : (np == 1 ? launch_big_1_128(gb, am, bmode, sp, stream) : launch_big_3_128(gb, am, bmode, sp, stream));
+      if (rc != -1) return rc;
+    }
+  }
   if (bm == 128 && bn == 128) return launch_modes<128, 128>(g, am, bmode, splits, prec, stream);
   if (bm == 64 && bn == 64) return launch_modes64(g, am, bmode, splits, stream);
   return -1;

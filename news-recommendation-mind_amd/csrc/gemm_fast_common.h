@@ -19,30 +19,30 @@ __device__ __forceinline__ uint32_t bf_rne(float x) {
   return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
 }
 __device__ __forceinline__ float bf_f(uint32_t b) { return __uint_as_float(b << 16); }
-// hardware conversions: the compiler pairs the casts into v_cvt_pk_bf16_f32 (round to nearest even)
+// hardware conversions, two values per v_cvt_pk_bf16_f32 (round to nearest even); a packed pair's
+// bf16 halves widen back to fp32 with one shift / mask each
 __device__ __forceinline__ uint32_t bf_bits(__bf16 v) { return (uint32_t)__builtin_bit_cast(uint16_t, v); }
-__device__ __forceinline__ void split1(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
-  const __bf16 hb = (__bf16)x;
-  const float r = x - (float)hb;   // exact
-  const __bf16 mb = (__bf16)r;
-  const __bf16 lb = (__bf16)(r - (float)mb);
-  h = bf_bits(hb);
-  m = bf_bits(mb);
-  l = bf_bits(lb);
+typedef float nr_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 nr_b2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((nr_f2){a, b}, nr_b2));
+}
+__device__ __forceinline__ float pk_lo(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float pk_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
+// a, b -> the packed (h, m, l) terms of both: 3 conversions, 4 bit ops, 4 subtractions per pair
+__device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = pk_bf16(a, b);
+  const float ra = a - pk_lo(h), rb = b - pk_hi(h);   // exact
+  m = pk_bf16(ra, rb);
+  l = pk_bf16(ra - pk_lo(m), rb - pk_hi(m));
 }
 __device__ __forceinline__ void split4(float a, float b, float c, float d, uint2& p0, uint2& p1, uint2& p2) {
-  uint32_t h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
-  split1(a, h0, m0, l0);
-  split1(b, h1, m1, l1);
-  split1(c, h2, m2, l2);
-  split1(d, h3, m3, l3);
-  p0 = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
-  p1 = make_uint2(m0 | (m1 << 16), m2 | (m3 << 16));
-  p2 = make_uint2(l0 | (l1 << 16), l2 | (l3 << 16));
+  split2(a, b, p0.x, p1.x, p2.x);
+  split2(c, d, p0.y, p1.y, p2.y);
 }
 // bf16 arithmetic (one product): the four values rounded to bf16 (RNE), packed
 __device__ __forceinline__ uint2 hi4(float a, float b, float c, float d) {
-  return make_uint2(bf_bits((__bf16)a) | (bf_bits((__bf16)b) << 16), bf_bits((__bf16)c) | (bf_bits((__bf16)d) << 16));
+  return make_uint2(pk_bf16(a, b), pk_bf16(c, d));
 }
 constexpr int SROW = 40;          // split LDS image: [plane][row][k] bf16, 32 k + 8 pad (80-B rows)
 constexpr int SPL = 128 * SROW;   // one plane of a 128-row operand tile

@@ -1,1 +1,1 @@
-extern "C" const char* nr_build_hash(void) { return "1a3fe6a1a1ec32bd"; }
+extern "C" const char* nr_build_hash(void) { return "a4fdf88e0055dd65"; }

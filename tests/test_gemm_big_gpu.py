@@ -1,0 +1,118 @@
+"""The large-tile bf16 GEMM kernel (gemm_big_impl.h: 256 x BN tiles, 8 waves, double-buffered LDS),
+which nr_gemm_f32 picks for big contractions under NR_GEMM_BF16X6 / NR_GEMM_BF16: every operand-mode
+combination it instantiates, ragged M / N (tiles cut by the extents), device-resident M and K, both
+tile widths (BN = 256 for N % 256 == 0 or N >= 1024, else 128), against fp64 references:
+bf16x6 to the fp32-class bound of tests/test_gemm_split_gpu.py, bf16 to fp32 accumulation error of
+the bf16-rounded operands."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from newsrec_amd import _lib as L
+from newsrec_amd import kernels as K
+
+PRECS = [L.GEMM_BF16X6, L.GEMM_BF16]
+
+
+def _ref(a, b, prec):
+    if prec == L.GEMM_BF16:
+        return a.bfloat16().double() @ b.bfloat16().double()
+    return a.double() @ b.double()
+
+
+def _tol(a, b, k, prec):
+    s = a.abs().max().item() * b.abs().max().item()
+    if prec == L.GEMM_BF16:
+        return 4e-7 * s * k + 1e-6
+    return 1e-5 * s * k ** 0.5 + 1e-6
+
+
+def _err(C, want):
+    return (C.double().cpu() - want).abs().max().item()
+
+
+@pytest.mark.parametrize("prec", PRECS)
+@pytest.mark.parametrize("N", [1152, 520, 768])
+def test_big_gather_projection(prec, N):
+    """Y = table[ids] Wᵀ + b (KC_GATHER x KC_PLAIN), M = 3000 rows (ragged last 256-row tile),
+    device-resident M smaller than the host bound."""
+    g = torch.Generator().manual_seed(N)
+    V, E, M = 5000, 768, 3000
+    table = torch.randn(V, E, generator=g)
+    ids = torch.randint(0, V, (M,), generator=g)
+    W = torch.randn(N, E, generator=g) / 16
+    bias = torch.randn(N, generator=g)
+    Y = torch.full((M, N), float("nan"), device="cuda")
+    m_dev = torch.tensor([2900], dtype=torch.int32, device="cuda")
+    K.gemm_dyn(M, N, E, K.operand(table.cuda(), L.KCONTIG, rows=ids.cuda(), mapping=L.ROWS_GATHER),
+               K.operand(W.cuda(), L.KCONTIG), Y, m_dev=m_dev, bias=bias.cuda(), prec=prec)
+    want = _ref(table[ids], W.t(), prec) + bias.double()
+    assert _err(Y[:2900], want[:2900]) <= _tol(table, W, E, prec)
+    assert torch.isnan(Y[2900:]).all()   # rows past the device M untouched
+
+
+@pytest.mark.parametrize("prec", PRECS)
+@pytest.mark.parametrize("epi", [L.EPI_STORE_TANH, L.EPI_STORE_GELU])
+def test_big_plain_epilogues(prec, epi):
+    g = torch.Generator().manual_seed(7)
+    M, N, Kd = 2600, 3072, 768
+    a = torch.randn(M, Kd, generator=g)
+    w = torch.randn(N, Kd, generator=g) / 28
+    b = torch.randn(N, generator=g) * 0.1
+    C = torch.empty(M, N, device="cuda")
+    aux = torch.empty(M, N, device="cuda") if epi == L.EPI_STORE_GELU else None
+    K.gemm(M, N, Kd, K.operand(a.cuda(), L.KCONTIG), K.operand(w.cuda(), L.KCONTIG), C, bias=b.cuda(), epilogue=epi,
+           c_rows=K.operand(aux, L.KCONTIG) if aux is not None else None, prec=prec)
+    pre = _ref(a, w.t(), prec) + b.double()
+    if epi == L.EPI_STORE_TANH:
+        want = torch.tanh(pre)
+        assert _err(C, want) <= _tol(a, w, Kd, prec)
+    else:
+        assert _err(aux, pre) <= _tol(a, w, Kd, prec)
+        want = 0.5 * pre * (1 + torch.erf(pre / 2 ** 0.5))
+        assert _err(C, want) <= 2 * _tol(a, w, Kd, prec)
+
+
+@pytest.mark.parametrize("prec", PRECS)
+def test_big_dgrad_store_and_scatter_store(prec):
+    """dX = dY W (KC_PLAIN x MN_PLAIN), plain store and the distinct-row scatter-store into a table."""
+    g = torch.Generator().manual_seed(3)
+    U, N, E, V = 2800, 1152, 768, 40000
+    dY = torch.randn(U, N, generator=g)
+    W = torch.randn(N, E, generator=g) / 30
+    dX = torch.empty(U, E, device="cuda")
+    K.gemm(U, E, N, K.operand(dY.cuda(), L.KCONTIG), K.operand(W.cuda(), L.MNCONTIG), dX, prec=prec)
+    want = _ref(dY, W, prec)
+    tol = _tol(dY, W, N, prec)
+    assert _err(dX, want) <= tol
+    rows = torch.randperm(V - 1, generator=g)[:U] + 1
+    rows[17] = 0
+    dt = torch.zeros(V, E, device="cuda")
+    K.gemm(U, E, N, K.operand(dY.cuda(), L.KCONTIG), K.operand(W.cuda(), L.MNCONTIG), dt,
+           epilogue=L.EPI_SCATTER_STORE, c_rows=K.rows_map(rows.cuda(), L.ROWS_GATHER), pad_row=0, prec=prec)
+    full = torch.zeros(V, E, dtype=torch.float64)
+    full[rows] = want
+    full[0] = 0
+    assert _err(dt, full) <= tol
+
+
+@pytest.mark.parametrize("prec", PRECS)
+@pytest.mark.parametrize("gather", [False, True])
+def test_big_wgrad_split_k(prec, gather):
+    """dW = dYᵀ X over K = rows (MN_PLAIN x MN_PLAIN / MN_GATHER), split-K atomics, device-resident K."""
+    g = torch.Generator().manual_seed(5 + gather)
+    R, N, E, V = 24576, 1152, 768, 30000
+    dY = torch.randn(R, N, generator=g)
+    table = torch.randn(V, E, generator=g) * 0.5
+    ids = torch.randint(0, V, (R,), generator=g)
+    X = table[ids]
+    dW = torch.zeros(N, E, device="cuda")
+    k_dev = torch.tensor([R - 4096], dtype=torch.int32, device="cuda")
+    Bop = (K.operand(table.cuda(), L.MNCONTIG, rows=ids.cuda(), mapping=L.ROWS_GATHER) if gather
+           else K.operand(X.cuda(), L.MNCONTIG))
+    K.gemm_dyn(N, E, R, K.operand(dY.cuda(), L.MNCONTIG), Bop, dW, k_dev=k_dev, epilogue=L.EPI_ATOMIC, split_k=9,
+               prec=prec)
+    Kr = R - 4096
+    want = _ref(dY[:Kr].t(), X[:Kr], prec)
+    assert _err(dW, want) <= _tol(dY, X, Kr, prec)

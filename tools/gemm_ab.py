@@ -1,0 +1,85 @@
+"""A/B timing of the GEMM kernels on the step's shapes: each NR_GEMM_BIG mode (0 = 128x128 kernel,
+128 / 256 = the large-tile kernel's BN, 1 = automatic) in its own process (the mode is read once),
+bf16x6 and bf16.  python tools/gemm_ab.py [--modes 0,1,128,256]"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r'''
+import json, sys, torch
+sys.path.insert(0, "%s/news-recommendation-mind_amd")
+from newsrec_amd import _lib as L, kernels as K, functions as F
+def bench(fn, reps=10):
+    fn(); torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps): fn()
+    e.record(); torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+dev = "cuda"; torch.manual_seed(0)
+V, E, U = 30522, 768, 24576
+table = torch.randn(V, E, device=dev); ids = torch.randint(1, V, (U,), device=dev)
+W = torch.randn(1152, E, device=dev) / 30
+Y = torch.empty(U, 1152, device=dev); dY = torch.randn(U, 1152, device=dev)
+dX = torch.empty(U, E, device=dev); dW = torch.zeros(1152, E, device=dev)
+T = 20832
+x = torch.randn(T, 768, device=dev); wqkv = torch.randn(2304, 768, device=dev) / 30
+qkv = torch.empty(T, 2304, device=dev); wi = torch.randn(3072, 768, device=dev) / 30
+G = torch.empty(T, 3072, device=dev); Ub = torch.empty(T, 3072, device=dev)
+wo2 = torch.randn(768, 3072, device=dev) / 50; o = torch.empty(T, 768, device=dev)
+dWi = torch.zeros(3072, 768, device=dev)
+P = torch.empty(U, 480, device=dev); w3 = torch.randn(480, E, device=dev)
+cases = {
+ "nrms_proj_fwd": (2*U*E*1152, lambda p: K.gemm_dyn(U, 1152, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(W, L.KCONTIG), Y, prec=p)),
+ "nrms_proj_dgrad": (2*U*E*1152, lambda p: K.gemm_dyn(U, E, 1152, K.operand(dY, L.KCONTIG), K.operand(W, L.MNCONTIG), dX, prec=p)),
+ "nrms_proj_wgrad": (2*U*E*1152, lambda p: K.gemm_dyn(1152, E, U, K.operand(dY, L.MNCONTIG), K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dW, epilogue=L.EPI_ATOMIC, split_k=F._split_k(1152, E, U), prec=p)),
+ "cnn_tap_proj": (2*U*E*480, lambda p: K.gemm_dyn(U, 480, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(w3, L.KCONTIG), P, prec=p)),
+ "bert_qkv": (2*T*768*2304, lambda p: K.gemm(T, 2304, 768, K.operand(x, L.KCONTIG), K.operand(wqkv, L.KCONTIG), qkv, prec=p)),
+ "bert_ffn1_gelu": (2*T*768*3072, lambda p: K.gemm(T, 3072, 768, K.operand(x, L.KCONTIG), K.operand(wi, L.KCONTIG), G, epilogue=L.EPI_STORE_GELU, c_rows=K.operand(Ub, L.KCONTIG), prec=p)),
+ "bert_ffn2": (2*T*768*3072, lambda p: K.gemm(T, 768, 3072, K.operand(G, L.KCONTIG), K.operand(wo2, L.KCONTIG), o, prec=p)),
+ "bert_ffn1_wgrad": (2*T*768*3072, lambda p: K.gemm(3072, 768, T, K.operand(G, L.MNCONTIG), K.operand(x, L.MNCONTIG), dWi, epilogue=L.EPI_ATOMIC, split_k=F._split_k(3072, 768, T), prec=p)),
+}
+out = {}
+import os
+only = os.environ.get("NR_AB_CASES")
+for pn, p in (("bf16x6", L.GEMM_BF16X6), ("bf16", L.GEMM_BF16)):
+    for k, (fl, fn) in cases.items():
+        if only and k not in only.split(","):
+            continue
+        ms = bench(lambda: fn(p))
+        out.setdefault(k, {})[pn] = {"us": round(ms * 1e3, 1), "tflops": round(fl / ms / 1e9, 1)}
+print(json.dumps(out))
+''' % ROOT
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--modes", default="0,1,128,256")
+    ap.add_argument("--variants", default=None,
+                    help="';'-separated env sets, e.g. 'NR_GEMM_BIG=1;NR_GEMM_BIG=1,NR_GEMM_DEBUG=2' (instead of --modes)")
+    ap.add_argument("--cases", default=None, help="comma-separated case names (default: all)")
+    a = ap.parse_args()
+    res = {}
+    variants = ([dict(kv.split("=") for kv in v.split(",")) for v in a.variants.split(";")] if a.variants
+                else [{"NR_GEMM_BIG": m} for m in a.modes.split(",")])
+    for var in variants:
+        m = ",".join("%s=%s" % kv for kv in var.items())
+        env = dict(os.environ, **var)
+        if a.cases:
+            env["NR_AB_CASES"] = a.cases
+        r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            res[m] = {"error": r.stderr[-2000:]}
+            print(json.dumps({m: res[m]}), flush=True)
+            break
+        res[m] = json.loads(r.stdout.strip().splitlines()[-1])
+        print(json.dumps({m: res[m]}), flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
