@@ -162,6 +162,9 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
   f32x16 acc[TI][TJ];
   LA la;
   LB lb;
+  // static arbitration priority for one half of the workgroup (waves w and w + 4 share a SIMD):
+  // NR_GEMM_DEBUG bit 8 raises waves 4-7, bit 16 waves 0-3 (A/B timing)
+  if (((g.dbg & 8) && w >= 4) || ((g.dbg & 16) && w < 4)) __builtin_amdgcn_s_setprio(1);
 
   // persistent over this block's units (virtual ids blockIdx.x + j * gridDim.x); each unit runs its
   // own two-deep pipeline, so the k-loop carries no unit bookkeeping (a pipeline refill per unit

@@ -29,19 +29,38 @@ int launch_big_1_128(const Args& g, int am, int bm, int splits, hipStream_t s);
 int launch_big_3_128(const Args& g, int am, int bm, int splits, hipStream_t s);
 
 // Large-tile (256 x BN) bf16 kernel choice: 0 = stay on the 128x128 kernel.  NR_GEMM_BIG = 0 disables
-// it, 128 / 256 forces BN where eligible (A/B timing); auto: enough 256-row tiles to fill the chip,
-// BN = 256 when N fills 256-wide tiles well (N % 256 == 0 or N >= 1024), else 128.
-int big_bn(int64_t M, int64_t N, int splits) {
+// it, 128 / 256 forces BN where eligible (A/B timing); auto: 256 x 256 tiles unless their units fill
+// the 256 CUs clearly worse ("round efficiency" = units / (256 * rounds), times the useful fraction
+// of padded columns) than the 128x128 kernel's at two workgroups per CU.
+// Split-K callers (atomic epilogues) are re-split for the chosen tile, so they always fill the chip.
+double round_eff(int64_t units, int64_t slots) {
+  if (units <= 0) return 0.0;
+  const int64_t rounds = (units + slots - 1) / slots;
+  return (double)units / (double)(rounds * slots);
+}
+
+int big_bn(int64_t M, int64_t N, int64_t K, int splits, bool resplit, bool m_dyn) {
   static int mode = -1;
   if (mode < 0) {
     const char* e = getenv("NR_GEMM_BIG");
     mode = e ? atoi(e) : 1;
   }
   if (mode == 0 || N < 128) return 0;
+  // a short contraction (K < 512: < 32 k-tiles) does not amortise the per-unit pipeline fill
+  if (!resplit && K < 512) return 0;
   const int64_t gm = (M + 255) / 256;
-  if (gm * splits < 8) return 0;
+  if (!resplit && gm * splits < 8) return 0;
   if (mode == 128 || mode == 256) return mode;
-  return (N % 256 == 0 || N >= 1024) ? 256 : 128;
+  if (resplit) return (N % 256 == 0 || N >= 1024) ? 256 : 128;
+  // device-resident M (distinct-row counts): the host M is only a bound, so the round efficiency is
+  // unknown; the persistent grid absorbs the actual count -- take the big tiles for wide N
+  if (m_dyn) return N >= 1024 ? 256 : 0;
+  // padded-N MFMA work counts against a tile width too; measured on the step's shapes, the
+  // 256 x 256 core is ~15 % faster per unit of work than the 128 x 128 kernel, 256 x 128 is not
+  const double e256 = round_eff(gm * ((N + 255) / 256) * splits, 256) * (double)N / (double)((N + 255) / 256 * 256);
+  const double e_old = round_eff(((M + 127) / 128) * ((N + 127) / 128) * splits, 512) * (double)N /
+                       (double)((N + 127) / 128 * 128);
+  return e256 >= 0.87 * e_old ? 256 : 0;
 }
 }  // namespace nrfast
 
@@ -104,11 +123,12 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   if (g.kchunk == 0) g.kchunk = 32;
   const int splits = (int)((K + g.kchunk - 1) / g.kchunk) > 0 ? (int)((K + g.kchunk - 1) / g.kchunk) : 1;
   if (bm == 128 && bn == 128 && prec != NR_GEMM_F32) {
-    const int BN = big_bn(M, N, splits);
+    const bool resplit = split_k > 1 && (epilogue == NR_EPI_ATOMIC || epilogue == NR_EPI_SCATTER);
+    const int BN = big_bn(M, N, K, splits, resplit, m_dev != nullptr);
     if (BN) {
       Args gb = g;
       int sp = splits;
-      if (split_k > 1 && (epilogue == NR_EPI_ATOMIC || epilogue == NR_EPI_SCATTER)) {
+      if (resplit) {
         // re-split for 256 x BN tiles: one wave of units over the 256 CUs, >= 512 k per split
         const int64_t tiles = ((M + 255) / 256) * ((N + BN - 1) / BN);
         int64_t want = 256 / (tiles > 0 ? tiles : 1);

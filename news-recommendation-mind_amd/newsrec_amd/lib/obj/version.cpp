@@ -1,1 +1,1 @@
-extern "C" const char* nr_build_hash(void) { return "a4fdf88e0055dd65"; }
+extern "C" const char* nr_build_hash(void) { return "4069e3e6178bd802"; }
