@@ -565,45 +565,116 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
 }
 
 // Split backward, kernel 1 (forward saved O): pooling/LN backward per title from the saved O
-// rows; dO rows to global.
+// rows; dO rows to global.  Register-resident: wave w owns rows w, w + 4, ... of the title and keeps
+// them (and their dropout keep-bits) in registers through both passes; only the 32 pooling scores
+// and the cross-wave dgamma / dbeta / dq partials go through LDS (~19 KB instead of ~68 KB staging
+// the whole O tile, so several titles share a CU and their loads overlap).
 template <int NH64>
 __global__ __launch_bounds__(256) void mha_ln_bwd_kernel(MPArgs g) {
   if (g.rng) g.dkey = nr_dropout_key(g.rng[0], g.rng[1] + g.offset);   // graph-replay RNG
-  extern __shared__ __attribute__((aligned(16))) float sm[];
   constexpr int H = NH64 * 64;
-  constexpr int SO = H + 1;
-  float* os = sm;                       // [32][SO]  O, then dO
-  float* ps = os + 32 * SO;             // [32]
-  float* ds = ps + 32;                  // [32]
-  float* st = ds + 32;                  // [32][2]
-  uint64_t* kb = reinterpret_cast<uint64_t*>(st + 64);   // [32][NH64]
-  float* red = st + 64 + 2 * 32 * NH64; // [nw][3][H]
+  constexpr int RW = 8;                 // rows per wave (L <= 32, 4 waves)
+  __shared__ float sdp[32], sps[32];
+  __shared__ float red[4][3][H];
   const int64_t seq = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
-  {   // O rows (32 x H, rows >= L zero): every load in flight before the first LDS store
-    constexpr int PER = 32 * H / 4 / 256;   // float4 per thread (256 threads)
-    const float* o0 = g.o + seq * g.L * g.ldo;
-    float4 v[PER];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int L = g.L;
+  const bool drop = g.p_drop > 0.f;
+  const float dsc = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+  float x[RW][NH64];
+  // every O load of the wave in flight at once (rows past L clamped, their values unused)
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int e = tid + 256 * i, r = e / (H / 4), c4 = e % (H / 4);
-      v[i] = *reinterpret_cast<const float4*>(o0 + (int64_t)(r < g.L ? r : 0) * g.ldo + 4 * c4);
-      if (r >= g.L) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+  for (int i = 0; i < RW; ++i) {
+    const int l = w + 4 * i;
+    const float* orow = g.o + (seq * L + (l < L ? l : 0)) * g.ldo;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int e = tid + 256 * i, r = e / (H / 4), c4 = e % (H / 4);
-      float* d = os + r * SO + 4 * c4;
-      d[0] = v[i].x; d[1] = v[i].y; d[2] = v[i].z; d[3] = v[i].w;
-    }
+    for (int k = 0; k < NH64; ++k) x[i][k] = orow[lane + 64 * k];
   }
-  if (tid < 32) {
-    ps[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
-    st[2 * tid] = tid < g.L ? g.stats[2 * (seq * g.L + tid)] : 0.f;
-    st[2 * tid + 1] = tid < g.L ? g.stats[2 * (seq * g.L + tid) + 1] : 0.f;
+  float gam[NH64], bet[NH64], qv[NH64], dnv[NH64];
+#pragma unroll
+  for (int k = 0; k < NH64; ++k) {
+    gam[k] = g.gamma[lane + 64 * k];
+    bet[k] = g.beta[lane + 64 * k];
+    qv[k] = g.q[lane + 64 * k];
+    dnv[k] = g.news[seq * g.ldn + lane + 64 * k];
+  }
+  if (tid < 32) sps[tid] = tid < L ? g.probs[seq * L + tid] : 0.f;
+  // (1) normalise in place (x -> x_hat), dp_l = dnews · Z_l, keep-bits kept per row
+  uint64_t kbit[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const int l = w + 4 * i;
+    kbit[i] = 0;
+    if (l >= L) continue;
+    const int64_t row = seq * L + l;
+    const float mean = g.stats[2 * row], rstd = g.stats[2 * row + 1];
+    float dot = 0.f;
+    uint32_t kb = 0;
+#pragma unroll
+    for (int k = 0; k < NH64; ++k) {
+      const int d = lane + 64 * k;
+      const bool keep = !drop || nr_dropout_keep(g.dkey, (uint32_t)(row * H + d), g.dthresh);
+      kb |= (keep ? 1u : 0u) << k;
+      x[i][k] = (x[i][k] - mean) * rstd;
+      const float z = keep ? (x[i][k] * gam[k] + bet[k]) * dsc : 0.f;
+      dot = fmaf(dnv[k], z, dot);
+    }
+    kbit[i] = kb;
+    dot = nr_wave_sum(dot);
+    if (lane == 0) sdp[l] = dot;
   }
   __syncthreads();
-  pool_ln_bwd<NH64>(g, seq, os, ps, ds, st, red, kb, g.dob, g.lddob);
+  if (w == 0) {   // pooling softmax backward: ds_l = p_l (dp_l - Σ p dp) / sqrt(H)
+    const float pl = lane < 32 ? sps[lane & 31] : 0.f;
+    const float dp = lane < L ? sdp[lane & 31] : 0.f;
+    const float r = nr_wave_sum(pl * dp);
+    if (lane < L) sdp[lane] = pl * (dp - r) * g.scale_pool;
+  }
+  __syncthreads();
+  // (2) dq += ds_l Z_l;  dZ = p_l dnews + ds_l q (+ dz) -> dropout -> LayerNorm backward -> dO
+  float dgam[NH64], dbet[NH64], dqp[NH64];
+#pragma unroll
+  for (int k = 0; k < NH64; ++k) { dgam[k] = 0.f; dbet[k] = 0.f; dqp[k] = 0.f; }
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const int l = w + 4 * i;
+    if (l >= L) continue;
+    const int64_t row = seq * L + l;
+    const float rstd = g.stats[2 * row + 1], pl = sps[l], dsl = sdp[l];
+    float dyv[NH64];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int k = 0; k < NH64; ++k) {
+      const int d = lane + 64 * k;
+      const float sk = ((kbit[i] >> k) & 1u) ? dsc : 0.f;
+      dqp[k] = fmaf(dsl, (x[i][k] * gam[k] + bet[k]) * sk, dqp[k]);
+      float dz = fmaf(pl, dnv[k], dsl * qv[k]);
+      if (g.dz) dz += g.dz[row * g.lddz + d];
+      dyv[k] = dz * sk;
+      const float gg = dyv[k] * gam[k];
+      sg += gg;
+      sgx = fmaf(gg, x[i][k], sgx);
+      dgam[k] = fmaf(dyv[k], x[i][k], dgam[k]);
+      dbet[k] += dyv[k];
+    }
+    sg = nr_wave_sum(sg) * (1.f / H);
+    sgx = nr_wave_sum(sgx) * (1.f / H);
+    float* drow = g.dob + row * g.lddob;
+#pragma unroll
+    for (int k = 0; k < NH64; ++k) drow[lane + 64 * k] = rstd * (dyv[k] * gam[k] - sg - x[i][k] * sgx);
+  }
+#pragma unroll
+  for (int k = 0; k < NH64; ++k) {
+    red[w][0][lane + 64 * k] = dgam[k];
+    red[w][1][lane + 64 * k] = dbet[k];
+    red[w][2][lane + 64 * k] = dqp[k];
+  }
+  __syncthreads();
+  for (int d = tid; d < H; d += 256) {
+    atomicAdd(&g.dgamma[d], (red[0][0][d] + red[1][0][d]) + (red[2][0][d] + red[3][0][d]));
+    atomicAdd(&g.dbeta[d], (red[0][1][d] + red[1][1][d]) + (red[2][1][d] + red[3][1][d]));
+    atomicAdd(&g.dq[d], (red[0][2][d] + red[1][2][d]) + (red[2][2][d] + red[3][2][d]));
+  }
 }
 
 // Split backward, kernel 2: attention backward, one wave per head, HB_TITLES titles per
@@ -664,9 +735,6 @@ size_t bwd_smem(int H, int nw) {
   return (size_t)(32 + 32 * (H + 1) + 32 + 32 + 64 + 2 * 32 * (H / 64) + (tiles > red ? tiles : red)) * sizeof(float);
 }
 
-size_t ln_bwd_smem(int H, int nw) {
-  return (size_t)(32 * (H + 1) + 32 + 32 + 64 + 2 * 32 * (H / 64) + nw * 3 * H) * sizeof(float);
-}
 size_t head_bwd_smem(int nw, int dv) { return (size_t)(32 * nw + nw * 32 * 33 + nw * 32 * (dv + 1)) * sizeof(float); }
 
 enum Pass { FWD = 0, BWD_FUSED = 1, BWD_SPLIT = 2 };
@@ -692,9 +760,7 @@ int launch(const MPArgs& g, Pass pass, hipStream_t s) {
     allow_smem(mha_pool_bwd_kernel<DK, DV, NH64>, sz);
     hipLaunchKernelGGL((mha_pool_bwd_kernel<DK, DV, NH64>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
   } else {
-    const size_t s1 = ln_bwd_smem(H, 4);
-    allow_smem(mha_ln_bwd_kernel<NH64>, s1);
-    hipLaunchKernelGGL((mha_ln_bwd_kernel<NH64>), dim3((unsigned)g.nseq), dim3(256), s1, s, g);
+    hipLaunchKernelGGL((mha_ln_bwd_kernel<NH64>), dim3((unsigned)g.nseq), dim3(256), 0, s, g);
     MPArgs g2 = g;
     g2.rows_per_wave = 1;
     const unsigned gx = (unsigned)((g.nseq + HB_TITLES - 1) / HB_TITLES), gy = (unsigned)((g.heads + 3) / 4);

@@ -1,1 +1,1 @@
-extern "C" const char* nr_build_hash(void) { return "4069e3e6178bd802"; }
+extern "C" const char* nr_build_hash(void) { return "c87863d217cf7e0c"; }
