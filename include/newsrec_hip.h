@@ -158,6 +158,15 @@ int nr_conv3_rows_fwd(const float* P, int64_t ldp, int32_t tap_width, int32_t H,
                       int64_t T, int32_t L, const float* bias, int32_t relu, float* out, int64_t ldo,
                       hipStream_t stream);
 
+/* The distinct-row CNN encoder's weight operands in one launch: w3t [3*Hp][E] (row tap*Hp + h =
+ * conv_w[h][:][tap], the Conv1d weight [H][E][3]; rows h >= H zero), wqp [Hp][Hp] and bqp [Hp] (the
+ * key projection zero-padded).  nr_cnn_unpack_grads maps the gradients of those operands back to the
+ * parameters' layouts (dconv_w [H][E][3], dwq [H][H], dbq [H]; stored, not accumulated). */
+int nr_cnn_pack_weights(const float* conv_w, const float* wq, const float* bq, int32_t H, int32_t E,
+                        int32_t Hp, float* w3t, float* wqp, float* bqp, hipStream_t stream);
+int nr_cnn_unpack_grads(const float* dw3t, const float* dwqp, const float* dbqp, int32_t H, int32_t E,
+                        int32_t Hp, float* dconv_w, float* dwq, float* dbq, hipStream_t stream);
+
 /* ------------------------------------------------------------------ attention */
 
 /* Tied-QK multi-head self attention core, one sequence of L <= 64 tokens per (seq, head):
@@ -245,6 +254,27 @@ int nr_attn_pool_bwd(const float* x, int64_t ldx, const float* key, int64_t ldk,
                      const float* dout, int64_t lddo, const float* dz, int64_t lddz, float* dx,
                      int64_t lddx, float* dk, int64_t lddk, int32_t key_tanh, float* dq,
                      float* dgamma, float* dbeta, hipStream_t stream);
+
+/* Learned-query pooling without LayerNorm / dropout, one wave per sequence (rows as coalesced float4
+ * segments, per-row dot products as wave reductions, no LDS staging):
+ *   out[s] = Σ_l XSoftmax(scale * q·K_l, mask)_l X_l,  K = key rows, or X when key == NULL.
+ * Replaces CNN_Encoder's pooling (CNN.py:46, key = tanh(W c + b)) and Attention_Pooling
+ * (Pooling.py:22-24).  D <= 256, L <= 64; the row matrices (x, key, out, dx, dk, dz) 16-B aligned with
+ * ld % 4 == 0 and ld >= D; q (and each dout row) hold qn <= D valid floats, any alignment, features
+ * past qn taken as zero (a zero-padded row width D > qn then pools exact zeros there).  Saves
+ * probs [nseq*L]. */
+int nr_seq_pool_fwd(const float* x, int64_t ldx, const float* key, int64_t ldk, const float* q, int32_t qn,
+                    const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L, int32_t D, float scale,
+                    float* out, int64_t ldo, float* probs, hipStream_t stream);
+
+/* Backward of nr_seq_pool_fwd: dx = p dout (+ ds q when tied) (+ dz), dk = ds q (* (1 - K²) when
+ * key_tanh) for a separate key; ATOMICALLY ACCUMULATES dq[0 .. qn) (one add per feature per
+ * workgroup). */
+int nr_seq_pool_bwd(const float* x, int64_t ldx, const float* key, int64_t ldk, const float* q, int32_t qn,
+                    const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L, int32_t D, float scale,
+                    const float* probs, const float* dout, int64_t lddo, const float* dz, int64_t lddz,
+                    float* dx, int64_t lddx, float* dk, int64_t lddk, int32_t key_tanh, float* dq,
+                    hipStream_t stream);
 
 /* ------------------------------------------------------------------ recurrent user encoders */
 

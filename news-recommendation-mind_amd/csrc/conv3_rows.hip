@@ -62,3 +62,73 @@ extern "C" int nr_conv3_rows_fwd(const float* P, int64_t ldp, int32_t tap_width,
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
+
+// ---- the distinct-row encoder's weight operands, one launch each way (the step's weights change
+// every optimizer step, so they are re-laid out every step: one kernel instead of a permute copy
+// and three pads, and one for their gradients instead of the matching slice / permute copies)
+namespace {
+
+__global__ __launch_bounds__(256) void cnn_pack_kernel(const float* __restrict__ cw, const float* __restrict__ wq,
+                                                       const float* __restrict__ bq, int H, int E, int Hp,
+                                                       float* __restrict__ w3t, float* __restrict__ wqp,
+                                                       float* __restrict__ bqp) {
+  const int64_t n3 = (int64_t)3 * Hp * E, nq = (int64_t)Hp * Hp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n3 + nq + Hp;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < n3) {   // w3t[tap*Hp + h][e] = conv.weight[h][e][tap]
+      const int64_t r = i / E, e = i - r * E;
+      const int tap = (int)(r / Hp), h = (int)(r - (int64_t)tap * Hp);
+      w3t[i] = h < H ? cw[((int64_t)h * E + e) * 3 + tap] : 0.f;
+    } else if (i < n3 + nq) {
+      const int64_t k = i - n3;
+      const int r = (int)(k / Hp), c = (int)(k - (int64_t)r * Hp);
+      wqp[k] = (r < H && c < H) ? wq[(int64_t)r * H + c] : 0.f;
+    } else {
+      const int h = (int)(i - n3 - nq);
+      bqp[h] = h < H ? bq[h] : 0.f;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void cnn_unpack_kernel(const float* __restrict__ dw3t, const float* __restrict__ dwqp,
+                                                         const float* __restrict__ dbqp, int H, int E, int Hp,
+                                                         float* __restrict__ dcw, float* __restrict__ dwq,
+                                                         float* __restrict__ dbq) {
+  const int64_t n3 = (int64_t)3 * H * E, nq = (int64_t)H * H;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n3 + nq + H;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < n3) {   // dconv.weight[h][e][tap] = dw3t[tap*Hp + h][e]
+      const int64_t he = i / 3;
+      const int tap = (int)(i - he * 3);
+      const int64_t h = he / E, e = he - h * E;
+      dcw[i] = dw3t[((int64_t)tap * Hp + h) * E + e];
+    } else if (i < n3 + nq) {
+      const int64_t k = i - n3;
+      const int r = (int)(k / H), c = (int)(k - (int64_t)r * H);
+      dwq[k] = dwqp[(int64_t)r * Hp + c];
+    } else {
+      const int h = (int)(i - n3 - nq);
+      dbq[h] = dbqp[h];
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int nr_cnn_pack_weights(const float* conv_w, const float* wq, const float* bq, int32_t H, int32_t E,
+                                   int32_t Hp, float* w3t, float* wqp, float* bqp, hipStream_t stream) {
+  if (H < 1 || E < 1 || Hp < H) return NR_EINVAL(0);
+  if (!conv_w || !wq || !bq || !w3t || !wqp || !bqp) return NR_EINVAL(1);
+  hipLaunchKernelGGL(cnn_pack_kernel, dim3(1024), dim3(256), 0, stream, conv_w, wq, bq, H, E, Hp, w3t, wqp, bqp);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_cnn_unpack_grads(const float* dw3t, const float* dwqp, const float* dbqp, int32_t H, int32_t E,
+                                   int32_t Hp, float* dconv_w, float* dwq, float* dbq, hipStream_t stream) {
+  if (H < 1 || E < 1 || Hp < H) return NR_EINVAL(0);
+  if (!dw3t || !dwqp || !dbqp || !dconv_w || !dwq || !dbq) return NR_EINVAL(1);
+  hipLaunchKernelGGL(cnn_unpack_kernel, dim3(1024), dim3(256), 0, stream, dw3t, dwqp, dbqp, H, E, Hp, dconv_w, dwq, dbq);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}

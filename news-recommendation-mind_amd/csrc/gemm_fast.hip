@@ -124,7 +124,9 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   const int splits = (int)((K + g.kchunk - 1) / g.kchunk) > 0 ? (int)((K + g.kchunk - 1) / g.kchunk) : 1;
   if (bm == 128 && bn == 128 && prec != NR_GEMM_F32) {
     const bool resplit = split_k > 1 && (epilogue == NR_EPI_ATOMIC || epilogue == NR_EPI_SCATTER);
-    const int BN = big_bn(M, N, K, splits, resplit, m_dev != nullptr);
+    // bf16 split-K (atomic) launches stay on the 128x128 kernel: with one product per tile they are
+    // bound by the atomic traffic of the re-split, not by the matrix cores
+    const int BN = (resplit && prec == NR_GEMM_BF16) ? 0 : big_bn(M, N, K, splits, resplit, m_dev != nullptr);
     if (BN) {
       Args gb = g;
       int sp = splits;

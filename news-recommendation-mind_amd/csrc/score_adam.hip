@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const float* dout, i
 // segments, 8 loads in flight), the waves combine in LDS and store the block's partial row; pass 2
 // sums the partials per column in row-block order.  No atomics: a few thousand blocks adding into
 // the same H addresses serialise on the L2 (the old one-pass form ran at ~1 TB/s on [52800, 150]).
-constexpr int kColsumBlocks = 2048;
+constexpr int kColsumBlocks = 1024;
 
 __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows,
                                                           int64_t cols, int64_t rb_rows, float* __restrict__ part) {
@@ -264,18 +264,30 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restric
   if (w == 0 && c < cols) part[(int64_t)blockIdx.y * cols + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int64_t nrb, int64_t cols,
-                                                           float* __restrict__ out) {
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
+// 16 row groups x 64 columns per workgroup: each thread sums nrb / 16 partials (4 in flight), the
+// 16 groups combine in LDS in a fixed order
+__global__ __launch_bounds__(1024) void colsum_final_kernel(const float* __restrict__ part, int64_t nrb, int64_t cols,
+                                                            float* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
   float a[4] = {0.f, 0.f, 0.f, 0.f};
-  int64_t b = 0;
-  for (; b + 4 <= nrb; b += 4) {
+  if (c < cols) {
+    int64_t b = grp;
+    for (; b + 48 < nrb; b += 64) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) a[u] += part[(b + u) * cols + c];
+      for (int u = 0; u < 4; ++u) a[u] += part[(b + 16 * u) * cols + c];
+    }
+    for (; b < nrb; b += 16) a[0] += part[b * cols + c];
   }
-  for (; b < nrb; ++b) a[0] += part[b * cols + c];
-  out[c] += (a[0] + a[1]) + (a[2] + a[3]);
+  red[grp][lane] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (grp == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += red[q][lane];
+    out[c] += t;
+  }
 }
 
 void colsum_grid(int64_t rows, int64_t cols, int64_t* nrb, int64_t* rb_rows) {
@@ -376,7 +388,7 @@ extern "C" int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols
   colsum_grid(rows, cols, &nrb, &rb_rows);
   hipLaunchKernelGGL(colsum_part_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)nrb), dim3(256), 0, stream, x,
                      ldx, rows, cols, rb_rows, work);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, stream, work, nrb, cols,
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((cols + 63) / 64)), dim3(1024), 0, stream, work, nrb, cols,
                      out);
   NR_LAUNCH_CHECK();
   return NR_OK;

@@ -57,6 +57,8 @@ _SIGS = {
     "nr_segment_rows_sum_workspace": [c_i64, c_i64],
     "nr_segment_rows_sum_conv3": [c_ptr, c_i64, c_i64, c_i32, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr,
                                   c_i64, c_ptr],
+    "nr_cnn_pack_weights": [c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
+    "nr_cnn_unpack_grads": [c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
     "nr_conv3_rows_fwd": [c_ptr, c_i64, c_i32, c_i32, c_ptr, c_i64, c_i32, c_ptr, c_i32, c_ptr, c_i64, c_ptr],
     "nr_mha_attn_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
                         c_f32, c_ptr, c_i64, c_ptr],
@@ -67,6 +69,10 @@ _SIGS = {
     "nr_attn_pool_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_ptr, c_ptr, c_f32, c_u64, c_u64,
                          c_ptr, c_i64, c_i32, c_i32, c_f32, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64,
                          c_ptr, c_i64, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
+    "nr_seq_pool_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_ptr,
+                        c_i64, c_ptr, c_ptr],
+    "nr_seq_pool_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_ptr,
+                        c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_ptr, c_ptr],
     "nr_rnn_fwd": [c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i32, c_i64, c_i32,
                    c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr],
     "nr_rnn_bwd": [c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_i64, c_i32, c_i32, c_ptr, c_i64,

@@ -75,10 +75,7 @@ class CNN_Encoder(nn.Module):
         weight[h, :, tap]) and the key projection zero-padded to Hp = ceil32(H) (K % 32 == 0)."""
         H = self.hidden_dim
         Hp = (H + 31) // 32 * 32
-        w3t = torch.nn.functional.pad(self.cnn.weight.permute(2, 0, 1), (0, 0, 0, Hp - H))
-        w3t = w3t.reshape(3 * Hp, self.embedding_dim)
-        wq = torch.nn.functional.pad(self.wordQueryProject.weight, (0, Hp - H, 0, Hp - H))
-        bq = torch.nn.functional.pad(self.wordQueryProject.bias, (0, Hp - H))
+        w3t, wq, bq = F.CNNWeightsFn.apply(self.cnn.weight, self.wordQueryProject.weight, self.wordQueryProject.bias, Hp)
         return w3t, wq, bq
 
     def encode_tokens(self, table, token_ids, attn_mask, pad_row=0):

@@ -346,6 +346,41 @@ class CNNNewsFn(torch.autograd.Function):
         return dtable, None, None, dw3, dconv_b, dwq, dbq, dq.view_as(query), None, None
 
 
+class CNNWeightsFn(torch.autograd.Function):
+    """The distinct-row CNN encoder's weight operands (nr_cnn_pack_weights): the Conv1d weight
+    [H, E, 3] as w3t [3*Hp, E] (row tap*Hp + h) and the key projection zero-padded to [Hp, Hp] / [Hp],
+    in one launch; the backward maps the three gradients back in one launch."""
+
+    @staticmethod
+    def forward(ctx, conv_w, wq, bq, Hp):
+        H, E = conv_w.shape[0], conv_w.shape[1]
+        dev = conv_w.device
+        w3t = torch.empty(3 * Hp, E, device=dev)
+        wqp = torch.empty(Hp, Hp, device=dev)
+        bqp = torch.empty(Hp, device=dev)
+        for t in (conv_w, wq, bq):
+            if not t.is_contiguous():
+                raise L.HipError("cnn weights must be contiguous")
+        L.call("nr_cnn_pack_weights", L.ptr(conv_w), L.ptr(wq), L.ptr(bq), H, E, Hp, L.ptr(w3t), L.ptr(wqp),
+               L.ptr(bqp), L.stream_ptr(conv_w))
+        ctx.cfg = (H, E, Hp)
+        return w3t, wqp, bqp
+
+    @staticmethod
+    def backward(ctx, dw3t, dwqp, dbqp):
+        H, E, Hp = ctx.cfg
+        dev = (dw3t if dw3t is not None else dwqp).device
+        dw3t = dw3t.contiguous() if dw3t is not None else torch.zeros(3 * Hp, E, device=dev)
+        dwqp = dwqp.contiguous() if dwqp is not None else torch.zeros(Hp, Hp, device=dev)
+        dbqp = dbqp.contiguous() if dbqp is not None else torch.zeros(Hp, device=dev)
+        dcw = torch.empty(H, E, 3, device=dev)
+        dwq = torch.empty(H, H, device=dev)
+        dbq = torch.empty(H, device=dev)
+        L.call("nr_cnn_unpack_grads", L.ptr(dw3t), L.ptr(dwqp), L.ptr(dbqp), H, E, Hp, L.ptr(dcw), L.ptr(dwq),
+               L.ptr(dbq), L.stream_ptr(dw3t))
+        return dcw, dwq, dbq, None
+
+
 class CNNNewsRowsFn(torch.autograd.Function):
     """CNN_Encoder.forward (models/Encoders/CNN.py:30-50) over DISTINCT word rows.
 
@@ -358,8 +393,10 @@ class CNNNewsRowsFn(torch.autograd.Function):
     (Sᵀ · table[uids]) are GEMMs over U rows instead of T tokens.
 
     w3t: [3*Hp, E] with row tap*Hp + h = Conv1d.weight[h, :, tap] (rows h >= H zero); wq, bq: the
-    key projection zero-padded to [Hp, Hp] / [Hp] so every contraction has K % 32 == 0.
-    Returns (news [n, H], C [T, H] view)."""
+    key projection zero-padded to [Hp, Hp] / [Hp] so every contraction has K % 32 == 0; query: the
+    pooling query [1, H] (the pooling runs over the padded width, nr_seq_pool_*, with features past
+    H of the query and of dnews taken as zero).
+    Returns (news [n, H] view, C [T, H] view)."""
 
     @staticmethod
     def forward(ctx, table, ids, mask, w3t, conv_b, wq, bq, query, seq_len, pad_row, H):
@@ -378,14 +415,15 @@ class CNNNewsRowsFn(torch.autograd.Function):
         K.conv3_rows_fwd(P, Hp, H, ur.inv, seq_len, conv_b, C, relu=True)
         Kq = _empty(T, Hp, table)
         K.gemm(T, Hp, Hp, K.operand(C, L.KCONTIG), K.operand(wq, L.KCONTIG), Kq, bias=bq, epilogue=L.EPI_STORE_TANH)
-        news = _empty(n, H, table)
+        # pooling over the padded width: C and Kq are exactly zero past H, and so is the padded query
+        news = _empty(n, Hp, table)
         probs = torch.empty(T, device=table.device)
-        K.attn_pool_fwd(C, query, mask, n, seq_len, news, probs, key=Kq)
+        K.seq_pool_fwd(C, query, mask, n, seq_len, Hp, news, probs, key=Kq, qn=H)
         ctx.save_for_backward(table, ids, mask, w3t, wq, query, C, Kq, probs)
         ctx.cfg = (seq_len, pad_row, H)
         ctx.table_ref = table
         ctx.ur = ur
-        return news, C[:, :H]
+        return news[:, :H], C[:, :H]
 
     @staticmethod
     @_gemm_backward
@@ -399,9 +437,15 @@ class CNNNewsRowsFn(torch.autograd.Function):
         Hp = w3t.shape[0] // 3
         dev = table.device
         dC = _empty(T, Hp, table)
-        dwq, dbq, dconv_b, dw3t, dq, dKq = _zeros_views(dev, (Hp, Hp), (Hp,), (H,), (3 * Hp, E), (H,), (T, Hp))
-        K.attn_pool_bwd(C, query, mask, n, seq_len, probs, dnews.contiguous(), dC, dq, key=Kq, dk=dKq, key_tanh=True,
-                        dz=dC_out.contiguous() if dC_out is not None else None)
+        dKq = _empty(T, Hp, table)
+        dwq, dbq, dconv_b, dw3t, dq = _zeros_views(dev, (Hp, Hp), (Hp,), (H,), (3 * Hp, E), (H,))
+        # dC = p dnews (+ dC_out), dKq = ds q (1 - Kq²) over the padded width: exactly zero past H
+        # (dnews and the query count as zero there)
+        dz = torch.nn.functional.pad(dC_out, (0, Hp - H)) if dC_out is not None else None
+        if dnews.stride(-1) != 1:
+            dnews = dnews.contiguous()
+        K.seq_pool_bwd(C, query, mask, n, seq_len, Hp, probs, dnews, dC, dq, key=Kq, dk=dKq, key_tanh=True, dz=dz,
+                       qn=H)
         # key projection: dWq = dKqᵀ C, dbq = colsum(dKq); dC = ReLU'(C) ⊙ (dC + dKq Wq) (padded
         # columns of C are zero, so the gate also zeroes dC's padding)
         _proj_wgrad(dKq, K.operand(C, L.MNCONTIG), dwq, dbq, T)
@@ -433,18 +477,27 @@ class AttnPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, query, mask, B, N):
         H = query.numel()
-        out = _empty(B, H, x)
         probs = torch.empty(B * N, device=x.device)
-        K.attn_pool_fwd(x, query, mask, B, N, out, probs)
+        # one wave per sequence (nr_seq_pool_*) when the rows are float4-addressable
+        sp = K.seq_pool_supported(H, N) and x.stride(-1) == 1 and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0
+        out = _empty(B, H, x)
+        if sp:
+            K.seq_pool_fwd(x, query, mask, B, N, H, out, probs)
+        else:
+            K.attn_pool_fwd(x, query, mask, B, N, out, probs)
         ctx.save_for_backward(x, query, mask, probs)
-        ctx.cfg = (B, N)
+        ctx.cfg = (B, N, H, sp)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         x, query, mask, probs = ctx.saved_tensors
-        B, N = ctx.cfg
-        H = query.numel()
+        B, N, H, sp = ctx.cfg
+        if sp:
+            dx = _empty(B * N, H, x)
+            dq = torch.zeros(H, device=x.device)
+            K.seq_pool_bwd(x, query, mask, B, N, H, probs, dout if dout.stride(-1) == 1 else dout.contiguous(), dx, dq)
+            return dx, dq.view_as(query), None, None, None
         dx = _empty(B * N, H, x)
         dq = torch.zeros(H, device=x.device)
         K.attn_pool_bwd(x, query, mask, B, N, probs, dout.contiguous(), dx, dq)

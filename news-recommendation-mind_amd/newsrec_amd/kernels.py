@@ -312,6 +312,64 @@ def attn_pool_bwd(x, q, mask, nseq, seq_len, probs, dout, dx, dq, key=None, dk=N
            L.stream_ptr(x))
 
 
+def seq_pool_supported(D, L):
+    return 1 <= D <= 256 and 1 <= L <= 64
+
+
+def _sp_rows(t, rows, D, name):
+    if t is None:
+        return
+    _al(t, name)
+    _rows_ok(t, rows, D, name)
+
+
+def _vec_ok(v, n, name):
+    if v.numel() < n or (v.dim() > 1 and v.stride(-1) != 1):
+        raise L.HipError("%s: needs %d contiguous floats" % (name, n))
+
+
+def seq_pool_fwd(x, q, mask, nseq, seq_len, D, out, probs, key=None, scale=None, qn=None):
+    """nr_seq_pool_fwd: pooling of nseq sequences of seq_len rows of D features (row matrices 16-B
+    aligned, ld % 4 == 0); q holds qn <= D valid floats (features past qn count as zero)."""
+    _f32(x, q, out, probs, key)
+    qn = D if qn is None else qn
+    if not seq_pool_supported(D, seq_len):
+        raise L.HipError("seq_pool: D <= 256, L <= 64 required (D=%d, L=%d)" % (D, seq_len))
+    _sp_rows(x, nseq * seq_len, D, "seq_pool x")
+    _sp_rows(key, nseq * seq_len, D, "seq_pool key")
+    _sp_rows(out, nseq, D, "seq_pool out")
+    _vec_ok(q, qn, "seq_pool q")
+    if probs.numel() < nseq * seq_len:
+        raise L.HipError("seq_pool: probs needs nseq*L floats")
+    mp, mdt = mask_arg(mask, nseq * seq_len)
+    scale = 1.0 / float(qn) ** 0.5 if scale is None else scale
+    L.call("nr_seq_pool_fwd", L.ptr(x), x.stride(0), L.ptr(key), key.stride(0) if key is not None else 0, L.ptr(q),
+           qn, mp, mdt, nseq, seq_len, D, scale, L.ptr(out), out.stride(0), L.ptr(probs), L.stream_ptr(x))
+
+
+def seq_pool_bwd(x, q, mask, nseq, seq_len, D, probs, dout, dx, dq, key=None, dk=None, key_tanh=False, dz=None,
+                 scale=None, qn=None):
+    """dout [nseq, >= qn] (any alignment, row stride dout.stride(0)); dq accumulates qn floats."""
+    _f32(x, q, probs, dout, dx, dq, key, dk, dz)
+    qn = D if qn is None else qn
+    if not seq_pool_supported(D, seq_len):
+        raise L.HipError("seq_pool: D <= 256, L <= 64 required (D=%d, L=%d)" % (D, seq_len))
+    for t, r, n in ((x, nseq * seq_len, "x"), (key, nseq * seq_len, "key"), (dk, nseq * seq_len, "dk"),
+                    (dx, nseq * seq_len, "dx"), (dz, nseq * seq_len, "dz")):
+        _sp_rows(t, r, D, "seq_pool_bwd " + n)
+    _rows_ok(dout, nseq, qn, "seq_pool_bwd dout")
+    if key is not None and dk is None:
+        raise L.HipError("seq_pool_bwd: a separate key needs dk")
+    _vec_ok(q, qn, "seq_pool_bwd q")
+    _vec_ok(dq, qn, "seq_pool_bwd dq")
+    mp, mdt = mask_arg(mask, nseq * seq_len)
+    scale = 1.0 / float(qn) ** 0.5 if scale is None else scale
+    L.call("nr_seq_pool_bwd", L.ptr(x), x.stride(0), L.ptr(key), key.stride(0) if key is not None else 0, L.ptr(q),
+           qn, mp, mdt, nseq, seq_len, D, scale, L.ptr(probs), L.ptr(dout), dout.stride(0), L.ptr(dz),
+           dz.stride(0) if dz is not None else 0, L.ptr(dx), dx.stride(0), L.ptr(dk),
+           dk.stride(0) if dk is not None else 0, int(key_tanh), L.ptr(dq), L.stream_ptr(x))
+
+
 def rnn_fwd(cell, gx, whh_t, bhh, B, N, H, gates, hprev, cprev, hout, h0=None, h0_idx=None, mask=None,
             reverse=False):
     G = 4 if cell == L.CELL_LSTM else 3

@@ -1,1 +1,1 @@
-extern "C" const char* nr_build_hash(void) { return "c87863d217cf7e0c"; }
+extern "C" const char* nr_build_hash(void) { return "3f09500434c8ddd3"; }
