@@ -70,8 +70,11 @@ enum nr_epilogue {
                             the table gradient over nr_unique_rows' ids, plain vector stores */
   NR_EPI_STORE_GELU = 8, /* aux[m][n] = acc + bias[n]; C[m][n] = gelu(aux[m][n]) (exact erf GELU,
                             BertIntermediate); aux = c_rows->data, ld c_rows->ld               */
-  NR_EPI_GELU_GRAD = 9   /* C[m][n] = acc * gelu'(aux[m][n]), aux = c_rows->data (ld c_rows->ld):
+  NR_EPI_GELU_GRAD = 9,  /* C[m][n] = acc * gelu'(aux[m][n]), aux = c_rows->data (ld c_rows->ld):
                             the dgrad of the intermediate dense through its GELU               */
+  NR_EPI_SCATTER_ZEROED = 10 /* NR_EPI_SCATTER_STORE whose destination rows are ZERO on entry (the
+                            zero-filled table gradient): the large-tile kernel may split K over the
+                            last partial round of its tiles and add those pieces atomically   */
 };
 
 /* GEMM arithmetic, chosen PER CALL (the `prec` argument of nr_gemm_f32 / nr_gemm_f32_dyn; the

@@ -130,6 +130,39 @@ struct BigMN {
 template <int R, int MODE>
 using BigLoader = typename std::conditional<is_kc(MODE), BigKC<R, MODE>, BigMN<R, MODE>>::type;
 
+// Atomic scatter-add of a tail piece in the transposed accumulator layout (lane (h, c) holds row c,
+// columns 8q + 4h + 0..3 of each 32 x 32 block): one block at a time goes through LDS (waves 0-3 in
+// the A image, 4-7 in the B image, 32 x 36 floats each) and is read back two rows x 32 consecutive
+// columns per instruction, so each atomic instruction touches two cache lines instead of 32 (device
+// atomics are resolved past the XCD's L2: their cost is per line, not per element).
+template <int TI, int TJ>
+__device__ __forceinline__ void tail_scatter_tr(const Args& g, f32x16 (&acc)[TI][TJ], int64_t m0, int64_t n0, int wm,
+                                                int wn, int h, int c, int w, int lane, float* chunk) {
+  constexpr int CS = 36;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      __syncthreads();   // previous block read back (or the k-loop's last stage reads done)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<float4*>(chunk + c * CS + 8 * q + 4 * h) =
+            make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+      __syncthreads();
+      const int64_t col = n0 + wn + 32 * j + (lane & 31);
+#pragma unroll 4
+      for (int rr = 0; rr < 16; ++rr) {
+        const int rl = 2 * rr + (lane >> 5);
+        const int64_t row = m0 + wm + 32 * i + rl;
+        if (row >= g.M || col >= g.N) continue;
+        const int64_t tok = g.Cm.idx[row];
+        if (tok == g.pad_row || (g.dbg & 32)) continue;   // dbg bit 32: timing only, no tail adds
+        atomicAdd(g.C + tok * g.ldc + col, chunk[rl * CS + (lane & 31)]);
+      }
+    }
+  (void)w;
+}
+
 template <int AM, int BMODE, bool TR, int NP, int BN>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
   constexpr int BM = BIG_BM;
@@ -153,7 +186,31 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c = lane & 31;
   const int gn = (int)((g.N + BN - 1) / BN);
   const int ntiles = (int)((g.M + BM - 1) / BM) * gn;
-  const int units = ntiles * g.splits;
+  int units = ntiles * g.splits;
+  // NR_EPI_SCATTER_ZEROED (destination rows zero on entry, splits == 1): the tiles of the last,
+  // partial round of the persistent grid are split along K into `pieces` units whose sums are added
+  // atomically, so that round costs 1/pieces of a unit instead of a whole one (a stream-K tail)
+  int full = units, rem = 0, pieces = 1;
+  int64_t kc_tail = g.kchunk;
+  if (g.tail > 1) {
+    const int G = (int)gridDim.x;
+    const int f = ntiles / G * G, r = ntiles - f;
+    if (r > 0 && 2 * r <= G) {
+      int p = G / r;
+      p = p < g.tail ? p : g.tail;
+      const int64_t pmax = g.K / 128;   // >= 8 k-tiles per piece
+      p = p < pmax ? p : (int)pmax;
+      if (p > 1) {
+        kc_tail = ((g.K + p - 1) / p + 31) / 32 * 32;
+        pieces = (int)((g.K + kc_tail - 1) / kc_tail);
+      }
+    }
+    if (pieces > 1) {
+      full = f;
+      rem = r;
+      units = f + r * pieces;
+    }
+  }
 
   // wave grid: BN = 256 -> 2 (M) x 4 (N) waves of 128x64; BN = 128 -> 4 x 2 waves of 64x64
   constexpr int WN = BN == 256 ? 4 : 2;
@@ -170,9 +227,22 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
   // own two-deep pipeline, so the k-loop carries no unit bookkeeping (a pipeline refill per unit
   // costs one load latency against ~48 k-tiles of MFMAs)
   for (int id = blockIdx.x; id < units; id += gridDim.x) {
-    const Unit u = decode_unit(g, id, units, ntiles, gn, BM, BN);
-    if (u.nt <= 0) continue;   // a k-split past a device-resident K
-    const int64_t kend = u.kbeg + g.kchunk < g.K ? u.kbeg + g.kchunk : g.K;
+    const bool tail_unit = id >= full;
+    Unit u;
+    int64_t kend;
+    if (!tail_unit) {
+      u = decode_unit(g, id, full, ntiles, gn, BM, BN);
+      if (u.nt <= 0) continue;   // a k-split past a device-resident K
+      kend = u.kbeg + g.kchunk < g.K ? u.kbeg + g.kchunk : g.K;
+    } else {   // tail: (tile full + j % rem, K piece j / rem)
+      const int j = id - full;
+      const int tile = full + j % rem;
+      u.m0 = (int64_t)(tile / gn) * BM;
+      u.n0 = (int64_t)(tile % gn) * BN;
+      u.kbeg = (int64_t)(j / rem) * kc_tail;
+      kend = u.kbeg + kc_tail < g.K ? u.kbeg + kc_tail : g.K;
+      if (kend <= u.kbeg) continue;
+    }
     const int nt = (int)((kend - u.kbeg + BIG_BK - 1) / BIG_BK);
 #pragma unroll
     for (int i = 0; i < TI; ++i)
@@ -257,7 +327,19 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
       ktile(S1{}, kt, 0);
       if (kt + 1 < nt) ktile(S0{}, kt + 1, 1);
     }
-    epilogue_any<TR, TI, TJ>(g, acc, u.m0, u.n0, wm, wn, h, c);
+    if (!tail_unit) {
+      epilogue_any<TR, TI, TJ>(g, acc, u.m0, u.n0, wm, wn, h, c);
+    } else if (TR) {   // pieces of one tile meet in C: atomic adds into the zeroed destination rows
+      static_assert(4 * 32 * 36 * 4 <= 2 * NP * PA * 2 || BN != 256, "tail chunks fit the A image");
+      if constexpr (BN == 256 && 4 * 32 * 36 * 4 <= 2 * NP * PB * 2) {
+        float* chunk = reinterpret_cast<float*>(w < 4 ? As : Bs) + (w & 3) * 32 * 36;
+        tail_scatter_tr<TI, TJ>(g, acc, u.m0, u.n0, wm, wn, h, c, w, lane, chunk);
+      } else {
+        epilogue_t<NR_EPI_SCATTER, TI, TJ>(g, acc, u.m0, u.n0, wm, wn, h, c, g.vec);
+      }
+    } else {
+      epilogue_cmajor<NR_EPI_SCATTER, TI, TJ>(g, acc, u.m0, u.n0, wm, wn, h, c);
+    }
   }
 }
 

@@ -316,6 +316,7 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
                            int32_t split_k, int32_t prec, hipStream_t stream) {
   if (M < 0 || N < 0 || K < 0) return NR_EINVAL(0);
   if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(12);
+  if (epilogue < NR_EPI_STORE || epilogue > NR_EPI_SCATTER_ZEROED) return NR_EINVAL(3);
   if (!A || !B || !C || !A->data || !B->data) return NR_EINVAL(1);
   if (((A->map != NR_ROWS_PLAIN) && (A->ld & 3)) || ((B->map != NR_ROWS_PLAIN) && (B->ld & 3)))
     return NR_EINVAL(2);   // gathered tables must be float4-addressable
@@ -337,7 +338,8 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
   if (g.kchunk == 0) g.kchunk = 32;
   const int splits = (int)((K + g.kchunk - 1) / g.kchunk) > 0 ? (int)((K + g.kchunk - 1) / g.kchunk) : 1;
 
-  if (epilogue == NR_EPI_SCATTER_STORE && (!c_rows || c_rows->map != NR_ROWS_GATHER || !c_rows->rows))
+  if ((epilogue == NR_EPI_SCATTER_STORE || epilogue == NR_EPI_SCATTER_ZEROED) &&
+      (!c_rows || c_rows->map != NR_ROWS_GATHER || !c_rows->rows))
     return NR_EINVAL(4);
   if (!getenv_generic()) {
     const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128) * splits;
@@ -349,7 +351,8 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
                                 nullptr, prec, stream);
     if (rc != -1) return rc;
   }
-  if (epilogue == NR_EPI_SCATTER_STORE) g.epi = NR_EPI_SCATTER;   // generic kernel: same sums via atomics
+  // generic kernel: same sums via atomics
+  if (epilogue == NR_EPI_SCATTER_STORE || epilogue == NR_EPI_SCATTER_ZEROED) g.epi = NR_EPI_SCATTER;
   int bm = pick_tile(M), bn = pick_tile(N);
   // small problems: prefer 64x64 tiles to fill the 256 CUs
   if ((int64_t)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * splits < 512) { bm = 64; bn = 64; }
@@ -379,6 +382,7 @@ extern "C" int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand
                                const int32_t* k_dev, int32_t prec, hipStream_t stream) {
   if (M < 0 || N < 0 || K < 0 || (K % 32)) return NR_EINVAL(0);
   if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(14);
+  if (epilogue < NR_EPI_STORE || epilogue > NR_EPI_SCATTER_ZEROED) return NR_EINVAL(3);
   if (!A || !B || !C || !A->data || !B->data) return NR_EINVAL(1);
   if ((A->ld & 3) || (B->ld & 3)) return NR_EINVAL(2);
   if (epilogue == NR_EPI_SCATTER && (!c_rows || (c_rows->map != NR_ROWS_PLAIN && !c_rows->rows)))
@@ -386,7 +390,8 @@ extern "C" int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand
   if ((epilogue == NR_EPI_ACCUM_GATE || epilogue == NR_EPI_STORE_GELU || epilogue == NR_EPI_GELU_GRAD) &&
       (!c_rows || !c_rows->data))
     return NR_EINVAL(4);
-  if (epilogue == NR_EPI_SCATTER_STORE && (!c_rows || c_rows->map != NR_ROWS_GATHER || !c_rows->rows))
+  if ((epilogue == NR_EPI_SCATTER_STORE || epilogue == NR_EPI_SCATTER_ZEROED) &&
+      (!c_rows || c_rows->map != NR_ROWS_GATHER || !c_rows->rows))
     return NR_EINVAL(4);
   if (split_k < 1) split_k = 1;
   if (split_k > 1 && epilogue != NR_EPI_ATOMIC && epilogue != NR_EPI_SCATTER) return NR_EINVAL(5);

@@ -45,7 +45,8 @@ int big_bn(int64_t M, int64_t N, int64_t K, int splits, bool resplit, bool m_dyn
     const char* e = getenv("NR_GEMM_BIG");
     mode = e ? atoi(e) : 1;
   }
-  if (mode == 0 || N < 128) return 0;
+  if (mode == 0) return -1;   // disabled (also for NR_EPI_SCATTER_ZEROED's tail split)
+  if (N < 128) return 0;
   // a short contraction (K < 512: < 32 k-tiles) does not amortise the per-unit pipeline fill
   if (!resplit && K < 512) return 0;
   const int64_t gm = (M + 255) / 256;
@@ -72,6 +73,10 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
                  hipStream_t stream) {
   using namespace nrfast;
   if (K <= 0) return -1;
+  // NR_EPI_SCATTER_ZEROED = NR_EPI_SCATTER_STORE whose destination rows are zero on entry: the big
+  // kernel may then split the K of its last partial round of tiles (atomic adds of the pieces)
+  const bool zeroed = epilogue == NR_EPI_SCATTER_ZEROED;
+  if (zeroed) epilogue = NR_EPI_SCATTER_STORE;
   auto aligned = [](const nr_operand* o) {
     return (o->ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(o->data) & 15) == 0);
   };
@@ -102,7 +107,7 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   if (epilogue == NR_EPI_SCATTER_STORE && (!c_rows || c_rows->map != NR_ROWS_GATHER || !c_rows->rows)) return -1;
   if (epilogue == NR_EPI_SCATTER && c_rows && c_rows->map == NR_ROWS_CONV3 && c_rows->seq_len == 1) return -1;
   g.C = C; g.ldc = ldc; g.bias = bias; g.epi = epilogue; g.pad_row = pad_row;
-  g.mdyn = m_dev; g.kdyn = k_dev; g.splits = 1;
+  g.mdyn = m_dev; g.kdyn = k_dev; g.splits = 1; g.tail = 0;
   {
     static int dbg = -1;
     if (dbg < 0) {
@@ -126,9 +131,12 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
     const bool resplit = split_k > 1 && (epilogue == NR_EPI_ATOMIC || epilogue == NR_EPI_SCATTER);
     // bf16 split-K (atomic) launches stay on the 128x128 kernel: with one product per tile they are
     // bound by the atomic traffic of the re-split, not by the matrix cores
-    const int BN = (resplit && prec == NR_GEMM_BF16) ? 0 : big_bn(M, N, K, splits, resplit, m_dev != nullptr);
+    const bool tailed = zeroed && splits == 1 && K >= 512 && N >= 256 && big_bn(M, N, K, 1, false, false) >= 0;
+    const int bb = (resplit && prec == NR_GEMM_BF16) ? 0 : big_bn(M, N, K, splits, resplit, m_dev != nullptr);
+    const int BN = tailed ? 256 : (bb > 0 ? bb : 0);
     if (BN) {
       Args gb = g;
+      if (tailed) gb.tail = 16;
       int sp = splits;
       if (resplit) {
         // re-split for 256 x BN tiles: one wave of units over the 256 CUs, >= 512 k per split

@@ -74,6 +74,7 @@ struct Args {
   const int32_t* mdyn;   // device-resident M (<= M), or null
   const int32_t* kdyn;   // device-resident K (<= K), or null
   int dbg;   // NR_GEMM_DEBUG bits (timing experiments only): 1 = skip the output stores
+  int tail;  // big kernel, NR_EPI_SCATTER_ZEROED: max K pieces of the last partial round's tiles (0 = off)
 };
 
 // Register-staged tile loader for an operand of R rows (the M or N extent) x 32 k.

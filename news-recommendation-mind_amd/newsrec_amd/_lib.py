@@ -26,7 +26,7 @@ KCONTIG, MNCONTIG = 0, 1
 EPI_STORE, EPI_STORE_RELU, EPI_ATOMIC, EPI_SCATTER = 0, 1, 2, 3
 MASK_U8, MASK_I64, MASK_F64, MASK_F32 = 0, 1, 2, 3
 EPI_STORE_TANH, EPI_ACCUM_GATE, EPI_ACCUM, EPI_SCATTER_STORE = 4, 5, 6, 7
-EPI_STORE_GELU, EPI_GELU_GRAD = 8, 9
+EPI_STORE_GELU, EPI_GELU_GRAD, EPI_SCATTER_ZEROED = 8, 9, 10
 GEMM_F32, GEMM_BF16X6, GEMM_BF16 = 0, 1, 2
 CELL_LSTM, CELL_GRU = 0, 1
 SCORE_RAW, SCORE_LOG_SOFTMAX, SCORE_SIGMOID = 0, 1, 2

@@ -260,7 +260,7 @@ class MHANewsFn(torch.autograd.Function):
                 dtable = torch.zeros(V, E, device=table.device)
                 # distinct rows (M = U, not U_pad: no duplicate pad ids): plain row stores
                 K.gemm_dyn(ur.cap, E, NY, K.operand(dYu, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dtable,
-                           m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_STORE,
+                           m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_ZEROED,
                            c_rows=K.rows_map(ur.uids, L.ROWS_GATHER), pad_row=pad_row)
                 if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
                     dtable = None
@@ -458,7 +458,7 @@ class CNNNewsRowsFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dtable = torch.zeros(V, E, device=dev)
             K.gemm_dyn(ur.cap, E, 3 * Hp, K.operand(S, L.KCONTIG), K.operand(w3t, L.MNCONTIG), dtable,
-                       m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_STORE, c_rows=K.rows_map(ur.uids, L.ROWS_GATHER),
+                       m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(ur.uids, L.ROWS_GATHER),
                        pad_row=pad_row)
             if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
                 dtable = None

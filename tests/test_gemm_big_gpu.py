@@ -116,3 +116,28 @@ def test_big_wgrad_split_k(prec, gather):
     Kr = R - 4096
     want = _ref(dY[:Kr].t(), X[:Kr], prec)
     assert _err(dW, want) <= _tol(dY, X, Kr, prec)
+
+
+@pytest.mark.parametrize("prec", PRECS)
+@pytest.mark.parametrize("U,u_dev", [(2800, None), (30000, 24600), (24576, None)])
+def test_big_dgrad_scatter_zeroed_tail(prec, U, u_dev):
+    """NR_EPI_SCATTER_ZEROED (the table dgrad into a zero-filled gradient): the tiles of the persistent
+    grid's last partial round are split along K and their pieces added atomically (a stream-K tail).
+    U = 2800: every tile split (33 tiles); device M 24,600: 291 tiles = one full round + 35 split
+    tiles; 24,576: 288 tiles."""
+    g = torch.Generator().manual_seed(U)
+    N, E, V = 1152, 768, 60000
+    dY = torch.randn(U, N, generator=g)
+    W = torch.randn(N, E, generator=g) / 30
+    rows = torch.randperm(V - 1, generator=g)[:U] + 1
+    rows[5] = 0   # the padding row is skipped
+    m = u_dev or U
+    dt = torch.zeros(V, E, device="cuda")
+    m_dev = torch.tensor([m], dtype=torch.int32, device="cuda")
+    K.gemm_dyn(U, E, N, K.operand(dY.cuda(), L.KCONTIG), K.operand(W.cuda(), L.MNCONTIG), dt, m_dev=m_dev,
+               epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(rows.cuda(), L.ROWS_GATHER), pad_row=0, prec=prec)
+    want = _ref(dY[:m], W, prec)
+    full = torch.zeros(V, E, dtype=torch.float64)
+    full[rows[:m]] = want
+    full[0] = 0
+    assert _err(dt, full) <= _tol(dY, W, N, prec)
