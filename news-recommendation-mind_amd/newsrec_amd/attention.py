@@ -50,6 +50,32 @@ def scaled_dp_attention(query, key, value, attn_mask=None):
     return torch.matmul(p, value)
 
 
+def _joined_view(a, b):
+    """[a; b] as one tensor when b's data directly follows a's in the same storage, else None."""
+    if (a.device != b.device or a.dtype != b.dtype or not a.is_contiguous() or not b.is_contiguous()
+            or a.shape[1:] != b.shape[1:]):
+        return None
+    sa, sb = a.untyped_storage(), b.untyped_storage()
+    if sa.data_ptr() != sb.data_ptr() or b.storage_offset() != a.storage_offset() + a.numel():
+        return None
+    return torch.empty(0, dtype=a.dtype, device=a.device).set_(
+        sa, a.storage_offset(), (a.shape[0] + b.shape[0],) + tuple(a.shape[1:]))
+
+
+class _Joined(torch.autograd.Function):
+    """The stacked [a; b] of two parameters that live back to back in one buffer, without a copy;
+    the backward hands each parameter its rows of the gradient (views, no copy either)."""
+
+    @staticmethod
+    def forward(ctx, a, b, joined):
+        ctx.n = a.shape[0]
+        return joined
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[:ctx.n], g[ctx.n:], None
+
+
 class MultiheadAttention(nn.Module):
     """Attention.py:83-147 with the same constructor, parameters and init."""
 
@@ -67,11 +93,31 @@ class MultiheadAttention(nn.Module):
         nn.init.xavier_normal_(self.keyProject.weight)
         nn.init.xavier_normal_(self.valueProject.weight)
 
+    def _join_storage(self):
+        """Re-home keyProject's and valueProject's weights (and biases) as the two halves of one
+        buffer each, so the stacked operand of the projection GEMM is a view, not a per-step cat.
+        The parameters stay the reference's (names, shapes, values, state_dict); only their storage
+        moves.  Done on first use and again if something (``.to()``) has separated them."""
+        kp, vp = self.keyProject, self.valueProject
+        with torch.no_grad():
+            for name in ("weight", "bias"):
+                a, b = getattr(kp, name), getattr(vp, name)
+                buf = torch.cat([a.detach(), b.detach()], 0)
+                a.data = buf[:a.shape[0]]
+                b.data = buf[a.shape[0]:]
+
     def fused_weight(self):
-        """[keyProject; valueProject] stacked for the single projection GEMM."""
-        w = torch.cat([self.keyProject.weight, self.valueProject.weight], 0)
-        b = torch.cat([self.keyProject.bias, self.valueProject.bias], 0)
-        return w, b
+        """[keyProject; valueProject] stacked for the single projection GEMM (weights and biases):
+        views of the joined storage, so no copy per step."""
+        kp, vp = self.keyProject, self.valueProject
+        jw, jb = _joined_view(kp.weight, vp.weight), _joined_view(kp.bias, vp.bias)
+        if jw is None or jb is None:
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                # never re-home storage inside a captured graph: stack by copy
+                return (torch.cat([kp.weight, vp.weight], 0), torch.cat([kp.bias, vp.bias], 0))
+            self._join_storage()
+            jw, jb = _joined_view(kp.weight, vp.weight), _joined_view(kp.bias, vp.bias)
+        return _Joined.apply(kp.weight, vp.weight, jw), _Joined.apply(kp.bias, vp.bias, jb)
 
     def forward(self, hidden_states, attention_mask=None):
         """hidden_states [N, L, D]; attention_mask: the pairwise [N, 1, L, L] mask built by

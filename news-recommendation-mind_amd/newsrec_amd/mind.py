@@ -244,6 +244,12 @@ class MINDStore:
                   "label": ((B,), torch.int64)}
         if out is None:
             x = {k: torch.empty(sh, dtype=dt, device=dev) for k, (sh, dt) in shapes.items()}
+            # candidate and history titles back to back (one buffer each for tokens and masks): the
+            # two-tower encoder reads them as one [B*(C+NH), Ls] batch without stacking them
+            for a, b in (("cdd_encoded_index", "his_encoded_index"), ("cdd_attn_mask", "his_attn_mask")):
+                buf = torch.empty(B * (C + NH) * Ls, dtype=torch.int64, device=dev)
+                x[a] = buf[:B * C * Ls].view(B, C, Ls)
+                x[b] = buf[B * C * Ls:].view(B, NH, Ls)
         else:
             x = out
             for k, (sh, dt) in shapes.items():

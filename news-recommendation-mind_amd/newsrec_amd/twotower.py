@@ -14,6 +14,7 @@ from torch import nn
 
 from . import _lib as L
 from . import kernels as K
+from .attention import _joined_view
 from .functions import ScoreFn
 
 
@@ -150,9 +151,16 @@ class TwoTower(TwoTowerBaseModel):
         his_t = x["his_encoded_index"].to(dev, non_blocking=True)
         B, C, Lq = cdd_t.shape
         N = his_t.shape[1]
-        tokens = torch.cat([cdd_t.reshape(B * C, Lq), his_t.reshape(B * N, Lq)], 0)
-        masks = torch.cat([x["cdd_attn_mask"].to(dev, non_blocking=True).reshape(B * C, Lq),
-                           x["his_attn_mask"].to(dev, non_blocking=True).reshape(B * N, Lq)], 0)
+        cdd_m = x["cdd_attn_mask"].to(dev, non_blocking=True)
+        his_m = x["his_attn_mask"].to(dev, non_blocking=True)
+        # one encoder pass over candidates + history: the device batch former lays both out back to
+        # back (joined views, no copy); other callers' batches are stacked
+        tokens = _joined_view(cdd_t.reshape(B * C, Lq), his_t.reshape(B * N, Lq))
+        if tokens is None:
+            tokens = torch.cat([cdd_t.reshape(B * C, Lq), his_t.reshape(B * N, Lq)], 0)
+        masks = _joined_view(cdd_m.reshape(B * C, Lq), his_m.reshape(B * N, Lq))
+        if masks is None:
+            masks = torch.cat([cdd_m.reshape(B * C, Lq), his_m.reshape(B * N, Lq)], 0)
         news = self.encoderN.encode_tokens(self.embedding.table, tokens, masks)[1]
         cdd = news[:B * C].reshape(B, C, -1)
         his = news[B * C:].reshape(B, N, -1)
