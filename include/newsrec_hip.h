@@ -259,10 +259,11 @@ int nr_attn_pool_bwd(const float* x, int64_t ldx, const float* key, int64_t ldk,
                      float* dgamma, float* dbeta, hipStream_t stream);
 
 /* Learned-query pooling without LayerNorm / dropout, one wave per sequence (rows as coalesced float4
- * segments, per-row dot products as wave reductions, no LDS staging):
+ * segments, per-row dot products as wave reductions, no LDS staging), or one workgroup per sequence
+ * (rows split over its 8 waves) for D > 256 or fewer than 1024 sequences:
  *   out[s] = Σ_l XSoftmax(scale * q·K_l, mask)_l X_l,  K = key rows, or X when key == NULL.
  * Replaces CNN_Encoder's pooling (CNN.py:46, key = tanh(W c + b)) and Attention_Pooling
- * (Pooling.py:22-24).  D <= 256, L <= 64; the row matrices (x, key, out, dx, dk, dz) 16-B aligned with
+ * (Pooling.py:22-24).  D <= 512, L <= 64; the row matrices (x, key, out, dx, dk, dz) 16-B aligned with
  * ld % 4 == 0 and ld >= D; q (and each dout row) hold qn <= D valid floats, any alignment, features
  * past qn taken as zero (a zero-padded row width D > qn then pools exact zeros there).  Saves
  * probs [nseq*L]. */

@@ -221,12 +221,169 @@ __global__ __launch_bounds__(64 * SP_WAVES) void seq_pool_bwd_kernel(SeqPoolArgs
   }
 }
 
+// ---- workgroup per sequence (L <= 64, D <= 64 * 4 * NF)
+constexpr int WG_WAVES = 8;
+constexpr int WG_RPW = 64 / WG_WAVES;   // rows per wave
+
+template <int NF>
+__global__ __launch_bounds__(64 * WG_WAVES) void seq_pool_wg_fwd_kernel(SeqPoolArgs g) {
+  __shared__ float sc[64];
+  __shared__ float4 red[WG_WAVES][64 * NF];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t seq = blockIdx.x;
+  const float* xb = g.x + seq * g.L * g.ldx;
+  const float* kb = g.key ? g.key + seq * g.L * g.ldk : xb;
+  const int64_t ldk = g.key ? g.ldk : g.ldx;
+  float4 qv[NF], kv[WG_RPW][NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) qv[f] = ldv(g.q, lane + 64 * f, g.qn);
+#pragma unroll
+  for (int k = 0; k < WG_RPW; ++k) {
+    const int l = w + WG_WAVES * k, lc = l < g.L ? l : g.L - 1;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) kv[k][f] = ld4(kb + lc * ldk, lane + 64 * f, g.D);
+  }
+#pragma unroll
+  for (int k = 0; k < WG_RPW; ++k) {
+    float d = 0.f;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) d += dot4(qv[f], kv[k][f]);
+    d = nr_wave_sum(d);
+    const int l = w + WG_WAVES * k;
+    if (lane == 0 && l < g.L) sc[l] = d * g.scale;
+  }
+  __syncthreads();
+  // softmax (every wave, lane l = row l) with XSoftmax's mask semantics
+  const bool keep = lane < g.L && nr_mask_at(g.mask, g.mask_dt, seq * g.L + lane);
+  const float v = keep ? sc[lane] : -INFINITY;
+  const float mx = nr_wave_max(v);
+  const float e = keep ? __expf(v - mx) : 0.f;
+  const float sum = nr_wave_sum(e);
+  const float p = sum > 0.f ? e / sum : 0.f;
+  if (w == 0 && lane < g.L) g.probs[seq * g.L + lane] = p;
+  float4 acc[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) acc[f] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < WG_RPW; ++k) {
+    const int l = w + WG_WAVES * k, lc = l < g.L ? l : g.L - 1;
+    const float pl = __shfl(p, l & 63, 64);   // 0 for l >= L (lane l has p = 0 there)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const float4 xv = g.key ? ld4(xb + lc * g.ldx, lane + 64 * f, g.D) : kv[k][f];
+      acc[f].x = fmaf(pl, xv.x, acc[f].x); acc[f].y = fmaf(pl, xv.y, acc[f].y);
+      acc[f].z = fmaf(pl, xv.z, acc[f].z); acc[f].w = fmaf(pl, xv.w, acc[f].w);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) red[w][lane + 64 * f] = acc[f];
+  __syncthreads();
+  for (int j = threadIdx.x; j < 64 * NF && 4 * j < g.D; j += 64 * WG_WAVES) {
+    float4 t = red[0][j];
+#pragma unroll
+    for (int ww = 1; ww < WG_WAVES; ++ww) {
+      const float4 u = red[ww][j];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    st4(g.out + seq * g.ldo, j, g.D, t);
+  }
+}
+
+template <int NF>
+__global__ __launch_bounds__(64 * WG_WAVES) void seq_pool_wg_bwd_kernel(SeqPoolArgs g) {
+  __shared__ float dps[64];
+  __shared__ float4 red[WG_WAVES][64 * NF];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t seq = blockIdx.x;
+  const float* xb = g.x + seq * g.L * g.ldx;
+  const float* kb = g.key ? g.key + seq * g.L * g.ldk : xb;
+  const int64_t ldk = g.key ? g.ldk : g.ldx;
+  float4 qv[NF], dov[NF], xv[WG_RPW][NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    qv[f] = ldv(g.q, lane + 64 * f, g.qn);
+    dov[f] = ldv(g.dout + seq * g.lddo, lane + 64 * f, g.qn);
+  }
+  const float pme = lane < g.L ? g.probs[seq * g.L + lane] : 0.f;   // lane l: p_l
+#pragma unroll
+  for (int k = 0; k < WG_RPW; ++k) {
+    const int l = w + WG_WAVES * k, lc = l < g.L ? l : g.L - 1;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) xv[k][f] = ld4(xb + lc * g.ldx, lane + 64 * f, g.D);
+  }
+  // dp_l = dout · X_l
+#pragma unroll
+  for (int k = 0; k < WG_RPW; ++k) {
+    float d = 0.f;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) d += dot4(dov[f], xv[k][f]);
+    d = nr_wave_sum(d);
+    const int l = w + WG_WAVES * k;
+    if (lane == 0 && l < g.L) dps[l] = d;
+  }
+  __syncthreads();
+  const float dpme = lane < g.L ? dps[lane] : 0.f;
+  const float r = nr_wave_sum(pme * dpme);
+  float4 dqa[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) dqa[f] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < WG_RPW; ++k) {
+    const int l = w + WG_WAVES * k;
+    const float pl = __shfl(pme, l & 63, 64), dpl = __shfl(dpme, l & 63, 64);
+    if (l >= g.L) continue;   // wave-uniform
+    const float ds = pl * (dpl - r) * g.scale;
+    const int64_t row = seq * g.L + l;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int j = lane + 64 * f;
+      const float4 kv = g.key ? ld4(kb + l * ldk, j, g.D) : xv[k][f];
+      dqa[f].x = fmaf(ds, kv.x, dqa[f].x); dqa[f].y = fmaf(ds, kv.y, dqa[f].y);
+      dqa[f].z = fmaf(ds, kv.z, dqa[f].z); dqa[f].w = fmaf(ds, kv.w, dqa[f].w);
+      const float4 zv = g.dz ? ld4(g.dz + row * g.lddz, j, g.D) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 dxv = make_float4(fmaf(pl, dov[f].x, zv.x), fmaf(pl, dov[f].y, zv.y), fmaf(pl, dov[f].z, zv.z),
+                               fmaf(pl, dov[f].w, zv.w));
+      if (g.key) {
+        float4 dkv = make_float4(ds * qv[f].x, ds * qv[f].y, ds * qv[f].z, ds * qv[f].w);
+        if (g.key_tanh) {
+          dkv.x *= 1.f - kv.x * kv.x; dkv.y *= 1.f - kv.y * kv.y;
+          dkv.z *= 1.f - kv.z * kv.z; dkv.w *= 1.f - kv.w * kv.w;
+        }
+        if (4 * j < g.D) st4(g.dk + row * g.lddk, j, g.D, dkv);
+      } else {
+        dxv.x = fmaf(ds, qv[f].x, dxv.x); dxv.y = fmaf(ds, qv[f].y, dxv.y);
+        dxv.z = fmaf(ds, qv[f].z, dxv.z); dxv.w = fmaf(ds, qv[f].w, dxv.w);
+      }
+      if (4 * j < g.D) st4(g.dx + row * g.lddx, j, g.D, dxv);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) red[w][lane + 64 * f] = dqa[f];
+  __syncthreads();
+  for (int j = threadIdx.x; j < 64 * NF && 4 * j < g.qn; j += 64 * WG_WAVES) {
+    float4 t = red[0][j];
+#pragma unroll
+    for (int ww = 1; ww < WG_WAVES; ++ww) {
+      const float4 u = red[ww][j];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    const float e4[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (4 * j + u < g.qn) atomicAdd(&g.dq[4 * j + u], e4[u]);
+  }
+}
+
+// the workgroup form for long features (D > 256) or few sequences (< 4 waves per CU of the
+// wave-per-sequence form)
+bool use_wg(int64_t nseq, int D) { return D > 256 || nseq < 1024; }
+
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 int64_t r4(int D) { return (D + 3) & ~3; }
 
 bool shape_ok(int L, int D, int qn, int64_t ldx, int64_t ldk, const void* x, const void* key) {
-  return L >= 1 && L <= 64 && D >= 1 && D <= 256 && qn >= 1 && qn <= D && ldx >= r4(D) && (ldx & 3) == 0 && al16(x) &&
+  return L >= 1 && L <= 64 && D >= 1 && D <= 512 && qn >= 1 && qn <= D && ldx >= r4(D) && (ldx & 3) == 0 && al16(x) &&
          (!key || ((ldk & 3) == 0 && ldk >= r4(D) && al16(key)));
 }
 
@@ -242,6 +399,14 @@ extern "C" int nr_seq_pool_fwd(const float* x, int64_t ldx, const float* key, in
   SeqPoolArgs g{};
   g.x = x; g.ldx = ldx; g.key = key; g.ldk = ldk; g.q = q; g.mask = mask; g.mask_dt = mask_dtype;
   g.nseq = nseq; g.L = L; g.D = D; g.qn = qn; g.scale = scale; g.out = out; g.ldo = ldo; g.probs = probs;
+  if (use_wg(nseq, D)) {
+    if (D <= 256)
+      hipLaunchKernelGGL(seq_pool_wg_fwd_kernel<1>, dim3((unsigned)nseq), dim3(64 * WG_WAVES), 0, stream, g);
+    else
+      hipLaunchKernelGGL(seq_pool_wg_fwd_kernel<2>, dim3((unsigned)nseq), dim3(64 * WG_WAVES), 0, stream, g);
+    NR_LAUNCH_CHECK();
+    return NR_OK;
+  }
   const dim3 grid((unsigned)((nseq + SP_WAVES - 1) / SP_WAVES));
   if (L <= 32)
     hipLaunchKernelGGL(seq_pool_fwd_kernel<32>, grid, dim3(64 * SP_WAVES), 0, stream, g);
@@ -267,6 +432,14 @@ extern "C" int nr_seq_pool_bwd(const float* x, int64_t ldx, const float* key, in
   g.nseq = nseq; g.L = L; g.D = D; g.qn = qn; g.scale = scale; g.probs = const_cast<float*>(probs);
   g.dout = dout; g.lddo = lddo; g.dz = dz; g.lddz = lddz; g.dx = dx; g.lddx = lddx; g.dk = dk; g.lddk = lddk;
   g.key_tanh = key_tanh; g.dq = dq;
+  if (use_wg(nseq, D)) {
+    if (D <= 256)
+      hipLaunchKernelGGL(seq_pool_wg_bwd_kernel<1>, dim3((unsigned)nseq), dim3(64 * WG_WAVES), 0, stream, g);
+    else
+      hipLaunchKernelGGL(seq_pool_wg_bwd_kernel<2>, dim3((unsigned)nseq), dim3(64 * WG_WAVES), 0, stream, g);
+    NR_LAUNCH_CHECK();
+    return NR_OK;
+  }
   int64_t blocks = (nseq + SP_WAVES - 1) / SP_WAVES;
   if (blocks > 1024) blocks = 1024;   // dq: one atomic per feature per workgroup
   if (L <= 32)

@@ -313,7 +313,7 @@ def attn_pool_bwd(x, q, mask, nseq, seq_len, probs, dout, dx, dq, key=None, dk=N
 
 
 def seq_pool_supported(D, L):
-    return 1 <= D <= 256 and 1 <= L <= 64
+    return 1 <= D <= 512 and 1 <= L <= 64
 
 
 def _sp_rows(t, rows, D, name):
@@ -334,7 +334,7 @@ def seq_pool_fwd(x, q, mask, nseq, seq_len, D, out, probs, key=None, scale=None,
     _f32(x, q, out, probs, key)
     qn = D if qn is None else qn
     if not seq_pool_supported(D, seq_len):
-        raise L.HipError("seq_pool: D <= 256, L <= 64 required (D=%d, L=%d)" % (D, seq_len))
+        raise L.HipError("seq_pool: D <= 512, L <= 64 required (D=%d, L=%d)" % (D, seq_len))
     _sp_rows(x, nseq * seq_len, D, "seq_pool x")
     _sp_rows(key, nseq * seq_len, D, "seq_pool key")
     _sp_rows(out, nseq, D, "seq_pool out")
@@ -353,7 +353,7 @@ def seq_pool_bwd(x, q, mask, nseq, seq_len, D, probs, dout, dx, dq, key=None, dk
     _f32(x, q, probs, dout, dx, dq, key, dk, dz)
     qn = D if qn is None else qn
     if not seq_pool_supported(D, seq_len):
-        raise L.HipError("seq_pool: D <= 256, L <= 64 required (D=%d, L=%d)" % (D, seq_len))
+        raise L.HipError("seq_pool: D <= 512, L <= 64 required (D=%d, L=%d)" % (D, seq_len))
     for t, r, n in ((x, nseq * seq_len, "x"), (key, nseq * seq_len, "key"), (dk, nseq * seq_len, "dk"),
                     (dx, nseq * seq_len, "dx"), (dz, nseq * seq_len, "dz")):
         _sp_rows(t, r, D, "seq_pool_bwd " + n)

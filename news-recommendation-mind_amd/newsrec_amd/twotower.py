@@ -162,6 +162,9 @@ class TwoTower(TwoTowerBaseModel):
         if masks is None:
             masks = torch.cat([cdd_m.reshape(B * C, Lq), his_m.reshape(B * N, Lq)], 0)
         news = self.encoderN.encode_tokens(self.embedding.table, tokens, masks)[1]
-        cdd = news[:B * C].reshape(B, C, -1)
-        his = news[B * C:].reshape(B, N, -1)
+        # split, not two slices: the backward joins the two gradients with one copy (two slices'
+        # backwards would zero-fill and copy a full-size gradient each, then add them)
+        cdd, his = torch.split(news, [B * C, B * N])
+        cdd = cdd.reshape(B, C, -1)
+        his = his.reshape(B, N, -1)
         return cdd, self._user_from_his(his, x), None

@@ -76,7 +76,9 @@ def _worker(rank, world, port, q):
     _grads(model, x, use_hook=True)
     scale = sync()
     sync.close()
-    q.put((rank, scale, {n: (p.grad * scale).clone() for n, p in model.named_parameters()}))
+    # numpy copies travel by value: a tensor would be shared through a file descriptor that the
+    # parent can only fetch while this process is still alive
+    q.put((rank, scale, {n: (p.grad * scale).numpy().copy() for n, p in model.named_parameters()}))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -102,7 +104,7 @@ def test_grad_sync_mean_gloo_world2():
     for rank, scale, g in res:
         assert scale == 0.5
         for n in want:
-            torch.testing.assert_close(g[n], want[n], rtol=1e-6, atol=1e-6)
+            torch.testing.assert_close(torch.from_numpy(g[n]), want[n], rtol=1e-6, atol=1e-6)
 
 
 def test_shard_train_matches_distributed_sampler():
