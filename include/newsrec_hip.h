@@ -203,14 +203,18 @@ int nr_mha_attn_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v
  * (training: lets nr_mha_pool_bwd skip the attention recompute).
  * yrows (optional): token t reads projection row yrows[t] (distinct-row projections).
  * rng (optional, all dropout entries): the dropout key comes from the device pair
- * (rng[0], rng[1] + offset) instead of (seed, offset), so a replayed graph draws new masks. */
+ * (rng[0], rng[1] + offset) instead of (seed, offset), so a replayed graph draws new masks.
+ * prec (enum nr_gemm_precision, fwd and bwd): the arithmetic of the attention products (S = K Kᵀ,
+ * O = P V and their backward) -- NR_GEMM_F32 exact fp32 MFMA products, NR_GEMM_BF16X6 the
+ * fp32-class six-product bf16 form in the forward and exact fp32 products in the backward (faster
+ * there), NR_GEMM_BF16 one bf16 product; softmax, LayerNorm and pooling stay fp32 in every mode. */
 int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,
                     int32_t mask_dtype, int64_t nseq,
                     int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
                     const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset,
                     const uint64_t* rng, const float* q, float* news, int64_t ldn, float* zout,
                     int64_t ldz, float* oout, int64_t ldo, float* stats, float* probs,
-                    hipStream_t stream);
+                    int32_t prec, hipStream_t stream);
 
 /* Backward of nr_mha_pool_fwd: writes dy [T][heads*(dk+dv)] and ATOMICALLY ACCUMULATES dbias
  * (= column sums of dy), dq, dgamma, dbeta (caller zeroes).  dy stays per token (row t) when
@@ -226,7 +230,8 @@ int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const voi
                     const float* dnews,
                     int64_t ldn, const float* dz, int64_t lddz, const float* o, int64_t ldo,
                     float* dob, int64_t lddob, float* dy, int64_t lddy,
-                    float* dbias, float* dq, float* dgamma, float* dbeta, hipStream_t stream);
+                    float* dbias, float* dq, float* dgamma, float* dbeta, int32_t prec,
+                    hipStream_t stream);
 
 /* ------------------------------------------------------------------ pooling */
 

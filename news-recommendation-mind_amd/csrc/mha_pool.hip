@@ -24,9 +24,67 @@
 #include "../../include/newsrec_hip.h"
 #include <stdlib.h>
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+#include "gemm_fast_common.h"   // bf16 split helpers (nrfast::split2 / pk_bf16), f32x16, bf16x8
 
 namespace {
+
+// ---- Attention products in the caller's GEMM arithmetic (MPArgs::np, from nr_gemm_precision):
+// NP = 0: v_mfma_f32_32x32x2_f32 (exact fp32 products); NP = 3: bf16x6 (three bf16 terms per fp32
+// value, six v_mfma_f32_32x32x16_bf16 products -- the GEMMs' fp32-class arithmetic at 2.7x the f32
+// MFMA's rate here); NP = 1: bf16 (one product).  A 32x32x16 bf16 operand gives lane (c, h) eight
+// k-slots 8h .. 8h + 7; every product below feeds the lane eight consecutive values of a register
+// array it already holds in the f32 form's k order, so the C layouts are the f32 form's.
+template <int NP>
+struct Planes {
+  bf16x8 v[NP];
+};
+
+template <int NP>
+__device__ __forceinline__ Planes<NP> planes8(const float* x) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  uint32_t h[4], m[4], l[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    if constexpr (NP == 1) {
+      h[u] = nrfast::pk_bf16(x[2 * u], x[2 * u + 1]);
+    } else {
+      nrfast::split2(x[2 * u], x[2 * u + 1], h[u], m[u], l[u]);
+    }
+  }
+  Planes<NP> r;
+  r.v[0] = __builtin_bit_cast(bf16x8, (u32x4){h[0], h[1], h[2], h[3]});
+  if constexpr (NP == 3) {
+    r.v[1] = __builtin_bit_cast(bf16x8, (u32x4){m[0], m[1], m[2], m[3]});
+    r.v[2] = __builtin_bit_cast(bf16x8, (u32x4){l[0], l[1], l[2], l[3]});
+  }
+  return r;
+}
+
+// acc += A B over one 16-deep step (smallest terms first)
+template <int NP>
+__device__ __forceinline__ void mfma_x(f32x16& acc, const Planes<NP>& a, const Planes<NP>& b) {
+  if constexpr (NP == 3) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v[2], b.v[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v[1], b.v[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v[0], b.v[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v[1], b.v[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v[0], b.v[1], acc, 0, 0, 0);
+  }
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v[0], b.v[0], acc, 0, 0, 0);
+}
+
+// acc += Σ_s A[s] B[s] over 16 register values per lane (the f32 form's 16 k-steps of 32x32x2):
+// two bf16 steps of eight values each
+template <int NP>
+__device__ __forceinline__ void mfma16(f32x16& acc, const float* a, const float* b) {
+  if constexpr (NP == 0) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) mfma_x<NP>(acc, planes8<NP>(a + 8 * m), planes8<NP>(b + 8 * m));
+  }
+}
 
 // row of accumulator register r in lane half h (32x32 C/D layout)
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
@@ -59,6 +117,7 @@ struct MPArgs {
   float* o; int64_t ldo;              // fwd: optional saved attention output O (pre-LN); bwd: its input
   float* dob; int64_t lddob;          // split bwd: dO rows (kernel 1 writes, kernel 2 reads)
   int rows_per_wave;                  // staged row indices per wave (split bwd kernel 2) or per block
+  int np;                             // attention products: 0 = f32 MFMA, 3 = bf16x6, 1 = bf16
 };
 
 // Projection rows of the workgroup's title are staged once per title as 32-bit BYTE offsets
@@ -103,11 +162,24 @@ __device__ __forceinline__ uint64_t token_bits(const MPArgs& g, int64_t seq) {
 }
 
 // Loads this lane's half of key row c = lane & 31 for one head (see below for the order).
-template <int DK>
+template <int DK, int NP>
 __device__ __forceinline__ void load_krow(const MPArgs& g, int64_t seq, int head, float (&a)[DK / 2]) {
   const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
   constexpr int HK = DK / 2;
-  {
+  if constexpr (NP > 0) {
+    // bf16 steps: a[8t + u] = K[c][16t + 8h + u] (step t's eight k-slots of this lane half)
+    const bool ok = c < g.L;
+    const float* kr = yrow(g, ok ? c : 0) + head * DK + 8 * h;
+#pragma unroll
+    for (int t = 0; t < DK / 16; ++t) {
+#pragma unroll
+      for (int q4 = 0; q4 < 2; ++q4) {
+        const float4 v = *reinterpret_cast<const float4*>(kr + 16 * t + 4 * q4);
+        float* d = a + 8 * t + 4 * q4;
+        d[0] = ok ? v.x : 0.f; d[1] = ok ? v.y : 0.f; d[2] = ok ? v.z : 0.f; d[3] = ok ? v.w : 0.f;
+      }
+    }
+  } else {
     // lane (c, h) takes the 16-B chunks 2*s4 + h of row c: the two halves of the wave read the
     // two halves of the same 32-B span (the k order inside S = K Kᵀ is free).  Rows past L are
     // clamped and zeroed by a select, never a branch: a branch around a load makes hipcc wait
@@ -124,7 +196,7 @@ __device__ __forceinline__ void load_krow(const MPArgs& g, int64_t seq, int head
 
 // S and P of one head for this lane's row c = lane & 31 from its key half-row a[];
 // returns P in p[16] (C layout).
-template <int DK>
+template <int DK, int NP>
 __device__ __forceinline__ void head_probs_from(const MPArgs& g, uint64_t bits, const float (&a)[DK / 2],
                                                 float (&p)[16]) {
   const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
@@ -132,8 +204,16 @@ __device__ __forceinline__ void head_probs_from(const MPArgs& g, uint64_t bits, 
   f32x16 S;
 #pragma unroll
   for (int r = 0; r < 16; ++r) S[r] = 0.f;
+  if constexpr (NP == 0) {
 #pragma unroll
-  for (int s = 0; s < HK; ++s) S = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], a[s], S, 0, 0, 0);
+    for (int s = 0; s < HK; ++s) S = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], a[s], S, 0, 0, 0);
+  } else {   // K is both operands: the lane's own key chunk, split once
+#pragma unroll
+    for (int t = 0; t < DK / 16; ++t) {
+      const Planes<NP> pk = planes8<NP>(a + 8 * t);
+      mfma_x<NP>(S, pk, pk);
+    }
+  }
   const bool mj = (bits >> c) & 1ull;
   float mx = -INFINITY;
 #pragma unroll
@@ -156,11 +236,11 @@ __device__ __forceinline__ void head_probs_from(const MPArgs& g, uint64_t bits, 
   for (int r = 0; r < 16; ++r) p[r] *= inv;
 }
 
-template <int DK>
+template <int DK, int NP>
 __device__ __forceinline__ void head_probs(const MPArgs& g, int64_t seq, int head, uint64_t bits, float (&p)[16]) {
   float a[DK / 2];
-  load_krow<DK>(g, seq, head, a);
-  head_probs_from<DK>(g, bits, a, p);
+  load_krow<DK, NP>(g, seq, head, a);
+  head_probs_from<DK, NP>(g, bits, a, p);
 }
 
 // V operand of O = P V: lane (c, h) needs V[crow(s, h)][vb*32 + c] (rows past L -> 0)
@@ -179,7 +259,7 @@ __device__ __forceinline__ void load_vop(const MPArgs& g, int64_t seq, int head,
 }
 
 // O_h = P V_h into the LDS image os[32][so] at columns head*DV ..
-template <int DK, int DV>
+template <int DK, int DV, int NP>
 __device__ __forceinline__ void head_out(const float (&bv)[DV / 2], int head, const float (&p)[16], float* os,
                                          int so) {
   const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
@@ -188,28 +268,27 @@ __device__ __forceinline__ void head_out(const float (&bv)[DV / 2], int head, co
     f32x16 O;
 #pragma unroll
     for (int r = 0; r < 16; ++r) O[r] = 0.f;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) O = __builtin_amdgcn_mfma_f32_32x32x2f32(p[s], bv[vb * 16 + s], O, 0, 0, 0);
+    mfma16<NP>(O, p, bv + vb * 16);
 #pragma unroll
     for (int r = 0; r < 16; ++r) os[crow(r, h) * so + head * DV + vb * 32 + c] = O[r];
   }
 }
 
-template <int DK, int DV>
+template <int DK, int DV, int NP>
 __device__ void attention_to_lds(const MPArgs& g, int64_t seq, uint64_t bits, float* os, int so) {
   const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int head = w; head < g.heads; head += nw) {
     // issue the key and value loads together: one memory latency per head, not two
     float a[DK / 2], bv[DV / 2];
-    load_krow<DK>(g, seq, head, a);
+    load_krow<DK, NP>(g, seq, head, a);
     load_vop<DK, DV>(g, seq, head, bv);
     float p[16];
-    head_probs_from<DK>(g, bits, a, p);
-    head_out<DK, DV>(bv, head, p, os, so);
+    head_probs_from<DK, NP>(g, bits, a, p);
+    head_out<DK, DV, NP>(bv, head, p, os, so);
   }
 }
 
-template <int DK, int DV, int NH64>
+template <int DK, int DV, int NH64, int NP>
 __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
   if (g.rng) g.dkey = nr_dropout_key(g.rng[0], g.rng[1] + g.offset);   // graph-replay RNG
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -228,7 +307,7 @@ __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
     qv[k] = g.q[lane + 64 * k];
   }
   stage_rows(g, seq);
-  if (!(g.dbg & 1)) attention_to_lds<DK, DV>(g, seq, bits, os, SO);
+  if (!(g.dbg & 1)) attention_to_lds<DK, DV, NP>(g, seq, bits, os, SO);
   __syncthreads();
   if (g.dbg & 2) return;
   // LayerNorm + dropout in place, scores; one wave per row
@@ -408,14 +487,14 @@ struct DoSource {
 // stage_rows*): recompute P from the key rows, dV = Pᵀ dO, dPᵀ = V dOᵀ, dS (XSoftmax
 // backward), W = dS + dSᵀ (tied Q = K), dK = W K; dV / dK rows to dy, their column sums added
 // to cs[] (dbias: cs[vb] for the value columns, cs[DV/32 + kb] for the key columns).
-template <int DK, int DV>
+template <int DK, int DV, int NP>
 __device__ __forceinline__ void head_bwd(const MPArgs& g, int64_t seq, int head, uint64_t bits, float* tw,
                                          const DoSource<DV>& dO, float (&cs)[DV / 32 + DK / 32]) {
   const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
   const int nq = g.heads * DK;
   float* dyt = g.dy + seq * g.L * g.lddy;   // the title's dy rows (wave-uniform base)
   float p[16];
-  head_probs<DK>(g, seq, head, bits, p);
+  head_probs<DK, NP>(g, seq, head, bits, p);
   // phase fences: keep each phase's loads inside it (hoisting them all to the top costs more
   // registers than the latency they would hide; the split kernel runs 4 waves per SIMD)
   __builtin_amdgcn_sched_barrier(0);
@@ -436,8 +515,7 @@ __device__ __forceinline__ void head_bwd(const MPArgs& g, int64_t seq, int head,
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-      for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pt[s], bo[s], acc, 0, 0, 0);
+      mfma16<NP>(acc, pt, bo);
       float sum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -457,16 +535,33 @@ __device__ __forceinline__ void head_bwd(const MPArgs& g, int64_t seq, int head,
     for (int r = 0; r < 16; ++r) dpt[r] = 0.f;
     constexpr int HV = DV / 2;
     const bool rv = c < g.L;
-    const float* vrr = yrow(g, rv ? c : 0) + nq + head * DV + 4 * h;   // clamp, zero by select
+    if constexpr (NP == 0) {
+      const float* vrr = yrow(g, rv ? c : 0) + nq + head * DV + 4 * h;   // clamp, zero by select
 #pragma unroll
-    for (int s = 0; s < HV; s += 4) {
-      float4 v4 = *reinterpret_cast<const float4*>(vrr + 2 * s);
-      if (!rv) v4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      const int col = 4 * h + 2 * s;
-      dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.x, dO.at(c, col), dpt, 0, 0, 0);
-      dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.y, dO.at(c, col + 1), dpt, 0, 0, 0);
-      dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.z, dO.at(c, col + 2), dpt, 0, 0, 0);
-      dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.w, dO.at(c, col + 3), dpt, 0, 0, 0);
+      for (int s = 0; s < HV; s += 4) {
+        float4 v4 = *reinterpret_cast<const float4*>(vrr + 2 * s);
+        if (!rv) v4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int col = 4 * h + 2 * s;
+        dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.x, dO.at(c, col), dpt, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.y, dO.at(c, col + 1), dpt, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.z, dO.at(c, col + 2), dpt, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x2f32(v4.w, dO.at(c, col + 3), dpt, 0, 0, 0);
+      }
+    } else {   // features 16t + 8h + u of V row c and dO row c
+      const float* vrr = yrow(g, rv ? c : 0) + nq + head * DV + 8 * h;
+#pragma unroll
+      for (int t = 0; t < DV / 16; ++t) {
+        float va[8], oa[8];
+#pragma unroll
+        for (int q4 = 0; q4 < 2; ++q4) {
+          const float4 v4 = *reinterpret_cast<const float4*>(vrr + 16 * t + 4 * q4);
+          va[4 * q4] = rv ? v4.x : 0.f; va[4 * q4 + 1] = rv ? v4.y : 0.f;
+          va[4 * q4 + 2] = rv ? v4.z : 0.f; va[4 * q4 + 3] = rv ? v4.w : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) oa[u] = dO.at(c, 16 * t + 8 * h + u);
+        mfma_x<NP>(dpt, planes8<NP>(va), planes8<NP>(oa));
+      }
     }
     float rs = 0.f;
 #pragma unroll
@@ -496,8 +591,7 @@ __device__ __forceinline__ void head_bwd(const MPArgs& g, int64_t seq, int head,
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(dsv[s], bk[s], acc, 0, 0, 0);
+    mfma16<NP>(acc, dsv, bk);
     float sum = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -526,7 +620,7 @@ __device__ __forceinline__ void flush_dbias(const MPArgs& g, int head, float (&c
 
 // Fused backward (no saved O): recompute the attention into LDS, pooling/LN backward in
 // place, then the attention backward of every head with dO from LDS.
-template <int DK, int DV, int NH64>
+template <int DK, int DV, int NH64, int NP>
 __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
   if (g.rng) g.dkey = nr_dropout_key(g.rng[0], g.rng[1] + g.offset);   // graph-replay RNG
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -544,7 +638,7 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
   const int tid = threadIdx.x, w = tid >> 6;
   const uint64_t bits = token_bits(g, seq);
   stage_rows(g, seq);
-  if (!(g.dbg & 1)) attention_to_lds<DK, DV>(g, seq, bits, os, SO);
+  if (!(g.dbg & 1)) attention_to_lds<DK, DV, NP>(g, seq, bits, os, SO);
   if (tid < 32) {
     ps[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
     st[2 * tid] = tid < g.L ? g.stats[2 * (seq * g.L + tid)] : 0.f;
@@ -559,7 +653,7 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
     float cs[DV / 32 + DK / 32];
 #pragma unroll
     for (int i = 0; i < DV / 32 + DK / 32; ++i) cs[i] = 0.f;
-    head_bwd<DK, DV>(g, seq, head, bits, tw, dO, cs);
+    head_bwd<DK, DV, NP>(g, seq, head, bits, tw, dO, cs);
     flush_dbias<DK, DV>(g, head, cs);
   }
 }
@@ -683,7 +777,7 @@ __global__ __launch_bounds__(256) void mha_ln_bwd_kernel(MPArgs g) {
 // projection-row indices in a private slice of LDS.
 constexpr int HB_TITLES = 1;
 
-template <int DK, int DV>
+template <int DK, int DV, int NP>
 __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -723,7 +817,7 @@ __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
     }
     wave_lds_fence();
     DoSource<DV> dO{dot, DV + 1, g.L, false};
-    head_bwd<DK, DV>(g, seq, head, bits, tw, dO, cs);
+    head_bwd<DK, DV, NP>(g, seq, head, bits, tw, dO, cs);
     wave_lds_fence();   // the next title's row indices / dO overwrite these
   }
   flush_dbias<DK, DV>(g, head, cs);
@@ -744,30 +838,38 @@ void allow_smem(K kern, size_t sz) {
   if (sz > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sz);
 }
 
-template <int DK, int DV, int NH64>
-int launch(const MPArgs& g, Pass pass, hipStream_t s) {
+template <int DK, int DV, int NH64, int NP>
+int launch_np(const MPArgs& g, Pass pass, hipStream_t s) {
   const int H = NH64 * 64;
   if (pass == FWD) {   // one wave per head (>= 4 waves for the LN phase)
     const int nw = g.heads < 4 ? 4 : g.heads;
     const size_t sz = fwd_smem(H);
-    allow_smem(mha_pool_fwd_kernel<DK, DV, NH64>, sz);
-    hipLaunchKernelGGL((mha_pool_fwd_kernel<DK, DV, NH64>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
+    allow_smem(mha_pool_fwd_kernel<DK, DV, NH64, NP>, sz);
+    hipLaunchKernelGGL((mha_pool_fwd_kernel<DK, DV, NH64, NP>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
   } else if (pass == BWD_FUSED) {
     // one wave per two heads (its per-head state needs ~200 VGPRs, more than a 12-wave
     // workgroup can give a wave)
     const int nw = (g.heads + 1) / 2 < 4 ? 4 : (g.heads + 1) / 2;
     const size_t sz = bwd_smem(H, nw);
-    allow_smem(mha_pool_bwd_kernel<DK, DV, NH64>, sz);
-    hipLaunchKernelGGL((mha_pool_bwd_kernel<DK, DV, NH64>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
+    allow_smem(mha_pool_bwd_kernel<DK, DV, NH64, NP>, sz);
+    hipLaunchKernelGGL((mha_pool_bwd_kernel<DK, DV, NH64, NP>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
   } else {
     hipLaunchKernelGGL((mha_ln_bwd_kernel<NH64>), dim3((unsigned)g.nseq), dim3(256), 0, s, g);
     MPArgs g2 = g;
     g2.rows_per_wave = 1;
     const unsigned gx = (unsigned)((g.nseq + HB_TITLES - 1) / HB_TITLES), gy = (unsigned)((g.heads + 3) / 4);
-    hipLaunchKernelGGL((mha_head_bwd_kernel<DK, DV>), dim3(gx, gy), dim3(256), head_bwd_smem(4, DV), s, g2);
+    hipLaunchKernelGGL((mha_head_bwd_kernel<DK, DV, NP>), dim3(gx, gy), dim3(256), head_bwd_smem(4, DV), s, g2);
   }
   NR_LAUNCH_CHECK();
   return NR_OK;
+}
+
+// the attention products' arithmetic follows the caller's GEMM precision (nr_gemm_precision)
+template <int DK, int DV, int NH64>
+int launch(const MPArgs& g, Pass pass, hipStream_t s) {
+  if (g.np == 3) return launch_np<DK, DV, NH64, 3>(g, pass, s);
+  if (g.np == 1) return launch_np<DK, DV, NH64, 1>(g, pass, s);
+  return launch_np<DK, DV, NH64, 0>(g, pass, s);
 }
 
 int dispatch(const MPArgs& g, int dk, int dv, Pass pass, hipStream_t s) {
@@ -793,8 +895,9 @@ extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows
                                int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
                                const float* beta, float eps, float p_drop, uint64_t seed, uint64_t offset, const uint64_t* rng,
                                const float* q, float* news, int64_t ldn, float* zout, int64_t ldz, float* oout,
-                               int64_t ldo, float* stats, float* probs, hipStream_t stream) {
+                               int64_t ldo, float* stats, float* probs, int32_t prec, hipStream_t stream) {
   if (L < 1 || L > 32 || heads < 1 || heads > 12) return NR_EINVAL(0);
+  if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(4);
   if (!y || !mask || !gamma || !beta || !q || !news || !stats || !probs) return NR_EINVAL(1);
   if ((ldy & 3) || !al16(y)) return NR_EINVAL(2);
   if (nseq == 0) return NR_OK;
@@ -806,6 +909,7 @@ extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows
   g.news = news; g.ldn = ldn; g.zout = zout; g.ldz = ldz; g.stats = stats; g.probs = probs;
   g.o = oout; g.ldo = ldo;
   if (oout && ((ldo & 3) || ldo < (int64_t)heads * dv)) return NR_EINVAL(3);
+  g.np = prec == NR_GEMM_BF16X6 ? 3 : prec == NR_GEMM_BF16 ? 1 : 0;
   {
     const char* e = getenv("NR_DEBUG_MHAPOOL");
     g.dbg = e ? atoi(e) : 0;
@@ -820,8 +924,9 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
                                const float* stats, const float* probs, const float* dnews, int64_t ldn,
                                const float* dz, int64_t lddz, const float* o, int64_t ldo, float* dob,
                                int64_t lddob, float* dy, int64_t lddy, float* dbias, float* dq, float* dgamma,
-                               float* dbeta, hipStream_t stream) {
+                               float* dbeta, int32_t prec, hipStream_t stream) {
   if (L < 1 || L > 32 || heads < 1 || heads > 12) return NR_EINVAL(0);
+  if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(4);
   if (!y || !mask || !gamma || !beta || !q || !stats || !probs || !dnews || !dy || !dbias || !dq || !dgamma ||
       !dbeta)
     return NR_EINVAL(1);
@@ -838,6 +943,10 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
   g.o = const_cast<float*>(o); g.ldo = ldo; g.dob = dob; g.lddob = lddob;
   if (o && (!dob || lddob < (int64_t)heads * dv || ldo < (int64_t)heads * dv || (ldo & 3) || !al16(o)))
     return NR_EINVAL(3);
+  // backward: the six-product form measured slower than exact f32 MFMA products here (the split
+  // VALU work lands on a latency-bound kernel: head pass 170 -> 189 us), so bf16x6 callers get the
+  // exact (more accurate) f32 products; bf16 callers get bf16
+  g.np = prec == NR_GEMM_BF16 ? 1 : 0;
   {
     const char* e = getenv("NR_DEBUG_MHAPOOL");
     g.dbg = e ? atoi(e) : 0;

@@ -526,10 +526,11 @@ def _yrows_ok(y, yrows, T, ncols, name):
 
 
 def mha_pool_fwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, news, stats, probs, eps=1e-5,
-                 p_drop=0.0, seed=0, offset=0, zout=None, yrows=None, rng=None, oout=None):
+                 p_drop=0.0, seed=0, offset=0, zout=None, yrows=None, rng=None, oout=None, prec=None):
     """Fused tied-QK attention + LayerNorm + dropout + query pooling per title.  ``yrows``:
     token t reads projection row yrows[t] (distinct-row projections).  ``rng``: int64 CUDA
-    (seed, offset base) read by the kernel (graph replays draw fresh masks)."""
+    (seed, offset base) read by the kernel (graph replays draw fresh masks).  ``prec``: the
+    attention products' arithmetic (default: this thread's GEMM precision)."""
     _rng_ok(rng)
     H = heads * dv
     _f32(y, gamma, beta, q, news, stats, probs, zout)
@@ -544,11 +545,12 @@ def mha_pool_fwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, news, st
     L.call("nr_mha_pool_fwd", L.ptr(y), y.stride(0), L.ptr(yrows), mp, mdt, nseq, seq_len, heads, dk, dv, L.ptr(gamma),
            L.ptr(beta), eps, p_drop, seed, offset, L.ptr(rng), L.ptr(q), L.ptr(news), news.stride(0), L.ptr(zout),
            zout.stride(0) if zout is not None else 0, L.ptr(oout), oout.stride(0) if oout is not None else 0,
-           L.ptr(stats), L.ptr(probs), L.stream_ptr(y))
+           L.ptr(stats), L.ptr(probs), _prec(prec), L.stream_ptr(y))
 
 
 def mha_pool_bwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, dbias, dq,
-                 dgamma, dbeta, p_drop=0.0, seed=0, offset=0, dz=None, yrows=None, rng=None, o=None, dob=None):
+                 dgamma, dbeta, p_drop=0.0, seed=0, offset=0, dz=None, yrows=None, rng=None, o=None, dob=None,
+                 prec=None):
     """``o`` (the forward's ``oout``) selects the split backward; ``dob`` [T, heads*dv] is its
     dO workspace."""
     _rng_ok(rng)
@@ -565,7 +567,7 @@ def mha_pool_bwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, stats, p
            L.ptr(beta), p_drop, seed, offset, L.ptr(rng), L.ptr(q), L.ptr(stats), L.ptr(probs), L.ptr(dnews), dnews.stride(0),
            L.ptr(dz), dz.stride(0) if dz is not None else 0, L.ptr(o), o.stride(0) if o is not None else 0,
            L.ptr(dob), dob.stride(0) if dob is not None else 0, L.ptr(dy), dy.stride(0), L.ptr(dbias), L.ptr(dq),
-           L.ptr(dgamma), L.ptr(dbeta), L.stream_ptr(y))
+           L.ptr(dgamma), L.ptr(dbeta), _prec(prec), L.stream_ptr(y))
 
 
 # ---------------------------------------------------------------------- BERT towers

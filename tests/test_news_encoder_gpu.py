@@ -23,8 +23,17 @@ def _params(g, E=768, H=384, dk=64):
     return {k: v.requires_grad_(True) for k, v in P.items()}
 
 
+@pytest.mark.parametrize("prec", ["f32", "bf16x6"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.2])
-def test_fused_mha_news_encoder(p_drop):
+def test_fused_mha_news_encoder(p_drop, prec):
+    """Under both fp32-class arithmetics of the projection GEMM and the attention products
+    (nr_mha_pool_* prec: exact f32 MFMA / six-product bf16)."""
+    from newsrec_amd import _lib as L
+    with K.gemm_precision(L.GEMM_F32 if prec == "f32" else L.GEMM_BF16X6):
+        _fused_mha_news_encoder(p_drop)
+
+
+def _fused_mha_news_encoder(p_drop):
     g = torch.Generator().manual_seed(11)
     V, E, H, n, Lq = 500, 768, 384, 37, 30
     table = torch.randn(V, E, generator=g, dtype=torch.float64).requires_grad_(True)
