@@ -221,7 +221,11 @@ int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows, const voi
  * yrows is given; rows of masked tokens are exactly zero.  With o (the forward's oout) the
  * backward runs split: a per-title pooling/LN pass writes dO into dob [T][heads*dv] (caller's
  * workspace), then a per-(title, head) attention pass at high occupancy; without o one fused
- * kernel recomputes the attention. */
+ * kernel recomputes the attention.
+ * ws (optional, split form only): ws_copies x ceil4(3*heads*dv + heads*(dk+dv)) floats, ZERO on entry
+ * and left zero on return -- workgroups spread their dgamma / dbeta / dq / dbias atomics over the
+ * copies (one address per title would serialise them at L2) and a last kernel adds the copy sums
+ * into the outputs. */
 int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,
                     int32_t mask_dtype, int64_t nseq,
                     int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
@@ -230,8 +234,8 @@ int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const voi
                     const float* dnews,
                     int64_t ldn, const float* dz, int64_t lddz, const float* o, int64_t ldo,
                     float* dob, int64_t lddob, float* dy, int64_t lddy,
-                    float* dbias, float* dq, float* dgamma, float* dbeta, int32_t prec,
-                    hipStream_t stream);
+                    float* dbias, float* dq, float* dgamma, float* dbeta, float* ws,
+                    int32_t ws_copies, int32_t prec, hipStream_t stream);
 
 /* ------------------------------------------------------------------ pooling */
 

@@ -113,12 +113,22 @@ struct MPArgs {
   const float* dz; int64_t lddz;      // bwd: optional grad of Z
   float* dy; int64_t lddy;            // bwd: [T][heads*dk + heads*dv]
   float* dbias; float* dq; float* dgamma; float* dbeta;
-  int dbg;                            // timing-only ablations (NR_DEBUG_MHAPOOL): 1 = skip attention, 2 = skip LN/pool
+  int dbg;                            // timing-only ablations (NR_DEBUG_MHAPOOL): 1 = skip attention, 2 = skip LN/pool,
+                                      // 8 / 16 = skip the LN-pass / head-pass parameter-gradient atomics
   float* o; int64_t ldo;              // fwd: optional saved attention output O (pre-LN); bwd: its input
   float* dob; int64_t lddob;          // split bwd: dO rows (kernel 1 writes, kernel 2 reads)
   int rows_per_wave;                  // staged row indices per wave (split bwd kernel 2) or per block
   int np;                             // attention products: 0 = f32 MFMA, 3 = bf16x6, 1 = bf16
+  float* ws; int ws_copies; int64_t ws_ld;   // split bwd: parameter-gradient copies (see nr_mha_pool_bwd)
 };
+
+// Parameter-gradient partials of the split backward: workgroup b adds into copy b % ws_copies of
+// [dgamma | dbeta | dq | dbias] instead of the single vectors -- 1,760 titles' atomics on the same
+// 2,304 addresses serialise at L2 (measured: ≈ 38 us of the backward); copies_reduce_kernel then
+// folds the copies into the outputs.
+__device__ __forceinline__ float* grad_slot(const MPArgs& g, int64_t col_in_ws) {
+  return g.ws + (int64_t)(blockIdx.x % g.ws_copies) * g.ws_ld + col_in_ws;
+}
 
 // Projection rows of the workgroup's title are staged once per title as 32-bit BYTE offsets
 // from y (yrows[token] * ldy * 4, or the token's own row) in the first 32 words of the dynamic
@@ -613,7 +623,7 @@ __device__ __forceinline__ void flush_dbias(const MPArgs& g, int head, float (&c
   for (int i = 0; i < DV / 32 + DK / 32; ++i) {
     const float v = cs[i] + __shfl_xor(cs[i], 32, 64);
     const int col = i < DV / 32 ? nq + head * DV + i * 32 + c : head * DK + (i - DV / 32) * 32 + c;
-    if (h == 0) atomicAdd(&g.dbias[col], v);
+    if (h == 0) atomicAdd(g.ws ? grad_slot(g, 3 * (int64_t)g.heads * DV + col) : &g.dbias[col], v);
     cs[i] = 0.f;
   }
 }
@@ -764,10 +774,14 @@ __global__ __launch_bounds__(256) void mha_ln_bwd_kernel(MPArgs g) {
     red[w][2][lane + 64 * k] = dqp[k];
   }
   __syncthreads();
+  if (g.dbg & 8) return;   // timing experiment only: no parameter-gradient atomics
+  float* ogam = g.ws ? grad_slot(g, 0) : g.dgamma;
+  float* obet = g.ws ? grad_slot(g, H) : g.dbeta;
+  float* oq = g.ws ? grad_slot(g, 2 * H) : g.dq;
   for (int d = tid; d < H; d += 256) {
-    atomicAdd(&g.dgamma[d], (red[0][0][d] + red[1][0][d]) + (red[2][0][d] + red[3][0][d]));
-    atomicAdd(&g.dbeta[d], (red[0][1][d] + red[1][1][d]) + (red[2][1][d] + red[3][1][d]));
-    atomicAdd(&g.dq[d], (red[0][2][d] + red[1][2][d]) + (red[2][2][d] + red[3][2][d]));
+    atomicAdd(&ogam[d], (red[0][0][d] + red[1][0][d]) + (red[2][0][d] + red[3][0][d]));
+    atomicAdd(&obet[d], (red[0][1][d] + red[1][1][d]) + (red[2][1][d] + red[3][1][d]));
+    atomicAdd(&oq[d], (red[0][2][d] + red[1][2][d]) + (red[2][2][d] + red[3][2][d]));
   }
 }
 
@@ -820,7 +834,27 @@ __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
     head_bwd<DK, DV, NP>(g, seq, head, bits, tw, dO, cs);
     wave_lds_fence();   // the next title's row indices / dO overwrite these
   }
-  flush_dbias<DK, DV>(g, head, cs);
+  if (!(g.dbg & 16)) flush_dbias<DK, DV>(g, head, cs);   // (bit 16: timing experiment only)
+}
+
+// out[i] += Σ_c ws[c][i] over the copies, each copy re-zeroed (the workspace is left zero for the
+// next call); columns [0,H) dgamma, [H,2H) dbeta, [2H,3H) dq, [3H, 3H+NY) dbias
+__global__ __launch_bounds__(64) void copies_reduce_kernel(MPArgs g, int H, int NY) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= 3 * H + NY) return;
+  float s = 0.f;
+  for (int c0 = 0; c0 < g.ws_copies; c0 += 16) {   // sixteen loads in flight, then the zero stores
+    float v[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) v[c] = c0 + c < g.ws_copies ? g.ws[(int64_t)(c0 + c) * g.ws_ld + i] : 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      s += v[c];
+      if (c0 + c < g.ws_copies) g.ws[(int64_t)(c0 + c) * g.ws_ld + i] = 0.f;
+    }
+  }
+  float* out = i < H ? g.dgamma + i : i < 2 * H ? g.dbeta + (i - H) : i < 3 * H ? g.dq + (i - 2 * H) : g.dbias + (i - 3 * H);
+  *out += s;
 }
 
 size_t fwd_smem(int H) { return (size_t)(32 + 32 * (H + 1) + 32) * sizeof(float); }
@@ -859,6 +893,10 @@ int launch_np(const MPArgs& g, Pass pass, hipStream_t s) {
     g2.rows_per_wave = 1;
     const unsigned gx = (unsigned)((g.nseq + HB_TITLES - 1) / HB_TITLES), gy = (unsigned)((g.heads + 3) / 4);
     hipLaunchKernelGGL((mha_head_bwd_kernel<DK, DV, NP>), dim3(gx, gy), dim3(256), head_bwd_smem(4, DV), s, g2);
+    if (g.ws) {
+      const int NY = g.heads * (DK + DV);
+      hipLaunchKernelGGL(copies_reduce_kernel, dim3((unsigned)((3 * H + NY + 63) / 64)), dim3(64), 0, s, g, H, NY);
+    }
   }
   NR_LAUNCH_CHECK();
   return NR_OK;
@@ -924,7 +962,7 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
                                const float* stats, const float* probs, const float* dnews, int64_t ldn,
                                const float* dz, int64_t lddz, const float* o, int64_t ldo, float* dob,
                                int64_t lddob, float* dy, int64_t lddy, float* dbias, float* dq, float* dgamma,
-                               float* dbeta, int32_t prec, hipStream_t stream) {
+                               float* dbeta, float* ws, int32_t ws_copies, int32_t prec, hipStream_t stream) {
   if (L < 1 || L > 32 || heads < 1 || heads > 12) return NR_EINVAL(0);
   if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(4);
   if (!y || !mask || !gamma || !beta || !q || !stats || !probs || !dnews || !dy || !dbias || !dq || !dgamma ||
@@ -947,6 +985,9 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
   // VALU work lands on a latency-bound kernel: head pass 170 -> 189 us), so bf16x6 callers get the
   // exact (more accurate) f32 products; bf16 callers get bf16
   g.np = prec == NR_GEMM_BF16 ? 1 : 0;
+  if (ws && (!o || ws_copies < 1 || ws_copies > 1024)) return NR_EINVAL(5);
+  g.ws = ws; g.ws_copies = ws_copies;
+  g.ws_ld = ((int64_t)3 * heads * dv + (int64_t)heads * (dk + dv) + 3) & ~int64_t(3);
   {
     const char* e = getenv("NR_DEBUG_MHAPOOL");
     g.dbg = e ? atoi(e) : 0;

@@ -90,7 +90,7 @@ _SIGS = {
                         c_ptr],
     "nr_mha_pool_bwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_u64,
                         c_u64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64,
-                        c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i32, c_ptr],
+                        c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_ptr],
     "nr_form_train_batch": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
                             c_i32, c_i32, c_i32, c_i32, c_u64, c_u64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                             c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],

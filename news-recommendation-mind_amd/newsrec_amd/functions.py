@@ -39,6 +39,20 @@ def _empty(rows, cols, like, ld=None):
     return buf[:, :cols]
 
 
+GRAD_COPIES = 32
+_GRAD_COPIES_WS = {}
+
+
+def _grad_copies(dev, width):
+    """A persistent zeroed [GRAD_COPIES, ceil4(width)] workspace per (device, stream, width) for
+    nr_mha_pool_bwd's spread parameter-gradient atomics (the kernel leaves it zero again)."""
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream, width)
+    ws = _GRAD_COPIES_WS.get(key)
+    if ws is None:
+        ws = _GRAD_COPIES_WS[key] = torch.zeros(GRAD_COPIES, (width + 3) // 4 * 4, device=dev)
+    return ws
+
+
 def _zeros_views(dev, *shapes):
     """Views of ONE zero-filled buffer (one fill launch instead of one per gradient), each
     starting 16-B aligned."""
@@ -241,9 +255,11 @@ class MHANewsFn(torch.autograd.Function):
         ur = ctx.ur
         if fused:
             dob = _empty(T, H, table) if O is not None else None
+            ws = _grad_copies(table.device, 3 * H + NY) if O is not None else None
             K.mha_pool_bwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, stats, probs, dnews, dY, db, dq,
                            dgamma, dbeta, p_drop=p_drop, seed=seed, offset=0 if ctx.rng is not None else offset,
-                           dz=dz, yrows=ur.inv if ur else None, rng=ctx.rng, o=O, dob=dob)
+                           dz=dz, yrows=ur.inv if ur else None, rng=ctx.rng, o=O, dob=dob, ws=ws,
+                           ws_copies=GRAD_COPIES if ws is not None else 0)
         else:
             dO = _empty(T, H, table)
             K.attn_pool_bwd(O, query, mask, n, seq_len, probs, dnews, dO, dq, gamma=gamma, beta=beta, stats=stats,

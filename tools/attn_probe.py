@@ -52,8 +52,10 @@ def main():
     dob = torch.empty(T, H, device=dev)
     db, dq, dg, dbt = (torch.zeros(NY, device=dev), torch.zeros(H, device=dev), torch.zeros(H, device=dev),
                        torch.zeros(H, device=dev))
+    from newsrec_amd.functions import GRAD_COPIES, _grad_copies
+    ws = _grad_copies(torch.device(dev, 0), 3 * H + NY) if os.environ.get("NR_PROBE_WS", "1") == "1" else None
     bwd = lambda: K.mha_pool_bwd(Y, mask, n, L, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dY, db, dq, dg,  # noqa
-                                 dbt, o=O, dob=dob, **kw)
+                                 dbt, o=O, dob=dob, ws=ws, ws_copies=GRAD_COPIES if ws is not None else 0, **kw)
     t_bwd = timed(bwd, a.reps)
     print(json.dumps({"mha_pool_fwd_us": round(t_fwd, 1), "split_bwd_us": round(t_bwd, 1)}))
 
