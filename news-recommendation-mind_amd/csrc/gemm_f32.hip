@@ -346,7 +346,12 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
     // bf16x6: small problems (< 400 tiles of 128x128) take 64x64 tiles, which only the exact-f32
     // kernel has (they are latency-bound, and 128x128 bf16x6 tiles would leave most CUs idle).
     // bf16: every eligible shape runs on the bf16 kernel (one product per tile is cheap).
-    const int fb = (prec == NR_GEMM_BF16 || (prec == NR_GEMM_BF16X6 && t128 >= 400)) ? 128 : 64;
+    static int small_min = -1;   // NR_GEMM_SMALL128 = tile count from which bf16x6 takes 128x128 (A/B)
+    if (small_min < 0) {
+      const char* e = getenv("NR_GEMM_SMALL128");
+      small_min = e ? atoi(e) : 400;
+    }
+    const int fb = (prec == NR_GEMM_BF16 || (prec == NR_GEMM_BF16X6 && t128 >= small_min)) ? 128 : 64;
     const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, fb, fb, nullptr,
                                 nullptr, prec, stream);
     if (rc != -1) return rc;
