@@ -52,14 +52,14 @@ struct BigKC {
     }
   }
   template <int S, int NP>
-  __device__ __forceinline__ void store(uint16_t* lds, int tid, bool lite = false) const {
+  __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
     constexpr int PL = R * BIG_SR;   // one plane
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int f = tid + 512 * i;
       uint16_t* q = lds + (f >> 2) * BIG_SR + 4 * (f & 3);
       const float4 x = v[S][i];
-      if (NP == 1 || lite) {   // lite: timing experiment only (no split, one plane written)
+      if constexpr (NP == 1) {
         *reinterpret_cast<uint2*>(q) = hi4(x.x, x.y, x.z, x.w);
       } else {
         uint2 p0, p1, p2;
@@ -117,16 +117,8 @@ struct BigMN {
     }
   }
   template <int S, int NP>
-  __device__ __forceinline__ void store(uint16_t* lds, int tid, bool lite = false) const {
+  __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
     if (tid >= 2 * R) return;
-    if (lite) {   // timing experiment only: no split, one plane written
-      uint16_t* q = lds + (4 * (tid >> 3)) * BIG_SR + 2 * (tid & 7);
-      put<1>(q, v[S][0].x, v[S][1].x);
-      put<1>(q + BIG_SR, v[S][0].y, v[S][1].y);
-      put<1>(q + 2 * BIG_SR, v[S][0].z, v[S][1].z);
-      put<1>(q + 3 * BIG_SR, v[S][0].w, v[S][1].w);
-      return;
-    }
     uint16_t* q = lds + (4 * (tid >> 3)) * BIG_SR + 2 * (tid & 7);
     put<NP>(q, v[S][0].x, v[S][1].x);
     put<NP>(q + BIG_SR, v[S][0].y, v[S][1].y);
@@ -323,10 +315,9 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
 #undef NR_MF
         }
         // (g.dbg bits 2 / 4: timing experiments only -- skip the split-stores / the loads)
-        // (g.dbg bits 128 / 64: timing experiments only -- A / B stored unsplit, one plane)
-        if (i == 0 && stage_next && !(g.dbg & 2)) la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid, g.dbg & 128);
+        if (i == 0 && stage_next && !(g.dbg & 2)) la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid);
         if (i == 1 && stage_next) {
-          if (!(g.dbg & 2)) lb.template store<NS, NP>(Bs + (st ^ 1) * NP * PB, tid, g.dbg & 64);
+          if (!(g.dbg & 2)) lb.template store<NS, NP>(Bs + (st ^ 1) * NP * PB, tid);
           if (kt + 3 < nt && !(g.dbg & 4)) issue(nset, kt + 3);
         }
       }
