@@ -123,11 +123,14 @@ int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand* A, const 
  *                    gradient row is zero (masked tokens of nr_mha_pool_bwd: exactly zero).
  *   counts[4]        {U, U_pad, bad, T_csr} (bad = 1 if an id fell outside [0, V))
  * Equal ids are aggregated per workgroup (LDS hash) before the global atomics.
- * work: 5*V int32.  Capacity: uids / seg_off hold ceil32(min(T, V)) (+1) entries. */
+ * work: nr_unique_rows_workspace(V) int32 (5*V + 2*ceil(V/4096)).
+ * Capacity: uids / seg_off hold ceil32(min(T, V)) (+1) entries. */
 int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t fill_row,
                    const void* grad_mask, int32_t mask_dtype, int32_t* work, int64_t* uids,
                    int64_t* inv, int32_t* seg_off, int32_t* seg_tok, int32_t* seg_of,
                    int32_t* counts, hipStream_t stream);
+/* int32 elements of nr_unique_rows' work buffer for a vocabulary of V ids */
+int64_t nr_unique_rows_workspace(int64_t V);
 
 /* Bytes of `work` nr_segment_rows_sum needs for T tokens of `width` floats. */
 int64_t nr_segment_rows_sum_workspace(int64_t T, int64_t width);

@@ -23,7 +23,7 @@
 
 namespace {
 
-constexpr int SCAN_THREADS = 1024;
+constexpr int SCAN_THREADS = 256;
 constexpr int SEG_RANGE = 64;   // CSR positions per segment-sum workgroup
 constexpr int CNT_THREADS = 1024;
 constexpr int HASH_SLOTS = 2048;
@@ -73,22 +73,15 @@ __global__ __launch_bounds__(CNT_THREADS) void count_kernel(const int64_t* __res
     }
 }
 
-// Inclusive wave scan (Hillis-Steele over the 64 lanes).
-__device__ __forceinline__ int32_t wave_scan_incl(int32_t x) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int32_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  return x;
-}
-
-// One workgroup scans the vocabulary in tiles of SCAN_PER x 1024 entries: coalesced loads into
-// LDS, each thread scans SCAN_PER consecutive entries read back from LDS (1-word row pad: no
-// bank conflicts), block scan of the thread totals, and every output leaves through LDS with
-// coalesced stores.  Exclusive scans of (cnt_all[v] > 0) -> pos[v] and of cnt_csr[v] ->
-// off[v]; compaction uids[pos[v]] = v, seg_off[pos[v]] = off[v].
+// Vocabulary scan in two launches over tiles of SCAN_TILE = 16 x 256 entries (one workgroup per
+// tile, so the scan runs on ceil(V / 4096) CUs instead of one):
+//   scan_reduce: per-tile totals of (cnt_all[v] > 0) and cnt_csr[v] -> tot[2b], tot[2b + 1];
+//   scan_down:   each tile adds up the totals of the tiles before it, scans its own entries
+//                (coalesced loads into LDS, each thread scans 16 consecutive entries read back
+//                with a 1-word row pad, wave scans of the thread sums) and writes
+//                pos[v] / off[v] (exclusive scans), the compaction uids[pos[v]] = v,
+//                seg_off[pos[v]] = off[v], all leaving through LDS with coalesced stores; the last
+//                tile writes counts and the pad entries.
 constexpr int SCAN_PER = 16;
 constexpr int SCAN_TILE = SCAN_PER * SCAN_THREADS;
 constexpr int SCAN_LDS_WORDS = SCAN_TILE + SCAN_TILE / SCAN_PER;
@@ -107,92 +100,138 @@ __device__ __forceinline__ void scan_load(int32_t* tile, const int32_t* __restri
   for (int k = 0; k < SCAN_PER; ++k) tile[scan_lds_index(tid + k * SCAN_THREADS)] = ld[k];
 }
 
-__global__ __launch_bounds__(SCAN_THREADS) void scan_kernel(const int32_t* __restrict__ cnt_all,
-                                                            const int32_t* __restrict__ cnt_csr, int64_t V,
-                                                            int32_t* __restrict__ pos, int32_t* __restrict__ off,
-                                                            int64_t* __restrict__ uids, int32_t* __restrict__ seg_off,
-                                                            int32_t* __restrict__ counts, int64_t fill_row) {
-  extern __shared__ int32_t tile[];   // SCAN_LDS_WORDS
-  __shared__ int32_t wu[SCAN_THREADS / 64], wc[SCAN_THREADS / 64];
-  __shared__ int32_t carry[2];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid == 0) carry[0] = carry[1] = 0;
-  for (int64_t base = 0; base < V; base += SCAN_TILE) {
-    const int nv = (int)(V - base < SCAN_TILE ? V - base : SCAN_TILE);
-    int32_t f[SCAN_PER], c[SCAN_PER];   // f: id present, c: segment length
-    scan_load(tile, cnt_all, base, nv);
-    __syncthreads();
+// block-wide sums of two values (every thread gets both)
+__device__ __forceinline__ void block_sum2(int32_t& a, int32_t& b, int32_t* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-    for (int k = 0; k < SCAN_PER; ++k) f[k] = tile[scan_lds_index(SCAN_PER * tid + k)] > 0 ? 1 : 0;
-    __syncthreads();
-    scan_load(tile, cnt_csr, base, nv);
-    __syncthreads();
-    int32_t fu = 0, fc = 0;
-#pragma unroll
-    for (int k = 0; k < SCAN_PER; ++k) {
-      c[k] = tile[scan_lds_index(SCAN_PER * tid + k)];
-      fu += f[k];
-      fc += c[k];
-    }
-    const int32_t iu = wave_scan_incl(fu), ic = wave_scan_incl(fc);
-    if (lane == 63) { wu[w] = iu; wc[w] = ic; }
-    __syncthreads();
-    int32_t pu = carry[0], pc = carry[1];
-    for (int k = 0; k < w; ++k) { pu += wu[k]; pc += wc[k]; }
-    pu += iu - fu;   // exclusive
-    pc += ic - fc;
-    const int32_t pu0 = pu, pc0 = pc, ubase = carry[0];
-    __syncthreads();   // every thread has read carry
-#pragma unroll
-    for (int k = 0; k < SCAN_PER; ++k) {
-      tile[scan_lds_index(SCAN_PER * tid + k)] = pu;
-      pu += f[k];
-    }
-    __syncthreads();
-    for (int i = tid; i < nv; i += SCAN_THREADS) pos[base + i] = tile[scan_lds_index(i)];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < SCAN_PER; ++k) {
-      tile[scan_lds_index(SCAN_PER * tid + k)] = pc;
-      pc += c[k];
-    }
-    __syncthreads();
-    for (int i = tid; i < nv; i += SCAN_THREADS) off[base + i] = tile[scan_lds_index(i)];
-    __syncthreads();
-    pu = pu0;
-#pragma unroll
-    for (int k = 0; k < SCAN_PER; ++k) {   // compacted ids (tile-local positions)
-      if (f[k]) tile[pu - ubase] = SCAN_PER * tid + k;
-      pu += f[k];
-    }
-    if (tid == SCAN_THREADS - 1) { carry[0] = pu; carry[1] = pc; }
-    __syncthreads();
-    const int tu = carry[0] - ubase;
-    for (int i = tid; i < tu; i += SCAN_THREADS) uids[ubase + i] = base + tile[i];
-    __syncthreads();
-    pu = pu0;
-    pc = pc0;
-#pragma unroll
-    for (int k = 0; k < SCAN_PER; ++k) {
-      if (f[k]) tile[pu - ubase] = pc;
-      pu += f[k];
-      pc += c[k];
-    }
-    __syncthreads();
-    for (int i = tid; i < tu; i += SCAN_THREADS) seg_off[ubase + i] = tile[i];
-    __syncthreads();
+  for (int d = 32; d >= 1; d >>= 1) {
+    a += __shfl_xor(a, d, 64);
+    b += __shfl_xor(b, d, 64);
   }
-  if (tid == 0) {
-    const int32_t U = carry[0], Tv = carry[1];
-    const int32_t Up = (U + 31) / 32 * 32;
-    counts[0] = U;
-    counts[1] = Up;
-    counts[3] = Tv;
-    for (int32_t u = U; u < Up; ++u) {
-      uids[u] = fill_row;
-      seg_off[u] = Tv;
+  if (lane == 0) { red[2 * w] = a; red[2 * w + 1] = b; }
+  __syncthreads();
+  a = 0; b = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_THREADS / 64; ++k) { a += red[2 * k]; b += red[2 * k + 1]; }
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_reduce_kernel(const int32_t* __restrict__ cnt_all,
+                                                                   const int32_t* __restrict__ cnt_csr, int64_t V,
+                                                                   int32_t* __restrict__ tot) {
+  __shared__ int32_t red[2 * SCAN_THREADS / 64];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+  const int nv = (int)(V - base < SCAN_TILE ? V - base : SCAN_TILE);
+  int32_t fu = 0, fc = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) {   // coalesced: the order inside the tile is irrelevant to a sum
+    const int i = threadIdx.x + k * SCAN_THREADS;
+    if (i < nv) {
+      fu += cnt_all[base + i] > 0 ? 1 : 0;
+      fc += cnt_csr[base + i];
     }
-    seg_off[Up] = Tv;
+  }
+  block_sum2(fu, fc, red);
+  if (threadIdx.x == 0) { tot[2 * blockIdx.x] = fu; tot[2 * blockIdx.x + 1] = fc; }
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_down_kernel(const int32_t* __restrict__ cnt_all,
+                                                                 const int32_t* __restrict__ cnt_csr, int64_t V,
+                                                                 const int32_t* __restrict__ tot,
+                                                                 int32_t* __restrict__ pos, int32_t* __restrict__ off,
+                                                                 int64_t* __restrict__ uids,
+                                                                 int32_t* __restrict__ seg_off,
+                                                                 int32_t* __restrict__ counts, int64_t fill_row) {
+  extern __shared__ int32_t tile[];   // SCAN_LDS_WORDS
+  __shared__ int32_t wu[SCAN_THREADS / 64], wc[SCAN_THREADS / 64], red[2 * SCAN_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x;
+  const int64_t base = (int64_t)b * SCAN_TILE;
+  const int nv = (int)(V - base < SCAN_TILE ? V - base : SCAN_TILE);
+  // totals of the tiles before this one (their loads overlap this tile's loads)
+  int32_t ubase = 0, cbase = 0;
+  for (int j = tid; j < b; j += SCAN_THREADS) { ubase += tot[2 * j]; cbase += tot[2 * j + 1]; }
+  int32_t f[SCAN_PER], c[SCAN_PER];   // f: id present, c: segment length
+  scan_load(tile, cnt_all, base, nv);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) f[k] = tile[scan_lds_index(SCAN_PER * tid + k)] > 0 ? 1 : 0;
+  __syncthreads();
+  scan_load(tile, cnt_csr, base, nv);
+  block_sum2(ubase, cbase, red);   // (its barrier also publishes the tile)
+  int32_t fu = 0, fc = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) {
+    c[k] = tile[scan_lds_index(SCAN_PER * tid + k)];
+    fu += f[k];
+    fc += c[k];
+  }
+  int32_t iu = fu, ic = fc;   // inclusive wave scans
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t yu = __shfl_up(iu, d, 64), yc = __shfl_up(ic, d, 64);
+    if (lane >= d) { iu += yu; ic += yc; }
+  }
+  if (lane == 63) { wu[w] = iu; wc[w] = ic; }
+  __syncthreads();
+  int32_t pu = ubase, pc = cbase;
+  for (int k = 0; k < w; ++k) { pu += wu[k]; pc += wc[k]; }
+  pu += iu - fu;   // exclusive
+  pc += ic - fc;
+  const int32_t pu0 = pu, pc0 = pc;
+  int32_t tile_u = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_THREADS / 64; ++k) tile_u += wu[k];
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) {
+    tile[scan_lds_index(SCAN_PER * tid + k)] = pu;
+    pu += f[k];
+  }
+  __syncthreads();
+  for (int i = tid; i < nv; i += SCAN_THREADS) pos[base + i] = tile[scan_lds_index(i)];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) {
+    tile[scan_lds_index(SCAN_PER * tid + k)] = pc;
+    pc += c[k];
+  }
+  __syncthreads();
+  for (int i = tid; i < nv; i += SCAN_THREADS) off[base + i] = tile[scan_lds_index(i)];
+  __syncthreads();
+  pu = pu0;
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) {   // compacted ids (tile-local positions)
+    if (f[k]) tile[pu - ubase] = SCAN_PER * tid + k;
+    pu += f[k];
+  }
+  __syncthreads();
+  for (int i = tid; i < tile_u; i += SCAN_THREADS) uids[ubase + i] = base + tile[i];
+  __syncthreads();
+  pu = pu0;
+  pc = pc0;
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) {
+    if (f[k]) tile[pu - ubase] = pc;
+    pu += f[k];
+    pc += c[k];
+  }
+  __syncthreads();
+  for (int i = tid; i < tile_u; i += SCAN_THREADS) seg_off[ubase + i] = tile[i];
+  if (b == (int)gridDim.x - 1) {   // the last tile knows the totals
+    int32_t tile_c = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_THREADS / 64; ++k) tile_c += wc[k];
+    const int32_t U = ubase + tile_u, Tv = cbase + tile_c;
+    const int32_t Up = (U + 31) / 32 * 32;
+    if (tid == 0) {
+      counts[0] = U;
+      counts[1] = Up;
+      counts[3] = Tv;
+      seg_off[Up] = Tv;
+    }
+    if (tid < Up - U) {
+      uids[U + tid] = fill_row;
+      seg_off[U + tid] = Tv;
+    }
   }
 }
 
@@ -443,20 +482,20 @@ extern "C" int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t 
   if (T > 0)
     hipLaunchKernelGGL(count_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, grad_mask, mask_dtype, cnt_all,
                        cnt_csr, counts);
-  const size_t scan_lds = sizeof(int32_t) * SCAN_LDS_WORDS;
-  static bool scan_attr = false;
-  if (!scan_attr) {
-    e = hipFuncSetAttribute((const void*)scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)scan_lds);
-    if (e != hipSuccess) return -(int)e;
-    scan_attr = true;
-  }
-  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(SCAN_THREADS), scan_lds, stream, cnt_all, cnt_csr, V, pos, off, uids,
-                     seg_off, counts, fill_row);
+  const int64_t nb = (V + SCAN_TILE - 1) / SCAN_TILE;
+  int32_t* tot = work + 5 * V;   // [nb][2] tile totals
+  hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, stream, cnt_all, cnt_csr, V, tot);
+  hipLaunchKernelGGL(scan_down_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), sizeof(int32_t) * SCAN_LDS_WORDS, stream,
+                     cnt_all, cnt_csr, V, tot, pos, off, uids, seg_off, counts, fill_row);
   if (T > 0)
     hipLaunchKernelGGL(fill_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, grad_mask, mask_dtype, pos, off,
                        cursor, inv, seg_tok, seg_of);
   NR_LAUNCH_CHECK();
   return NR_OK;
+}
+
+extern "C" int64_t nr_unique_rows_workspace(int64_t V) {
+  return 5 * V + 2 * ((V + SCAN_TILE - 1) / SCAN_TILE);
 }
 
 extern "C" int64_t nr_segment_rows_sum_workspace(int64_t T, int64_t width) {

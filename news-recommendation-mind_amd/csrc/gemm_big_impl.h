@@ -116,14 +116,27 @@ struct BigMN {
       *reinterpret_cast<uint32_t*>(q + 2 * PL) = ll;
     }
   }
+  // Thread (column group cg = tid >> 3, k pair kp = tid & 7) writes its four rows 4cg .. 4cg + 3 as
+  // four ds_write_b32 per plane.  The row stride is 12 words, so row 4cg + i sits at bank
+  // 16 cg + 12 i + kp (mod 32): in natural order the four column groups of a 32-lane half land on
+  // two bank windows (a 2-way conflict on every write).  Column groups with cg ^ (cg >> 1) odd write
+  // their rows in the order 2, 3, 0, 1 instead, which puts the four windows 8 banks apart:
+  // conflict-free.  (The float4 halves are swapped to match: 4 selects per float4.)
   template <int S, int NP>
   __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
     if (tid >= 2 * R) return;
-    uint16_t* q = lds + (4 * (tid >> 3)) * BIG_SR + 2 * (tid & 7);
-    put<NP>(q, v[S][0].x, v[S][1].x);
-    put<NP>(q + BIG_SR, v[S][0].y, v[S][1].y);
-    put<NP>(q + 2 * BIG_SR, v[S][0].z, v[S][1].z);
-    put<NP>(q + 3 * BIG_SR, v[S][0].w, v[S][1].w);
+    const int cg = tid >> 3;
+    const bool rot = ((cg ^ (cg >> 1)) & 1) != 0;
+    uint16_t* q = lds + (4 * cg) * BIG_SR + 2 * (tid & 7);
+    uint16_t* qa = q + (rot ? 2 * BIG_SR : 0);   // rows 0, 1 (or 2, 3)
+    uint16_t* qb = q + (rot ? 0 : 2 * BIG_SR);   // rows 2, 3 (or 0, 1)
+    const float4 a = v[S][0], b = v[S][1];
+    const float a0 = rot ? a.z : a.x, a1 = rot ? a.w : a.y, a2 = rot ? a.x : a.z, a3 = rot ? a.y : a.w;
+    const float b0 = rot ? b.z : b.x, b1 = rot ? b.w : b.y, b2 = rot ? b.x : b.z, b3 = rot ? b.y : b.w;
+    put<NP>(qa, a0, b0);
+    put<NP>(qa + BIG_SR, a1, b1);
+    put<NP>(qb, a2, b2);
+    put<NP>(qb + BIG_SR, a3, b3);
   }
 };
 

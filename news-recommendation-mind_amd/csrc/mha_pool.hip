@@ -287,6 +287,41 @@ __device__ __forceinline__ void head_out(const float (&bv)[DV / 2], int head, co
 template <int DK, int DV, int NP>
 __device__ void attention_to_lds(const MPArgs& g, int64_t seq, uint64_t bits, float* os, int so) {
   const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (nw < g.heads) {
+    // several heads per wave (the four-wave forward): the next head's key / value loads are issued
+    // before this head's products, so each load latency hides behind the previous head's work.
+    // Heads w, w + nw, w + 2 nw; a prefetch past the last head re-reads the last one (clamped, no
+    // branch around a load: hipcc would wait for it at the join).
+    float a0[DK / 2], b0[DV / 2], a1[DK / 2], b1[DV / 2];
+    const int hl = g.heads - 1;
+    const int h0 = w, h1 = w + nw, h2 = w + 2 * nw;
+    load_krow<DK, NP>(g, seq, h0 < hl ? h0 : hl, a0);
+    load_vop<DK, DV>(g, seq, h0 < hl ? h0 : hl, b0);
+    load_krow<DK, NP>(g, seq, h1 < hl ? h1 : hl, a1);
+    load_vop<DK, DV>(g, seq, h1 < hl ? h1 : hl, b1);
+    float p[16];
+    if (h0 <= hl) {
+      head_probs_from<DK, NP>(g, bits, a0, p);
+      head_out<DK, DV, NP>(b0, h0, p, os, so);
+    }
+    load_krow<DK, NP>(g, seq, h2 < hl ? h2 : hl, a0);
+    load_vop<DK, DV>(g, seq, h2 < hl ? h2 : hl, b0);
+    if (h1 <= hl) {
+      head_probs_from<DK, NP>(g, bits, a1, p);
+      head_out<DK, DV, NP>(b1, h1, p, os, so);
+    }
+    if (h2 <= hl) {
+      head_probs_from<DK, NP>(g, bits, a0, p);
+      head_out<DK, DV, NP>(b0, h2, p, os, so);
+    }
+    for (int head = w + 3 * nw; head < g.heads; head += nw) {   // more than three heads per wave
+      load_krow<DK, NP>(g, seq, head, a0);
+      load_vop<DK, DV>(g, seq, head, b0);
+      head_probs_from<DK, NP>(g, bits, a0, p);
+      head_out<DK, DV, NP>(b0, head, p, os, so);
+    }
+    return;
+  }
   for (int head = w; head < g.heads; head += nw) {
     // issue the key and value loads together: one memory latency per head, not two
     float a[DK / 2], bv[DV / 2];
@@ -295,8 +330,7 @@ __device__ void attention_to_lds(const MPArgs& g, int64_t seq, uint64_t bits, fl
     float p[16];
     head_probs_from<DK, NP>(g, bits, a, p);
     head_out<DK, DV, NP>(bv, head, p, os, so);
-  }
-}
+  }}
 
 template <int DK, int DV, int NH64, int NP>
 __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
@@ -309,6 +343,10 @@ __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
   const int64_t seq = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
   const uint64_t bits = token_bits(g, seq);
+  stage_rows(g, seq);
+  if (!(g.dbg & 1)) attention_to_lds<DK, DV, NP>(g, seq, bits, os, SO);
+  // the LayerNorm / pooling vectors are loaded only now: held through the attention phase they
+  // would raise its register peak (and so lower the titles in flight per CU)
   float gam[NH64], bet[NH64], qv[NH64];
 #pragma unroll
   for (int k = 0; k < NH64; ++k) {
@@ -316,8 +354,6 @@ __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
     bet[k] = g.beta[lane + 64 * k];
     qv[k] = g.q[lane + 64 * k];
   }
-  stage_rows(g, seq);
-  if (!(g.dbg & 1)) attention_to_lds<DK, DV, NP>(g, seq, bits, os, SO);
   __syncthreads();
   if (g.dbg & 2) return;
   // LayerNorm + dropout in place, scores; one wave per row
@@ -875,8 +911,17 @@ void allow_smem(K kern, size_t sz) {
 template <int DK, int DV, int NH64, int NP>
 int launch_np(const MPArgs& g, Pass pass, hipStream_t s) {
   const int H = NH64 * 64;
-  if (pass == FWD) {   // one wave per head (>= 4 waves for the LN phase)
-    const int nw = g.heads < 4 ? 4 : g.heads;
+  if (pass == FWD) {
+    // FOUR waves per title, each taking heads w, w + 4, ...: the workgroup's 49.5 KB LDS image then
+    // lets three titles share a CU (one wave per head, 12 waves at 104 VGPRs, fit one title per CU,
+    // whose barrier-separated phases left the CU idle on every load latency: 105 us per NRMS step).
+    // NR_MHAPOOL_FWD_WAVES overrides (A/B timing).
+    static int env_nw = -1;
+    if (env_nw < 0) {
+      const char* e = getenv("NR_MHAPOOL_FWD_WAVES");
+      env_nw = e ? atoi(e) : 0;
+    }
+    const int nw = env_nw >= 4 && env_nw <= 12 ? env_nw : 4;
     const size_t sz = fwd_smem(H);
     allow_smem(mha_pool_fwd_kernel<DK, DV, NH64, NP>, sz);
     hipLaunchKernelGGL((mha_pool_fwd_kernel<DK, DV, NH64, NP>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);

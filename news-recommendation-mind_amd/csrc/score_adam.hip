@@ -188,20 +188,28 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
   const bool vec = ((reinterpret_cast<uintptr_t>(e.p) | reinterpret_cast<uintptr_t>(e.g) |
                      reinterpret_cast<uintptr_t>(e.m) | reinterpret_cast<uintptr_t>(e.v)) & 15) == 0;
   if (vec && end - base == kAdamChunk) {
+    // all sixteen float4 loads of the thread in flight before the first store (the four tensors
+    // are distinct allocations; without the explicit order the stores of one float4 would have
+    // to land before the next one's loads could be issued)
+    float4 pp[4], gg[4], mm[4], vv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t i = base / 4 + u * 256 + threadIdx.x;
-      float4 pp = reinterpret_cast<float4*>(e.p)[i];
-      const float4 gg = reinterpret_cast<const float4*>(e.g)[i];
-      float4 mm = reinterpret_cast<float4*>(e.m)[i];
-      float4 vv = reinterpret_cast<float4*>(e.v)[i];
-      adam_elem(pp.x, gg.x, mm.x, vv.x, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
-      adam_elem(pp.y, gg.y, mm.y, vv.y, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
-      adam_elem(pp.z, gg.z, mm.z, vv.z, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
-      adam_elem(pp.w, gg.w, mm.w, vv.w, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
-      reinterpret_cast<float4*>(e.p)[i] = pp;
-      reinterpret_cast<float4*>(e.m)[i] = mm;
-      reinterpret_cast<float4*>(e.v)[i] = vv;
+      pp[u] = reinterpret_cast<const float4*>(e.p)[i];
+      gg[u] = reinterpret_cast<const float4*>(e.g)[i];
+      mm[u] = reinterpret_cast<const float4*>(e.m)[i];
+      vv[u] = reinterpret_cast<const float4*>(e.v)[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = base / 4 + u * 256 + threadIdx.x;
+      adam_elem(pp[u].x, gg[u].x, mm[u].x, vv[u].x, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
+      adam_elem(pp[u].y, gg[u].y, mm[u].y, vv[u].y, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
+      adam_elem(pp[u].z, gg[u].z, mm[u].z, vv[u].z, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
+      adam_elem(pp[u].w, gg[u].w, mm[u].w, vv[u].w, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
+      reinterpret_cast<float4*>(e.p)[i] = pp[u];
+      reinterpret_cast<float4*>(e.m)[i] = mm[u];
+      reinterpret_cast<float4*>(e.v)[i] = vv[u];
     }
   } else {
     for (int64_t i = base + threadIdx.x; i < end; i += 256) {

@@ -55,6 +55,7 @@ _SIGS = {
     "nr_segment_rows_sum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
                             c_ptr],
     "nr_segment_rows_sum_workspace": [c_i64, c_i64],
+    "nr_unique_rows_workspace": [c_i64],
     "nr_segment_rows_sum_conv3": [c_ptr, c_i64, c_i64, c_i32, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr,
                                   c_i64, c_ptr],
     "nr_cnn_pack_weights": [c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
@@ -118,7 +119,7 @@ _SIGS = {
     "nr_build_hash": [],
 }
 
-_RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64,
+_RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_unique_rows_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64,
              "nr_colsum_workspace": c_i64,
              "nr_build_hash": ctypes.c_char_p}
 

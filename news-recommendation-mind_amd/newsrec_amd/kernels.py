@@ -114,7 +114,7 @@ class UniqueRows:
         self.T, self.vocab = T, vocab
         self.cap = max(32, _ceil32(min(T, vocab)))
         i32 = dict(device=dev, dtype=torch.int32)
-        work = torch.empty(5 * vocab, **i32)
+        work = torch.empty(int(L.load().nr_unique_rows_workspace(vocab)), **i32)
         self.uids = torch.empty(self.cap, device=dev, dtype=torch.int64)
         self.inv = torch.empty(T, device=dev, dtype=torch.int64)
         self.seg_off = torch.empty(self.cap + 1, **i32)

@@ -34,7 +34,7 @@ wo2 = torch.randn(768, 3072, device=dev) / 50; o = torch.empty(T, 768, device=de
 dWi = torch.zeros(3072, 768, device=dev)
 P = torch.empty(U, 480, device=dev); w3 = torch.randn(480, E, device=dev)
 uids = torch.randperm(V - 1, device=dev)[:24600] + 1; dT = torch.zeros(V, E, device=dev)
-dYc = torch.randn(52800, 1152, device=dev)
+dYc = torch.randn(52800, 1152, device=dev); WT = W.t().contiguous()
 ux = torch.randn(1600, 384, device=dev); uw = torch.randn(768, 384, device=dev) / 20; ub = torch.randn(768, device=dev)
 uy = torch.empty(1600, 768, device=dev); udy = torch.randn(1600, 768, device=dev); udx = torch.empty(1600, 384, device=dev)
 udw = torch.zeros(768, 384, device=dev); m_dev = torch.tensor([24600], dtype=torch.int32, device=dev)
@@ -42,6 +42,7 @@ cases = {
  "nrms_proj_fwd": (2*U*E*1152, lambda p: K.gemm_dyn(U, 1152, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(W, L.KCONTIG), Y, prec=p)),
  "nrms_proj_dgrad": (2*U*E*1152, lambda p: K.gemm_dyn(U, E, 1152, K.operand(dY, L.KCONTIG), K.operand(W, L.MNCONTIG), dX, prec=p)),
  "nrms_dgrad_table": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), K.operand(W, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
+ "nrms_dgrad_table_kc": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), K.operand(WT, L.KCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
  "nrms_dgrad_table_store": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), K.operand(W, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_STORE, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
  "user_fwd": (2*1600*768*384, lambda p: K.gemm(1600, 768, 384, K.operand(ux, L.KCONTIG), K.operand(uw, L.KCONTIG), uy, bias=ub, prec=p)),
  "user_dgrad": (2*1600*768*384, lambda p: K.gemm(1600, 384, 768, K.operand(udy, L.KCONTIG), K.operand(uw, L.MNCONTIG), udx, prec=p)),
