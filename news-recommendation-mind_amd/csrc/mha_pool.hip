@@ -740,7 +740,8 @@ __global__ __launch_bounds__(256) void mha_ln_bwd_kernel(MPArgs g) {
   }
   if (tid < 32) sps[tid] = tid < L ? g.probs[seq * L + tid] : 0.f;
   // (1) normalise in place (x -> x_hat), dp_l = dnews · Z_l, keep-bits kept per row
-  uint64_t kbit[RW];
+  static_assert(NH64 <= 32, "keep-bits of a row fit one word");
+  uint32_t kbit[RW];
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
     const int l = w + 4 * i;
