@@ -149,12 +149,12 @@ __global__ __launch_bounds__(64 * SP_WAVES) void seq_pool_bwd_kernel(SeqPoolArgs
     const float* xb = g.x + seq * g.L * g.ldx;
     const float* kb = g.key ? g.key + seq * g.L * g.ldk : xb;
     const int64_t ldk = g.key ? g.ldk : g.ldx;
-    float p[SP_MAXL];
-#pragma unroll
-    for (int l = 0; l < SP_MAXL; ++l) p[l] = l < g.L ? g.probs[seq * g.L + l] : 0.f;
+    // per-row scalars live one per lane (lane l: p_l, dp_l, ds_l) and are broadcast with v_readlane
+    // where a row is used: two VGPRs instead of two 32-entry arrays replicated in every lane
+    const float pv = lane < g.L ? g.probs[seq * g.L + lane] : 0.f;
     const float4 dov = ldv(g.dout + seq * g.lddo, lane, g.qn);
     // dp_l = dout · X_l
-    float dp[SP_MAXL];
+    float dpv = 0.f;
 #pragma unroll
     for (int l0 = 0; l0 < SP_MAXL; l0 += 8) {
       float part[8];
@@ -164,11 +164,13 @@ __global__ __launch_bounds__(64 * SP_WAVES) void seq_pool_bwd_kernel(SeqPoolArgs
         part[u] = dot4(dov, ld4(xb + l * g.ldx, lane, g.D));
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) dp[l0 + u] = nr_wave_sum(part[u]);
+      for (int u = 0; u < 8; ++u) {
+        const float t = nr_wave_sum(part[u]);
+        dpv = lane == l0 + u ? t : dpv;
+      }
     }
-    float r = 0.f;
-#pragma unroll
-    for (int l = 0; l < SP_MAXL; ++l) r = l < g.L ? fmaf(p[l], dp[l], r) : r;
+    const float r = nr_wave_sum(lane < g.L ? pv * dpv : 0.f);
+    const float dsv = pv * (dpv - r) * g.scale;
     // ds_l = p_l (dp_l - r) scale;  dq += ds_l K_l;  dK_l = ds_l q (tanh');  dX_l = p_l dout (+ ds_l q tied) (+ dz)
     // eight rows at a time: their key / dz loads go out together before any store of the batch
 #pragma unroll
@@ -185,7 +187,8 @@ __global__ __launch_bounds__(64 * SP_WAVES) void seq_pool_bwd_kernel(SeqPoolArgs
       for (int u = 0; u < 8; ++u) {
         const int l = l0 + u;
         if (l >= g.L) break;
-        const float pl = p[l0 + u], ds = pl * (dp[l0 + u] - r) * g.scale;
+        const float pl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pv), l));
+        const float ds = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dsv), l));
         dqa.x = fmaf(ds, kv[u].x, dqa.x); dqa.y = fmaf(ds, kv[u].y, dqa.y);
         dqa.z = fmaf(ds, kv[u].z, dqa.z); dqa.w = fmaf(ds, kv[u].w, dqa.w);
         const int64_t row = seq * g.L + l;
