@@ -460,6 +460,25 @@ __global__ __launch_bounds__(FIX_THREADS) void segsum_fix_kernel(int64_t w4, con
   }
 }
 
+// work[0, n) = 0 and counts[0..3] = 0 (int4 stores when work is 16-B aligned, scalar tail)
+__global__ __launch_bounds__(256) void zero_work_kernel(int32_t* __restrict__ work, int64_t n,
+                                                        int32_t* __restrict__ counts) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (reinterpret_cast<uintptr_t>(work) & 15) {
+    for (int64_t i = i0; i < n; i += stride) work[i] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 4) counts[threadIdx.x] = 0;
+    return;
+  }
+  const int64_t n4 = n / 4;
+  int4* w4 = reinterpret_cast<int4*>(work);
+  for (int64_t i = i0; i < n4; i += stride) w4[i] = make_int4(0, 0, 0, 0);
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < n - 4 * n4) work[4 * n4 + threadIdx.x] = 0;
+    if (threadIdx.x < 4) counts[threadIdx.x] = 0;
+  }
+}
+
 }  // namespace
 
 extern "C" int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t fill_row, const void* grad_mask,
@@ -474,10 +493,12 @@ extern "C" int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t 
   int32_t* cursor = work + 2 * V;
   int32_t* pos = work + 3 * V;
   int32_t* off = work + 4 * V;
-  hipError_t e = hipMemsetAsync(work, 0, sizeof(int32_t) * 3 * V, stream);
-  if (e != hipSuccess) return -(int)e;
-  e = hipMemsetAsync(counts, 0, sizeof(int32_t) * 4, stream);
-  if (e != hipSuccess) return -(int)e;
+  {   // the three per-id counters and `counts` zeroed by ONE launch (two memsets cost two graph nodes)
+    const int64_t n = 3 * V;
+    int64_t zb = (n / 4 + 255) / 256;
+    zb = zb < 1 ? 1 : (zb > 1024 ? 1024 : zb);
+    hipLaunchKernelGGL(zero_work_kernel, dim3((unsigned)zb), dim3(256), 0, stream, work, n, counts);
+  }
   const unsigned gb = (unsigned)((T + CNT_THREADS - 1) / CNT_THREADS);
   if (T > 0)
     hipLaunchKernelGGL(count_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, grad_mask, mask_dtype, cnt_all,
