@@ -405,6 +405,12 @@ int nr_form_train_batch(const int64_t* sample_idx, int64_t B, const int32_t* imp
                         double* his_mask, int64_t* user_id, int64_t* label, int32_t* status,
                         hipStream_t stream);
 
+/* Device RNG pair bookkeeping for graph-replayed steps: snap = state (the (seed, offset) pair the
+ * kernels of this forward/backward read), then state[1] += n (the elements the step's dropout
+ * draws -- nn.Dropout's RNG consumption in MHA_Encoder / CNN_Encoder, models/Encoders/MHA.py:38,
+ * CNN.py:44), in ONE launch (torch clone + add cost two).  snap may be null (advance only). */
+int nr_rng_take(uint64_t* state, uint64_t* snap, uint64_t n, hipStream_t stream);
+
 /* History side of B consecutive dev/test impression chunks chunk0 .. chunk0+B-1
  * (utils/MIND.py:367-449; chunk_impr[c] = impression of chunk c).  his_tok/his_attn may be null
  * (fast eval reads history representations from the news table instead).  impr_index[b] =

@@ -415,3 +415,22 @@ extern "C" int nr_impression_metrics(const float* preds, const int32_t* labels, 
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
+
+namespace {
+__global__ void rng_take_kernel(uint64_t* state, uint64_t* snap, uint64_t n) {
+  if (threadIdx.x != 0) return;
+  const uint64_t seed = state[0], off = state[1];
+  if (snap) {
+    snap[0] = seed;
+    snap[1] = off;
+  }
+  state[1] = off + n;
+}
+}  // namespace
+
+extern "C" int nr_rng_take(uint64_t* state, uint64_t* snap, uint64_t n, hipStream_t stream) {
+  if (!state) return NR_EINVAL(0);
+  hipLaunchKernelGGL(rng_take_kernel, dim3(1), dim3(64), 0, stream, state, snap, n);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}

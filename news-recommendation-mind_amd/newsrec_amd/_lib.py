@@ -95,6 +95,7 @@ _SIGS = {
     "nr_form_train_batch": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
                             c_i32, c_i32, c_i32, c_i32, c_u64, c_u64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                             c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+    "nr_rng_take": [c_ptr, c_ptr, c_u64, c_ptr],
     "nr_form_eval_batch": [c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_i32, c_i32,
                            c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
     "nr_gather_news_rows": [c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],

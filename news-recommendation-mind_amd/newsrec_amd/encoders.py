@@ -43,8 +43,8 @@ class _DropoutStream:
         """-> (seed, offset, rng): rng = int64 CUDA (seed, offset) snapshot for the kernels."""
         if self.state is None or self.state.device != device:
             self.state = torch.tensor([self.seed, self.offset], dtype=torch.int64, device=device)
-        snap = self.state.clone()
-        self.state[1:].add_(int(n))
+        snap = torch.empty_like(self.state)
+        L.call("nr_rng_take", L.ptr(self.state), L.ptr(snap), int(n), L.stream_ptr(self.state))
         off = self.offset
         self.offset += int(n)   # host mirror (eager bookkeeping; replays advance only the device pair)
         return self.seed, off, snap
