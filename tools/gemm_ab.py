@@ -37,7 +37,7 @@ uids = torch.randperm(V - 1, device=dev)[:24600] + 1; dT = torch.zeros(V, E, dev
 dYc = torch.randn(52800, 1152, device=dev); WT = W.t().contiguous()
 ux = torch.randn(1600, 384, device=dev); uw = torch.randn(768, 384, device=dev) / 20; ub = torch.randn(768, device=dev)
 uy = torch.empty(1600, 768, device=dev); udy = torch.randn(1600, 768, device=dev); udx = torch.empty(1600, 384, device=dev)
-udw = torch.zeros(768, 384, device=dev); m_dev = torch.tensor([24600], dtype=torch.int32, device=dev)
+udw = torch.zeros(768, 384, device=dev); uwT = uw.t().contiguous(); m_dev = torch.tensor([24600], dtype=torch.int32, device=dev)
 cases = {
  "nrms_proj_fwd": (2*U*E*1152, lambda p: K.gemm_dyn(U, 1152, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(W, L.KCONTIG), Y, prec=p)),
  "nrms_proj_dgrad": (2*U*E*1152, lambda p: K.gemm_dyn(U, E, 1152, K.operand(dY, L.KCONTIG), K.operand(W, L.MNCONTIG), dX, prec=p)),
@@ -46,6 +46,7 @@ cases = {
  "nrms_dgrad_table_store": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), K.operand(W, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_STORE, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
  "user_fwd": (2*1600*768*384, lambda p: K.gemm(1600, 768, 384, K.operand(ux, L.KCONTIG), K.operand(uw, L.KCONTIG), uy, bias=ub, prec=p)),
  "user_dgrad": (2*1600*768*384, lambda p: K.gemm(1600, 384, 768, K.operand(udy, L.KCONTIG), K.operand(uw, L.MNCONTIG), udx, prec=p)),
+ "user_dgrad_kc": (2*1600*768*384, lambda p: K.gemm(1600, 384, 768, K.operand(udy, L.KCONTIG), K.operand(uwT, L.KCONTIG), udx, prec=p)),
  "user_wgrad": (2*1600*768*384, lambda p: K.gemm(768, 384, 1600, K.operand(udy, L.MNCONTIG), K.operand(ux, L.MNCONTIG), udw, epilogue=L.EPI_ATOMIC, split_k=F._split_k(768, 384, 1600), prec=p)),
  "nrms_proj_wgrad": (2*U*E*1152, lambda p: K.gemm_dyn(1152, E, U, K.operand(dY, L.MNCONTIG), K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dW, epilogue=L.EPI_ATOMIC, split_k=F._split_k(1152, E, U), prec=p)),
  "cnn_tap_proj": (2*U*E*480, lambda p: K.gemm_dyn(U, 480, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(w3, L.KCONTIG), P, prec=p)),
