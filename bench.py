@@ -17,7 +17,8 @@ MIND-large-shaped dev split (376,471 impressions, ~37 candidates each), and cal_
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--data device|resident]
 
-Rank 0 prints ONE JSON line.  For N > 1 launch with torch.distributed.run (one rank/GPU).
+Rank 0 prints ONE JSON line.  N > 1: either launch with torch.distributed.run (one rank/GPU), or
+run ``bench.py --gpus N`` directly and it spawns the N ranks itself (twotower.py:62-73).
 """
 import argparse
 import json
@@ -424,7 +425,9 @@ def cpu_baseline(seconds=20.0):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment this process "
+                         "spawns them itself (default 1, or WORLD_SIZE under torch.distributed.run)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -441,17 +444,39 @@ def main():
                          "optimizer graphs with the RCCL collectives between them)")
     a = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per GPU over RCCL; NR_DIST_BACKEND=gloo lets a 1-GPU box rehearse the N > 1 path
     backend = os.environ.get("NR_DIST_BACKEND", "nccl")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        world = a.gpus if a.gpus is not None else 1
+        if world > 1:
+            # twotower.py:62-73 (mp.spawn, one process per GPU): this process only launches and
+            # joins the ranks -- it must not touch the GPU (device_count() does not initialise it)
+            if backend == "nccl" and torch.cuda.device_count() < world:
+                print("bench.py: --gpus %d needs %d GPUs, %d visible" % (world, world, torch.cuda.device_count()),
+                      file=sys.stderr)
+                sys.exit(2)
+            from newsrec_amd.dist import spawn_ranks
+            sys.exit(spawn_ranks(world, [os.path.abspath(__file__)] + sys.argv[1:]))
+    else:
+        world = int(env_world)
+        if a.gpus is not None and a.gpus != world:
+            print("bench.py: --gpus %d but WORLD_SIZE=%d" % (a.gpus, world), file=sys.stderr)
+            sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and backend == "nccl" and torch.cuda.device_count() < world:
+        print("bench.py: WORLD_SIZE=%d needs %d GPUs under nccl, %d visible" % (world, world, torch.cuda.device_count()),
+              file=sys.stderr)
+        sys.exit(2)
     dev_index = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(dev_index)
         kw = {"device_id": torch.device("cuda", dev_index)} if backend == "nccl" else {}
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        if dist.get_world_size() != world:
+            raise RuntimeError("process group has %d ranks, expected %d" % (dist.get_world_size(), world))
     dev = torch.device("cuda", dev_index)
     from newsrec_amd.dist import GradSync
     torch.cuda.set_device(dev)

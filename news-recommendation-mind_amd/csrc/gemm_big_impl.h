@@ -169,7 +169,7 @@ __device__ __forceinline__ void tail_scatter_tr(const Args& g, f32x16 (&acc)[TI]
         const int64_t row = m0 + wm + 32 * i + rl;
         if (row >= g.M || col >= g.N) continue;
         const int64_t tok = g.Cm.idx[row];
-        if (tok == g.pad_row || (g.dbg & 32)) continue;   // dbg bit 32: timing only, no tail adds
+        if (tok == g.pad_row) continue;
         atomicAdd(g.C + tok * g.ldc + col, chunk[rl * CS + (lane & 31)]);
       }
     }
@@ -232,9 +232,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
   f32x16 acc[TI][TJ];
   LA la;
   LB lb;
-  // static arbitration priority for one half of the workgroup (waves w and w + 4 share a SIMD):
-  // NR_GEMM_DEBUG bit 8 raises waves 4-7, bit 16 waves 0-3 (A/B timing)
-  if (((g.dbg & 8) && w >= 4) || ((g.dbg & 16) && w < 4)) __builtin_amdgcn_s_setprio(1);
 
   // persistent over this block's units (virtual ids blockIdx.x + j * gridDim.x); each unit runs its
   // own two-deep pipeline, so the k-loop carries no unit bookkeeping (a pipeline refill per unit
@@ -327,11 +324,10 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
           NR_MF(0, 0);
 #undef NR_MF
         }
-        // (g.dbg bits 2 / 4: timing experiments only -- skip the split-stores / the loads)
-        if (i == 0 && stage_next && !(g.dbg & 2)) la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid);
+        if (i == 0 && stage_next) la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid);
         if (i == 1 && stage_next) {
-          if (!(g.dbg & 2)) lb.template store<NS, NP>(Bs + (st ^ 1) * NP * PB, tid);
-          if (kt + 3 < nt && !(g.dbg & 4)) issue(nset, kt + 3);
+          lb.template store<NS, NP>(Bs + (st ^ 1) * NP * PB, tid);
+          if (kt + 3 < nt) issue(nset, kt + 3);
         }
       }
       __syncthreads();   // stage st fully read; stage st^1 fully written

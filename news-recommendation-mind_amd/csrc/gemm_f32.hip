@@ -294,15 +294,6 @@ int launch_kc(const Args& g, int ak, int bk, int splits, hipStream_t s) {
   return launch<BM, BN, false, false>(g, splits, s);
 }
 
-bool getenv_generic() {   // NR_GEMM_GENERIC=1 forces the generic kernel (A/B testing)
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NR_GEMM_GENERIC");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v == 1;
-}
-
 int pick_tile(int64_t n) {  // 64 or 128: least padding, ties -> 128
   const int64_t p64 = (n + 63) / 64 * 64, p128 = (n + 127) / 128 * 128;
   return p128 <= p64 ? 128 : 64;
@@ -341,17 +332,14 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
   if ((epilogue == NR_EPI_SCATTER_STORE || epilogue == NR_EPI_SCATTER_ZEROED) &&
       (!c_rows || c_rows->map != NR_ROWS_GATHER || !c_rows->rows))
     return NR_EINVAL(4);
-  if (!getenv_generic()) {
+  {
     const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128) * splits;
-    // bf16x6: small problems (< 400 tiles of 128x128) take 64x64 tiles, which only the exact-f32
-    // kernel has (they are latency-bound, and 128x128 bf16x6 tiles would leave most CUs idle).
+    // bf16x6 and f32: small problems (< 400 tiles of 128x128) take 64x64 tiles, which only the
+    // exact-f32 kernel has (they are latency-bound, and 128x128 tiles would leave most CUs idle);
+    // larger ones take 128x128 tiles (bf16x6: the split kernels; f32: the exact-f32 128x128 kernel).
     // bf16: every eligible shape runs on the bf16 kernel (one product per tile is cheap).
-    static int small_min = -1;   // NR_GEMM_SMALL128 = tile count from which bf16x6 takes 128x128 (A/B)
-    if (small_min < 0) {
-      const char* e = getenv("NR_GEMM_SMALL128");
-      small_min = e ? atoi(e) : 400;
-    }
-    const int fb = (prec == NR_GEMM_BF16 || (prec == NR_GEMM_BF16X6 && t128 >= small_min)) ? 128 : 64;
+    const int64_t small_min = 400;
+    const int fb = (prec == NR_GEMM_BF16 || t128 >= small_min) ? 128 : 64;
     const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, fb, fb, nullptr,
                                 nullptr, prec, stream);
     if (rc != -1) return rc;

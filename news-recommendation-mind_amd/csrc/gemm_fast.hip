@@ -40,18 +40,11 @@ double round_eff(int64_t units, int64_t slots) {
 }
 
 int big_bn(int64_t M, int64_t N, int64_t K, int splits, bool resplit, bool m_dyn, int kmin) {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("NR_GEMM_BIG");
-    mode = e ? atoi(e) : 1;
-  }
-  if (mode == 0) return -1;   // disabled (also for NR_EPI_SCATTER_ZEROED's tail split)
   if (N < 128) return 0;
   // a short contraction (K < kmin) does not amortise the per-unit pipeline fill
   if (!resplit && K < kmin) return 0;
   const int64_t gm = (M + 255) / 256;
   if (!resplit && gm * splits < 8) return 0;
-  if (mode == 128 || mode == 256) return mode;
   if (resplit) return (N % 256 == 0 || N >= 1024) ? 256 : 128;
   // device-resident M (distinct-row counts): the host M is only a bound, so the round efficiency is
   // unknown; the persistent grid absorbs the actual count -- take the big tiles for wide N
@@ -109,14 +102,6 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   g.C = C; g.ldc = ldc; g.bias = bias; g.epi = epilogue; g.pad_row = pad_row;
   g.mdyn = m_dev; g.kdyn = k_dev; g.splits = 1; g.tail = 0;
   {
-    static int dbg = -1;
-    if (dbg < 0) {
-      const char* e = getenv("NR_GEMM_DEBUG");
-      dbg = e ? atoi(e) : 0;
-    }
-    g.dbg = dbg;
-  }
-  {
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     bool v = N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!bias || al16(bias));
     if (epilogue == NR_EPI_ACCUM_GATE || epilogue == NR_EPI_STORE_GELU || epilogue == NR_EPI_GELU_GRAD)
@@ -129,26 +114,13 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   const int splits = (int)((K + g.kchunk - 1) / g.kchunk) > 0 ? (int)((K + g.kchunk - 1) / g.kchunk) : 1;
   if (bm == 128 && bn == 128 && prec != NR_GEMM_F32) {
     const bool resplit = split_k > 1 && (epilogue == NR_EPI_ATOMIC || epilogue == NR_EPI_SCATTER);
-    // shortest contraction the big kernel takes: 512 (32 k-tiles of MFMAs per unit fill); under bf16
-    // NR_GEMM_BIG_MINK_BF16 lowers it (A/B: the CNN table dgrad, K = 480, ran 94 us on the 128x128
-    // kernel and 114 us on the big one)
-    static int kmin_bf16 = -1;
-    if (kmin_bf16 < 0) {
-      const char* e = getenv("NR_GEMM_BIG_MINK_BF16");
-      kmin_bf16 = e ? atoi(e) : 512;
-    }
-    const int kmin = prec == NR_GEMM_BF16 ? kmin_bf16 : 512;
+    // shortest contraction the big kernel takes: 512 (32 k-tiles of MFMAs per unit fill), in bf16 too
+    // (A/B: the CNN table dgrad, K = 480, ran 94 us on the 128x128 kernel and 114 us on the big one)
+    const int kmin = 512;
     const bool tailed = zeroed && splits == 1 && K >= kmin && N >= 256 && big_bn(M, N, K, 1, false, false, kmin) >= 0;
     // bf16 split-K (atomic) launches take the big kernel too: its fewer, larger units halve the operand
-    // re-reads and keep three k-tiles of loads in flight (CNN conv weight gradient 200 -> 138 us;
-    // NR_GEMM_BIG_BF16_SPLIT=0: the 128x128 kernel)
-    static int big_bf16_split = -1;
-    if (big_bf16_split < 0) {
-      const char* e = getenv("NR_GEMM_BIG_BF16_SPLIT");
-      big_bf16_split = e ? atoi(e) : 1;
-    }
-    const int bb = (resplit && prec == NR_GEMM_BF16 && !big_bf16_split)
-                       ? 0 : big_bn(M, N, K, splits, resplit, m_dev != nullptr, kmin);
+    // re-reads and keep three k-tiles of loads in flight (CNN conv weight gradient 200 -> 138 us)
+    const int bb = big_bn(M, N, K, splits, resplit, m_dev != nullptr, kmin);
     const int BN = tailed ? 256 : (bb > 0 ? bb : 0);
     if (BN) {
       Args gb = g;

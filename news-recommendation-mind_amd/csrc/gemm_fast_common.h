@@ -73,7 +73,6 @@ struct Args {
   int splits;
   const int32_t* mdyn;   // device-resident M (<= M), or null
   const int32_t* kdyn;   // device-resident K (<= K), or null
-  int dbg;   // NR_GEMM_DEBUG bits (timing experiments only): 1 = skip the output stores
   int tail;  // big kernel, NR_EPI_SCATTER_ZEROED: max K pieces of the last partial round's tiles (0 = off)
 };
 
@@ -487,17 +486,6 @@ __device__ __forceinline__ void epilogue_cmajor(const Args& g, f32x16 (&acc)[TI]
 template <int TI, int TJ>
 __device__ __forceinline__ void epilogue(const Args& g, f32x16 (&acc)[TI][TJ], int64_t m0, int64_t n0, int wm,
                                          int wn, int h, int c) {
-  if (g.dbg & 1) {   // timing experiment: keep the accumulators live, store nothing
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s += acc[i][j][r];
-    if (s == 1234.5678f) g.C[0] = s;
-    return;
-  }
   const bool vec = g.vec;
   switch (g.epi) {
     case NR_EPI_STORE: epilogue_t<NR_EPI_STORE, TI, TJ>(g, acc, m0, n0, wm, wn, h, c, vec); break;
@@ -518,15 +506,6 @@ __device__ __forceinline__ void epilogue_any(const Args& g, f32x16 (&acc)[TI][TJ
                                              int wn, int h, int c) {
   if (TR) {
     epilogue<TI, TJ>(g, acc, m0, n0, wm, wn, h, c);
-  } else if (g.dbg & 1) {   // timing experiment: keep the accumulators live, add nothing
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s += acc[i][j][r];
-    if (s == 1234.5678f) g.C[0] = s;
   } else if (g.epi == NR_EPI_ATOMIC) {
     epilogue_cmajor<NR_EPI_ATOMIC, TI, TJ>(g, acc, m0, n0, wm, wn, h, c);
   } else {
@@ -576,15 +555,6 @@ int resident_slots(Kern k) {
     cache[dev] = cus * per;
   }
   return cache[dev];
-}
-
-inline bool persistent_disabled() {   // NR_GEMM_NOPERSIST=1: one unit per block (A/B testing)
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NR_GEMM_NOPERSIST");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v == 1;
 }
 
 // bf16 launches of the 128x128 fast-path operand combinations (gemm_split_*.hip), np = 3 (bf16x6)

@@ -188,7 +188,7 @@ int launch(const Args& g, int splits, hipStream_t s) {
   if (units <= 0) return NR_OK;
   if (units > 0x7fffffff) return NR_EINVAL(0);
   int grid = (int)units;
-  if (!persistent_disabled()) {
+  {
     const int slots = resident_slots(gemm_fast_kernel<BM, BN, AM, BMODE, TR>);
     if (slots > 0 && slots < grid) grid = slots;
   }

@@ -113,8 +113,6 @@ struct MPArgs {
   const float* dz; int64_t lddz;      // bwd: optional grad of Z
   float* dy; int64_t lddy;            // bwd: [T][heads*dk + heads*dv]
   float* dbias; float* dq; float* dgamma; float* dbeta;
-  int dbg;                            // timing-only ablations (NR_DEBUG_MHAPOOL): 1 = skip attention, 2 = skip LN/pool,
-                                      // 8 / 16 = skip the LN-pass / head-pass parameter-gradient atomics
   float* o; int64_t ldo;              // fwd: optional saved attention output O (pre-LN); bwd: its input
   float* dob; int64_t lddob;          // split bwd: dO rows (kernel 1 writes, kernel 2 reads)
   int rows_per_wave;                  // staged row indices per wave (split bwd kernel 2) or per block
@@ -344,7 +342,7 @@ __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
   const uint64_t bits = token_bits(g, seq);
   stage_rows(g, seq);
-  if (!(g.dbg & 1)) attention_to_lds<DK, DV, NP>(g, seq, bits, os, SO);
+  attention_to_lds<DK, DV, NP>(g, seq, bits, os, SO);
   // the LayerNorm / pooling vectors are loaded only now: held through the attention phase they
   // would raise its register peak (and so lower the titles in flight per CU)
   float gam[NH64], bet[NH64], qv[NH64];
@@ -355,7 +353,6 @@ __global__ __launch_bounds__(768) void mha_pool_fwd_kernel(MPArgs g) {
     qv[k] = g.q[lane + 64 * k];
   }
   __syncthreads();
-  if (g.dbg & 2) return;
   // LayerNorm + dropout in place, scores; one wave per row
   for (int l = w; l < g.L; l += nw) {
     const int64_t row = seq * g.L + l;
@@ -684,7 +681,7 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
   const int tid = threadIdx.x, w = tid >> 6;
   const uint64_t bits = token_bits(g, seq);
   stage_rows(g, seq);
-  if (!(g.dbg & 1)) attention_to_lds<DK, DV, NP>(g, seq, bits, os, SO);
+  attention_to_lds<DK, DV, NP>(g, seq, bits, os, SO);
   if (tid < 32) {
     ps[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
     st[2 * tid] = tid < g.L ? g.stats[2 * (seq * g.L + tid)] : 0.f;
@@ -692,7 +689,6 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
   }
   __syncthreads();
   pool_ln_bwd<NH64>(g, seq, os, ps, ds, st, red, kb, nullptr, 0);
-  if (g.dbg & 4) return;
   float* tw = ts + w * 32 * 33;
   for (int head = w; head < g.heads; head += nw) {
     DoSource<DV> dO{os + head * DV, SO, g.L, false};
@@ -811,7 +807,6 @@ __global__ __launch_bounds__(256) void mha_ln_bwd_kernel(MPArgs g) {
     red[w][2][lane + 64 * k] = dqp[k];
   }
   __syncthreads();
-  if (g.dbg & 8) return;   // timing experiment only: no parameter-gradient atomics
   float* ogam = g.ws ? grad_slot(g, 0) : g.dgamma;
   float* obet = g.ws ? grad_slot(g, H) : g.dbeta;
   float* oq = g.ws ? grad_slot(g, 2 * H) : g.dq;
@@ -871,7 +866,7 @@ __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
     head_bwd<DK, DV, NP>(g, seq, head, bits, tw, dO, cs);
     wave_lds_fence();   // the next title's row indices / dO overwrite these
   }
-  if (!(g.dbg & 16)) flush_dbias<DK, DV>(g, head, cs);   // (bit 16: timing experiment only)
+  flush_dbias<DK, DV>(g, head, cs);
 }
 
 // out[i] += Σ_c ws[c][i] over the copies, each copy re-zeroed (the workspace is left zero for the
@@ -916,13 +911,7 @@ int launch_np(const MPArgs& g, Pass pass, hipStream_t s) {
     // FOUR waves per title, each taking heads w, w + 4, ...: the workgroup's 49.5 KB LDS image then
     // lets three titles share a CU (one wave per head, 12 waves at 104 VGPRs, fit one title per CU,
     // whose barrier-separated phases left the CU idle on every load latency: 105 us per NRMS step).
-    // NR_MHAPOOL_FWD_WAVES overrides (A/B timing).
-    static int env_nw = -1;
-    if (env_nw < 0) {
-      const char* e = getenv("NR_MHAPOOL_FWD_WAVES");
-      env_nw = e ? atoi(e) : 0;
-    }
-    const int nw = env_nw >= 4 && env_nw <= 12 ? env_nw : 4;
+    const int nw = 4;
     const size_t sz = fwd_smem(H);
     allow_smem(mha_pool_fwd_kernel<DK, DV, NH64, NP>, sz);
     hipLaunchKernelGGL((mha_pool_fwd_kernel<DK, DV, NH64, NP>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
@@ -994,10 +983,6 @@ extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows
   g.o = oout; g.ldo = ldo;
   if (oout && ((ldo & 3) || ldo < (int64_t)heads * dv)) return NR_EINVAL(3);
   g.np = prec == NR_GEMM_BF16X6 ? 3 : prec == NR_GEMM_BF16 ? 1 : 0;
-  {
-    const char* e = getenv("NR_DEBUG_MHAPOOL");
-    g.dbg = e ? atoi(e) : 0;
-  }
   return dispatch(g, dk, dv, FWD, stream);
 }
 
@@ -1034,9 +1019,5 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
   if (ws && (!o || ws_copies < 1 || ws_copies > 1024)) return NR_EINVAL(5);
   g.ws = ws; g.ws_copies = ws_copies;
   g.ws_ld = ((int64_t)3 * heads * dv + (int64_t)heads * (dk + dv) + 3) & ~int64_t(3);
-  {
-    const char* e = getenv("NR_DEBUG_MHAPOOL");
-    g.dbg = e ? atoi(e) : 0;
-  }
   return dispatch(g, dk, dv, o ? BWD_SPLIT : BWD_FUSED, stream);
 }

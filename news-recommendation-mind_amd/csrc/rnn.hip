@@ -398,15 +398,6 @@ __global__ __launch_bounds__(((G * H + 63) / 64) * 64) void rnn_bwd_reg_kernel(R
 
 size_t rnn_smem(int cell, int H) { return (size_t)(2 * H + (cell == NR_CELL_LSTM ? 4 : 3) * H + 4) * sizeof(float); }
 
-bool reg_disabled() {   // NR_RNN_STREAM=1: the L2-streaming kernels (A/B, any H)
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("NR_RNN_STREAM");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v == 1;
-}
-
 }  // namespace
 
 extern "C" int nr_rnn_fwd(int32_t cell, const float* gx, int64_t ldgx, const float* whh_t, const float* bhh,
@@ -420,7 +411,7 @@ extern "C" int nr_rnn_fwd(int32_t cell, const float* gx, int64_t ldgx, const flo
   g.cell = cell; g.gx = gx; g.ldgx = ldgx; g.whh = whh_t; g.bhh = bhh; g.h0 = h0; g.ldh0 = ldh0;
   g.h0_idx = h0_idx; g.mask = mask; g.mask_dt = mask_dtype; g.reverse = reverse; g.B = B; g.N = N; g.H = H;
   g.gates = gates; g.hprev = hprev; g.cprev = cprev; g.hout = hout; g.ldho = ldho;
-  if (H == 150 && !reg_disabled()) {
+  if (H == 150) {
     if (cell == NR_CELL_LSTM) hipLaunchKernelGGL((rnn_fwd_reg_kernel<150, 4, 88>), dim3((unsigned)B), dim3(640), 0, stream, g);
     else hipLaunchKernelGGL((rnn_fwd_reg_kernel<150, 3, 150>), dim3((unsigned)B), dim3(512), 0, stream, g);
     NR_LAUNCH_CHECK();
@@ -445,7 +436,7 @@ extern "C" int nr_rnn_bwd(int32_t cell, const float* whh, const float* gates, co
   g.cprev = const_cast<float*>(cprev); g.mask = mask; g.mask_dt = mask_dtype; g.reverse = reverse; g.B = B;
   g.N = N; g.H = H; g.dhout = dhout; g.lddho = lddho; g.dgi = dgi; g.dgh = dgh; g.lddg = lddg; g.dh0 = dh0;
   g.lddh0 = lddh0;
-  if (H == 150 && !reg_disabled()) {
+  if (H == 150) {
     if (cell == NR_CELL_LSTM) hipLaunchKernelGGL((rnn_bwd_reg_kernel<150, 4>), dim3((unsigned)B), dim3(640), 0, stream, g);
     else hipLaunchKernelGGL((rnn_bwd_reg_kernel<150, 3>), dim3((unsigned)B), dim3(512), 0, stream, g);
     NR_LAUNCH_CHECK();

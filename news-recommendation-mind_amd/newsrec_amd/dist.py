@@ -30,6 +30,59 @@ def setup(rank, world_size, backend="nccl", master_port="12355"):
     dist.init_process_group(backend, rank=rank, world_size=world_size, timeout=timedelta(minutes=30), **kw)
 
 
+def free_port(host="127.0.0.1"):
+    """An unused TCP port on ``host`` for the rendezvous (the reference hard-codes 12355,
+    Manager.py:160, which collides when two jobs share a node)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind((host, 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(world_size, argv, env=None, timeout=None):
+    """twotower.py:62-73 (``mp.spawn(main, nprocs=world_size, join=True)``) for a script: start
+    ``world_size`` fresh interpreters running ``argv`` with RANK / LOCAL_RANK / WORLD_SIZE /
+    LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (torch.distributed.run's environment), wait
+    for all of them and return the first non-zero exit code (0 when every rank succeeded).
+
+    The caller must not have touched the GPU: each rank initialises its own device.  Like
+    ``mp.spawn(join=True)``, one failing rank ends the job: the others are terminated by PID."""
+    import subprocess
+    import sys
+    import time
+    base = dict(os.environ if env is None else env)
+    base.setdefault("MASTER_ADDR", "127.0.0.1")
+    base["MASTER_PORT"] = str(free_port(base["MASTER_ADDR"]))
+    procs = []
+    for r in range(world_size):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world_size),
+                 LOCAL_WORLD_SIZE=str(world_size), GROUP_RANK="0")
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=e))
+    t0 = time.monotonic()
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+        if rc != 0 or (timeout is not None and time.monotonic() - t0 > timeout):
+            rc = rc or 124
+            for p in procs:
+                p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        time.sleep(0.05)
+    return rc
+
+
 def shard_train(n, world_size, rank, shuffle=False, seed=0, epoch=0):
     """torch.utils.data.DistributedSampler index order (Manager.py:212): optional seeded
     shuffle, pad to a multiple of world_size by repeating from the front, take rank::world."""
@@ -142,6 +195,14 @@ class GradSync:
         return buf
 
     def _sparse_reduce(self, table, ids, gs):
+        buf = self._dense.get(id(table))
+        if buf is not None and table.grad is not None and table.grad.data_ptr() == buf.data_ptr() \
+                and not self.deferred:
+            # eager mode: the buffer still installed as .grad from the previous step (grads not set
+            # to None) could hold a dense gradient accumulated this step, which the row re-zeroing
+            # would partly erase and the exchange would never reduce
+            raise RuntimeError("GradSync: %s.grad is still the row-sparse exchange buffer; call "
+                               "optimizer.zero_grad(set_to_none=True) before backward" % type(table).__name__)
         g = self._sparse_buffer(table)
         for r in range(self.world):      # rank order: every rank forms the same sum
             g.index_add_(0, ids[r], gs[r])
@@ -153,6 +214,8 @@ class GradSync:
             functions.TABLE_GRAD_HOOK.set(None)
         if self.use_sparse:
             functions.SPARSE_GRAD_HOOK.set(None)
+        self._dense.clear()       # the row-sparse buffers (526 MB for the LSTUR user table)
+        self._touched.clear()
 
     def _buckets(self, params):
         """-> [(params, inplace)]: big gradients alone and in place, the rest in flat buckets."""

@@ -44,11 +44,18 @@ _GRAD_COPIES_WS = {}
 
 
 def _grad_copies(dev, width):
-    """A persistent zeroed [GRAD_COPIES, ceil4(width)] workspace per (device, stream, width) for
-    nr_mha_pool_bwd's spread parameter-gradient atomics (the kernel leaves it zero again)."""
-    key = (dev, torch.cuda.current_stream(dev).cuda_stream, width)
+    """A persistent zeroed [GRAD_COPIES, ceil4(width)] workspace per (device, width) for
+    nr_mha_pool_bwd's spread parameter-gradient atomics (the kernel leaves it zero again).
+
+    Created eagerly, never inside a graph capture: a buffer first allocated (and zero-filled) during
+    a capture would only be zero once that graph had replayed, and a later graph reusing it would
+    depend on that replay order.  Steps run one at a time on a device, so one workspace per
+    (device, width) serves every stream."""
+    key = (torch.device(dev), width)
     ws = _GRAD_COPIES_WS.get(key)
     if ws is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise L.HipError("nr_mha_pool_bwd workspace must be created by an eager step before graph capture")
         ws = _GRAD_COPIES_WS[key] = torch.zeros(GRAD_COPIES, (width + 3) // 4 * 4, device=dev)
     return ws
 
@@ -124,11 +131,12 @@ class _Probe:
 
 PROBE = _Probe()
 
-# Distinct-row projection in the MHA news tower (NR_DEDUP_ROWS=0 projects every token row).
-DEDUP_ROWS = os.environ.get("NR_DEDUP_ROWS", "1") != "0"
-# Training forward saves the attention output; the backward runs split (NR_SPLIT_BWD=0: fused
-# backward that recomputes the attention).
-SPLIT_BWD = os.environ.get("NR_SPLIT_BWD", "1") != "0"
+# Distinct-row projection in the news towers (False projects every token row: the token-wise form
+# the parity tests compare it with; module attributes, not environment switches).
+DEDUP_ROWS = True
+# Training forward saves the attention output; the backward runs split (False: the fused backward
+# that recomputes the attention).
+SPLIT_BWD = True
 
 
 class _TableGradHook:

@@ -122,3 +122,38 @@ def test_partition_sampler_contiguous():
     ds = list(range(10))
     parts = [list(D.Partition_Sampler(ds, 3, r)) for r in range(3)]
     assert parts == [[0, 1, 2], [3, 4, 5], [6, 7, 8, 9]]
+
+
+_CHILD = r"""
+import os, sys, torch.distributed as dist
+dist.init_process_group("gloo")
+assert dist.get_world_size() == int(os.environ["WORLD_SIZE"])
+assert os.environ["LOCAL_RANK"] == os.environ["RANK"]
+import torch
+t = torch.tensor([dist.get_rank() + 1.0])
+dist.all_reduce(t)
+if dist.get_rank() == 0:
+    print("SUM", float(t), flush=True)
+rank = dist.get_rank()
+dist.barrier()
+dist.destroy_process_group()
+sys.exit(3 if int(os.environ.get("FAIL_RANK", "-1")) == rank else 0)
+"""
+
+
+def test_spawn_ranks_world3(tmp_path, capfd):
+    """bench.py --gpus N without WORLD_SIZE: dist.spawn_ranks launches N fresh ranks with
+    torch.distributed.run's environment (twotower.py:62-73 mp.spawn) and joins them."""
+    script = tmp_path / "child.py"
+    script.write_text(_CHILD)
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    assert D.spawn_ranks(3, [str(script)], env=env, timeout=120) == 0
+    assert "SUM 6.0" in capfd.readouterr().out
+
+
+def test_spawn_ranks_failure_propagates(tmp_path):
+    script = tmp_path / "child.py"
+    script.write_text(_CHILD)
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["FAIL_RANK"] = "1"
+    assert D.spawn_ranks(2, [str(script)], env=env, timeout=120) == 3

@@ -143,3 +143,24 @@ def test_data_parallel_real_model_world2(case, mode):
             # 1e-3 lr.  A missing or wrong exchange moves most elements off.
             assert dmax <= 4 * 2 * 1e-4 + 1e-6, (rank, n, dmax)
             assert n_off <= max(4, 1e-3 * n_all), (rank, n, n_off, n_all)
+
+
+@pytest.mark.timeout(400)
+def test_bench_gpus2_spawns_two_ranks():
+    """`bench.py --gpus 2` (no WORLD_SIZE) must launch two ranks itself (twotower.py:62-73) and
+    report the live world size; gloo on the one leased GPU stands in for RCCL here."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["NR_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
+           "--eval-impr", "0", "--config-legs", "0", "--xformer-steps", "0", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=380)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-4000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    assert out["config"]["parallelism"] == "dp2"
+    assert out["config"]["global_batch"] == 64
+    assert out["value"] > 0

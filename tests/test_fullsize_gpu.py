@@ -1,7 +1,7 @@
 """End-to-end parity at the BENCHMARKED configuration (BASELINE configs[2], bench.py's headline):
 one NRMS train step at B = 32 impressions, V = 30522, H = 384, 12 heads, 5 candidates, 50-click
-history, 30-token titles — the bench's exact kernels (128x128 bf16x6 GEMMs over the distinct-row
-projection, the fused attention kernels, the split backward, Adam) — against the fp32 CPU oracle
+history, 30-token titles — the bench's exact kernels (the 256x256 persistent bf16x6 GEMMs over the
+distinct-row projection, the fused attention kernels, the split backward, Adam) — against the fp32 CPU oracle
 (oracle/restatement.py, which tests/test_oracle_golden.py pins to the reference's goldens):
 
 * logits within the north star's 1e-3 (models/TwoTowerBaseModel.py:65-75), the loss;

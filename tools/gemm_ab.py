@@ -1,6 +1,6 @@
-"""A/B timing of the GEMM kernels on the step's shapes: each NR_GEMM_BIG mode (0 = 128x128 kernel,
-128 / 256 = the large-tile kernel's BN, 1 = automatic) in its own process (the mode is read once),
-bf16x6 and bf16.  python tools/gemm_ab.py [--modes 0,1,128,256]"""
+"""A/B timing of the GEMM kernels on the step's shapes, bf16x6 and bf16: one process per library
+build (NR_LIB_PATH; variant builds come from tools/build_variant*.sh, the product library has no
+run-time switches).  python tools/gemm_ab.py [--libs base,ab/x/libnewsrec_hip.so] [--cases ...]"""
 import argparse
 import json
 import os
@@ -70,17 +70,16 @@ print(json.dumps(out))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--modes", default="0,1,128,256")
-    ap.add_argument("--variants", default=None,
-                    help="';'-separated env sets, e.g. 'NR_GEMM_BIG=1;NR_GEMM_BIG=1,NR_GEMM_DEBUG=2' (instead of --modes)")
+    ap.add_argument("--libs", default="base",
+                    help="comma-separated library paths ('base' = the in-tree build)")
     ap.add_argument("--cases", default=None, help="comma-separated case names (default: all)")
     a = ap.parse_args()
     res = {}
-    variants = ([dict(kv.split("=") for kv in v.split(",")) for v in a.variants.split(";")] if a.variants
-                else [{"NR_GEMM_BIG": m} for m in a.modes.split(",")])
-    for var in variants:
-        m = ",".join("%s=%s" % kv for kv in var.items())
-        env = dict(os.environ, **var)
+    for m in a.libs.split(","):
+        env = dict(os.environ)
+        env.pop("NR_LIB_PATH", None)
+        if m != "base":
+            env["NR_LIB_PATH"] = os.path.abspath(m)
         if a.cases:
             env["NR_AB_CASES"] = a.cases
         r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
