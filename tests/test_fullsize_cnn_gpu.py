@@ -37,17 +37,17 @@ LEGS = {"cnn_attn": "attn", "cnn_lstur": "lstur", "cnn_gru": "gru"}
 
 
 def _model(encU, dev):
+    """Reference init, then every parameter redrawn at the golden generator's scales
+    (tests/golden/params.py: candidate scores spread by O(1); reference init spreads them ~1e-4)."""
     from newsrec_amd.manager import build_model
+    from params import param_std
     torch.manual_seed(42)
     m = build_model("cnn", encU, H, vocab=V, device=dev, user_num=USERS)
-    with torch.no_grad():   # spread the candidate scores (reference init gives near-equal logits)
-        m.embedding.bert_word_embedding.weight.normal_(0, 0.5)
-        m.encoderN.query_words.normal_(0, 1.0)
-        if hasattr(m.encoderU, "query_news"):
-            m.encoderU.query_news.normal_(0, 1.0)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            p.normal_(0, float(param_std(n, tuple(p.shape))))
         if hasattr(m.encoderU, "userEmbedding"):
-            m.encoderU.userEmbedding.weight.normal_(0, 0.5)
-            m.encoderU.userEmbedding.weight[0].zero_()
+            m.encoderU.userEmbedding.weight[0].zero_()   # RNN.py:82
     return m
 
 
