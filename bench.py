@@ -131,10 +131,16 @@ class GraphedStep:
     captured input buffers; dropout draws, negative sampling and Adam step counts advance on the
     device, so replays are real training steps.
 
-    Data parallel (``sync`` = a GradSync, N > 1): two graphs per step -- forward/backward (ending in
-    GradSync.prepare: bucket packing) and the optimizer (starting with GradSync.unpack) -- with the
-    step's RCCL collectives issued eagerly between them (GradSync.exchange), so no collective is
-    ever captured."""
+    Data parallel (``sync`` = a GradSync, N > 1): three graphs per step, the RCCL collectives issued
+    eagerly between them (no collective is ever captured; GradSync's docstring):
+      graph 1   forward + backward up to the word-table gradient (the projection weight-gradient GEMM
+                deferred, WGRAD_DEFER_HOOK);
+      issue     the word-table all-reduce starts on RCCL's stream;
+      graph W   the deferred weight-gradient GEMM on all but GradSync.collective_cus CUs + bucket
+                packing -- it runs BESIDE the all-reduce (twotower.py:49-50: DDP overlaps its bucket
+                all-reduces with the rest of the backward);
+      exchange  the remaining bucket all-reduces and the sparse exchange; wait for all;
+      graph 2   bucket unpacking + Adam."""
 
     def __init__(self, model, opt, feed, sync, warmup):
         self.feed = feed
@@ -156,10 +162,15 @@ class GraphedStep:
                 self.loss = train_step(model, opt, feed.form(), sync).detach()
             self.opt_graph = None
         else:
-            pool = torch.cuda.graph_pool_handle()   # both graphs share one memory pool
+            pool = torch.cuda.graph_pool_handle()   # the graphs share one memory pool
             with torch.cuda.graph(self.graph, pool=pool):
                 self.loss = forward_backward(model, opt, feed.form()).detach()
-                self.packed, self.rec = sync.prepare()
+                self.rec = sync.take_sparse()
+            self.wgraph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.wgraph, pool=pool):
+                outs = sync.run_deferred()
+                self.early, self.packed = sync.pack(self.rec, outs)
+            self.kept = sync.kept   # the deferred GEMMs' operands (graph 1's outputs) stay allocated
             self.opt_graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.opt_graph, pool=pool):
                 sync.unpack(self.packed)
@@ -171,7 +182,9 @@ class GraphedStep:
         self.opt.sync_lr()   # a scheduler's lr changes reach the captured Adam
         self.graph.replay()
         if self.opt_graph is not None:
-            self.sync.exchange(self.packed, self.rec)
+            works = self.sync.issue(self.early)
+            self.wgraph.replay()
+            self.sync.exchange(self.packed, self.rec, works)
             self.opt_graph.replay()
 
 

@@ -111,6 +111,15 @@ int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand* A, const 
                     const int32_t* m_dev, const int32_t* k_dev, int32_t prec,
                     hipStream_t stream);
 
+/* nr_gemm_f32_dyn whose persistent grid occupies at most max_cus CUs (0 = every CU), so that a
+ * collective issued on another stream just before it (the data-parallel word-table all-reduce,
+ * twotower.py:49-50's DDP bucket reduction) finds CUs to run on while the GEMM computes. */
+int nr_gemm_f32_dyn_cus(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B,
+                        float* C, int64_t ldc, const float* bias, int32_t epilogue,
+                        const nr_operand* c_rows, int64_t pad_row, int32_t split_k,
+                        const int32_t* m_dev, const int32_t* k_dev, int32_t prec, int32_t max_cus,
+                        hipStream_t stream);
+
 /* ------------------------------------------------------------------ distinct token rows */
 
 /* Distinct ids of a token batch (the news tower projects each word-table row once, not once

@@ -373,7 +373,7 @@ int launch_big(const Args& g, int splits, hipStream_t s) {
   if (units <= 0) return NR_OK;
   if (units > 0x7fffffff) return NR_EINVAL(0);
   int grid = (int)units;
-  const int slots = resident_slots_512(gemm_big_kernel<AM, BMODE, TR, NP, BN>);
+  const int slots = capped_slots(resident_slots_512(gemm_big_kernel<AM, BMODE, TR, NP, BN>), g.max_cus);
   if (slots > 0 && slots < grid) grid = slots;
   Args a = g;
   a.splits = splits;

@@ -341,7 +341,7 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
     const int64_t small_min = 400;
     const int fb = (prec == NR_GEMM_BF16 || t128 >= small_min) ? 128 : 64;
     const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, fb, fb, nullptr,
-                                nullptr, prec, stream);
+                                nullptr, prec, 0, stream);
     if (rc != -1) return rc;
   }
   // generic kernel: same sums via atomics
@@ -373,6 +373,15 @@ extern "C" int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand
                                float* C, int64_t ldc, const float* bias, int32_t epilogue,
                                const nr_operand* c_rows, int64_t pad_row, int32_t split_k, const int32_t* m_dev,
                                const int32_t* k_dev, int32_t prec, hipStream_t stream) {
+  return nr_gemm_f32_dyn_cus(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, m_dev, k_dev, prec, 0,
+                             stream);
+}
+
+extern "C" int nr_gemm_f32_dyn_cus(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B,
+                                   float* C, int64_t ldc, const float* bias, int32_t epilogue,
+                                   const nr_operand* c_rows, int64_t pad_row, int32_t split_k, const int32_t* m_dev,
+                                   const int32_t* k_dev, int32_t prec, int32_t max_cus, hipStream_t stream) {
+  if (max_cus < 0) return NR_EINVAL(15);
   if (M < 0 || N < 0 || K < 0 || (K % 32)) return NR_EINVAL(0);
   if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(14);
   if (epilogue < NR_EPI_STORE || epilogue > NR_EPI_SCATTER_ZEROED) return NR_EINVAL(3);
@@ -390,6 +399,6 @@ extern "C" int nr_gemm_f32_dyn(int64_t M, int64_t N, int64_t K, const nr_operand
   if (split_k > 1 && epilogue != NR_EPI_ATOMIC && epilogue != NR_EPI_SCATTER) return NR_EINVAL(5);
   if (M == 0 || N == 0 || K == 0) return NR_OK;
   const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, 128, 128, m_dev,
-                              k_dev, prec, stream);
+                              k_dev, prec, max_cus, stream);
   return rc == -1 ? NR_EINVAL(7) : rc;
 }

@@ -63,7 +63,7 @@ int big_bn(int64_t M, int64_t N, int64_t K, int splits, bool resplit, bool m_dyn
 int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B, float* C,
                  int64_t ldc, const float* bias, int32_t epilogue, const nr_operand* c_rows, int64_t pad_row,
                  int32_t split_k, int bm, int bn, const int32_t* m_dev, const int32_t* k_dev, int32_t prec,
-                 hipStream_t stream) {
+                 int32_t max_cus, hipStream_t stream) {
   using namespace nrfast;
   if (K <= 0) return -1;
   // NR_EPI_SCATTER_ZEROED = NR_EPI_SCATTER_STORE whose destination rows are zero on entry: the big
@@ -100,7 +100,7 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   if (epilogue == NR_EPI_SCATTER_STORE && (!c_rows || c_rows->map != NR_ROWS_GATHER || !c_rows->rows)) return -1;
   if (epilogue == NR_EPI_SCATTER && c_rows && c_rows->map == NR_ROWS_CONV3 && c_rows->seq_len == 1) return -1;
   g.C = C; g.ldc = ldc; g.bias = bias; g.epi = epilogue; g.pad_row = pad_row;
-  g.mdyn = m_dev; g.kdyn = k_dev; g.splits = 1; g.tail = 0;
+  g.mdyn = m_dev; g.kdyn = k_dev; g.splits = 1; g.tail = 0; g.max_cus = max_cus > 0 ? max_cus : 0;
   {
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     bool v = N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!bias || al16(bias));
@@ -127,9 +127,10 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
       if (tailed) gb.tail = 16;
       int sp = splits;
       if (resplit) {
-        // re-split for 256 x BN tiles: one wave of units over the 256 CUs, >= 512 k per split
+        // re-split for 256 x BN tiles: one wave of units over the CUs it may use, >= 512 k per split
         const int64_t tiles = ((M + 255) / 256) * ((N + BN - 1) / BN);
-        int64_t want = 256 / (tiles > 0 ? tiles : 1);
+        const int cus = g.max_cus > 0 ? g.max_cus : 256;
+        int64_t want = cus / (tiles > 0 ? tiles : 1);
         if (want > K / 512) want = K / 512;
         if (want > 64) want = 64;
         if (want < 1) want = 1;

@@ -74,7 +74,29 @@ struct Args {
   const int32_t* mdyn;   // device-resident M (<= M), or null
   const int32_t* kdyn;   // device-resident K (<= K), or null
   int tail;  // big kernel, NR_EPI_SCATTER_ZEROED: max K pieces of the last partial round's tiles (0 = off)
+  int max_cus;   // persistent grid limited to this many CUs (0 = all): leaves CUs to a concurrent collective
 };
+
+// CUs of the current device (cached)
+inline int device_cus() {
+  static int cache[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
+  if (cache[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cache[dev] = cus;
+  }
+  return cache[dev];
+}
+
+// persistent grid of `slots` resident workgroups (all CUs) capped to max_cus CUs' worth
+inline int capped_slots(int slots, int max_cus) {
+  const int cus = device_cus();
+  if (max_cus <= 0 || cus <= 0 || max_cus >= cus || slots <= 0) return slots;
+  const int per = slots / cus > 0 ? slots / cus : 1;
+  return per * max_cus;
+}
 
 // Register-staged tile loader for an operand of R rows (the M or N extent) x 32 k.
 template <int R, int MODE>

@@ -189,7 +189,7 @@ int launch(const Args& g, int splits, hipStream_t s) {
   if (units > 0x7fffffff) return NR_EINVAL(0);
   int grid = (int)units;
   {
-    const int slots = resident_slots(gemm_fast_kernel<BM, BN, AM, BMODE, TR>);
+    const int slots = capped_slots(resident_slots(gemm_fast_kernel<BM, BN, AM, BMODE, TR>), g.max_cus);
     if (slots > 0 && slots < grid) grid = slots;
   }
   Args a = g;

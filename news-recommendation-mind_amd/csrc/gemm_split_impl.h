@@ -193,7 +193,7 @@ int launch_split(const Args& g, int splits, hipStream_t s) {
   if (units > 0x7fffffff) return NR_EINVAL(0);
   int grid = (int)units;
   {
-    const int slots = resident_slots(gemm_split_kernel<AM, BMODE, TR, NP>);
+    const int slots = capped_slots(resident_slots(gemm_split_kernel<AM, BMODE, TR, NP>), g.max_cus);
     if (slots > 0 && slots < grid) grid = slots;
   }
   Args a = g;

@@ -129,37 +129,80 @@ class GradSync:
       bucket (a few large collectives over xGMI instead of one per parameter); a gradient of
       >= ``inplace_mb`` MB is all-reduced in place, never copied into a bucket.
 
-    ``deferred`` (a train step replayed as HIP graphs, bench.GraphedStep at N > 1): the collectives
-    run between two graphs instead of inside the backward.  ``prepare()`` (captured at the end of
-    the forward/backward graph) packs the dense buckets and installs the sparse tables' persistent
-    gradient buffers, ``exchange(packed, records)`` (eager, between the graphs) runs every
-    collective, and ``unpack(packed)`` (captured at the head of the optimizer graph) copies the
-    reduced buckets back.  No RCCL call is ever captured, and the gradient tensors keep the graph
-    pool's static addresses.
+    ``deferred`` (a train step replayed as HIP graphs, bench.GraphedStep at N > 1): no collective
+    is ever captured; they run between graphs.  The news tower's projection weight-gradient GEMM
+    (WGRAD_DEFER_HOOK) is taken out of the backward, so the step is three graphs:
+      1. forward + backward up to the word-table gradient, then ``take_sparse()`` (the sparse
+         tables' persistent gradient buffers);
+      -- ``issue(early)``: the word-table all-reduce (and any other in-place bucket complete after
+         graph 1) starts on RCCL's stream;
+      2. ``run_deferred()`` (the weight-gradient GEMMs, on ``gemm_cus`` CUs so RCCL keeps some)
+         + ``pack()`` of the remaining dense buckets -- this graph runs BESIDE the all-reduce;
+      -- ``exchange(packed, records, works)``: the bucket all-reduces and the sparse exchange, then
+         every collective is waited for;
+      3. ``unpack(packed)`` + the optimizer.
+    The gradient tensors keep the graph pool's static addresses.
     """
 
     def __init__(self, model, group=None, overlap_tables=True, sparse_tables=True, bucket_mb=128, inplace_mb=16,
-                 deferred=False):
+                 deferred=False, collective_cus=16):
         self.model = model
         self.group = group
         self.world = dist.get_world_size(group)
         self.pending = []
         self.sparse = []
-        self._dense, self._touched = {}, {}
+        self._dense, self._touched, self._gather_bufs = {}, {}, {}
         self.bucket_elems = int(bucket_mb * (1 << 20) // 4)
         self.inplace_elems = int(inplace_mb * (1 << 20) // 4)
         self.overlap = overlap_tables and self.world > 1
         self.use_sparse = sparse_tables and self.world > 1
-        self.deferred = deferred
+        self.collective_cus = int(collective_cus)
         self._rec = []
+        self._runs = []
+        self._deferred = False
         if self.overlap:
             functions.TABLE_GRAD_HOOK.set(self._table_hook)
         if self.use_sparse:
             functions.SPARSE_GRAD_HOOK.set(self._sparse_hook)
+        self.deferred = deferred
+
+    @property
+    def deferred(self):
+        return self._deferred
+
+    @deferred.setter
+    def deferred(self, on):
+        self._deferred = bool(on)
+        if self.overlap:
+            functions.WGRAD_DEFER_HOOK.set(self._defer_hook if self._deferred else None, self.gemm_cus)
+
+    @property
+    def gemm_cus(self):
+        """CUs a weight-gradient GEMM running beside a collective may use (the rest stay free for
+        RCCL's kernels; 0 = no limit, e.g. without a GPU)."""
+        if not torch.cuda.is_available():
+            return 0
+        cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+        return max(1, cus - self.collective_cus) if self.collective_cus > 0 else 0
 
     @property
     def scale(self):
         return 1.0 / self.world
+
+    def _defer_hook(self, run, out):
+        self._runs.append((run, out))
+        return True
+
+    def run_deferred(self):
+        """Launch the weight-gradient GEMMs the backward deferred (graph 2 of the graphed step);
+        -> their output tensors.  ``self.kept`` holds the closures (and so their operands) alive
+        for a graph that captured them."""
+        runs, self._runs = self._runs, []
+        cus = self.gemm_cus
+        for run, _ in runs:
+            run(cus)
+        self.kept = runs
+        return [out for _, out in runs]
 
     def _table_hook(self, table, dtable):
         if self.deferred:          # an ordinary gradient: all-reduced in exchange()
@@ -174,12 +217,23 @@ class GradSync:
         if self.deferred:          # recorded; exchanged between the graphs
             self._rec.append((table, rows, grads))
             return True
-        ids = [torch.empty_like(rows) for _ in range(self.world)]
-        gs = [torch.empty_like(grads) for _ in range(self.world)]
-        w1 = dist.all_gather(ids, rows, group=self.group, async_op=True)
-        w2 = dist.all_gather(gs, grads, group=self.group, async_op=True)
+        ids, gs, w1, w2 = self._gather(table, rows, grads)
         self.sparse.append((table, ids, gs, w1, w2))
         return True
+
+    def _gather(self, table, rows, grads):
+        """Async all-gather of one sparse table's (row ids, gradient rows) into persistent
+        [world, n] / [world, n, E] buffers (no per-step allocation); -> (ids, grads, work, work)."""
+        key = id(table)
+        bufs = self._gather_bufs.get(key)
+        n = rows.numel()
+        if bufs is None or bufs[0].shape != (self.world, n) or bufs[1].shape[1:] != grads.shape:
+            bufs = (torch.empty(self.world, n, dtype=rows.dtype, device=rows.device),
+                    torch.empty((self.world,) + tuple(grads.shape), dtype=grads.dtype, device=grads.device))
+            self._gather_bufs[key] = bufs
+        w1 = dist.all_gather_into_tensor(bufs[0].view(-1), rows, group=self.group, async_op=True)
+        w2 = dist.all_gather_into_tensor(bufs[1].view(-1, *grads.shape[1:]), grads, group=self.group, async_op=True)
+        return bufs[0], bufs[1], w1, w2
 
     def _sparse_buffer(self, table):
         """The dense gradient of a row-sparse table, allocated and zeroed ONCE: each step only
@@ -206,16 +260,18 @@ class GradSync:
         g = self._sparse_buffer(table)
         for r in range(self.world):      # rank order: every rank forms the same sum
             g.index_add_(0, ids[r], gs[r])
-        self._touched[id(table)] = torch.cat(ids)
+        self._touched[id(table)] = ids.reshape(-1).clone()   # the gather buffer is reused next step
         return g
 
     def close(self):
         if self.overlap:
             functions.TABLE_GRAD_HOOK.set(None)
+            functions.WGRAD_DEFER_HOOK.set(None)
         if self.use_sparse:
             functions.SPARSE_GRAD_HOOK.set(None)
         self._dense.clear()       # the row-sparse buffers (526 MB for the LSTUR user table)
         self._touched.clear()
+        self._gather_bufs.clear()
 
     def _buckets(self, params):
         """-> [(params, inplace)]: big gradients alone and in place, the rest in flat buckets."""
@@ -237,19 +293,49 @@ class GradSync:
         return [p for p in self.model.parameters() if p.grad is not None and id(p) not in skip]
 
     # ---- deferred (graph) mode
-    def prepare(self):
-        """End of the forward/backward (graph): takes the step's sparse records, gives each sparse
-        table its persistent gradient buffer as .grad (the optimizer reads it) and packs the dense
-        gradients into flat buckets.  -> (packed, records) for exchange() / unpack()."""
+    def take_sparse(self):
+        """End of the forward/backward (graph 1): takes the step's sparse records and gives each
+        sparse table its persistent gradient buffer as .grad (the optimizer reads it)."""
         rec, self._rec = self._rec, []
         for table, _, _ in rec:
             table.grad = self._sparse_buffer_noreset(table)
+        return rec
+
+    def pack(self, rec, deferred_outs=()):
+        """-> (early, packed): in-place buckets complete after graph 1 (all-reduced while the
+        deferred GEMMs run), and the rest (in-place buckets a deferred GEMM writes, and flat copies
+        of the small gradients) for exchange() / unpack()."""
         skip = {id(t) for t, _, _ in rec}
-        packed = []
+        spans = [(o.data_ptr(), o.data_ptr() + o.numel() * o.element_size()) for o in deferred_outs]
+        grads = [p.grad for p in self.model.parameters() if p.grad is not None]
+        for s, e in spans:
+            # the deferred GEMM writes into the tensor the backward returned: autograd must have
+            # installed it (or views of it) as the parameters' .grad, not a copy
+            if not any(g.data_ptr() < e and s < g.data_ptr() + g.numel() * g.element_size() for g in grads):
+                raise RuntimeError("GradSync: a deferred weight gradient is not any parameter's .grad "
+                                   "(autograd copied it); its GEMM would write a detached buffer")
+        early, packed = [], []
         for bucket, inplace in self._buckets(self._dense_params(skip)):
-            flat = bucket[0].grad.view(-1) if inplace else torch.cat([p.grad.reshape(-1) for p in bucket])
-            packed.append((bucket, flat, inplace))
-        return packed, rec
+            if inplace:
+                g = bucket[0].grad
+                a, b = g.data_ptr(), g.data_ptr() + g.numel() * g.element_size()
+                late = any(a < e and s < b for s, e in spans)
+                (packed if late else early).append((bucket, g.view(-1), True))
+            else:
+                packed.append((bucket, torch.cat([p.grad.reshape(-1) for p in bucket]), False))
+        return early, packed
+
+    def prepare(self):
+        """The whole deferred preparation in one go (eager steps of a graphed run):
+        -> (buckets, records) for exchange() / unpack()."""
+        rec = self.take_sparse()
+        outs = self.run_deferred()
+        early, packed = self.pack(rec, outs)
+        return early + packed, rec
+
+    def issue(self, early):
+        """Start the all-reduce of the buckets complete after graph 1 (async, RCCL's stream)."""
+        return [dist.all_reduce(flat, group=self.group, async_op=True) for _, flat, _ in early]
 
     def _sparse_buffer_noreset(self, table):
         buf = self._dense.get(id(table))
@@ -258,14 +344,14 @@ class GradSync:
             self._dense[id(table)] = buf
         return buf
 
-    def exchange(self, packed, rec):
-        """Eager, between the graphs: every collective of the step."""
-        works = [dist.all_reduce(flat, group=self.group, async_op=True) for _, flat, _ in packed]
-        for table, rows, grads in rec:
-            ids = [torch.empty_like(rows) for _ in range(self.world)]
-            gs = [torch.empty_like(grads) for _ in range(self.world)]
-            dist.all_gather(ids, rows, group=self.group)
-            dist.all_gather(gs, grads, group=self.group)
+    def exchange(self, packed, rec, works=()):
+        """Eager, between the graphs: the remaining collectives of the step, then wait for all of
+        them (``works``: those ``issue`` started)."""
+        works = list(works) + [dist.all_reduce(flat, group=self.group, async_op=True) for _, flat, _ in packed]
+        gathers = [(table,) + self._gather(table, rows, grads) for table, rows, grads in rec]
+        for table, ids, gs, w1, w2 in gathers:
+            w1.wait()
+            w2.wait()
             self._sparse_reduce(table, ids, gs)
         for w in works:
             w.wait()

@@ -187,6 +187,34 @@ class _SparseGradHook:
 SPARSE_GRAD_HOOK = _SparseGradHook()
 
 
+class _WgradDeferHook:
+    """Optional callback ``hook(run, out) -> bool`` for the news tower's projection weight-gradient
+    GEMM (the longest kernel of the backward, issued after the word-table gradient).  ``run(max_cus)``
+    launches the GEMM into ``out`` (the zero-filled weight gradient already handed to autograd);
+    returning True means the callback launches it later itself -- GradSync's graphed data-parallel
+    step runs it in its own graph, beside the word-table all-reduce (twotower.py:49-50's DDP
+    overlap of the bucket reduction with the rest of the backward).
+
+    ``max_cus``: CUs the weight-gradient GEMM may occupy while a collective is in flight
+    (0 = all), so that RCCL's kernels are not locked out by the GEMM's one-workgroup-per-CU grid."""
+
+    def __init__(self):
+        self.fn = None
+        self.max_cus = 0
+
+    def set(self, fn, max_cus=0):
+        self.fn = fn
+        self.max_cus = int(max_cus)
+
+    def __call__(self, run, out):
+        if self.fn is None:
+            return False
+        return bool(self.fn(run, out))
+
+
+WGRAD_DEFER_HOOK = _WgradDeferHook()
+
+
 # ---------------------------------------------------------------------- MHA news encoder
 
 class MHANewsFn(torch.autograd.Function):
@@ -280,6 +308,7 @@ class MHANewsFn(torch.autograd.Function):
             # per-distinct-row gradient, then the two GEMMs over U rows instead of T tokens
             dYu = _empty(ur.cap, NY, table)
             ur.segment_sum(dY, dYu)
+            inflight = False
             if ctx.needs_input_grad[0]:
                 dtable = torch.zeros(V, E, device=table.device)
                 # distinct rows (M = U, not U_pad: no duplicate pad ids): plain row stores
@@ -288,9 +317,15 @@ class MHANewsFn(torch.autograd.Function):
                            c_rows=K.rows_map(ur.uids, L.ROWS_GATHER), pad_row=pad_row)
                 if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
                     dtable = None
-            K.gemm_dyn(NY, E, ur.cap, K.operand(dYu, L.MNCONTIG),
-                       K.operand(table, L.MNCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER), dw, k_dev=ur.u_pad,
-                       epilogue=L.EPI_ATOMIC, split_k=_split_k(NY, E, ur.cap))
+                    inflight = True   # the table's all-reduce runs beside the weight gradient
+            prec = ctx.prec
+
+            def wgrad(max_cus=0):
+                K.gemm_dyn(NY, E, ur.cap, K.operand(dYu, L.MNCONTIG),
+                           K.operand(table, L.MNCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER), dw, k_dev=ur.u_pad,
+                           epilogue=L.EPI_ATOMIC, split_k=_split_k(NY, E, ur.cap), prec=prec, max_cus=max_cus)
+            if not WGRAD_DEFER_HOOK(wgrad, dw):
+                wgrad(WGRAD_DEFER_HOOK.max_cus if inflight else 0)
         else:
             if ctx.needs_input_grad[0]:
                 dtable = torch.zeros(V, E, device=table.device)
@@ -479,6 +514,7 @@ class CNNNewsRowsFn(torch.autograd.Function):
         S = _empty(ur.cap, 3 * Hp, table)
         ur.segment_sum_conv3(dC, S, Hp, seq_len)
         dtable = None
+        inflight = False
         if ctx.needs_input_grad[0]:
             dtable = torch.zeros(V, E, device=dev)
             K.gemm_dyn(ur.cap, E, 3 * Hp, K.operand(S, L.KCONTIG), K.operand(w3t, L.MNCONTIG), dtable,
@@ -486,9 +522,11 @@ class CNNNewsRowsFn(torch.autograd.Function):
                        pad_row=pad_row)
             if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
                 dtable = None
+                inflight = True
         K.gemm_dyn(3 * Hp, E, ur.cap, K.operand(S, L.MNCONTIG),
                    K.operand(table, L.MNCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER), dw3t, k_dev=ur.u_pad,
-                   epilogue=L.EPI_ATOMIC, split_k=_split_k(3 * Hp, E, ur.cap))
+                   epilogue=L.EPI_ATOMIC, split_k=_split_k(3 * Hp, E, ur.cap),
+                   max_cus=WGRAD_DEFER_HOOK.max_cus if inflight else 0)
         return (dtable, None, None, dw3t, dconv_b, dwq, dbq, dq.view_as(query), None, None, None)
 
 

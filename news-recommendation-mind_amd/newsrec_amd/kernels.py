@@ -79,9 +79,10 @@ def gemm(M, N, K, A, B, C, ldc=None, bias=None, epilogue=L.EPI_STORE, c_rows=Non
 
 
 def gemm_dyn(M, N, K, A, B, C, m_dev=None, k_dev=None, ldc=None, bias=None, epilogue=L.EPI_STORE,
-             c_rows=None, pad_row=-1, split_k=1, prec=None):
+             c_rows=None, pad_row=-1, split_k=1, prec=None, max_cus=0):
     """``gemm`` with device-resident extents: M, K are upper bounds, the kernel reads the actual
-    M / K from the int32 CUDA scalars ``m_dev`` / ``k_dev`` (e.g. ``UniqueRows.counts[1:2]``)."""
+    M / K from the int32 CUDA scalars ``m_dev`` / ``k_dev`` (e.g. ``UniqueRows.counts[1:2]``).
+    ``max_cus`` > 0 limits the persistent grid to that many CUs (nr_gemm_f32_dyn_cus)."""
     _f32(C, bias)
     for t in (m_dev, k_dev):
         if t is not None and (t.dtype != torch.int32 or not t.is_cuda):
@@ -90,6 +91,11 @@ def gemm_dyn(M, N, K, A, B, C, m_dev=None, k_dev=None, ldc=None, bias=None, epil
         raise L.HipError("gemm_dyn: bias has %d < N=%d entries" % (bias.numel(), N))
     if K % 32:
         raise L.HipError("gemm_dyn: K must be a multiple of 32")
+    if max_cus:
+        L.call("nr_gemm_f32_dyn_cus", M, N, K, A, B, L.ptr(C), ldc if ldc is not None else C.stride(0),
+               L.ptr(bias), epilogue, c_rows, pad_row, split_k, L.ptr(m_dev), L.ptr(k_dev), _prec(prec),
+               int(max_cus), L.stream_ptr(C))
+        return
     L.call("nr_gemm_f32_dyn", M, N, K, A, B, L.ptr(C), ldc if ldc is not None else C.stride(0),
            L.ptr(bias), epilogue, c_rows, pad_row, split_k, L.ptr(m_dev), L.ptr(k_dev), _prec(prec),
            L.stream_ptr(C))

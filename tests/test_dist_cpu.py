@@ -157,3 +157,84 @@ def test_spawn_ranks_failure_propagates(tmp_path):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     env["FAIL_RANK"] = "1"
     assert D.spawn_ranks(2, [str(script)], env=env, timeout=120) == 3
+
+
+def _deferred_worker(rank, world, port, q):
+    """GradSync in deferred (graphed-step) mode: the weight gradient of ``lin`` comes from a
+    closure the backward hands to WGRAD_DEFER_HOOK; in-place buckets written by a deferred GEMM
+    must be reduced after it (pack() 'late'), the others may start early."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    D.setup(rank, world, backend="gloo", master_port=str(port))
+    try:
+        model = Tiny()
+        x = torch.tensor([rank, rank + 3, 7])
+
+        class LinDeferred(torch.autograd.Function):
+            @staticmethod
+            def forward(ctx, h, w, b):
+                ctx.save_for_backward(h, w)
+                return h @ w.t() + b
+
+            @staticmethod
+            def backward(ctx, g):
+                h, w = ctx.saved_tensors
+                dw = torch.zeros_like(w)
+
+                def run(max_cus=0):
+                    dw.add_(g.t() @ h)
+                if not F.WGRAD_DEFER_HOOK(run, dw):
+                    run()
+                # a fresh view (as MHANewsFn's joined weights hand back): autograd installs it as
+                # .grad without a copy, so the deferred GEMM's writes land in the gradient
+                return g @ w, dw[:], g.sum(0)
+
+        sync = D.GradSync(model, bucket_mb=1e-4, inplace_mb=1e-5, deferred=True)
+        model.zero_grad(set_to_none=True)
+        h = model.table[x]
+        out = model.lin2(LinDeferred.apply(h, model.lin.weight, model.lin.bias))
+        (out ** 2).sum().backward()
+        assert len(sync._runs) == 1 and float(model.lin.weight.grad.abs().sum()) == 0.0   # deferred
+        rec = sync.take_sparse()
+        outs = sync.run_deferred()
+        early, packed = sync.pack(rec, outs)
+        late_ids = {id(b[0]) for b, _, inplace in packed if inplace}
+        assert id(model.lin.weight) in late_ids, "the deferred gradient's bucket must run after the GEMM"
+        assert all(id(b[0]) != id(model.lin.weight) for b, _, _ in early)
+        works = sync.issue(early)
+        sync.exchange(packed, rec, works)
+        sync.unpack(packed)
+        sync.close()
+        q.put((rank, None, {n: (p.grad * sync.scale).numpy().copy() for n, p in model.named_parameters()
+                            if p.grad is not None}))
+    except Exception as e:
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e), None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grad_sync_deferred_wgrad_gloo_world2():
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_deferred_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    want = {}
+    for r in range(world):
+        m = Tiny()
+        m.zero_grad(set_to_none=True)
+        out = m.lin2(m.lin(m.table[torch.tensor([r, r + 3, 7])]))
+        (out ** 2).sum().backward()
+        for n, p in m.named_parameters():
+            if p.grad is not None:
+                want[n] = want.get(n, 0) + p.grad / world
+    for rank, err, g in res:
+        assert err is None, err
+        assert set(g) == set(want), (set(g), set(want))
+        for n in want:
+            torch.testing.assert_close(torch.from_numpy(g[n]), want[n], rtol=1e-6, atol=1e-6)
