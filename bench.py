@@ -570,20 +570,39 @@ def main():
     if rank == 0:
         ms = el / a.steps * 1e3
         value = world * B * a.steps / el
-        gemm_ms = probe.get("proj_fwd_ms")
-        # per launch: [rows, 768] x [768, 1152], rows = the distinct word rows of the batch
-        # (device-side count, read back after the timed region) or T tokens without dedup
-        gemm_rows = probe.get("proj_fwd_rows", float(B * (C + NH) * L))
-        gemm_flops = 2.0 * gemm_rows * E * (E + H)
-        achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms else None
         from newsrec_amd import _lib as Lb, kernels as Kn
         split = Kn.get_gemm_precision() == Lb.GEMM_BF16X6
         # bf16x6: six bf16 MFMAs per fp32 multiply-add -> fp32-equivalent peak = bf16 dense peak / 6
         peak = BF16_MFMA_PEAK_TF / 6 if split else FP32_MFMA_PEAK_TF
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_proj_fwd.json")
-        if os.path.exists(pmc):
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        # the news tower's three projection GEMMs, each timed per launch with HIP events on its
+        # stream: forward (gathered table rows x [Wk; Wv]^T), table dgrad (dY W -> distinct table
+        # rows), weight gradient (dY^T x gathered rows).  Each is 2 x rows x 768 x 1152 FLOP with
+        # rows = the batch's distinct word rows (device-side count read back after the timed region)
+        gemms = {}
+        for name, what in (("proj_fwd", "forward: gathered rows x [Wk;Wv]^T"),
+                           ("proj_dgrad", "table dgrad: dY x [Wk;Wv] -> distinct table rows"),
+                           ("proj_wgrad", "weight gradient: dY^T x gathered rows (split-K)")):
+            g_ms = probe.get(name + "_ms")
+            if not g_ms:
+                continue
+            rows = probe.get(name + "_rows", float(B * (C + NH) * L))
+            fl = 2.0 * rows * E * (E + H)
+            ach = fl / (g_ms * 1e-3) / 1e12
+            tr = None
+            pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % name)
+            if os.path.exists(pmc):
+                tr = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            gemms[name] = {"what": what, "launch_ms": round(g_ms, 4), "rows_per_launch": rows,
+                           "flops_per_launch": fl, "achieved": round(ach, 2), "frac": round(ach / peak, 4),
+                           "traffic": tr}
+        # the roofline line names the DOMINANT kernel of the step: the longest of the three
+        dom = max(gemms, key=lambda k: gemms[k]["launch_ms"]) if gemms else None
+        gd = gemms.get(dom, {})
+        achieved = gd.get("achieved")
+        traffic = gd.get("traffic")
+        gemm_ms = gd.get("launch_ms")
+        gemm_flops = gd.get("flops_per_launch")
+        gemm_rows = gd.get("rows_per_launch")
         out = {
             "metric": "impressions/sec (train) + candidates scored/sec (eval), NRMS MIND-large 1/8 GPU",
             "value": round(value, 1), "unit": "impressions/s", "n_gpus": world, "steps": a.steps,
@@ -603,7 +622,8 @@ def main():
             "eval": dict(fast or {}, forward={"candidates_per_s": round(world * B * C * ne / el_eval, 1),
                                               "impressions_per_s": round(world * B * ne / el_eval, 1),
                                               "mode": "model(x) in eval mode (sigmoid) on train-shaped batches"}),
-            "roofline": {"kernel": "gemm gather+key/value projection (fwd)", "bound": "mfma",
+            "roofline": {"kernel": "%s GEMM of the news-tower key/value projection (%s)"
+                                   % (dom, gd.get("what")) if dom else None, "bound": "mfma",
                          "achieved": round(achieved, 2) if achieved else None, "peak": round(peak, 1),
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4) if achieved else None,
                          "peak_basis": ("fp32-equivalent: 2.5 PF bf16 dense MFMA / 6 (bf16x6 split arithmetic)"
@@ -611,7 +631,7 @@ def main():
                          "frac_of_fp32_peak": round(achieved / FP32_MFMA_PEAK_TF, 4) if achieved else None,
                          "traffic": traffic, "launch_ms": round(gemm_ms, 4) if gemm_ms else None,
                          "flops_per_launch": gemm_flops, "rows_per_launch": gemm_rows,
-                         "tokens_per_launch": B * (C + NH) * L},
+                         "tokens_per_launch": B * (C + NH) * L, "projection_gemms": gemms},
         }
         if xf is not None:
             out["xformer"] = xf

@@ -312,9 +312,11 @@ class MHANewsFn(torch.autograd.Function):
             if ctx.needs_input_grad[0]:
                 dtable = torch.zeros(V, E, device=table.device)
                 # distinct rows (M = U, not U_pad: no duplicate pad ids): plain row stores
+                ev0 = PROBE.record()
                 K.gemm_dyn(ur.cap, E, NY, K.operand(dYu, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dtable,
                            m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_ZEROED,
                            c_rows=K.rows_map(ur.uids, L.ROWS_GATHER), pad_row=pad_row)
+                PROBE.add("proj_dgrad", ev0, PROBE.record(), ur)
                 if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
                     dtable = None
                     inflight = True   # the table's all-reduce runs beside the weight gradient
@@ -325,7 +327,9 @@ class MHANewsFn(torch.autograd.Function):
                            K.operand(table, L.MNCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER), dw, k_dev=ur.u_pad,
                            epilogue=L.EPI_ATOMIC, split_k=_split_k(NY, E, ur.cap), prec=prec, max_cus=max_cus)
             if not WGRAD_DEFER_HOOK(wgrad, dw):
+                ev0 = PROBE.record()
                 wgrad(WGRAD_DEFER_HOOK.max_cus if inflight else 0)
+                PROBE.add("proj_wgrad", ev0, PROBE.record(), ur)
         else:
             if ctx.needs_input_grad[0]:
                 dtable = torch.zeros(V, E, device=table.device)
