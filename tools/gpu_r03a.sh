@@ -10,4 +10,5 @@ B="python bench.py --steps 3 --warmup 2 --eval-impr 0 --config-legs 0 --xformer-
 echo trace; timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- $B > $O/kt.log 2>&1 || exit 4
 echo pmc; bash tools/pmc_passes.sh $O/pmc $B || exit 5
 echo rccl; timeout -k 10 120 python tools/rccl_shared_probe.py > $O/rccl.log 2>&1; echo "rccl rc=$?" >> $O/rccl.log
+echo ab; timeout -k 10 400 python tools/gemm_ab.py --libs base,ab/bn128/libnewsrec_hip.so,ab/bn256/libnewsrec_hip.so --cases nrms_proj_fwd,nrms_dgrad_table,nrms_proj_wgrad > $O/ab.json 2>&1 || exit 6
 echo done
