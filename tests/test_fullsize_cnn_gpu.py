@@ -45,7 +45,9 @@ def _model(encU, dev):
     m = build_model("cnn", encU, H, vocab=V, device=dev, user_num=USERS)
     with torch.no_grad():
         for n, p in m.named_parameters():
-            p.normal_(0, float(param_std(n, tuple(p.shape))))
+            # x4 on the conv: 1,760 titles of random words give news vectors with a large common
+            # part, and the user vector (a pooled mean of 50 of them) mostly scores that part
+            p.normal_(0, float(param_std(n, tuple(p.shape))) * (4.0 if n == "encoderN.cnn.weight" else 1.0))
         if hasattr(m.encoderU, "userEmbedding"):
             m.encoderU.userEmbedding.weight[0].zero_()   # RNN.py:82
     return m
