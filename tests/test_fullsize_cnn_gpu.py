@@ -126,7 +126,7 @@ def test_lstur_fullsize_graph_replay_matches_eager():
     dev = torch.device("cuda", 0)
     m_eager = _model("lstur", dev)
     m_graph = copy.deepcopy(m_eager)
-    keep = _keep(9)
+    keep = _keep(9).to(dev)   # device-resident: read inside the captured graph
     m_eager.encoderU.keep_override = keep
     m_graph.encoderU.keep_override = keep
     batches = [{k: v.to(dev) for k, v in _batch(20 + i).items()} for i in range(4)]
