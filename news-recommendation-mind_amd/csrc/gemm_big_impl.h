@@ -23,20 +23,28 @@
 namespace nrfast {
 
 constexpr int BIG_BM = 256;
-constexpr int BIG_BK = 16;
-constexpr int BIG_SR = 24;   // bf16 per LDS row: 16 k + 8 pad (48 B: odd multiple of 16 B)
+// k-tile depth: bf16x6 (three planes) 16, bf16 (one plane) 32 -- one barrier per k-tile either way,
+// so the one-product form gets as many MFMAs between barriers as its LDS budget allows
+template <int NP>
+constexpr int big_bk() { return NP == 1 ? 32 : 16; }
+// bf16 per LDS row: BK k + 8 pad (48 / 80 B: odd multiples of 16 B, conflict-free ds_read_b128)
+template <int BK>
+constexpr int big_sr() { return BK + 8; }
 
-// K-contiguous operand, R rows x 16 k: 512 threads x (R / 128) float4 (row f >> 2, k quad f & 3)
-template <int R, int MODE>
+// K-contiguous operand, R rows x BK k: 512 threads x (R BK / 2048) float4 (row f / (BK / 4), k
+// quad f % (BK / 4))
+template <int R, int MODE, int BK>
 struct BigKC {
-  static constexpr int NV = R / 128;
+  static constexpr int QPR = BK / 4;           // float4 per row
+  static constexpr int NV = R * QPR / 512;
+  static constexpr int SR = big_sr<BK>();
   float4 v[2][NV];   // two register sets: k-tile t lives in set t % 2 (loads issued 3 tiles ahead)
   const float* rowp[NV];
   __device__ __forceinline__ void init(const Op& d, int64_t r0, int64_t rlim, int tid) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int f = tid + 512 * i;
-      int64_t row = r0 + (f >> 2);
+      int64_t row = r0 + f / QPR;
       row = row < rlim ? row : rlim - 1;   // clamp: rows >= M are computed and discarded
       rowp[i] = MODE == KC_GATHER ? d.base + d.idx[row] * d.ld : d.base + row * d.ld;
     }
@@ -48,16 +56,16 @@ struct BigKC {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int f = tid + 512 * i;
-      v[S][i] = *reinterpret_cast<const float4*>(rowp[i] + k0 + 4 * (f & 3));
+      v[S][i] = *reinterpret_cast<const float4*>(rowp[i] + k0 + 4 * (f % QPR));
     }
   }
   template <int S, int NP>
   __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
-    constexpr int PL = R * BIG_SR;   // one plane
+    constexpr int PL = R * SR;   // one plane
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int f = tid + 512 * i;
-      uint16_t* q = lds + (f >> 2) * BIG_SR + 4 * (f & 3);
+      uint16_t* q = lds + (f / QPR) * SR + 4 * (f % QPR);
       const float4 x = v[S][i];
       if constexpr (NP == 1) {
         *reinterpret_cast<uint2*>(q) = hi4(x.x, x.y, x.z, x.w);
@@ -72,40 +80,55 @@ struct BigKC {
   }
 };
 
-// MN-contiguous operand (stored rows = k), R rows x 16 k: thread t < 2R loads the 2 (k) x 4 (row)
-// block k = k0 + 2 (t & 7) + {0, 1}, rows r0 + 4 (t >> 3) .. + 3 as two float4 and writes each row's
-// two consecutive k as one 32-bit word per plane.
-template <int R, int MODE>
+// MN-contiguous operand (stored rows = k), R rows x BK k, in chunks of 2 (k) x 4 (row): chunk
+// (kp, cg) = k0 + 2 kp + {0, 1}, rows r0 + 4 cg .. + 3, loaded as two float4; each row's two
+// consecutive k go to LDS as one 32-bit word per plane.  Thread t takes chunks c = t + 2R j
+// (kp = c & (BK/2 - 1) ... for BK = 16 the original mapping: kp = t & 7, cg = t >> 3).
+template <int R, int MODE, int BK>
 struct BigMN {
   static_assert(MODE == MN_PLAIN || MODE == MN_GATHER, "BigMN: plain or gathered stored rows");
-  float4 v[2][2];     // [register set][k of the pair]
-  int64_t kid[2][2];  // MN_GATHER: stored-row ids of a set's next tile (prefetched one load ahead)
+  static constexpr int KP = BK / 2;                            // k pairs per tile
+  static constexpr int CH = (R / 4) * KP;                      // chunks per tile
+  static constexpr int NC = CH >= 512 ? CH / 512 : 1;          // chunks per thread
+  static constexpr int ACT = CH >= 512 ? 512 : CH;             // active threads
+  static constexpr int SR = big_sr<BK>();
+  static_assert(CH % 512 == 0 || CH < 512, "BigMN: whole chunks per thread");
+  float4 v[2][NC][2];     // [register set][chunk][k of the pair]
+  int64_t kid[2][NC][2];  // MN_GATHER: stored-row ids of a set's next tile (prefetched one load ahead)
   __device__ __forceinline__ void init(const Op&, int64_t, int64_t, int) {}
+  __device__ __forceinline__ static int kp_of(int c) { return c % KP; }
+  __device__ __forceinline__ static int cg_of(int c) { return c / KP; }
   template <int S>
   __device__ __forceinline__ void prefetch_idx(const Op& d, int64_t k0, int64_t K, int tid) {
-    if (MODE == MN_GATHER && tid < 2 * R) {
+    if (MODE == MN_GATHER && tid < ACT) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int64_t k = k0 + 2 * (tid & 7) + u;
-        kid[S][u] = d.idx[k < K ? k : K - 1];
-      }
+      for (int j = 0; j < NC; ++j)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int64_t k = k0 + 2 * kp_of(tid + 512 * j) + u;
+          kid[S][j][u] = d.idx[k < K ? k : K - 1];
+        }
     }
   }
   template <int S>
   __device__ __forceinline__ void load(const Op& d, int64_t r0, int64_t rlim, int64_t k0, int tid) {
-    if (tid >= 2 * R) return;
-    int64_t col = r0 + 4 * (tid >> 3);
+    if (tid >= ACT) return;
     const int64_t cmax = ((rlim + 3) & ~int64_t(3)) - 4;
-    col = col < cmax ? col : cmax;   // clamp inside the padded row; rows >= M are discarded
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t row = MODE == MN_PLAIN ? k0 + 2 * (tid & 7) + u : kid[S][u];
-      v[S][u] = *reinterpret_cast<const float4*>(d.base + row * d.ld + col);
+    for (int j = 0; j < NC; ++j) {
+      const int c = tid + 512 * j;
+      int64_t col = r0 + 4 * cg_of(c);
+      col = col < cmax ? col : cmax;   // clamp inside the padded row; rows >= M are discarded
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t row = MODE == MN_PLAIN ? k0 + 2 * kp_of(c) + u : kid[S][j][u];
+        v[S][j][u] = *reinterpret_cast<const float4*>(d.base + row * d.ld + col);
+      }
     }
   }
   template <int NP>
   __device__ __forceinline__ void put(uint16_t* q, float a, float b) const {
-    constexpr int PL = R * BIG_SR;
+    constexpr int PL = R * SR;
     if constexpr (NP == 1) {
       *reinterpret_cast<uint32_t*>(q) = pk_bf16(a, b);
     } else {
@@ -116,32 +139,36 @@ struct BigMN {
       *reinterpret_cast<uint32_t*>(q + 2 * PL) = ll;
     }
   }
-  // Thread (column group cg = tid >> 3, k pair kp = tid & 7) writes its four rows 4cg .. 4cg + 3 as
-  // four ds_write_b32 per plane.  The row stride is 12 words, so row 4cg + i sits at bank
-  // 16 cg + 12 i + kp (mod 32): in natural order the four column groups of a 32-lane half land on
-  // two bank windows (a 2-way conflict on every write).  Column groups with cg ^ (cg >> 1) odd write
-  // their rows in the order 2, 3, 0, 1 instead, which puts the four windows 8 banks apart:
-  // conflict-free.  (The float4 halves are swapped to match: 4 selects per float4.)
+  // Chunk (column group cg, k pair kp) writes its four rows 4cg .. 4cg + 3 as four ds_write_b32 per
+  // plane.  At BK = 16 the row stride is 12 words, so row 4cg + i sits at bank 16 cg + 12 i + kp
+  // (mod 32): in natural order the four column groups of a 32-lane half land on two bank windows (a
+  // 2-way conflict on every write).  Column groups with cg ^ (cg >> 1) odd write their rows in the
+  // order 2, 3, 0, 1 instead, which puts the four windows 8 banks apart: conflict-free.  (The float4
+  // halves are swapped to match: 4 selects per float4.)
   template <int S, int NP>
   __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
-    if (tid >= 2 * R) return;
-    const int cg = tid >> 3;
-    const bool rot = ((cg ^ (cg >> 1)) & 1) != 0;
-    uint16_t* q = lds + (4 * cg) * BIG_SR + 2 * (tid & 7);
-    uint16_t* qa = q + (rot ? 2 * BIG_SR : 0);   // rows 0, 1 (or 2, 3)
-    uint16_t* qb = q + (rot ? 0 : 2 * BIG_SR);   // rows 2, 3 (or 0, 1)
-    const float4 a = v[S][0], b = v[S][1];
-    const float a0 = rot ? a.z : a.x, a1 = rot ? a.w : a.y, a2 = rot ? a.x : a.z, a3 = rot ? a.y : a.w;
-    const float b0 = rot ? b.z : b.x, b1 = rot ? b.w : b.y, b2 = rot ? b.x : b.z, b3 = rot ? b.y : b.w;
-    put<NP>(qa, a0, b0);
-    put<NP>(qa + BIG_SR, a1, b1);
-    put<NP>(qb, a2, b2);
-    put<NP>(qb + BIG_SR, a3, b3);
+    if (tid >= ACT) return;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int c = tid + 512 * j;
+      const int cg = cg_of(c);
+      const bool rot = BK == 16 && ((cg ^ (cg >> 1)) & 1) != 0;
+      uint16_t* q = lds + (4 * cg) * SR + 2 * kp_of(c);
+      uint16_t* qa = q + (rot ? 2 * SR : 0);   // rows 0, 1 (or 2, 3)
+      uint16_t* qb = q + (rot ? 0 : 2 * SR);   // rows 2, 3 (or 0, 1)
+      const float4 a = v[S][j][0], b = v[S][j][1];
+      const float a0 = rot ? a.z : a.x, a1 = rot ? a.w : a.y, a2 = rot ? a.x : a.z, a3 = rot ? a.y : a.w;
+      const float b0 = rot ? b.z : b.x, b1 = rot ? b.w : b.y, b2 = rot ? b.x : b.z, b3 = rot ? b.y : b.w;
+      put<NP>(qa, a0, b0);
+      put<NP>(qa + SR, a1, b1);
+      put<NP>(qb, a2, b2);
+      put<NP>(qb + SR, a3, b3);
+    }
   }
 };
 
-template <int R, int MODE>
-using BigLoader = typename std::conditional<is_kc(MODE), BigKC<R, MODE>, BigMN<R, MODE>>::type;
+template <int R, int MODE, int BK>
+using BigLoader = typename std::conditional<is_kc(MODE), BigKC<R, MODE, BK>, BigMN<R, MODE, BK>>::type;
 
 // Atomic scatter-add of a tail piece in the transposed accumulator layout (lane (h, c) holds row c,
 // columns 8q + 4h + 0..3 of each 32 x 32 block): one block at a time goes through LDS (waves 0-3 in
@@ -179,9 +206,10 @@ __device__ __forceinline__ void tail_scatter_tr(const Args& g, f32x16 (&acc)[TI]
 template <int AM, int BMODE, bool TR, int NP, int BN>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
   constexpr int BM = BIG_BM;
-  using LA = BigLoader<BM, AM>;
-  using LB = BigLoader<BN, BMODE>;
-  constexpr int PA = BM * BIG_SR, PB = BN * BIG_SR;   // one plane
+  constexpr int BK = big_bk<NP>(), SR = big_sr<BK>(), KS = BK / 16;   // KS: 16-deep MFMA steps per k-tile
+  using LA = BigLoader<BM, AM, BK>;
+  using LB = BigLoader<BN, BMODE, BK>;
+  constexpr int PA = BM * SR, PB = BN * SR;   // one plane
   __shared__ __attribute__((aligned(16))) uint16_t As[2 * NP * PA];
   __shared__ __attribute__((aligned(16))) uint16_t Bs[2 * NP * PB];
   constexpr bool IDX_AHEAD = AM == MN_GATHER || BMODE == MN_GATHER;
@@ -253,7 +281,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
       kend = u.kbeg + kc_tail < g.K ? u.kbeg + kc_tail : g.K;
       if (kend <= u.kbeg) continue;
     }
-    const int nt = (int)((kend - u.kbeg + BIG_BK - 1) / BIG_BK);
+    const int nt = (int)((kend - u.kbeg + BK - 1) / BK);
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -267,12 +295,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
     // the gathered rows come from the Infinity Cache / HBM)
     auto issue = [&](auto set, int kt) {
       constexpr int S = decltype(set)::value;
-      const int64_t k = u.kbeg + (int64_t)kt * BIG_BK;
+      const int64_t k = u.kbeg + (int64_t)kt * BK;
       la.template load<S>(g.A, u.m0, g.M, k, tid);
       lb.template load<S>(g.B, u.n0, g.N, k, tid);
       if (IDX_AHEAD && kt + 2 < nt) {   // ids of the set's next tile (kt + 2)
-        la.template prefetch_idx<S>(g.A, k + 2 * BIG_BK, g.K, tid);
-        lb.template prefetch_idx<S>(g.B, k + 2 * BIG_BK, g.K, tid);
+        la.template prefetch_idx<S>(g.A, k + 2 * BK, g.K, tid);
+        lb.template prefetch_idx<S>(g.B, k + 2 * BK, g.K, tid);
       }
     };
     using S0 = std::integral_constant<int, 0>;
@@ -280,8 +308,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
     if (IDX_AHEAD) {
       la.template prefetch_idx<0>(g.A, u.kbeg, g.K, tid);
       lb.template prefetch_idx<0>(g.B, u.kbeg, g.K, tid);
-      la.template prefetch_idx<1>(g.A, u.kbeg + BIG_BK, g.K, tid);
-      lb.template prefetch_idx<1>(g.B, u.kbeg + BIG_BK, g.K, tid);
+      la.template prefetch_idx<1>(g.A, u.kbeg + BK, g.K, tid);
+      lb.template prefetch_idx<1>(g.B, u.kbeg + BK, g.K, tid);
     }
     __syncthreads();   // the previous unit's last stage reads are done before stage 0 is rewritten
     issue(S0{}, 0);
@@ -290,25 +318,28 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
     lb.template store<0, NP>(Bs, tid);
     if (nt > 2) issue(S0{}, 2);
     __syncthreads();
-    // one k-tile: MFMAs from stage st; behind row blocks 0 / 1 the wave splits k-tile kt+1 (set
-    // (kt+1) % 2 = NS) into the other stage, then reuses that set for k-tile kt+3's loads
+    // one k-tile (KS MFMA steps of 16): MFMAs from stage st; behind the first row blocks the wave
+    // splits k-tile kt+1 (set (kt+1) % 2 = NS) into the other stage, then reuses that set for k-tile
+    // kt+3's loads
     auto ktile = [&](auto nset, int kt, int st) {
       constexpr int NS = decltype(nset)::value;
       const bool stage_next = kt + 1 < nt;
       const uint16_t* a_s = As + st * NP * PA;
       const uint16_t* b_s = Bs + st * NP * PB;
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
       bf16x8 b[TJ][NP];
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
         for (int p = 0; p < NP; ++p)
-          b[j][p] = *reinterpret_cast<const bf16x8*>(b_s + p * PB + (wn + 32 * j + c) * BIG_SR + 8 * h);
+          b[j][p] = *reinterpret_cast<const bf16x8*>(b_s + p * PB + (wn + 32 * j + c) * SR + 16 * kk + 8 * h);
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         bf16x8 a[NP];
 #pragma unroll
         for (int p = 0; p < NP; ++p)
-          a[p] = *reinterpret_cast<const bf16x8*>(a_s + p * PA + (wm + 32 * i + c) * BIG_SR + 8 * h);
+          a[p] = *reinterpret_cast<const bf16x8*>(a_s + p * PA + (wm + 32 * i + c) * SR + 16 * kk + 8 * h);
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
 #define NR_MF(X, Y)                                                                                    \
@@ -324,11 +355,14 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
           NR_MF(0, 0);
 #undef NR_MF
         }
-        if (i == 0 && stage_next) la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid);
-        if (i == 1 && stage_next) {
+        // split-stores of the next stage: A behind step 0's first row block, B (then the loads of
+        // k-tile kt+3 into the freed register set) behind step KS/2's second (KS = 1) or first row block
+        if (kk == 0 && i == 0 && stage_next) la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid);
+        if (kk == KS / 2 && i == (KS == 1 ? 1 : 0) && stage_next) {
           lb.template store<NS, NP>(Bs + (st ^ 1) * NP * PB, tid);
           if (kt + 3 < nt) issue(nset, kt + 3);
         }
+      }
       }
       __syncthreads();   // stage st fully read; stage st^1 fully written
     };
