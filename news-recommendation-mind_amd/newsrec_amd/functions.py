@@ -141,6 +141,7 @@ SPLIT_BWD = True
 # order, loaded by every wave straight from L2) under the bf16x6 / bf16 arithmetics; False: split
 # inside every tile like the other operand (the both-operands-in-LDS kernel).
 SPLIT_B = True
+SPLIT_B_DGRAD = False   # the table dgrad's transposed weights likewise (measured slower: DESIGN §4.1)
 
 
 def _weight_operand(w, layout, n, k, prec):
@@ -324,7 +325,8 @@ class MHANewsFn(torch.autograd.Function):
             inflight = False
             if ctx.needs_input_grad[0]:
                 dtable = torch.zeros(V, E, device=table.device)
-                wtop = _weight_operand(w_cat, L.MNCONTIG, E, NY, ctx.prec)
+                wtop = (_weight_operand(w_cat, L.MNCONTIG, E, NY, ctx.prec) if SPLIT_B_DGRAD
+                        else K.operand(w_cat, L.MNCONTIG))
                 # distinct rows (M = U, not U_pad: no duplicate pad ids): plain row stores
                 ev0 = PROBE.record()
                 K.gemm_dyn(ur.cap, E, NY, K.operand(dYu, L.KCONTIG), wtop, dtable,
