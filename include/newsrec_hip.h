@@ -42,9 +42,7 @@ enum nr_rows_map {
 
 enum nr_layout {
   NR_KCONTIG = 0, /* stored rows are the M (or N) index, k contiguous: A[M][K], B[N][K]   */
-  NR_MNCONTIG = 1, /* stored rows are the k index, M (or N) contiguous: A[K][M], B[K][N]  */
-  NR_BSPLIT = 2   /* B only: `data` is nr_split_b's output for this GEMM's N and K (ld = K),
-                     planes matching `prec` (3 for NR_GEMM_BF16X6, 1 for NR_GEMM_BF16)     */
+  NR_MNCONTIG = 1 /* stored rows are the k index, M (or N) contiguous: A[K][M], B[K][N]   */
 };
 
 typedef struct nr_operand {
@@ -121,18 +119,6 @@ int nr_gemm_f32_dyn_cus(int64_t M, int64_t N, int64_t K, const nr_operand* A, co
                         const nr_operand* c_rows, int64_t pad_row, int32_t split_k,
                         const int32_t* m_dev, const int32_t* k_dev, int32_t prec, int32_t max_cus,
                         hipStream_t stream);
-
-/* Pre-split B operand: the fp32 matrix B of a GEMM (layout NR_KCONTIG: b[n * ld + k]; NR_MNCONTIG:
- * b[k * ld + n]) as np bf16 planes (np = 3: the bf16x6 terms h, m, l of each value; np = 1: the
- * value rounded to bf16) in MFMA fragment order,
- *   out[((p * NB + n / 32) * KB + k / 16) * 512 + (n % 32) * 16 + k % 16],  NB = ceil(N / 32), KB = K / 16,
- * zero for n >= N.  A GEMM then takes it as a B operand of layout NR_BSPLIT: every wave loads its B
- * fragments straight from memory, and only A is staged through LDS (the weights of
- * Attention.py:107-108 and BertModel's dense layers are split once per step instead of in every
- * tile).  K % 32 == 0; out 8-B aligned, nr_split_b_elems(N, K, np) bf16. */
-int64_t nr_split_b_elems(int64_t N, int64_t K, int32_t np);
-int nr_split_b(const float* b, int64_t ld, int32_t layout, int64_t N, int64_t K, int32_t np,
-               uint16_t* out, hipStream_t stream);
 
 /* ------------------------------------------------------------------ distinct token rows */
 

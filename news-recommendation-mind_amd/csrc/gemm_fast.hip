@@ -27,7 +27,6 @@ int launch_big_1_256(const Args& g, int am, int bm, int splits, hipStream_t s); 
 int launch_big_3_256(const Args& g, int am, int bm, int splits, hipStream_t s);
 int launch_big_1_128(const Args& g, int am, int bm, int splits, hipStream_t s);
 int launch_big_3_128(const Args& g, int am, int bm, int splits, hipStream_t s);
-int launch_bg_modes(const Args& g, int am, int np, int splits, hipStream_t s);    // gemm_bg.hip
 
 // Large-tile (256 x BN) bf16 kernel choice: 0 = stay on the 128x128 kernel.  NR_GEMM_BIG = 0 disables
 // it, 128 / 256 forces BN where eligible (A/B timing); auto: 256 x 256 tiles unless their units fill
@@ -77,37 +76,6 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   auto aligned = [](const nr_operand* o) {
     return (o->ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(o->data) & 15) == 0);
   };
-  if (B->layout == NR_BSPLIT) {
-    // pre-split B (nr_split_b): the B-from-global large-tile kernel, A K-contiguous plain / gathered
-    if (prec == NR_GEMM_F32 || !aligned(A) || (K % 32) || B->ld != K || A->layout != NR_KCONTIG ||
-        (A->map != NR_ROWS_PLAIN && A->map != NR_ROWS_GATHER) || split_k != 1 ||
-        (reinterpret_cast<uintptr_t>(B->data) & 15))
-      return NR_EINVAL(8);
-    if (epilogue == NR_EPI_ATOMIC || epilogue == NR_EPI_SCATTER) return NR_EINVAL(8);
-    if ((epilogue == NR_EPI_SCATTER_STORE || epilogue == NR_EPI_SCATTER_ZEROED) &&
-        (!c_rows || c_rows->map != NR_ROWS_GATHER || !c_rows->rows))
-      return NR_EINVAL(8);
-    const bool zeroed = epilogue == NR_EPI_SCATTER_ZEROED;
-    Args g{};
-    g.M = M; g.N = N; g.K = K;
-    g.A = Op{A->data, A->ld, A->rows, A->seq_len, A->seg};
-    g.B = Op{B->data, B->ld, nullptr, 1, 1};
-    g.Cm = Op{c_rows ? c_rows->data : nullptr, c_rows ? c_rows->ld : 0, c_rows ? c_rows->rows : nullptr, 1,
-              c_rows ? c_rows->seg : 1};
-    g.C = C; g.ldc = ldc; g.bias = bias; g.epi = zeroed ? NR_EPI_SCATTER_STORE : epilogue; g.pad_row = pad_row;
-    g.mdyn = m_dev; g.kdyn = nullptr; g.splits = 1; g.tail = zeroed ? 16 : 0; g.max_cus = max_cus > 0 ? max_cus : 0;
-    g.kchunk = (K + 31) / 32 * 32;
-    {
-      auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-      bool v = N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!bias || al16(bias));
-      if (epilogue == NR_EPI_ACCUM_GATE || epilogue == NR_EPI_STORE_GELU || epilogue == NR_EPI_GELU_GRAD)
-        v = v && c_rows && c_rows->ld % 4 == 0 && al16(c_rows->data);
-      g.vec = v ? 1 : 0;
-    }
-    const int am = A->map == NR_ROWS_PLAIN ? KC_PLAIN : KC_GATHER;
-    const int rc = launch_bg_modes(g, am, prec == NR_GEMM_BF16 ? 1 : 3, 1, stream);
-    return rc == -1 ? NR_EINVAL(8) : rc;
-  }
   if (!aligned(A) || !aligned(B) || (K % 32)) return -1;
   int am, bmode;
   if (A->layout == NR_KCONTIG) {

@@ -22,7 +22,7 @@ c_ptr = ctypes.c_void_p
 
 # enum nr_rows_map / nr_layout / nr_epilogue / nr_mask_dtype
 ROWS_PLAIN, ROWS_GATHER, ROWS_CONV3 = 0, 1, 2
-KCONTIG, MNCONTIG, BSPLIT = 0, 1, 2
+KCONTIG, MNCONTIG = 0, 1
 EPI_STORE, EPI_STORE_RELU, EPI_ATOMIC, EPI_SCATTER = 0, 1, 2, 3
 MASK_U8, MASK_I64, MASK_F64, MASK_F32 = 0, 1, 2, 3
 EPI_STORE_TANH, EPI_ACCUM_GATE, EPI_ACCUM, EPI_SCATTER_STORE = 4, 5, 6, 7
@@ -53,8 +53,6 @@ _SIGS = {
     "nr_gemm_f32_dyn_cus": [c_i64, c_i64, c_i64, ctypes.POINTER(nr_operand), ctypes.POINTER(nr_operand),
                             c_ptr, c_i64, c_ptr, c_i32, ctypes.POINTER(nr_operand), c_i64, c_i32, c_ptr, c_ptr, c_i32,
                             c_i32, c_ptr],
-    "nr_split_b_elems": [c_i64, c_i64, c_i32],
-    "nr_split_b": [c_ptr, c_i64, c_i32, c_i64, c_i64, c_i32, c_ptr, c_ptr],
     "nr_unique_rows": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                        c_ptr],
     "nr_segment_rows_sum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
@@ -125,7 +123,7 @@ _SIGS = {
     "nr_build_hash": [],
 }
 
-_RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_split_b_elems": c_i64, "nr_unique_rows_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64,
+_RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_unique_rows_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64,
              "nr_colsum_workspace": c_i64,
              "nr_build_hash": ctypes.c_char_p}
 

@@ -137,21 +137,6 @@ DEDUP_ROWS = True
 # Training forward saves the attention output; the backward runs split (False: the fused backward
 # that recomputes the attention).
 SPLIT_BWD = True
-# The projection weights enter their GEMMs pre-split (nr_split_b: bf16 planes in MFMA fragment
-# order, loaded by every wave straight from L2) under the bf16x6 / bf16 arithmetics; False: split
-# inside every tile like the other operand (the both-operands-in-LDS kernel).
-SPLIT_B = True
-SPLIT_B_DGRAD = False   # the table dgrad's transposed weights likewise (measured slower: DESIGN §4.1)
-
-
-def _weight_operand(w, layout, n, k, prec):
-    """B operand (n output columns, k contraction) of a projection GEMM: pre-split when the
-    arithmetic allows (SPLIT_B)."""
-    if SPLIT_B and k % 32 == 0 and K.split_planes(prec) is not None:
-        return K.split_b(w, layout, n, k, prec)[1]
-    return K.operand(w, layout)
-
-
 class _TableGradHook:
     """Optional callback ``hook(table_param, dtable) -> bool`` run inside a news-tower backward
     as soon as the dense word-table gradient exists (before the weight-gradient GEMMs).  When it
@@ -253,10 +238,9 @@ class MHANewsFn(torch.autograd.Function):
             # tail gives masked tokens an exactly-zero dY (their P rows and columns are zero)
             ur = K.UniqueRows(ids, V, fill_row=pad_row if 0 <= pad_row < V else 0, grad_mask=mask)
             Y = _empty(ur.cap, NY, table)
-            wop = _weight_operand(w_cat, L.KCONTIG, NY, E, ctx.prec)
             ev0 = PROBE.record()
             K.gemm_dyn(ur.cap, NY, E, K.operand(table, L.KCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER),
-                       wop, Y, m_dev=ur.u_pad, bias=b_cat)
+                       K.operand(w_cat, L.KCONTIG), Y, m_dev=ur.u_pad, bias=b_cat)
         else:
             Y = _empty(T, NY, table)
             ev0 = PROBE.record()
@@ -325,11 +309,9 @@ class MHANewsFn(torch.autograd.Function):
             inflight = False
             if ctx.needs_input_grad[0]:
                 dtable = torch.zeros(V, E, device=table.device)
-                wtop = (_weight_operand(w_cat, L.MNCONTIG, E, NY, ctx.prec) if SPLIT_B_DGRAD
-                        else K.operand(w_cat, L.MNCONTIG))
                 # distinct rows (M = U, not U_pad: no duplicate pad ids): plain row stores
                 ev0 = PROBE.record()
-                K.gemm_dyn(ur.cap, E, NY, K.operand(dYu, L.KCONTIG), wtop, dtable,
+                K.gemm_dyn(ur.cap, E, NY, K.operand(dYu, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dtable,
                            m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_ZEROED,
                            c_rows=K.rows_map(ur.uids, L.ROWS_GATHER), pad_row=pad_row)
                 PROBE.add("proj_dgrad", ev0, PROBE.record(), ur)

@@ -197,33 +197,6 @@ def operand(t, layout, rows=None, mapping=L.ROWS_PLAIN, seq_len=1, seg=1, ld=Non
     return op
 
 
-def split_planes(prec):
-    """bf16 planes of a pre-split B operand for a GEMM arithmetic (None: not pre-splittable)."""
-    p = _prec(prec)
-    return 3 if p == L.GEMM_BF16X6 else 1 if p == L.GEMM_BF16 else None
-
-
-def split_b(b, layout, N, K, prec=None, out=None):
-    """nr_split_b: the GEMM B operand ``b`` (fp32; layout KCONTIG: b[n][k], MNCONTIG: b[k][n]) as the
-    bf16 planes of the arithmetic ``prec`` in MFMA fragment order -> (planes uint16 tensor, operand
-    of layout BSPLIT for a GEMM of this N and K).  ``out``: a buffer from an earlier call to refill."""
-    _f32(b)
-    np_ = split_planes(prec)
-    if np_ is None:
-        raise L.HipError("split_b: only the bf16x6 / bf16 arithmetics take a pre-split B")
-    if b.dim() != 2 or b.stride(1) != 1:
-        raise L.HipError("split_b: b must be a 2-D row-major tensor")
-    n_el = int(L.load().nr_split_b_elems(int(N), int(K), np_))
-    if n_el < 0:
-        raise L.HipError("split_b: K must be a multiple of 32 (K=%d)" % K)
-    if out is None or out.numel() != n_el:
-        out = torch.empty(n_el, dtype=torch.int16, device=b.device)
-    L.call("nr_split_b", L.ptr(b), b.stride(0), layout, int(N), int(K), np_, L.ptr(out), L.stream_ptr(b))
-    op = L.nr_operand(out.data_ptr(), int(K), 0, L.ROWS_PLAIN, 1, 1, L.BSPLIT)
-    op._keep = (out,)
-    return out, op
-
-
 def rows_map(rows, mapping, seq_len=1, seg=1):
     """A row map for the SCATTER epilogue (no data)."""
     _check_rows(rows, None, "rows_map")

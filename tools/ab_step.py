@@ -1,6 +1,6 @@
 """A/B of the NRMS train step (bench.py's headline, graphed, device-formed batches) under module-level
 switches of newsrec_amd.functions, interleaved in ONE process (rounds x variants), so box-to-box and
-clock drift cancel.  python tools/ab_step.py SPLIT_B=1 SPLIT_B=0 [--rounds 3 --steps 20]"""
+clock drift cancel.  python tools/ab_step.py DEDUP_ROWS=1 DEDUP_ROWS=0 [--rounds 3 --steps 20]"""
 import argparse
 import json
 import os

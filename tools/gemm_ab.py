@@ -38,15 +38,7 @@ dYc = torch.randn(52800, 1152, device=dev); WT = W.t().contiguous()
 ux = torch.randn(1600, 384, device=dev); uw = torch.randn(768, 384, device=dev) / 20; ub = torch.randn(768, device=dev)
 uy = torch.empty(1600, 768, device=dev); udy = torch.randn(1600, 768, device=dev); udx = torch.empty(1600, 384, device=dev)
 udw = torch.zeros(768, 384, device=dev); uwT = uw.t().contiguous(); m_dev = torch.tensor([24600], dtype=torch.int32, device=dev)
-def S(w, lay, n, k, p):
-    return K.split_b(w, lay, n, k, p)[1]
 cases = {
- "nrms_proj_fwd_bs": (2*U*E*1152, lambda p: K.gemm_dyn(U, 1152, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), S(W, L.KCONTIG, 1152, E, p), Y, prec=p)),
- "nrms_dgrad_table_bs": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), S(W, L.MNCONTIG, E, 1152, p), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
- "cnn_tap_proj_bs": (2*U*E*480, lambda p: K.gemm_dyn(U, 480, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), S(w3, L.KCONTIG, 480, E, p), P, prec=p)),
- "bert_qkv_bs": (2*T*768*2304, lambda p: K.gemm(T, 2304, 768, K.operand(x, L.KCONTIG), S(wqkv, L.KCONTIG, 2304, 768, p), qkv, prec=p)),
- "bert_ffn1_gelu_bs": (2*T*768*3072, lambda p: K.gemm(T, 3072, 768, K.operand(x, L.KCONTIG), S(wi, L.KCONTIG, 3072, 768, p), G, epilogue=L.EPI_STORE_GELU, c_rows=K.operand(Ub, L.KCONTIG), prec=p)),
- "bert_ffn2_bs": (2*T*768*3072, lambda p: K.gemm(T, 768, 3072, K.operand(G, L.KCONTIG), S(wo2, L.KCONTIG, 768, 3072, p), o, prec=p)),
  "nrms_proj_fwd": (2*U*E*1152, lambda p: K.gemm_dyn(U, 1152, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(W, L.KCONTIG), Y, prec=p)),
  "nrms_proj_dgrad": (2*U*E*1152, lambda p: K.gemm_dyn(U, E, 1152, K.operand(dY, L.KCONTIG), K.operand(W, L.MNCONTIG), dX, prec=p)),
  "nrms_dgrad_table": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), K.operand(W, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
