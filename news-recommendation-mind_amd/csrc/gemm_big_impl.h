@@ -228,17 +228,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
   const int gn = (int)((g.N + BN - 1) / BN);
   const int ntiles = (int)((g.M + BM - 1) / BM) * gn;
   int units = ntiles * g.splits;
-  // balanced split-K: the last row of tiles has <= 128 live rows, so its waves 4-7 idle (one per
-  // SIMD) and a unit of it costs half of one elsewhere; it gets hsplits (~ splits / 2) units of
-  // twice the k range, so every unit of the single round costs the same
-  const bool halfrow = g.hsplits > 0 && g.splits > 1;
-  const int nfull = halfrow ? ntiles - gn : ntiles;
-  int64_t kchunk_h = g.kchunk;
-  if (halfrow) {
-    const int64_t kc = (g.K + g.hsplits - 1) / g.hsplits;
-    kchunk_h = kc > 0 ? (kc + 31) / 32 * 32 : 32;
-    units = nfull * g.splits + gn * g.hsplits;
-  }
   // NR_EPI_SCATTER_ZEROED (destination rows zero on entry, splits == 1): the tiles of the last,
   // partial round of the persistent grid are split along K into `pieces` units whose sums are added
   // atomically, so that round costs 1/pieces of a unit instead of a whole one (a stream-K tail)
@@ -266,8 +255,9 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
 
   // wave grid: BN = 256 -> 2 (M) x 4 (N) waves of 128x64; BN = 128 -> 4 x 2 waves of 64x64.  Waves
   // w and w + 4 share a SIMD, so at BN = 256 wave w + 4 takes the column block two to the right of
-  // wave w's: in a tile cut at half its rows (or half its columns) every SIMD keeps exactly one wave
-  // with live MFMAs (the other skips them), and the tile costs half a unit
+  // wave w's: in a tile cut at half its rows (or columns) every SIMD keeps one wave with live MFMAs.
+  // (Such a unit does NOT take half the time -- one wave per SIMD hides less latency -- so the
+  // split-K scheduler keeps equal units: balancing them as half-cost measured 362 -> 441 us.)
   constexpr int WN = BN == 256 ? 4 : 2;
   constexpr int TI = (BM / (8 / WN)) / 32, TJ = (BN / WN) / 32;
   const int wm = (w / WN) * (BM / (8 / WN));
@@ -280,29 +270,10 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
   // own two-deep pipeline, so the k-loop carries no unit bookkeeping (a pipeline refill per unit
   // costs one load latency against ~48 k-tiles of MFMAs)
   for (int id = blockIdx.x; id < units; id += gridDim.x) {
-    const bool tail_unit = !halfrow && id >= full;
+    const bool tail_unit = id >= full;
     Unit u;
     int64_t kend;
-    if (halfrow) {   // XCD-contiguous runs as decode_unit; full-row tiles first, then the half row
-      const int xcd = id & 7, q8 = units >> 3, rr = units & 7;
-      const int v = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (id >> 3);
-      int tile;
-      int64_t kc;
-      if (v < nfull * g.splits) {
-        tile = v % nfull;
-        u.kbeg = (int64_t)(v / nfull) * g.kchunk;
-        kc = g.kchunk;
-      } else {
-        const int r = v - nfull * g.splits;
-        tile = nfull + r % gn;
-        u.kbeg = (int64_t)(r / gn) * kchunk_h;
-        kc = kchunk_h;
-      }
-      u.m0 = (int64_t)(tile / gn) * BM;
-      u.n0 = (int64_t)(tile % gn) * BN;
-      kend = u.kbeg + kc < g.K ? u.kbeg + kc : g.K;
-      if (kend <= u.kbeg) continue;
-    } else if (!tail_unit) {
+    if (!tail_unit) {
       u = decode_unit(g, id, full, ntiles, gn, BM, BN);
       if (u.nt <= 0) continue;   // a k-split past a device-resident K
       kend = u.kbeg + g.kchunk < g.K ? u.kbeg + g.kchunk : g.K;
@@ -443,7 +414,7 @@ int resident_slots_512(Kern k) {
 template <int AM, int BMODE, bool TR, int NP, int BN>
 int launch_big(const Args& g, int splits, hipStream_t s) {
   const int64_t gm = (g.M + BIG_BM - 1) / BIG_BM, gn = (g.N + BN - 1) / BN;
-  const int64_t units = g.hsplits > 0 && splits > 1 ? (gm - 1) * gn * splits + gn * g.hsplits : gm * gn * splits;
+  const int64_t units = gm * gn * splits;
   if (units <= 0) return NR_OK;
   if (units > 0x7fffffff) return NR_EINVAL(0);
   int grid = (int)units;

@@ -104,7 +104,6 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   if (epilogue == NR_EPI_SCATTER && c_rows && c_rows->map == NR_ROWS_CONV3 && c_rows->seq_len == 1) return -1;
   g.C = C; g.ldc = ldc; g.bias = bias; g.epi = epilogue; g.pad_row = pad_row;
   g.mdyn = m_dev; g.kdyn = k_dev; g.splits = 1; g.tail = 0; g.max_cus = max_cus > 0 ? max_cus : 0;
-  g.hsplits = 0;
   {
     auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
     bool v = N % 4 == 0 && ldc % 4 == 0 && al16(C) && (!bias || al16(bias));
@@ -136,31 +135,14 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
       int sp = splits;
       if (resplit) {
         // re-split for 256 x BN tiles: one wave of units over the CUs it may use, >= 512 k per split
-        const int64_t gm = (M + 255) / 256, gn = (N + BN - 1) / BN, tiles = gm * gn;
+        const int64_t tiles = ((M + 255) / 256) * ((N + BN - 1) / BN);
         const int cus = g.max_cus > 0 ? g.max_cus : 256;
         int64_t want = cus / (tiles > 0 ? tiles : 1);
-        // a last row of tiles with <= 128 live rows costs half per unit (its waves 4-7 idle): it
-        // takes about half the splits, and the others one round's worth of the rest
-        const bool halfrow = BN == 256 && m_dev == nullptr && gm > 1 && (M - (gm - 1) * 256) <= 128;
-        int64_t hs = 0;
-        if (halfrow) {
-          int64_t best = 0, best_s = 0;
-          for (int64_t s = 2; s <= 64; ++s) {   // max over units of (k range x live fraction), minimised
-            const int64_t h2 = (cus - (gm - 1) * gn * s) / gn;
-            if (h2 < 1) break;
-            const int64_t hh = h2 < (s + 1) / 2 ? h2 : (s + 1) / 2;
-            // cost ~ max(1 / s, 1 / (2 hh)); compare as the smaller of s and 2 hh
-            const int64_t q = s < 2 * hh ? s : 2 * hh;
-            if (q > best) { best = q; best_s = s; hs = hh; }
-          }
-          if (best_s > 0 && K / 512 >= best_s) want = best_s; else hs = 0;
-        }
         if (want > K / 512) want = K / 512;
         if (want > 64) want = 64;
         if (want < 1) want = 1;
         gb.kchunk = ((K + want - 1) / want + 31) / 32 * 32;
         sp = (int)((K + gb.kchunk - 1) / gb.kchunk);
-        gb.hsplits = (hs > 0 && sp > 1) ? (int)hs : 0;
       }
       const int np = prec == NR_GEMM_BF16 ? 1 : 3;
       const int rc = BN == 256 ? (np == 1 ? launch_big_1_256(gb, am, bmode, sp, stream) : launch_big_3_256(gb, am, bmode, sp, stream))

@@ -75,8 +75,6 @@ struct Args {
   const int32_t* kdyn;   // device-resident K (<= K), or null
   int tail;  // big kernel, NR_EPI_SCATTER_ZEROED: max K pieces of the last partial round's tiles (0 = off)
   int max_cus;   // persistent grid limited to this many CUs (0 = all): leaves CUs to a concurrent collective
-  int hsplits;   // big kernel, split-K: K splits of the LAST row of tiles when it holds <= 128 live rows
-                 // (0 = uniform splits); its units then carry twice the k range of the others
 };
 
 // CUs of the current device (cached)
