@@ -189,9 +189,14 @@ class GraphedStep:
 
 
 def forward_backward(model, opt, x):
+    """Manager._train :636-644: zero_grad, forward, NLLLoss, backward (the two-tower models fuse the
+    loss into their head: TwoTowerBaseModel.forward_loss)."""
     opt.zero_grad(set_to_none=True)
-    logits, _ = model(x)
-    loss = torch.nn.functional.nll_loss(logits, x["label"])
+    if hasattr(model, "forward_loss"):
+        _, loss = model.forward_loss(x)
+    else:
+        logits, _ = model(x)
+        loss = torch.nn.functional.nll_loss(logits, x["label"])
     loss.backward()
     return loss
 

@@ -335,6 +335,21 @@ int nr_score_fwd(const float* cdd, int64_t ldc, const int64_t* cdd_idx, const fl
                  int64_t ldu, int64_t B, int32_t C, int32_t H, int32_t mode, float* logits,
                  hipStream_t stream);
 
+/* The training head with its loss: logits = log_softmax(cdd_row(b,c) · user[b] / sqrt(H)) as
+ * nr_score_fwd (NR_SCORE_LOG_SOFTMAX) AND loss[0] = mean_b -logits[b][label[b]] -- Manager.py:641's
+ * NLLLoss (reduction 'mean') on TwoTowerBaseModel.forward's output, in one launch (no separate loss
+ * kernels, no zero fill).  B * C <= 16384. */
+int nr_score_nll_fwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
+                     const int64_t* label, int64_t B, int32_t C, int32_t H, float* logits, float* loss,
+                     hipStream_t stream);
+
+/* Backward of nr_score_nll_fwd: the gradient of the loss (dloss, a device scalar, or NULL) plus an
+ * optional gradient of the logits themselves (dlogits [B][C] or NULL). */
+int nr_score_nll_bwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
+                     const float* logits, const int64_t* label, const float* dloss,
+                     const float* dlogits, int64_t B, int32_t C, int32_t H, float* dcdd, int64_t lddc,
+                     float* duser, int64_t lddu, hipStream_t stream);
+
 /* Backward of nr_score_fwd (cdd_idx == NULL form) given dlogits [B][C]. */
 int nr_score_bwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
                  const float* logits, const float* dlogits, int64_t B, int32_t C, int32_t H,

@@ -84,6 +84,87 @@ __global__ __launch_bounds__(256) void score_bwd_kernel(const float* cdd, int64_
   }
 }
 
+// The training head in ONE workgroup for the whole batch (B <= 64 impressions of C candidates):
+// log-softmax logits (as score_fwd_kernel) AND the mean NLL over the batch (Manager.py:382,641,
+// nn.NLLLoss(reduction='mean')): the loss needs no cross-block reduction, zero fill or extra launch.
+// One wave per impression row (strided).
+__global__ __launch_bounds__(1024) void score_nll_fwd_kernel(const float* cdd, int64_t ldc, const float* user,
+                                                             int64_t ldu, const int64_t* label, int B, int C, int H,
+                                                             float scale, float* logits, float* loss) {
+  extern __shared__ float sh[];   // [B * C] scores, then [B] per-row loss terms
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
+  float* sc = sh;
+  float* rl = sh + B * C;
+  for (int r = w; r < B * C; r += nw) {   // one wave per (impression, candidate) dot product
+    const int b = r / C;
+    const float* x = cdd + (int64_t)r * ldc;
+    const float* u = user + (int64_t)b * ldu;
+    float s = 0.f;
+    for (int d = lane; d < H; d += 64) s = fmaf(x[d], u[d], s);
+    s = nr_wave_sum(s);
+    if (lane == 0) sc[r] = s * scale;
+  }
+  __syncthreads();
+  for (int b = w; b < B; b += nw) {
+    float mx = -INFINITY;
+    for (int c = lane; c < C; c += 64) mx = fmaxf(mx, sc[b * C + c]);
+    mx = nr_wave_max(mx);
+    float sum = 0.f;
+    for (int c = lane; c < C; c += 64) sum += __expf(sc[b * C + c] - mx);
+    const float lse = mx + __logf(nr_wave_sum(sum));
+    for (int c = lane; c < C; c += 64) logits[(int64_t)b * C + c] = sc[b * C + c] - lse;
+    if (lane == 0) {
+      const int64_t y = label[b];
+      rl[b] = (y >= 0 && y < C) ? -(sc[b * C + y] - lse) : 0.f;   // out-of-range labels: no term
+    }
+  }
+  __syncthreads();
+  if (w == 0) {   // fixed-order sum of the rows (deterministic)
+    float s = 0.f;
+    for (int b = lane; b < B; b += 64) s += rl[b];
+    s = nr_wave_sum(s);
+    if (lane == 0) loss[0] = s / (float)B;
+  }
+}
+
+// Backward of score_nll_fwd_kernel: d logits = dlogits (optional) - dloss / B at the label, then the
+// log-softmax and dot-product backward (as score_bwd_kernel), one workgroup per impression.
+__global__ __launch_bounds__(256) void score_nll_bwd_kernel(const float* cdd, int64_t ldc, const float* user,
+                                                            int64_t ldu, const float* logits, const int64_t* label,
+                                                            const float* dloss, const float* dlogits, int B, int C,
+                                                            int H, float scale, float* dcdd, int64_t lddc,
+                                                            float* duser, int64_t lddu) {
+  extern __shared__ float ds[];
+  const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  if (w == 0) {
+    const int64_t y = label[b];
+    const float gl = dloss ? -dloss[0] / (float)B : 0.f;
+    float sg = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      const int64_t o = (int64_t)b * C + c;
+      sg += (dlogits ? dlogits[o] : 0.f) + (c == y ? gl : 0.f);
+    }
+    sg = nr_wave_sum(sg);
+    for (int c = lane; c < C; c += 64) {
+      const int64_t o = (int64_t)b * C + c;
+      const float g = (dlogits ? dlogits[o] : 0.f) + (c == y ? gl : 0.f);
+      ds[c] = (g - __expf(logits[o]) * sg) * scale;
+    }
+  }
+  __syncthreads();
+  const float* u = user + (int64_t)b * ldu;
+  for (int d = tid; d < H; d += 256) {
+    float acc = 0.f;
+    const float ud = u[d];
+    for (int c = 0; c < C; ++c) {
+      const float* x = cdd + ((int64_t)b * C + c) * ldc;
+      acc = fmaf(ds[c], x[d], acc);
+      dcdd[((int64_t)b * C + c) * lddc + d] = ds[c] * ud;
+    }
+    duser[(int64_t)b * lddu + d] = acc;
+  }
+}
+
 // torch.optim.Adam (foreach=False, maximize=False, amsgrad=False) per element:
 //   g += wd * p;  m = lerp(m, g, 1 - b1);  v = b2 v + (1 - b2) g²
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
@@ -332,6 +413,31 @@ extern "C" int nr_score_bwd(const float* cdd, int64_t ldc, const float* user, in
   hipLaunchKernelGGL(score_bwd_kernel, dim3((unsigned)B), dim3(256), (size_t)C * sizeof(float), stream, cdd,
                      ldc, user, ldu, logits, dlogits, C, H, 1.0f / sqrtf((float)H), mode, dcdd, lddc,
                      duser, lddu);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_score_nll_fwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
+                                const int64_t* label, int64_t B, int32_t C, int32_t H, float* logits, float* loss,
+                                hipStream_t stream) {
+  if (B < 1 || B > 4096 || C < 1 || H < 1 || B * C > 16384) return NR_EINVAL(0);
+  if (!cdd || !user || !label || !logits || !loss) return NR_EINVAL(1);
+  hipLaunchKernelGGL(score_nll_fwd_kernel, dim3(1), dim3(1024), (size_t)(B * C + B) * sizeof(float), stream, cdd,
+                     ldc, user, ldu, label, (int)B, C, H, 1.0f / sqrtf((float)H), logits, loss);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_score_nll_bwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
+                                const float* logits, const int64_t* label, const float* dloss,
+                                const float* dlogits, int64_t B, int32_t C, int32_t H, float* dcdd, int64_t lddc,
+                                float* duser, int64_t lddu, hipStream_t stream) {
+  if (B < 0 || C < 1 || H < 1) return NR_EINVAL(0);
+  if (!cdd || !user || !logits || !label || !dcdd || !duser) return NR_EINVAL(1);
+  if (B == 0) return NR_OK;
+  hipLaunchKernelGGL(score_nll_bwd_kernel, dim3((unsigned)B), dim3(256), (size_t)C * sizeof(float), stream, cdd,
+                     ldc, user, ldu, logits, label, dloss, dlogits, (int)B, C, H, 1.0f / sqrtf((float)H), dcdd,
+                     lddc, duser, lddu);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

@@ -53,6 +53,9 @@ _SIGS = {
     "nr_gemm_f32_dyn_cus": [c_i64, c_i64, c_i64, ctypes.POINTER(nr_operand), ctypes.POINTER(nr_operand),
                             c_ptr, c_i64, c_ptr, c_i32, ctypes.POINTER(nr_operand), c_i64, c_i32, c_ptr, c_ptr, c_i32,
                             c_i32, c_ptr],
+    "nr_score_nll_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_i32, c_ptr, c_ptr, c_ptr],
+    "nr_score_nll_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_i32, c_i32, c_ptr, c_i64,
+                         c_ptr, c_i64, c_ptr],
     "nr_unique_rows": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                        c_ptr],
     "nr_segment_rows_sum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,

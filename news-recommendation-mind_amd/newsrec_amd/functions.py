@@ -692,6 +692,37 @@ class ScoreFn(torch.autograd.Function):
         return dcdd, duser, None, None, None
 
 
+class ScoreNLLFn(torch.autograd.Function):
+    """compute_score + log_softmax (models/TwoTowerBaseModel.py:51-75) and Manager._train's
+    NLLLoss (utils/Manager.py:382,641; reduction 'mean') in one kernel each way.
+    -> (logits [B, C], loss []); the backward takes either gradient or both."""
+
+    @staticmethod
+    def forward(ctx, cdd, user, B, C, label):
+        H = user.shape[1]
+        logits = torch.empty(B, C, device=user.device)
+        loss = torch.empty((), device=user.device)
+        label = label.to(user.device).reshape(-1)
+        label = label if label.is_contiguous() else label.contiguous()
+        K.score_nll_fwd(cdd, user, label, B, C, H, logits, loss)
+        ctx.save_for_backward(cdd, user, logits, label)
+        ctx.cfg = (B, C)
+        ctx.set_materialize_grads(False)
+        return logits, loss
+
+    @staticmethod
+    def backward(ctx, dlogits, dloss):
+        cdd, user, logits, label = ctx.saved_tensors
+        B, C = ctx.cfg
+        H = user.shape[1]
+        dcdd = _empty(B * C, H, user)
+        duser = _empty(B, H, user)
+        if dlogits is not None and not dlogits.is_contiguous():
+            dlogits = dlogits.contiguous()
+        K.score_nll_bwd(cdd, user, logits, label, dloss, dlogits, B, C, H, dcdd, duser)
+        return dcdd, duser, None, None, None
+
+
 class EmbeddingFn(torch.autograd.Function):
     """BERT_Embedding.forward (models/Embeddings/BERT.py:24-40): row gather; the backward is
     a padding_idx-aware scatter-add into a dense table gradient (embedding_dense_backward)."""

@@ -441,6 +441,31 @@ def score_bwd(cdd, user, logits, dlogits, B, C, H, mode, dcdd, duser):
            L.stream_ptr(user))
 
 
+def score_nll_fwd(cdd, user, label, B, C, H, logits, loss):
+    """Training head + mean NLL in one launch (nr_score_nll_fwd)."""
+    _f32(cdd, user, logits, loss)
+    _rows_ok(cdd, B * C, H, "cdd")
+    _rows_ok(user, B, H, "user")
+    _check_rows(label, None, "label")
+    if label.numel() != B or not logits.is_contiguous() or logits.numel() < B * C:
+        raise L.HipError("score_nll_fwd: label [B] int64, logits contiguous [B, C]")
+    L.call("nr_score_nll_fwd", L.ptr(cdd), cdd.stride(0), L.ptr(user), user.stride(0), L.ptr(label), B, C, H,
+           L.ptr(logits), L.ptr(loss), L.stream_ptr(user))
+
+
+def score_nll_bwd(cdd, user, logits, label, dloss, dlogits, B, C, H, dcdd, duser):
+    _f32(cdd, user, logits, dcdd, duser)
+    _rows_ok(cdd, B * C, H, "cdd")
+    _rows_ok(dcdd, B * C, H, "dcdd")
+    _rows_ok(user, B, H, "user")
+    _rows_ok(duser, B, H, "duser")
+    if dlogits is not None and not dlogits.is_contiguous():
+        raise L.HipError("score_nll_bwd: dlogits must be contiguous")
+    L.call("nr_score_nll_bwd", L.ptr(cdd), cdd.stride(0), L.ptr(user), user.stride(0), L.ptr(logits), L.ptr(label),
+           L.ptr(dloss), L.ptr(dlogits), B, C, H, L.ptr(dcdd), dcdd.stride(0), L.ptr(duser), duser.stride(0),
+           L.stream_ptr(user))
+
+
 def adam(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
     """``step``: an int (host count) or an int64 CUDA scalar tensor (device count, graph replays)."""
     _f32(param, grad, exp_avg, exp_avg_sq)

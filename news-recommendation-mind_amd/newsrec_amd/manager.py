@@ -68,8 +68,11 @@ def train_step(model, optimizer, x, grad_sync=None):
     """Manager._train :636-647 (zero_grad(set_to_none), forward, NLLLoss, backward, step);
     ``grad_sync`` averages gradients over data-parallel ranks before the step."""
     optimizer.zero_grad(set_to_none=True)
-    logits = model(x)[0]
-    loss = torch.nn.functional.nll_loss(logits, x["label"].to(logits.device))
+    if hasattr(model, "forward_loss") and model.training:
+        loss = model.forward_loss(x)[1]   # NLLLoss fused into the head (same numbers)
+    else:
+        logits = model(x)[0]
+        loss = torch.nn.functional.nll_loss(logits, x["label"].to(logits.device))
     loss.backward()
     if grad_sync is not None:
         grad_sync()

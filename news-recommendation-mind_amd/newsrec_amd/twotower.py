@@ -15,7 +15,7 @@ from torch import nn
 from . import _lib as L
 from . import kernels as K
 from .attention import _joined_view
-from .functions import ScoreFn
+from .functions import ScoreFn, ScoreNLLFn
 
 
 class TwoTowerBaseModel(nn.Module):
@@ -76,6 +76,23 @@ class TwoTowerBaseModel(nn.Module):
             cdd_repr, user_repr, kid = self._encode_both(x)
             mode = L.SCORE_LOG_SOFTMAX if self.training else L.SCORE_SIGMOID
             return self.compute_score(cdd_repr, user_repr, mode), kid
+
+    def forward_loss(self, x):
+        """Training forward with the loss of Manager._train (utils/Manager.py:641, NLLLoss on
+        forward(x)'s log-softmax logits) fused into the head: -> (logits, loss).  The same numbers
+        as ``nll_loss(self(x)[0], x["label"])``, one kernel each way instead of three and two."""
+        if not self.training:
+            raise RuntimeError("forward_loss is the training head (log-softmax logits)")
+        with self.arithmetic():
+            cdd_repr, user_repr, _ = self._encode_both(x)
+            B, C, H = cdd_repr.shape
+            cdd = cdd_repr.reshape(B * C, H)
+            user = user_repr.reshape(B, H)
+            if cdd.stride(-1) != 1:
+                cdd = cdd.contiguous()
+            if user.stride(-1) != 1:
+                user = user.contiguous()
+            return ScoreNLLFn.apply(cdd, user, B, C, x["label"])
 
     def _encode_both(self, x):
         cdd_repr = self.encode_news(x)

@@ -142,3 +142,41 @@ def test_unfused_composition_matches_fused():
         emb = model.embedding(x["cdd_encoded_index"])
         _, unfused = model.encoderN(emb, x["cdd_attn_mask"])
     torch.testing.assert_close(unfused, fused, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("cfg", ["cnn_attn", "nrms", "cnn_lstur"])
+def test_forward_loss_fused_head(cfg):
+    """TwoTowerBaseModel.forward_loss (scorer + log-softmax + NLLLoss in one kernel, one kernel back)
+    against forward(x) followed by torch's nll_loss (Manager.py:641): logits, loss and every
+    gradient; also the reference golden loss."""
+    g, model, x = _setup(cfg)
+    model.train()
+    logits_f, loss_f = model.forward_loss(x)
+    loss_f.backward()
+    grads_f = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    model.zero_grad(set_to_none=True)
+    logits, _ = model(x)
+    loss = torch.nn.functional.nll_loss(logits, x["label"])
+    loss.backward()
+    torch.testing.assert_close(logits_f, logits, rtol=0, atol=1e-6)
+    assert abs(loss_f.item() - loss.item()) <= 1e-6
+    assert abs(loss_f.item() - float(g["out.loss"])) < 1e-4
+    for n, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        scale = max(p.grad.abs().max().item(), 1e-6)
+        torch.testing.assert_close(grads_f[n], p.grad, rtol=0, atol=1e-5 * scale, msg=n)
+    # both gradients at once: d(loss + sum(logits * w)) through the fused head
+    model.zero_grad(set_to_none=True)
+    w = torch.randn_like(logits_f)
+    lf, lo = model.forward_loss(x)
+    (lo + (lf * w).sum()).backward()
+    gf = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    model.zero_grad(set_to_none=True)
+    lr_, _ = model(x)
+    (torch.nn.functional.nll_loss(lr_, x["label"]) + (lr_ * w).sum()).backward()
+    for n, p in model.named_parameters():
+        if p.grad is None:
+            continue
+        scale = max(p.grad.abs().max().item(), 1e-6)
+        torch.testing.assert_close(gf[n], p.grad, rtol=0, atol=1e-5 * scale, msg=n)
