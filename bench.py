@@ -99,9 +99,10 @@ class ResidentFeed:
 class DeviceFeed:
     """Batches formed on the device each step from a MIND-large-shaped train split in HBM
     (MINDStore + nr_form_train_batch).  The sampler's epoch order (DistributedSampler: shuffled,
-    strided over ranks) is uploaded once; feed(i) copies step i's B indices into a static buffer
-    and form() launches the formation kernel, which draws negatives from the device RNG pair
-    (captured in the graph, every replay draws fresh negatives)."""
+    strided over ranks) is uploaded once; form() launches the formation kernel, which takes the
+    next B indices of that order at a device cursor and draws negatives from the device RNG pair,
+    advancing both itself (captured in the graph: every replay forms the next batch with fresh
+    negatives, no per-step copy)."""
 
     def __init__(self, device, world, rank, b=B, n_impr=TRAIN_IMPR_SYNTH):
         from newsrec_amd.dist import shard_train
@@ -112,16 +113,13 @@ class DeviceFeed:
         order = shard_train(len(self.store), world, rank, shuffle=True, seed=0)
         self.order = torch.tensor(order, dtype=torch.int64, device=device)
         self.b = b
-        self.idx = self.order[:b].clone()
-        self.x = self.store.train_batch(self.idx, device_rng=True)
+        self.x = self.store.train_batch(self.order, device_rng=True, epoch_batch=b)
 
     def feed(self, i):
-        n = self.order.numel() // self.b
-        s = (i % n) * self.b
-        self.idx.copy_(self.order[s:s + self.b], non_blocking=True)
+        pass   # the formation kernel walks the epoch order itself
 
     def form(self):
-        return self.store.train_batch(self.idx, out=self.x, device_rng=True)
+        return self.store.train_batch(self.order, out=self.x, device_rng=True, epoch_batch=self.b)
 
 
 class GraphedStep:
@@ -188,6 +186,18 @@ class GraphedStep:
             self.opt_graph.replay()
 
 
+_ONES = {}
+
+
+def _one(t):
+    """A persistent 1.0 on t's device as the loss gradient: autograd's implicit ones_like would be a
+    fill launch per step (created by the eager warm-up, so a captured step reads it)."""
+    one = _ONES.get(t.device)
+    if one is None:
+        one = _ONES[t.device] = torch.ones((), device=t.device)
+    return one
+
+
 def forward_backward(model, opt, x):
     """Manager._train :636-644: zero_grad, forward, NLLLoss, backward (the two-tower models fuse the
     loss into their head: TwoTowerBaseModel.forward_loss)."""
@@ -197,7 +207,7 @@ def forward_backward(model, opt, x):
     else:
         logits, _ = model(x)
         loss = torch.nn.functional.nll_loss(logits, x["label"])
-    loss.backward()
+    loss.backward(_one(loss))
     return loss
 
 
@@ -255,27 +265,21 @@ def fast_eval_leg(model, dev, world, rank, n_impr):
 def xformer_leg(dev, steps=5, warmup=2, b=B):
     """configs[4] beside the headline: XFormer (bert-base news encoder + 501-token user sequence,
     12 layers, dropout 0.1, Adam) train steps and eval forwards on synthetic MIND-shaped batches,
-    one GPU, eager.  FLOPs are algorithmic (dense layers + attention + pooler, train = 3x fwd)."""
+    one GPU; the train step replayed as a HIP graph like the headline (dropout draws advance on the
+    device).  FLOPs are algorithmic (dense layers + attention + pooler, train = 3x fwd)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_bert as BB
     from newsrec_amd.manager import get_optim
     model = BB.build("xformer", 12, dev)
-    opt = get_optim(model)
+    opt = get_optim(model, capturable=True)
     gen = torch.Generator().manual_seed(3)
     x = {k: v.to(dev) for k, v in BB.synth(gen, b).items()}
-
-    def step():
-        opt.zero_grad(set_to_none=True)
-        logits, _ = model(x)
-        torch.nn.functional.nll_loss(logits, x["label"]).backward()
-        opt.step()
     model.train()
-    for _ in range(warmup):
-        step()
+    step = GraphedStep(model, opt, ResidentFeed([x]), None, warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    for i in range(steps):
+        step(i)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / steps
     model.eval()
@@ -288,10 +292,11 @@ def xformer_leg(dev, steps=5, warmup=2, b=B):
         torch.cuda.synchronize()
         ev = (time.perf_counter() - t1) / steps
     f = BB.flops_per_impression("xformer", 12) * b
-    del model, opt
+    del step, model, opt
     torch.cuda.empty_cache()
     return {"workload": "XFormer train step: bert-base (12 layers, 768, 12 heads) over 5x30-token candidates + "
                         "501-token user sequence, dropout 0.1, Adam; synthetic batches, random init",
+            "launch": "hipGraph replay of the train step",
             "per_gpu_batch": b, "impressions_per_s": round(b / el, 1), "ms_per_step": round(el * 1e3, 2),
             "train_tflops": round(3 * f / el / 1e12, 1), "eval_impressions_per_s": round(b / ev, 1),
             "eval_tflops": round(f / ev / 1e12, 1),

@@ -120,6 +120,27 @@ int nr_gemm_f32_dyn_cus(int64_t M, int64_t N, int64_t K, const nr_operand* A, co
                         const int32_t* m_dev, const int32_t* k_dev, int32_t prec, int32_t max_cus,
                         hipStream_t stream);
 
+/* nr_gemm_f32 / nr_gemm_f32_dyn_cus with a caller-owned workspace (m_dev, k_dev NULL and max_cus 0:
+ * the static form).  When a split-K NR_EPI_ATOMIC contraction runs on the 256 x 256 kernel and
+ * `work` (16-B aligned, work_elems floats) holds its partial tiles, every split stores its partial
+ * tile with plain stores and one reduction launch adds the splits into C in split order
+ * (deterministic) -- instead of fp32 atomics.  Any other call ignores `work`.
+ * nr_gemm_splitk_workspace() elements always suffice.  Measured: without colsum this path is
+ * slower than the atomic epilogue on the NRMS weight gradient (292-301 vs 277 µs) and equal on
+ * BERT's; it pays when it also carries the bias gradient (below).
+ * colsum (device, [M], may be NULL; then colsum_folded may be NULL too): a weight gradient's bias
+ * gradient, colsum[m] += Σ_k A[k][m] for an MN-contiguous A (A = dY stored [K][M]).  On that path
+ * the units of the first column tile sum the A tiles they load anyway and the reduction adds the
+ * per-split sums: *colsum_folded (host) = 1.  Otherwise *colsum_folded = 0 and colsum is left
+ * alone -- the caller reduces it (nr_colsum). */
+int nr_gemm_f32_ws(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B, float* C,
+                   int64_t ldc, const float* bias, int32_t epilogue, const nr_operand* c_rows,
+                   int64_t pad_row, int32_t split_k, const int32_t* m_dev, const int32_t* k_dev,
+                   int32_t prec, int32_t max_cus, float* work, int64_t work_elems, float* colsum,
+                   int32_t* colsum_folded, hipStream_t stream);
+/* floats of split-K workspace that serve any nr_gemm_f32_ws call on the current device */
+int64_t nr_gemm_splitk_workspace(void);
+
 /* ------------------------------------------------------------------ distinct token rows */
 
 /* Distinct ids of a token batch (the news tower projects each word-table row once, not once
@@ -131,8 +152,11 @@ int nr_gemm_f32_dyn_cus(int64_t M, int64_t N, int64_t K, const nr_operand* A, co
  *                    distinct row owning CSR position p.  Leave a token out only when its
  *                    gradient row is zero (masked tokens of nr_mha_pool_bwd: exactly zero).
  *   counts[4]        {U, U_pad, bad, T_csr} (bad = 1 if an id fell outside [0, V))
- * Equal ids are aggregated per workgroup (LDS hash) before the global atomics.
- * work: nr_unique_rows_workspace(V) int32 (5*V + 2*ceil(V/4096)).
+ * Equal ids are aggregated per workgroup (LDS hash) before the global atomics; three launches
+ * (count, scan, fill), four above 65,536 ids (the scan's tile totals in a pass of their own).
+ * work: nr_unique_rows_workspace(V) int32 (4 + 4*ceil4(V) + 2*ceil(V/4096)), 16-B aligned, all zero
+ * before the first call; every call leaves its flag word and counters zero again (the fill pass
+ * clears them: no zero-fill launch), so one buffer serves every call on a stream, one call at a time.
  * Capacity: uids / seg_off hold ceil32(min(T, V)) (+1) entries. */
 int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t fill_row,
                    const void* grad_mask, int32_t mask_dtype, int32_t* work, int64_t* uids,
@@ -338,10 +362,15 @@ int nr_score_fwd(const float* cdd, int64_t ldc, const int64_t* cdd_idx, const fl
 /* The training head with its loss: logits = log_softmax(cdd_row(b,c) · user[b] / sqrt(H)) as
  * nr_score_fwd (NR_SCORE_LOG_SOFTMAX) AND loss[0] = mean_b -logits[b][label[b]] -- Manager.py:641's
  * NLLLoss (reduction 'mean') on TwoTowerBaseModel.forward's output, in one launch (no separate loss
- * kernels, no zero fill).  B * C <= 16384. */
+ * kernels, no zero fill): one workgroup per impression, the last to finish sums the B loss terms
+ * in a fixed order.  work: nr_score_nll_workspace(B) int32, all zero before the first call; every
+ * call leaves its first word zero again (the rest is scratch), so one buffer serves every call on
+ * a stream. */
 int nr_score_nll_fwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
                      const int64_t* label, int64_t B, int32_t C, int32_t H, float* logits, float* loss,
-                     hipStream_t stream);
+                     int32_t* work, hipStream_t stream);
+/* int32 elements of nr_score_nll_fwd's work buffer for B impressions */
+int64_t nr_score_nll_workspace(int64_t B);
 
 /* Backward of nr_score_nll_fwd: the gradient of the loss (dloss, a device scalar, or NULL) plus an
  * optional gradient of the logits themselves (dlogits [B][C] or NULL). */
@@ -383,6 +412,12 @@ typedef struct nr_adam_tensor {
 } nr_adam_tensor;
 int nr_adam_multi(const nr_adam_tensor* tensors, int32_t count, float beta1, float beta2, float eps,
                   float weight_decay, float grad_scale, hipStream_t stream);
+/* nr_adam_multi whose launches also advance the device step counts (tensors with step_dev): each
+ * tensor's bias correction uses *step_dev + 1 and the workgroup that finishes last adds 1 to every
+ * step_dev of its launch (torch's `state_steps += 1` without a launch of its own).  ticket: one
+ * int32, zero before the first call and left zero by every call. */
+int nr_adam_multi_step(const nr_adam_tensor* tensors, int32_t count, float beta1, float beta2, float eps,
+                       float weight_decay, float grad_scale, int32_t* ticket, hipStream_t stream);
 
 /* out[i] = table[idx[i]] rows of E floats (E % 4 == 0).  BERT_Embedding.forward, BERT.py:39. */
 int nr_embedding_fwd(const float* table, int64_t V, int64_t E, const int64_t* idx, int64_t n,
@@ -398,6 +433,11 @@ int nr_embedding_bwd(const float* dout, int64_t V, int64_t E, const int64_t* idx
 int64_t nr_colsum_workspace(int64_t rows, int64_t cols);
 int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out, float* work,
               hipStream_t stream);
+/* nr_colsum in one launch: the last workgroup to finish each 64-column chunk sums that chunk's
+ * partial rows (fixed order: the same result as nr_colsum).  tick: ceil(cols / 64) int32 arrival
+ * counters, zero before the first call and left zero by every call. */
+int nr_colsum_ws(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out, float* work,
+                 int32_t* tick, hipStream_t stream);
 
 /* ---------------------------------------------------------------- device-side MIND data path
  * (csrc/mind_batch.hip).  The dataset lives in HBM as CSR arrays:
@@ -409,13 +449,19 @@ int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* ou
  *   uindex       [I] int32 user index per impression ("uindexes")
  * status: int32 word OR-ed with 1 (sample index out of range), 2 (news id out of range),
  * 4 (candidate row / user row out of range); the caller zeroes it and checks it when it wants. */
-enum nr_batch_flags { NR_BATCH_REVERSE_HISTORY = 1, NR_BATCH_SHUFFLE_POS = 2 };
+enum nr_batch_flags { NR_BATCH_REVERSE_HISTORY = 1, NR_BATCH_SHUFFLE_POS = 2, NR_BATCH_CURSOR = 4 };
 
 /* One collated train batch of B impressions: MIND.__getitem__ train branch
  * (utils/MIND.py:311-365) with newsample (utils/utils.py:83-98) for every sample_idx[b] in [0, P),
  * then the DataLoader default collate.  Negatives: a uniform npratio-subset in uniform random
- * order drawn from the counter RNG (seed, offset [+ b * 4C + d]); or the rng device pair
- * {seed, offset} when non-null.  Outputs (C = npratio + 1): cdd_id [B,C] i64, his_id [B,his_size]
+ * order drawn from the counter RNG (seed, offset [+ b * 4C + d]); or, when rng is non-null, from
+ * the device words rng = {seed, offset, ticket, cursor, n_order}: the launch draws from (rng[0],
+ * rng[1]) and advances rng[1] by B * 4C itself (the workgroup that finishes last, counted on
+ * rng[2], which is zero on entry and left zero), so a replayed graph forms fresh batches with no
+ * extra launch.  NR_BATCH_CURSOR (rng required): sample_idx is a whole epoch order of rng[4]
+ * entries and batch b takes sample_idx[(rng[3] mod (rng[4] / B)) * B + b] (the sampler's
+ * DistributedSampler order walked on the device); the last workgroup also adds 1 to rng[3].
+ * Outputs (C = npratio + 1): cdd_id [B,C] i64, his_id [B,his_size]
  * i64, cdd_tok/cdd_attn [B,C,L] i64, his_tok/his_attn [B,his_size,L] i64, cdd_mask [B,C] f64,
  * his_mask [B,his_size] f64, user_id [B] i64, label [B] i64.  Replaces the Python
  * `random.sample` / `np.random.shuffle` streams (parity: structure exact, draws from this RNG). */
@@ -424,7 +470,7 @@ int nr_form_train_batch(const int64_t* sample_idx, int64_t B, const int32_t* imp
                         const int32_t* neg_ids, const int32_t* uindex, const int32_t* tok,
                         const int32_t* attn, int64_t n_news, int32_t L, int32_t npratio,
                         int32_t his_size, int32_t flags, uint64_t seed, uint64_t offset,
-                        const uint64_t* rng, int64_t* cdd_id, int64_t* his_id, int64_t* cdd_tok,
+                        uint64_t* rng, int64_t* cdd_id, int64_t* his_id, int64_t* cdd_tok,
                         int64_t* cdd_attn, int64_t* his_tok, int64_t* his_attn, double* cdd_mask,
                         double* his_mask, int64_t* user_id, int64_t* label, int32_t* status,
                         hipStream_t stream);

@@ -23,7 +23,6 @@
 
 namespace {
 
-constexpr int SCAN_THREADS = 256;
 constexpr int SEG_RANGE = 64;   // CSR positions per segment-sum workgroup
 constexpr int CNT_THREADS = 1024;
 constexpr int HASH_SLOTS = 2048;
@@ -46,118 +45,52 @@ __device__ __forceinline__ bool grad_on(const void* gm, int dt, int64_t t) {
   return gm == nullptr || nr_mask_at(gm, dt, t);
 }
 
-// cnt_all[v]: tokens of id v (distinctness), cnt_csr[v]: those with grad_mask set (segments)
-__global__ __launch_bounds__(CNT_THREADS) void count_kernel(const int64_t* __restrict__ ids, int64_t T, int64_t V,
-                                                            const void* gm, int gm_dt, int32_t* __restrict__ cnt_all,
-                                                            int32_t* __restrict__ cnt_csr,
-                                                            int32_t* __restrict__ counts) {
-  __shared__ int32_t hkey[HASH_SLOTS], hall[HASH_SLOTS], hcsr[HASH_SLOTS];
-  for (int i = threadIdx.x; i < HASH_SLOTS; i += blockDim.x) { hkey[i] = -1; hall[i] = 0; hcsr[i] = 0; }
-  __syncthreads();
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < T) {
-    const int64_t v = ids[t];
-    if (v < 0 || v >= V) {
-      counts[2] = 1;   // out-of-range id: flagged, token dropped
-    } else {
-      const int h = hash_slot(hkey, (int32_t)v);
-      atomicAdd(&hall[h], 1);
-      if (grad_on(gm, gm_dt, t)) atomicAdd(&hcsr[h], 1);
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < HASH_SLOTS; i += blockDim.x)
-    if (hkey[i] >= 0) {
-      atomicAdd(&cnt_all[hkey[i]], hall[i]);
-      if (hcsr[i]) atomicAdd(&cnt_csr[hkey[i]], hcsr[i]);
-    }
-}
+// Workspace (nr_unique_rows_workspace): ctrl[4] | cnt_all[V] | cnt_csr[V] | cursor[V] | pos[V] | tot[2 nb].
+// ctrl, cnt_all and cnt_csr are zero on entry and left zero on return (fill_kernel, the last pass,
+// clears the counters and the flag), so a call needs no zero-fill launch; cursor / pos / tot are
+// rewritten every call.
+constexpr int CTRL_BAD = 1;    // an id fell outside [0, V)
+constexpr int CTRL_WORDS = 4;
 
-// Vocabulary scan in two launches over tiles of SCAN_TILE = 16 x 256 entries (one workgroup per
-// tile, so the scan runs on ceil(V / 4096) CUs instead of one):
-//   scan_reduce: per-tile totals of (cnt_all[v] > 0) and cnt_csr[v] -> tot[2b], tot[2b + 1];
-//   scan_down:   each tile adds up the totals of the tiles before it, scans its own entries
-//                (coalesced loads into LDS, each thread scans 16 consecutive entries read back
-//                with a 1-word row pad, wave scans of the thread sums) and writes
-//                pos[v] / off[v] (exclusive scans), the compaction uids[pos[v]] = v,
-//                seg_off[pos[v]] = off[v], all leaving through LDS with coalesced stores; the last
-//                tile writes counts and the pad entries.
+// Vocabulary scan over tiles of SCAN_PER x NT entries: coalesced loads into LDS, each thread
+// scans SCAN_PER consecutive entries read back with a 1-word row pad, wave scans of the thread
+// sums; writes pos[v] (exclusive scan of "id present"),
+// cursor[v] (exclusive scan of the segment lengths: each segment's first CSR slot, advanced by
+// fill_kernel's atomics), the compaction uids[pos[v]] = v and seg_off[pos[v]] = cursor[v], all
+// leaving through LDS with coalesced stores.  Totals of the tile -> tile_u / tile_c.
 constexpr int SCAN_PER = 16;
-constexpr int SCAN_TILE = SCAN_PER * SCAN_THREADS;
-constexpr int SCAN_LDS_WORDS = SCAN_TILE + SCAN_TILE / SCAN_PER;
+template <int NT> constexpr int scan_tile_n() { return SCAN_PER * NT; }
+template <int NT> constexpr int scan_lds_words() { return scan_tile_n<NT>() + scan_tile_n<NT>() / SCAN_PER; }
 
 __device__ __forceinline__ int scan_lds_index(int v) { return v + v / SCAN_PER; }
 
+template <int NT>
 __device__ __forceinline__ void scan_load(int32_t* tile, const int32_t* __restrict__ src, int64_t base, int nv) {
   const int tid = threadIdx.x;
   int32_t ld[SCAN_PER];   // all loads in flight before the first LDS store
 #pragma unroll
   for (int k = 0; k < SCAN_PER; ++k) {
-    const int i = tid + k * SCAN_THREADS;
+    const int i = tid + k * NT;
     ld[k] = i < nv ? src[base + i] : 0;
   }
 #pragma unroll
-  for (int k = 0; k < SCAN_PER; ++k) tile[scan_lds_index(tid + k * SCAN_THREADS)] = ld[k];
+  for (int k = 0; k < SCAN_PER; ++k) tile[scan_lds_index(tid + k * NT)] = ld[k];
 }
 
-// block-wide sums of two values (every thread gets both)
-__device__ __forceinline__ void block_sum2(int32_t& a, int32_t& b, int32_t* red) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    a += __shfl_xor(a, d, 64);
-    b += __shfl_xor(b, d, 64);
-  }
-  if (lane == 0) { red[2 * w] = a; red[2 * w + 1] = b; }
-  __syncthreads();
-  a = 0; b = 0;
-#pragma unroll
-  for (int k = 0; k < SCAN_THREADS / 64; ++k) { a += red[2 * k]; b += red[2 * k + 1]; }
-}
-
-__global__ __launch_bounds__(SCAN_THREADS) void scan_reduce_kernel(const int32_t* __restrict__ cnt_all,
-                                                                   const int32_t* __restrict__ cnt_csr, int64_t V,
-                                                                   int32_t* __restrict__ tot) {
-  __shared__ int32_t red[2 * SCAN_THREADS / 64];
-  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
-  const int nv = (int)(V - base < SCAN_TILE ? V - base : SCAN_TILE);
-  int32_t fu = 0, fc = 0;
-#pragma unroll
-  for (int k = 0; k < SCAN_PER; ++k) {   // coalesced: the order inside the tile is irrelevant to a sum
-    const int i = threadIdx.x + k * SCAN_THREADS;
-    if (i < nv) {
-      fu += cnt_all[base + i] > 0 ? 1 : 0;
-      fc += cnt_csr[base + i];
-    }
-  }
-  block_sum2(fu, fc, red);
-  if (threadIdx.x == 0) { tot[2 * blockIdx.x] = fu; tot[2 * blockIdx.x + 1] = fc; }
-}
-
-__global__ __launch_bounds__(SCAN_THREADS) void scan_down_kernel(const int32_t* __restrict__ cnt_all,
-                                                                 const int32_t* __restrict__ cnt_csr, int64_t V,
-                                                                 const int32_t* __restrict__ tot,
-                                                                 int32_t* __restrict__ pos, int32_t* __restrict__ off,
-                                                                 int64_t* __restrict__ uids,
-                                                                 int32_t* __restrict__ seg_off,
-                                                                 int32_t* __restrict__ counts, int64_t fill_row) {
-  extern __shared__ int32_t tile[];   // SCAN_LDS_WORDS
-  __shared__ int32_t wu[SCAN_THREADS / 64], wc[SCAN_THREADS / 64], red[2 * SCAN_THREADS / 64];
+template <int NT>
+__device__ void scan_tile(int32_t* tile, int32_t* wu, int32_t* wc, const int32_t* __restrict__ cnt_all,
+                          const int32_t* __restrict__ cnt_csr, int64_t base, int nv, int32_t ubase, int32_t cbase,
+                          int32_t* __restrict__ pos, int32_t* __restrict__ cursor, int64_t* __restrict__ uids,
+                          int32_t* __restrict__ seg_off, int32_t& tile_u, int32_t& tile_c) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int b = blockIdx.x;
-  const int64_t base = (int64_t)b * SCAN_TILE;
-  const int nv = (int)(V - base < SCAN_TILE ? V - base : SCAN_TILE);
-  // totals of the tiles before this one (their loads overlap this tile's loads)
-  int32_t ubase = 0, cbase = 0;
-  for (int j = tid; j < b; j += SCAN_THREADS) { ubase += tot[2 * j]; cbase += tot[2 * j + 1]; }
   int32_t f[SCAN_PER], c[SCAN_PER];   // f: id present, c: segment length
-  scan_load(tile, cnt_all, base, nv);
+  scan_load<NT>(tile, cnt_all, base, nv);
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < SCAN_PER; ++k) f[k] = tile[scan_lds_index(SCAN_PER * tid + k)] > 0 ? 1 : 0;
   __syncthreads();
-  scan_load(tile, cnt_csr, base, nv);
-  block_sum2(ubase, cbase, red);   // (its barrier also publishes the tile)
+  scan_load<NT>(tile, cnt_csr, base, nv);
+  __syncthreads();
   int32_t fu = 0, fc = 0;
 #pragma unroll
   for (int k = 0; k < SCAN_PER; ++k) {
@@ -178,16 +111,17 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_down_kernel(const int32_t* 
   pu += iu - fu;   // exclusive
   pc += ic - fc;
   const int32_t pu0 = pu, pc0 = pc;
-  int32_t tile_u = 0;
+  tile_u = 0;
+  tile_c = 0;
 #pragma unroll
-  for (int k = 0; k < SCAN_THREADS / 64; ++k) tile_u += wu[k];
+  for (int k = 0; k < NT / 64; ++k) { tile_u += wu[k]; tile_c += wc[k]; }
 #pragma unroll
   for (int k = 0; k < SCAN_PER; ++k) {
     tile[scan_lds_index(SCAN_PER * tid + k)] = pu;
     pu += f[k];
   }
   __syncthreads();
-  for (int i = tid; i < nv; i += SCAN_THREADS) pos[base + i] = tile[scan_lds_index(i)];
+  for (int i = tid; i < nv; i += NT) pos[base + i] = tile[scan_lds_index(i)];
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < SCAN_PER; ++k) {
@@ -195,7 +129,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_down_kernel(const int32_t* 
     pc += c[k];
   }
   __syncthreads();
-  for (int i = tid; i < nv; i += SCAN_THREADS) off[base + i] = tile[scan_lds_index(i)];
+  for (int i = tid; i < nv; i += NT) cursor[base + i] = tile[scan_lds_index(i)];
   __syncthreads();
   pu = pu0;
 #pragma unroll
@@ -204,7 +138,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_down_kernel(const int32_t* 
     pu += f[k];
   }
   __syncthreads();
-  for (int i = tid; i < tile_u; i += SCAN_THREADS) uids[ubase + i] = base + tile[i];
+  for (int i = tid; i < tile_u; i += NT) uids[ubase + i] = base + tile[i];
   __syncthreads();
   pu = pu0;
   pc = pc0;
@@ -215,36 +149,150 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_down_kernel(const int32_t* 
     pc += c[k];
   }
   __syncthreads();
-  for (int i = tid; i < tile_u; i += SCAN_THREADS) seg_off[ubase + i] = tile[i];
-  if (b == (int)gridDim.x - 1) {   // the last tile knows the totals
-    int32_t tile_c = 0;
-#pragma unroll
-    for (int k = 0; k < SCAN_THREADS / 64; ++k) tile_c += wc[k];
-    const int32_t U = ubase + tile_u, Tv = cbase + tile_c;
-    const int32_t Up = (U + 31) / 32 * 32;
-    if (tid == 0) {
-      counts[0] = U;
-      counts[1] = Up;
-      counts[3] = Tv;
-      seg_off[Up] = Tv;
-    }
-    if (tid < Up - U) {
-      uids[U + tid] = fill_row;
-      seg_off[U + tid] = Tv;
-    }
+  for (int i = tid; i < tile_u; i += NT) seg_off[ubase + i] = tile[i];
+  __syncthreads();   // tile / wu / wc free for the next tile
+}
+
+// counts = {U, U_pad, bad, T_csr} and the pad entries of uids / seg_off (one workgroup)
+__device__ __forceinline__ void scan_finish(int32_t U, int32_t Tv, const int32_t* __restrict__ ctrl,
+                                            int64_t* __restrict__ uids, int32_t* __restrict__ seg_off,
+                                            int32_t* __restrict__ counts, int64_t fill_row) {
+  const int tid = threadIdx.x;
+  const int32_t Up = (U + 31) / 32 * 32;
+  if (tid == 0) {
+    counts[0] = U;
+    counts[1] = Up;
+    counts[2] = ctrl[CTRL_BAD];
+    counts[3] = Tv;
+    seg_off[Up] = Tv;
+  }
+  if (tid < Up - U) {
+    uids[U + tid] = fill_row;
+    seg_off[U + tid] = Tv;
   }
 }
 
+// cnt_all[v]: tokens of id v (distinctness), cnt_csr[v]: those with grad_mask set (segments)
+__global__ __launch_bounds__(CNT_THREADS) void count_kernel(const int64_t* __restrict__ ids, int64_t T, int64_t V,
+                                                            const void* gm, int gm_dt, int32_t* __restrict__ ctrl,
+                                                            int32_t* __restrict__ cnt_all,
+                                                            int32_t* __restrict__ cnt_csr) {
+  __shared__ int32_t hkey[HASH_SLOTS], hall[HASH_SLOTS], hcsr[HASH_SLOTS];
+  for (int i = threadIdx.x; i < HASH_SLOTS; i += blockDim.x) { hkey[i] = -1; hall[i] = 0; hcsr[i] = 0; }
+  __syncthreads();
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < T) {
+    const int64_t v = ids[t];
+    if (v < 0 || v >= V) {
+      ctrl[CTRL_BAD] = 1;   // out-of-range id: flagged, token dropped
+    } else {
+      const int h = hash_slot(hkey, (int32_t)v);
+      atomicAdd(&hall[h], 1);
+      if (grad_on(gm, gm_dt, t)) atomicAdd(&hcsr[h], 1);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < HASH_SLOTS; i += blockDim.x)
+    if (hkey[i] >= 0) {
+      atomicAdd(&cnt_all[hkey[i]], hall[i]);
+      if (hcsr[i]) atomicAdd(&cnt_csr[hkey[i]], hcsr[i]);
+    }
+}
+
+// The scan over tiles of 16 x 256 entries, one workgroup per tile (ceil(V / 4096) CUs):
+//   scan_down:   each tile finds the totals of the tiles before it and runs scan_tile; the last tile
+//                writes counts and the pad entries.  Up to SCAN_OWN_MAX ids a tile sums the counters
+//                before it itself (<= 56 K int32 reads: one launch);
+//   scan_reduce: larger vocabularies first reduce per-tile totals -> tot[2b], tot[2b + 1], which
+//                scan_down then adds up.
+constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_OWN_MAX = 16 * scan_tile_n<SCAN_THREADS>();
+
+// block-wide sums of two values (every thread gets both)
+__device__ __forceinline__ void block_sum2(int32_t& a, int32_t& b, int32_t* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    a += __shfl_xor(a, d, 64);
+    b += __shfl_xor(b, d, 64);
+  }
+  if (lane == 0) { red[2 * w] = a; red[2 * w + 1] = b; }
+  __syncthreads();
+  a = 0; b = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_THREADS / 64; ++k) { a += red[2 * k]; b += red[2 * k + 1]; }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void scan_reduce_kernel(const int32_t* __restrict__ cnt_all,
+                                                                   const int32_t* __restrict__ cnt_csr, int64_t V,
+                                                                   int32_t* __restrict__ tot) {
+  __shared__ int32_t red[2 * SCAN_THREADS / 64];
+  constexpr int TILE = scan_tile_n<SCAN_THREADS>();
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int nv = (int)(V - base < TILE ? V - base : TILE);
+  int32_t fu = 0, fc = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) {   // coalesced: the order inside the tile is irrelevant to a sum
+    const int i = threadIdx.x + k * SCAN_THREADS;
+    if (i < nv) {
+      fu += cnt_all[base + i] > 0 ? 1 : 0;
+      fc += cnt_csr[base + i];
+    }
+  }
+  block_sum2(fu, fc, red);
+  if (threadIdx.x == 0) { tot[2 * blockIdx.x] = fu; tot[2 * blockIdx.x + 1] = fc; }
+}
+
+template <bool OWN_PREFIX>
+__global__ __launch_bounds__(SCAN_THREADS) void scan_down_kernel(const int32_t* __restrict__ ctrl,
+                                                                 const int32_t* __restrict__ cnt_all,
+                                                                 const int32_t* __restrict__ cnt_csr, int64_t V,
+                                                                 const int32_t* __restrict__ tot,
+                                                                 int32_t* __restrict__ pos, int32_t* __restrict__ cursor,
+                                                                 int64_t* __restrict__ uids,
+                                                                 int32_t* __restrict__ seg_off,
+                                                                 int32_t* __restrict__ counts, int64_t fill_row) {
+  __shared__ int32_t tile[scan_lds_words<SCAN_THREADS>()];
+  __shared__ int32_t wu[SCAN_THREADS / 64], wc[SCAN_THREADS / 64], red[2 * SCAN_THREADS / 64];
+  constexpr int TILE = scan_tile_n<SCAN_THREADS>();
+  const int b = blockIdx.x;
+  const int64_t base = (int64_t)b * TILE;
+  const int nv = (int)(V - base < TILE ? V - base : TILE);
+  int32_t ubase = 0, cbase = 0;   // totals of the tiles before this one
+  if constexpr (OWN_PREFIX) {   // the counters themselves: int4 loads (both arrays 16-B aligned, base % 4096 == 0)
+    const int4* a4 = reinterpret_cast<const int4*>(cnt_all);
+    const int4* c4 = reinterpret_cast<const int4*>(cnt_csr);
+#pragma unroll 4
+    for (int64_t q = threadIdx.x; q < base / 4; q += SCAN_THREADS) {
+      const int4 a = a4[q], c = c4[q];
+      ubase += (a.x > 0) + (a.y > 0) + (a.z > 0) + (a.w > 0);
+      cbase += c.x + c.y + c.z + c.w;
+    }
+  } else {
+    for (int j = threadIdx.x; j < b; j += SCAN_THREADS) { ubase += tot[2 * j]; cbase += tot[2 * j + 1]; }
+  }
+  block_sum2(ubase, cbase, red);
+  int32_t tu, tc;
+  scan_tile<SCAN_THREADS>(tile, wu, wc, cnt_all, cnt_csr, base, nv, ubase, cbase, pos, cursor, uids, seg_off, tu, tc);
+  if (b == (int)gridDim.x - 1) scan_finish(ubase + tu, cbase + tc, ctrl, uids, seg_off, counts, fill_row);
+}
+
 // inv[t] for every token; CSR slots for the tokens with grad_mask set: slot = (block base of its
-// id) + (its rank in the block), one global atomic per distinct id of the block.
-// seg_of[p] = the distinct row of CSR position p.
+// id, an atomic on the segment cursor the scan left at the segment's first slot) + (its rank in
+// the block), one global atomic per distinct id of the block.  seg_of[p] = the distinct row of CSR
+// position p.
 __global__ __launch_bounds__(CNT_THREADS) void fill_kernel(const int64_t* __restrict__ ids, int64_t T, int64_t V,
                                                            const void* gm, int gm_dt,
                                                            const int32_t* __restrict__ pos,
-                                                           const int32_t* __restrict__ off,
                                                            int32_t* __restrict__ cursor, int64_t* __restrict__ inv,
                                                            int32_t* __restrict__ seg_tok,
-                                                           int32_t* __restrict__ seg_of) {
+                                                           int32_t* __restrict__ seg_of, int32_t* __restrict__ ctrl,
+                                                           int4* __restrict__ counters, int64_t n_counter4) {
+  // the call's last pass: both counters (2 x ceil4(V) int32, contiguous) and the flag back to zero
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n_counter4; q += (int64_t)gridDim.x * blockDim.x)
+    counters[q] = make_int4(0, 0, 0, 0);
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl[CTRL_BAD] = 0;
   __shared__ int32_t hkey[HASH_SLOTS], hcnt[HASH_SLOTS];
   for (int i = threadIdx.x; i < HASH_SLOTS; i += blockDim.x) { hkey[i] = -1; hcnt[i] = 0; }
   __syncthreads();
@@ -264,7 +312,7 @@ __global__ __launch_bounds__(CNT_THREADS) void fill_kernel(const int64_t* __rest
     if (hkey[i] >= 0) hcnt[i] = atomicAdd(&cursor[hkey[i]], hcnt[i]);
   __syncthreads();
   if (!seg) return;
-  const int32_t p = off[v] + hcnt[h] + rank;
+  const int32_t p = hcnt[h] + rank;
   seg_tok[p] = (int32_t)t;
   seg_of[p] = pos[v];
 }
@@ -460,63 +508,46 @@ __global__ __launch_bounds__(FIX_THREADS) void segsum_fix_kernel(int64_t w4, con
   }
 }
 
-// work[0, n) = 0 and counts[0..3] = 0 (int4 stores when work is 16-B aligned, scalar tail)
-__global__ __launch_bounds__(256) void zero_work_kernel(int32_t* __restrict__ work, int64_t n,
-                                                        int32_t* __restrict__ counts) {
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (reinterpret_cast<uintptr_t>(work) & 15) {
-    for (int64_t i = i0; i < n; i += stride) work[i] = 0;
-    if (blockIdx.x == 0 && threadIdx.x < 4) counts[threadIdx.x] = 0;
-    return;
-  }
-  const int64_t n4 = n / 4;
-  int4* w4 = reinterpret_cast<int4*>(work);
-  for (int64_t i = i0; i < n4; i += stride) w4[i] = make_int4(0, 0, 0, 0);
-  if (blockIdx.x == 0) {
-    if (threadIdx.x < n - 4 * n4) work[4 * n4 + threadIdx.x] = 0;
-    if (threadIdx.x < 4) counts[threadIdx.x] = 0;
-  }
-}
-
 }  // namespace
 
 extern "C" int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t fill_row, const void* grad_mask,
                               int32_t mask_dtype, int32_t* work, int64_t* uids, int64_t* inv, int32_t* seg_off,
                               int32_t* seg_tok, int32_t* seg_of, int32_t* counts, hipStream_t stream) {
   if (T < 0 || V < 1 || V > 0x7fffffff || T > 0x7fffffff) return NR_EINVAL(0);
-  if (!ids || !work || !uids || !inv || !seg_off || !seg_tok || !seg_of || !counts) return NR_EINVAL(1);
+  if ((T > 0 && (!ids || !inv || !seg_tok || !seg_of)) || !work || !uids || !seg_off || !counts) return NR_EINVAL(1);
   if (fill_row < 0 || fill_row >= V) return NR_EINVAL(2);
   if (grad_mask && (mask_dtype < NR_MASK_U8 || mask_dtype > NR_MASK_F32)) return NR_EINVAL(5);
-  int32_t* cnt_all = work;
-  int32_t* cnt_csr = work + V;
-  int32_t* cursor = work + 2 * V;
-  int32_t* pos = work + 3 * V;
-  int32_t* off = work + 4 * V;
-  {   // the three per-id counters and `counts` zeroed by ONE launch (two memsets cost two graph nodes)
-    const int64_t n = 3 * V;
-    int64_t zb = (n / 4 + 255) / 256;
-    zb = zb < 1 ? 1 : (zb > 1024 ? 1024 : zb);
-    hipLaunchKernelGGL(zero_work_kernel, dim3((unsigned)zb), dim3(256), 0, stream, work, n, counts);
+  if (reinterpret_cast<uintptr_t>(work) & 15) return NR_EINVAL(6);
+  const int64_t V4 = (V + 3) & ~int64_t(3);   // every array 16-B aligned
+  int32_t* ctrl = work;
+  int32_t* cnt_all = work + CTRL_WORDS;
+  int32_t* cnt_csr = cnt_all + V4;
+  int32_t* cursor = cnt_csr + V4;
+  int32_t* pos = cursor + V4;
+  int32_t* tot = pos + V4;   // [nb][2] tile totals (large vocabularies)
+  const int64_t nb = (V + scan_tile_n<SCAN_THREADS>() - 1) / scan_tile_n<SCAN_THREADS>();
+  // at least one count workgroup
+  const unsigned gb = (unsigned)(T > 0 ? (T + CNT_THREADS - 1) / CNT_THREADS : 1);
+  hipLaunchKernelGGL(count_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, grad_mask, mask_dtype, ctrl,
+                     cnt_all, cnt_csr);
+  if (V <= SCAN_OWN_MAX) {
+    hipLaunchKernelGGL(scan_down_kernel<true>, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, stream, ctrl, cnt_all,
+                       cnt_csr, V, tot, pos, cursor, uids, seg_off, counts, fill_row);
+  } else {
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, stream, cnt_all, cnt_csr, V, tot);
+    hipLaunchKernelGGL(scan_down_kernel<false>, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, stream, ctrl, cnt_all,
+                       cnt_csr, V, tot, pos, cursor, uids, seg_off, counts, fill_row);
   }
-  const unsigned gb = (unsigned)((T + CNT_THREADS - 1) / CNT_THREADS);
-  if (T > 0)
-    hipLaunchKernelGGL(count_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, grad_mask, mask_dtype, cnt_all,
-                       cnt_csr, counts);
-  const int64_t nb = (V + SCAN_TILE - 1) / SCAN_TILE;
-  int32_t* tot = work + 5 * V;   // [nb][2] tile totals
-  hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, stream, cnt_all, cnt_csr, V, tot);
-  hipLaunchKernelGGL(scan_down_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), sizeof(int32_t) * SCAN_LDS_WORDS, stream,
-                     cnt_all, cnt_csr, V, tot, pos, off, uids, seg_off, counts, fill_row);
-  if (T > 0)
-    hipLaunchKernelGGL(fill_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, grad_mask, mask_dtype, pos, off,
-                       cursor, inv, seg_tok, seg_of);
+  // fill runs even for T = 0: it is the pass that clears the counters and the flag
+  hipLaunchKernelGGL(fill_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, grad_mask, mask_dtype, pos,
+                     cursor, inv, seg_tok, seg_of, ctrl, reinterpret_cast<int4*>(cnt_all), 2 * V4 / 4);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
 
 extern "C" int64_t nr_unique_rows_workspace(int64_t V) {
-  return 5 * V + 2 * ((V + SCAN_TILE - 1) / SCAN_TILE);
+  const int64_t V4 = (V + 3) & ~int64_t(3);
+  return CTRL_WORDS + 4 * V4 + 2 * ((V + scan_tile_n<SCAN_THREADS>() - 1) / scan_tile_n<SCAN_THREADS>());
 }
 
 extern "C" int64_t nr_segment_rows_sum_workspace(int64_t T, int64_t width) {

@@ -96,6 +96,41 @@ struct BigMN {
   float4 v[2][NC][2];     // [register set][chunk][k of the pair]
   int64_t kid[2][NC][2];  // MN_GATHER: stored-row ids of a set's next tile (prefetched one load ahead)
   __device__ __forceinline__ void init(const Op&, int64_t, int64_t, int) {}
+  // column sums of register set S's tile (both k of each pair) into cs (the fused bias gradient)
+  template <int S>
+  __device__ __forceinline__ void add_colsum(float (&cs)[NC][4], int tid) const {
+    if (tid >= ACT) return;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      cs[j][0] += v[S][j][0].x + v[S][j][1].x;
+      cs[j][1] += v[S][j][0].y + v[S][j][1].y;
+      cs[j][2] += v[S][j][0].z + v[S][j][1].z;
+      cs[j][3] += v[S][j][0].w + v[S][j][1].w;
+    }
+  }
+  // the per-thread sums of the KP threads of one column group (adjacent lanes) combined; the
+  // group's first lane stores its four columns' sums (columns past M skipped)
+  __device__ __forceinline__ void put_colsum(float (&cs)[NC][4], int64_t r0, int64_t rlim, float* dst,
+                                             int tid) const {
+    if (tid >= ACT) return;
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = cs[j][e];
+#pragma unroll
+        for (int d = 1; d < KP; d <<= 1) x += __shfl_xor(x, d, 64);
+        cs[j][e] = x;
+      }
+    if (tid % KP) return;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int64_t col = r0 + 4 * cg_of(tid + 512 * j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (col + e < rlim) dst[col + e] = cs[j][e];
+    }
+  }
   __device__ __forceinline__ static int kp_of(int c) { return c % KP; }
   __device__ __forceinline__ static int cg_of(int c) { return c / KP; }
   template <int S>
@@ -265,6 +300,9 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
   f32x16 acc[TI][TJ];
   LA la;
   LB lb;
+#ifdef NR_AB_PRIO_STATIC   // A/B build knob (tools/build_variant.sh): the younger half at priority 1
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
 
   // persistent over this block's units (virtual ids blockIdx.x + j * gridDim.x); each unit runs its
   // own two-deep pipeline, so the k-loop carries no unit bookkeeping (a pipeline refill per unit
@@ -290,6 +328,14 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
     // a wave whose rows or columns all lie past M / N skips its fragment reads and MFMAs (it still
     // loads, splits and stores its share of the operand tiles)
     const bool live = u.m0 + wm < g.M && u.n0 + wn < g.N;
+    // fused bias gradient (slab path, MN-contiguous A): the first column tile's units sum A
+    constexpr bool CS_OK = AM == MN_PLAIN && !TR;
+    const bool do_cs = CS_OK && g.colsum && g.slab && u.n0 == 0 && !tail_unit;
+    float cs[CS_OK ? BigMN<BM, MN_PLAIN, BK>::NC : 1][4];
+    if constexpr (CS_OK) {
+#pragma unroll
+      for (int j = 0; j < BigMN<BM, MN_PLAIN, BK>::NC; ++j) cs[j][0] = cs[j][1] = cs[j][2] = cs[j][3] = 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -322,6 +368,9 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
     __syncthreads();   // the previous unit's last stage reads are done before stage 0 is rewritten
     issue(S0{}, 0);
     if (nt > 1) issue(S1{}, 1);
+    if constexpr (CS_OK) {
+      if (do_cs) la.template add_colsum<0>(cs, tid);
+    }
     la.template store<0, NP>(As, tid);
     lb.template store<0, NP>(Bs, tid);
     if (nt > 2) issue(S0{}, 2);
@@ -350,6 +399,9 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
 #pragma unroll
         for (int p = 0; p < NP; ++p)
           a[p] = *reinterpret_cast<const bf16x8*>(a_s + p * PA + (wm + 32 * i + c) * SR + 16 * kk + 8 * h);
+#ifdef NR_AB_PRIO_CLUSTER
+        __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
 #define NR_MF(X, Y)                                                                                    \
@@ -365,10 +417,18 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
           NR_MF(0, 0);
 #undef NR_MF
         }
+#ifdef NR_AB_PRIO_CLUSTER
+        __builtin_amdgcn_s_setprio(0);
+#endif
         }
         // split-stores of the next stage: A behind step 0's first row block, B (then the loads of
         // k-tile kt+3 into the freed register set) behind step KS/2's second (KS = 1) or first row block
-        if (kk == 0 && i == 0 && stage_next) la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid);
+        if (kk == 0 && i == 0 && stage_next) {
+          if constexpr (CS_OK) {
+            if (do_cs) la.template add_colsum<NS>(cs, tid);
+          }
+          la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid);
+        }
         if (kk == KS / 2 && i == (KS == 1 ? 1 : 0) && stage_next) {
           lb.template store<NS, NP>(Bs + (st ^ 1) * NP * PB, tid);
           if (kt + 3 < nt) issue(nset, kt + 3);
@@ -382,7 +442,16 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
       if (kt + 1 < nt) ktile(S0{}, kt + 1, 1);
     }
     if (!tail_unit) {
-      epilogue_any<TR, TI, TJ>(g, acc, u.m0, u.n0, wm, wn, h, c);
+      if constexpr (CS_OK) {
+        if (do_cs)
+          la.put_colsum(cs, u.m0, g.M,
+                        g.slab + (int64_t)g.splits * g.slab_stride + (u.kbeg / g.kchunk) * (g.slab_stride / g.slab_ld),
+                        tid);
+      }
+      if (!TR && g.slab)
+        epilogue_slab<TI, TJ>(g, acc, u.m0, u.n0, wm, wn, h, c, g.slab + (u.kbeg / g.kchunk) * g.slab_stride);
+      else
+        epilogue_any<TR, TI, TJ>(g, acc, u.m0, u.n0, wm, wn, h, c);
     } else if (TR) {   // pieces of one tile meet in C: atomic adds into the zeroed destination rows
       static_assert(4 * 32 * 36 * 4 <= 2 * NP * PA * 2 || BN != 256, "tail chunks fit the A image");
       if constexpr (BN == 256 && 4 * 32 * 36 * 4 <= 2 * NP * PB * 2) {

@@ -301,10 +301,11 @@ int pick_tile(int64_t n) {  // 64 or 128: least padding, ties -> 128
 
 }  // namespace
 
-extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
-                           const nr_operand* B, float* C, int64_t ldc, const float* bias,
-                           int32_t epilogue, const nr_operand* c_rows, int64_t pad_row,
-                           int32_t split_k, int32_t prec, hipStream_t stream) {
+namespace {
+int gemm_static(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B, float* C, int64_t ldc,
+                const float* bias, int32_t epilogue, const nr_operand* c_rows, int64_t pad_row, int32_t split_k,
+                int32_t prec, float* work, int64_t work_elems, float* colsum, int32_t* colsum_folded,
+                hipStream_t stream) {
   if (M < 0 || N < 0 || K < 0) return NR_EINVAL(0);
   if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(12);
   if (epilogue < NR_EPI_STORE || epilogue > NR_EPI_SCATTER_ZEROED) return NR_EINVAL(3);
@@ -341,7 +342,7 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
     const int64_t small_min = 400;
     const int fb = (prec == NR_GEMM_BF16 || t128 >= small_min) ? 128 : 64;
     const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, fb, fb, nullptr,
-                                nullptr, prec, 0, stream);
+                                nullptr, prec, 0, work, work_elems, colsum, colsum_folded, stream);
     if (rc != -1) return rc;
   }
   // generic kernel: same sums via atomics
@@ -366,6 +367,35 @@ extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
   return launch_kc<64, 64>(g, ak, bk, splits, stream);
 }
 
+int gemm_dyn(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B, float* C, int64_t ldc,
+             const float* bias, int32_t epilogue, const nr_operand* c_rows, int64_t pad_row, int32_t split_k,
+             const int32_t* m_dev, const int32_t* k_dev, int32_t prec, int32_t max_cus, float* work,
+             int64_t work_elems, float* colsum, int32_t* colsum_folded, hipStream_t stream);
+}  // namespace
+
+extern "C" int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A,
+                           const nr_operand* B, float* C, int64_t ldc, const float* bias,
+                           int32_t epilogue, const nr_operand* c_rows, int64_t pad_row,
+                           int32_t split_k, int32_t prec, hipStream_t stream) {
+  return gemm_static(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, prec, nullptr, 0, nullptr,
+                     nullptr, stream);
+}
+
+extern "C" int nr_gemm_f32_ws(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B, float* C,
+                              int64_t ldc, const float* bias, int32_t epilogue, const nr_operand* c_rows,
+                              int64_t pad_row, int32_t split_k, const int32_t* m_dev, const int32_t* k_dev,
+                              int32_t prec, int32_t max_cus, float* work, int64_t work_elems, float* colsum,
+                              int32_t* colsum_folded, hipStream_t stream) {
+  if (work_elems < 0 || (work_elems > 0 && !work)) return NR_EINVAL(16);
+  if (colsum_folded) *colsum_folded = 0;
+  if (colsum && !colsum_folded) return NR_EINVAL(17);
+  if (!m_dev && !k_dev && max_cus == 0)
+    return gemm_static(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, prec, work, work_elems,
+                       colsum, colsum_folded, stream);
+  return gemm_dyn(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, m_dev, k_dev, prec, max_cus, work,
+                  work_elems, colsum, colsum_folded, stream);
+}
+
 // Device-resident extents: M and K are upper bounds (grid sizing); the kernel reads the actual
 // values from m_dev / k_dev (either may be null).  Fast-path operand shapes only (K-contiguous
 // or MN-contiguous rows, 16-B aligned, ld % 4 == 0); the device K must be a multiple of 32.
@@ -381,6 +411,15 @@ extern "C" int nr_gemm_f32_dyn_cus(int64_t M, int64_t N, int64_t K, const nr_ope
                                    float* C, int64_t ldc, const float* bias, int32_t epilogue,
                                    const nr_operand* c_rows, int64_t pad_row, int32_t split_k, const int32_t* m_dev,
                                    const int32_t* k_dev, int32_t prec, int32_t max_cus, hipStream_t stream) {
+  return gemm_dyn(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, m_dev, k_dev, prec, max_cus,
+                  nullptr, 0, nullptr, nullptr, stream);
+}
+
+namespace {
+int gemm_dyn(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B, float* C, int64_t ldc,
+             const float* bias, int32_t epilogue, const nr_operand* c_rows, int64_t pad_row, int32_t split_k,
+             const int32_t* m_dev, const int32_t* k_dev, int32_t prec, int32_t max_cus, float* work,
+             int64_t work_elems, float* colsum, int32_t* colsum_folded, hipStream_t stream) {
   if (max_cus < 0) return NR_EINVAL(15);
   if (M < 0 || N < 0 || K < 0 || (K % 32)) return NR_EINVAL(0);
   if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(14);
@@ -399,6 +438,7 @@ extern "C" int nr_gemm_f32_dyn_cus(int64_t M, int64_t N, int64_t K, const nr_ope
   if (split_k > 1 && epilogue != NR_EPI_ATOMIC && epilogue != NR_EPI_SCATTER) return NR_EINVAL(5);
   if (M == 0 || N == 0 || K == 0) return NR_OK;
   const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, 128, 128, m_dev,
-                              k_dev, prec, max_cus, stream);
+                              k_dev, prec, max_cus, work, work_elems, colsum, colsum_folded, stream);
   return rc == -1 ? NR_EINVAL(7) : rc;
 }
+}  // namespace

@@ -28,9 +28,8 @@ int launch_big_3_256(const Args& g, int am, int bm, int splits, hipStream_t s);
 int launch_big_1_128(const Args& g, int am, int bm, int splits, hipStream_t s);
 int launch_big_3_128(const Args& g, int am, int bm, int splits, hipStream_t s);
 
-// Large-tile (256 x BN) bf16 kernel choice: 0 = stay on the 128x128 kernel.  NR_GEMM_BIG = 0 disables
-// it, 128 / 256 forces BN where eligible (A/B timing); auto: 256 x 256 tiles unless their units fill
-// the 256 CUs clearly worse ("round efficiency" = units / (256 * rounds), times the useful fraction
+// Large-tile (256 x BN) bf16 kernel choice: 0 = stay on the 128x128 kernel; 256 x 256 tiles unless
+// their units fill the 256 CUs clearly worse ("round efficiency" = units / (256 * rounds), times the useful fraction
 // of padded columns) than the 128x128 kernel's at two workgroups per CU.
 // Split-K callers (atomic epilogues) are re-split for the chosen tile, so they always fill the chip.
 double round_eff(int64_t units, int64_t slots) {
@@ -59,14 +58,79 @@ int big_bn(int64_t M, int64_t N, int64_t K, int splits, bool resplit, bool m_dyn
                        (double)((N + 127) / 128 * 128);
   return e256 >= 0.87 * e_old ? 256 : 0;
 }
+// Split-K slabs -> C: C[m][n] += sum over the valid splits of slab[s][m][n], in split order
+// (deterministic).  The valid split count and row count follow the GEMM kernel's own reading of
+// the device-resident K / M (a split whose k range starts past the device K wrote nothing).
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ C, int64_t ldc,
+                                                            const float* __restrict__ slab, int64_t ld,
+                                                            int64_t stride, int splits, int64_t M, int64_t N,
+                                                            int64_t K, int64_t kchunk, const int32_t* mdyn,
+                                                            const int32_t* kdyn, int vec, float* __restrict__ colsum) {
+  int64_t m_eff = M;
+  if (mdyn) {
+    const int64_t m = *mdyn;
+    m_eff = m < M ? (m > 0 ? m : 0) : M;
+  }
+  int ns = splits;
+  if (kdyn) {
+    int64_t k = *kdyn;
+    k = k < K ? (k > 0 ? k : 0) : K;
+    const int64_t kc = (k + splits - 1) / splits;
+    const int64_t kch = kc > 0 ? (kc + 31) / 32 * 32 : 32;
+    ns = (int)((k + kch - 1) / kch);
+  } else {
+    ns = (int)((K + kchunk - 1) / kchunk);
+  }
+  ns = ns < splits ? ns : splits;
+  const int64_t n4 = (N + 3) / 4, total = m_eff * n4;
+  if (colsum) {   // the fused bias gradient: per-split column sums after the partial tiles
+    const float* cs = slab + (int64_t)splits * stride;
+    const int64_t mh = stride / ld;
+    for (int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x; m < m_eff; m += (int64_t)gridDim.x * 256) {
+      float a = colsum[m];
+      for (int sp = 0; sp < ns; ++sp) a += cs[sp * mh + m];
+      colsum[m] = a;
+    }
+  }
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / n4, n = 4 * (i - m * n4);
+    const float* s = slab + m * ld + n;
+    float* c = C + m * ldc + n;
+    if (vec && n + 3 < N) {
+      float4 a = *reinterpret_cast<const float4*>(c);
+#pragma unroll 4
+      for (int sp = 0; sp < ns; ++sp) {
+        const float4 x = *reinterpret_cast<const float4*>(s + sp * stride);
+        a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+      }
+      *reinterpret_cast<float4*>(c) = a;
+    } else {
+      for (int e = 0; e < 4 && n + e < N; ++e) {
+        float a = c[e];
+        for (int sp = 0; sp < ns; ++sp) a += s[sp * stride + e];
+        c[e] = a;
+      }
+    }
+  }
+}
+
 }  // namespace nrfast
+
+// Elements of nr_gemm_f32_ws' split-K workspace that serve any shape: one round of 256 x 256
+// partial tiles over the device's CUs (the big kernel re-splits a split-K contraction to one unit
+// per CU), plus row padding and the per-split column sums.
+extern "C" int64_t nr_gemm_splitk_workspace(void) {
+  const int cus = nrfast::device_cus();
+  return (int64_t)(cus > 0 ? cus : 256) * 256 * 261;
+}
 
 
 // Returns -1 if the shape/operands are not eligible (the caller falls back), else a status.
 int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_operand* B, float* C,
                  int64_t ldc, const float* bias, int32_t epilogue, const nr_operand* c_rows, int64_t pad_row,
                  int32_t split_k, int bm, int bn, const int32_t* m_dev, const int32_t* k_dev, int32_t prec,
-                 int32_t max_cus, hipStream_t stream) {
+                 int32_t max_cus, float* work, int64_t work_elems, float* colsum, int32_t* colsum_folded,
+                 hipStream_t stream) {
   using namespace nrfast;
   if (K <= 0) return -1;
   // NR_EPI_SCATTER_ZEROED = NR_EPI_SCATTER_STORE whose destination rows are zero on entry: the big
@@ -144,9 +208,30 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
         gb.kchunk = ((K + want - 1) / want + 31) / 32 * 32;
         sp = (int)((K + gb.kchunk - 1) / gb.kchunk);
       }
+      // split-K partial tiles through a workspace (plain stores + one reduction launch) when the caller
+      // gave one: a round of 256 fp32 atomic tiles costs ~50 us at the chip's ~1.3 TB/s atomic rate
+      const int64_t sld = (N + 3) & ~int64_t(3);
+      const bool slab = epilogue == NR_EPI_ATOMIC && sp > 1 && work &&
+                        work_elems >= (int64_t)sp * M * sld + (colsum ? (int64_t)sp * M : 0) &&
+                        (reinterpret_cast<uintptr_t>(work) & 15) == 0;
+      const bool fold = slab && colsum && am == MN_PLAIN;
+      if (slab) {
+        gb.slab = work;
+        gb.slab_ld = sld;
+        gb.slab_stride = M * sld;
+        gb.colsum = fold ? colsum : nullptr;
+      }
       const int np = prec == NR_GEMM_BF16 ? 1 : 3;
       const int rc = BN == 256 ? (np == 1 ? launch_big_1_256(gb, am, bmode, sp, stream) : launch_big_3_256(gb, am, bmode, sp, stream))
                                : (np == 1 ? launch_big_1_128(gb, am, bmode, sp, stream) : launch_big_3_128(gb, am, bmode, sp, stream));
+      if (rc == NR_OK && slab) {
+        int64_t blocks = (M * ((N + 3) / 4) + 255) / 256;
+        blocks = blocks > 2048 ? 2048 : (blocks < 1 ? 1 : blocks);
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, C, ldc, work, sld,
+                           gb.slab_stride, sp, M, N, K, gb.kchunk, m_dev, k_dev, g.vec, gb.colsum);
+        NR_LAUNCH_CHECK();
+        if (fold && colsum_folded) *colsum_folded = 1;
+      }
       if (rc != -1) return rc;
     }
   }

@@ -30,11 +30,20 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
 __device__ __forceinline__ float pk_lo(uint32_t p) { return __uint_as_float(p << 16); }
 __device__ __forceinline__ float pk_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
 // a, b -> the packed (h, m, l) terms of both: 3 conversions, 4 bit ops, 4 subtractions per pair
+#ifdef NR_AB_ASM_SUB   // A/B build knob: the subtractions as scalar v_sub_f32 (no SLP packing)
+__device__ __forceinline__ float nr_sub(float a, float b) {
+  float r;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+#else
+__device__ __forceinline__ float nr_sub(float a, float b) { return a - b; }
+#endif
 __device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
   h = pk_bf16(a, b);
-  const float ra = a - pk_lo(h), rb = b - pk_hi(h);   // exact
+  const float ra = nr_sub(a, pk_lo(h)), rb = nr_sub(b, pk_hi(h));   // exact
   m = pk_bf16(ra, rb);
-  l = pk_bf16(ra - pk_lo(m), rb - pk_hi(m));
+  l = pk_bf16(nr_sub(ra, pk_lo(m)), nr_sub(rb, pk_hi(m)));
 }
 __device__ __forceinline__ void split4(float a, float b, float c, float d, uint2& p0, uint2& p1, uint2& p2) {
   split2(a, b, p0.x, p1.x, p2.x);
@@ -75,6 +84,14 @@ struct Args {
   const int32_t* kdyn;   // device-resident K (<= K), or null
   int tail;  // big kernel, NR_EPI_SCATTER_ZEROED: max K pieces of the last partial round's tiles (0 = off)
   int max_cus;   // persistent grid limited to this many CUs (0 = all): leaves CUs to a concurrent collective
+  // big kernel, split-K NR_EPI_ATOMIC: each split stores its partial tile to slab + split * slab_stride
+  // ([M][slab_ld], plain stores) and splitk_reduce adds the splits into C -- instead of fp32 atomics
+  float* slab = nullptr;
+  int64_t slab_ld = 0, slab_stride = 0;
+  // slab path with an MN-contiguous A (a weight gradient dYᵀ X): the units of the first column tile
+  // also sum A over their k range (the bias gradient, from the tiles they load anyway) into
+  // slab[splits * slab_stride + split * (slab_stride / slab_ld) + m]; splitk_reduce adds them to colsum
+  float* colsum = nullptr;
 };
 
 // CUs of the current device (cached)
@@ -501,6 +518,25 @@ __device__ __forceinline__ void epilogue_cmajor(const Args& g, f32x16 (&acc)[TI]
           if (tok == g.pad_row) continue;
           atomicAdd(&g.C[tok * g.ldc + scol], v);
         }
+      }
+    }
+}
+
+// Split-K partial tile -> its slab with plain stores, in the C-major accumulator layout (each store
+// instruction writes 32 consecutive columns of two rows).
+template <int TI, int TJ>
+__device__ __forceinline__ void epilogue_slab(const Args& g, f32x16 (&acc)[TI][TJ], int64_t m0, int64_t n0, int wm,
+                                              int wn, int h, int c, float* dst) {
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int64_t col = n0 + wn + 32 * j + c;
+      if (col >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < g.M) dst[row * g.slab_ld + col] = acc[i][j][r];
       }
     }
 }

@@ -70,7 +70,7 @@ struct TrainArgs {
   const int32_t* uindex;
   const int32_t* tok; const int32_t* attn; int64_t n_news; int L;
   int npratio, his_size, flags;
-  uint64_t seed, offset; const uint64_t* rng;
+  uint64_t seed, offset; uint64_t* rng;
   int64_t *cdd_id, *his_id, *cdd_tok, *cdd_attn, *his_tok, *his_attn;
   double *cdd_mask, *his_mask;
   int64_t *user_id, *label;
@@ -92,7 +92,12 @@ __global__ __launch_bounds__(256) void form_train_kernel(TrainArgs a) {
   const uint64_t ctr0 = off + (uint64_t)b * (uint64_t)(4 * C);
 
   if (threadIdx.x == 0) {
-    int64_t idx = a.sample_idx[b];
+    int64_t sb = b;
+    if (a.flags & NR_BATCH_CURSOR) {   // this launch's batch of the epoch order
+      const uint64_t nb = a.rng[4] / (uint64_t)gridDim.x;
+      sb += (int64_t)((nb > 0 ? a.rng[3] % nb : 0) * (uint64_t)gridDim.x);
+    }
+    int64_t idx = a.sample_idx[sb];
     if (idx < 0 || idx >= a.P) { atomicOr(a.status, 1); idx = 0; }
     const int64_t imp = a.imprs[2 * idx];
     s_imp = imp;
@@ -153,6 +158,20 @@ __global__ __launch_bounds__(256) void form_train_kernel(TrainArgs a) {
               a.cdd_attn ? a.cdd_attn + b * C * a.L : nullptr, a.status);
   gather_rows(s_ids + C, NH, a.tok, a.attn, a.n_news, a.L, a.his_tok + b * NH * a.L,
               a.his_attn ? a.his_attn + b * NH * a.L : nullptr, a.status);
+  if (a.rng) {
+    // every workgroup has read (rng[0], rng[1]) above; the last one to get here advances the
+    // offset for the next launch and resets the ticket (only thread 0 read the pair for its draws,
+    // and its loads completed before it used them)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned long long t = atomicAdd(reinterpret_cast<unsigned long long*>(a.rng + 2), 1ull);
+      if (t == (unsigned long long)gridDim.x - 1) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.rng + 1), (unsigned long long)(4 * C) * gridDim.x);
+        if (a.flags & NR_BATCH_CURSOR) atomicAdd(reinterpret_cast<unsigned long long*>(a.rng + 3), 1ull);
+        __hip_atomic_store(a.rng + 2, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 struct EvalArgs {
@@ -330,7 +349,7 @@ extern "C" int nr_form_train_batch(const int64_t* sample_idx, int64_t B, const i
                                    const int32_t* neg_ids, const int32_t* uindex, const int32_t* tok,
                                    const int32_t* attn, int64_t n_news, int32_t L, int32_t npratio,
                                    int32_t his_size, int32_t flags, uint64_t seed, uint64_t offset,
-                                   const uint64_t* rng, int64_t* cdd_id, int64_t* his_id, int64_t* cdd_tok,
+                                   uint64_t* rng, int64_t* cdd_id, int64_t* his_id, int64_t* cdd_tok,
                                    int64_t* cdd_attn, int64_t* his_tok, int64_t* his_attn, double* cdd_mask,
                                    double* his_mask, int64_t* user_id, int64_t* label, int32_t* status,
                                    hipStream_t stream) {
@@ -339,6 +358,7 @@ extern "C" int nr_form_train_batch(const int64_t* sample_idx, int64_t B, const i
   if (!cdd_id || !his_id || !cdd_tok || !his_tok || !cdd_mask || !his_mask || !user_id || !label)
     return NR_EINVAL(2);
   if (npratio > 0 && !neg_ids) return NR_EINVAL(3);
+  if ((flags & NR_BATCH_CURSOR) && !rng) return NR_EINVAL(5);
   if (B == 0) return NR_OK;
   TrainArgs a{sample_idx, B, imprs, P, his_off, his_ids, neg_off, neg_ids, uindex, tok, attn, n_news, L,
               npratio, his_size, flags, seed, offset, rng, cdd_id, his_id, cdd_tok, cdd_attn, his_tok,

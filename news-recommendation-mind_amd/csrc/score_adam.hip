@@ -84,46 +84,61 @@ __global__ __launch_bounds__(256) void score_bwd_kernel(const float* cdd, int64_
   }
 }
 
-// The training head in ONE workgroup for the whole batch (B <= 64 impressions of C candidates):
-// log-softmax logits (as score_fwd_kernel) AND the mean NLL over the batch (Manager.py:382,641,
-// nn.NLLLoss(reduction='mean')): the loss needs no cross-block reduction, zero fill or extra launch.
-// One wave per impression row (strided).
+// Training head + NLLLoss (Manager.py:641, reduction 'mean') in one launch: workgroup b forms the C
+// scores of impression b (one wave per candidate dot product), their log-softmax and its loss term
+// part[b]; the workgroup that arrives last (agent-scope release + ticket, acquire:
+// cdna_hip_programming.md §6 Guideline 16's counter form) sums the B terms in a fixed order
+// (deterministic) and resets the ticket, so `work` is zero again on return.
 __global__ __launch_bounds__(1024) void score_nll_fwd_kernel(const float* cdd, int64_t ldc, const float* user,
                                                              int64_t ldu, const int64_t* label, int B, int C, int H,
-                                                             float scale, float* logits, float* loss) {
-  extern __shared__ float sh[];   // [B * C] scores, then [B] per-row loss terms
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
-  float* sc = sh;
-  float* rl = sh + B * C;
-  for (int r = w; r < B * C; r += nw) {   // one wave per (impression, candidate) dot product
-    const int b = r / C;
-    const float* x = cdd + (int64_t)r * ldc;
-    const float* u = user + (int64_t)b * ldu;
+                                                             float scale, float* logits, float* loss,
+                                                             int32_t* work) {
+  extern __shared__ float sc[];   // [C] scores
+  __shared__ int last;
+  const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
+  float* part = reinterpret_cast<float*>(work + 4);
+  const float* u = user + (int64_t)b * ldu;
+  for (int c = w; c < C; c += nw) {
+    const float* x = cdd + ((int64_t)b * C + c) * ldc;
     float s = 0.f;
     for (int d = lane; d < H; d += 64) s = fmaf(x[d], u[d], s);
     s = nr_wave_sum(s);
-    if (lane == 0) sc[r] = s * scale;
+    if (lane == 0) sc[c] = s * scale;
   }
   __syncthreads();
-  for (int b = w; b < B; b += nw) {
+  if (w == 0) {
     float mx = -INFINITY;
-    for (int c = lane; c < C; c += 64) mx = fmaxf(mx, sc[b * C + c]);
+    for (int c = lane; c < C; c += 64) mx = fmaxf(mx, sc[c]);
     mx = nr_wave_max(mx);
     float sum = 0.f;
-    for (int c = lane; c < C; c += 64) sum += __expf(sc[b * C + c] - mx);
+    for (int c = lane; c < C; c += 64) sum += __expf(sc[c] - mx);
     const float lse = mx + __logf(nr_wave_sum(sum));
-    for (int c = lane; c < C; c += 64) logits[(int64_t)b * C + c] = sc[b * C + c] - lse;
+    for (int c = lane; c < C; c += 64) logits[(int64_t)b * C + c] = sc[c] - lse;
     if (lane == 0) {
       const int64_t y = label[b];
-      rl[b] = (y >= 0 && y < C) ? -(sc[b * C + y] - lse) : 0.f;   // out-of-range labels: no term
+      part[b] = (y >= 0 && y < C) ? -(sc[y] - lse) : 0.f;   // out-of-range labels: no term
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int ticket = atomicAdd(&work[0], 1);
+    last = ticket == B - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
   __syncthreads();
-  if (w == 0) {   // fixed-order sum of the rows (deterministic)
-    float s = 0.f;
-    for (int b = lane; b < B; b += 64) s += rl[b];
-    s = nr_wave_sum(s);
-    if (lane == 0) loss[0] = s / (float)B;
+  if (!last || w != 0) return;
+  float s = 0.f;   // fixed-order sum of the B terms
+  for (int r = lane; r < B; r += 64) s += part[r];
+  s = nr_wave_sum(s);
+  if (lane == 0) {
+    loss[0] = s / (float)B;
+    __hip_atomic_store(&work[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -227,7 +242,7 @@ constexpr int kAdamChunk = 4096;   // elements per block (256 threads x 4 float4
 struct AdamEntry {
   float* p; const float* g; float* m; float* v;
   int64_t n;
-  const int64_t* step_dev;   // device step count (graph replays) or null
+  int64_t* step_dev;         // device step count (graph replays) or null
   const float* lr_dev;       // device learning rate (a scheduler updates it between replays) or null
   float step_size;           // lr / (1 - beta1^t) when neither is on the device
   float bc2_sqrt;            // sqrt(1 - beta2^t) when step_dev is null
@@ -239,6 +254,7 @@ struct AdamMulti {
   AdamEntry e[kAdamMulti];
   int32_t blk_off[kAdamMulti + 1];
   int count;
+  int32_t* ticket;   // non-null: the launch advances the device step counts itself (nr_adam_multi_step)
   float b1, b2, eps, wd, gscale;
 };
 
@@ -259,7 +275,8 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
   const AdamEntry& e = a.e[t];
   float step = e.step_size, bc2_sqrt = e.bc2_sqrt;
   if (e.step_dev || e.lr_dev) {
-    const double st = e.step_dev ? (double)*e.step_dev : (double)e.step;
+    // with a ticket the device count is the one before this step: this step is count + 1
+    const double st = e.step_dev ? (double)*e.step_dev + (a.ticket ? 1.0 : 0.0) : (double)e.step;
     const double lr = e.lr_dev ? (double)*e.lr_dev : (double)e.lr;
     step = (float)(lr / (1.0 - pow((double)a.b1, st)));
     bc2_sqrt = (float)sqrt(1.0 - pow((double)a.b2, st));
@@ -301,6 +318,16 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
       e.v[i] = vv;
     }
   }
+  if (a.ticket) {
+    // every thread read its tensor's count at the top; the workgroup that finishes last advances
+    // the counts of this launch's tensors for the next step and resets the ticket
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(a.ticket, 1) == (int)gridDim.x - 1) {
+      for (int t2 = 0; t2 < a.count; ++t2)
+        if (a.e[t2].step_dev) atomicAdd(reinterpret_cast<unsigned long long*>(a.e[t2].step_dev), 1ull);
+      __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // one wave per output row, float4 along E
@@ -331,9 +358,16 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const float* dout, i
 // the same H addresses serialise on the L2 (the old one-pass form ran at ~1 TB/s on [52800, 150]).
 constexpr int kColsumBlocks = 1024;
 
+// tick (nr_colsum_ws): per 64-column chunk arrival counters, zero on entry; the chunk's last
+// workgroup to arrive sums the chunk's partial rows in row-block order and resets its counter, so the
+// final pass needs no launch of its own (cdna_hip_programming.md §6 Guideline 16's counter form:
+// plain partial stores, every storing wave's vmcnt drain, barrier, lane-0 agent release + ticket;
+// the last arriver's acquire, then plain loads)
 __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows,
-                                                          int64_t cols, int64_t rb_rows, float* __restrict__ part) {
+                                                          int64_t cols, int64_t rb_rows, float* __restrict__ part,
+                                                          int32_t* __restrict__ tick, float* __restrict__ out) {
   __shared__ float red[4][64];
+  __shared__ int last;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t c = (int64_t)blockIdx.x * 64 + lane;
   const int64_t r0 = (int64_t)blockIdx.y * rb_rows;
@@ -351,6 +385,28 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restric
   red[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   __syncthreads();
   if (w == 0 && c < cols) part[(int64_t)blockIdx.y * cols + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (!tick) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = atomicAdd(&tick[blockIdx.x], 1) == (int)gridDim.y - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  const int64_t nrb = gridDim.y;   // the chunk's partial rows, wave w taking rows w, w + 4, ...
+  float s = 0.f;
+  if (c < cols)
+    for (int64_t b = w; b < nrb; b += 4) s += part[b * cols + c];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < cols) out[c] += (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (threadIdx.x == 0) __hip_atomic_store(&tick[blockIdx.x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // 16 row groups x 64 columns per workgroup: each thread sums nrb / 16 partials (4 in flight), the
@@ -419,14 +475,17 @@ extern "C" int nr_score_bwd(const float* cdd, int64_t ldc, const float* user, in
 
 extern "C" int nr_score_nll_fwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
                                 const int64_t* label, int64_t B, int32_t C, int32_t H, float* logits, float* loss,
-                                hipStream_t stream) {
-  if (B < 1 || B > 4096 || C < 1 || H < 1 || B * C > 16384) return NR_EINVAL(0);
-  if (!cdd || !user || !label || !logits || !loss) return NR_EINVAL(1);
-  hipLaunchKernelGGL(score_nll_fwd_kernel, dim3(1), dim3(1024), (size_t)(B * C + B) * sizeof(float), stream, cdd,
-                     ldc, user, ldu, label, (int)B, C, H, 1.0f / sqrtf((float)H), logits, loss);
+                                int32_t* work, hipStream_t stream) {
+  if (B < 1 || B > 0x7fffffff || C < 1 || C > 16 * 1024 || H < 1) return NR_EINVAL(0);
+  if (!cdd || !user || !label || !logits || !loss || !work) return NR_EINVAL(1);
+  const int waves = C < 16 ? C : 16;
+  hipLaunchKernelGGL(score_nll_fwd_kernel, dim3((unsigned)B), dim3(64 * waves), (size_t)C * sizeof(float), stream,
+                     cdd, ldc, user, ldu, label, (int)B, C, H, 1.0f / sqrtf((float)H), logits, loss, work);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
+
+extern "C" int64_t nr_score_nll_workspace(int64_t B) { return 4 + (B < 0 ? 0 : B); }
 
 extern "C" int nr_score_nll_bwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
                                 const float* logits, const int64_t* label, const float* dloss,
@@ -501,9 +560,22 @@ extern "C" int nr_colsum(const float* x, int64_t ldx, int64_t rows, int64_t cols
   int64_t nrb, rb_rows;
   colsum_grid(rows, cols, &nrb, &rb_rows);
   hipLaunchKernelGGL(colsum_part_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)nrb), dim3(256), 0, stream, x,
-                     ldx, rows, cols, rb_rows, work);
+                     ldx, rows, cols, rb_rows, work, nullptr, nullptr);
   hipLaunchKernelGGL(colsum_final_kernel, dim3((unsigned)((cols + 63) / 64)), dim3(1024), 0, stream, work, nrb, cols,
                      out);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_colsum_ws(const float* x, int64_t ldx, int64_t rows, int64_t cols, float* out, float* work,
+                            int32_t* tick, hipStream_t stream) {
+  if (rows < 0 || cols < 0 || ldx < cols) return NR_EINVAL(0);
+  if (!x || !out || (rows > 0 && cols > 0 && (!work || !tick))) return NR_EINVAL(1);
+  if (rows == 0 || cols == 0) return NR_OK;
+  int64_t nrb, rb_rows;
+  colsum_grid(rows, cols, &nrb, &rb_rows);
+  hipLaunchKernelGGL(colsum_part_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)nrb), dim3(256), 0, stream, x,
+                     ldx, rows, cols, rb_rows, work, tick, out);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
@@ -518,8 +590,9 @@ int adam_multi_launch(AdamMulti& a, int64_t blocks, hipStream_t stream) {
 }
 }  // namespace
 
-extern "C" int nr_adam_multi(const nr_adam_tensor* tensors, int32_t count, float beta1, float beta2, float eps,
-                             float weight_decay, float grad_scale, hipStream_t stream) {
+namespace {
+int adam_multi_impl(const nr_adam_tensor* tensors, int32_t count, float beta1, float beta2, float eps,
+                    float weight_decay, float grad_scale, int32_t* ticket, hipStream_t stream) {
   if (count < 0 || (count > 0 && !tensors)) return NR_EINVAL(0);
   for (int32_t t = 0; t < count; ++t) {   // validate everything before the first launch
     const nr_adam_tensor& d = tensors[t];
@@ -530,6 +603,7 @@ extern "C" int nr_adam_multi(const nr_adam_tensor* tensors, int32_t count, float
   AdamMulti a;
   a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.wd = weight_decay; a.gscale = grad_scale;
   a.count = 0;
+  a.ticket = ticket;
   int64_t blocks = 0;
   for (int32_t t = 0; t < count; ++t) {
     const nr_adam_tensor& d = tensors[t];
@@ -543,7 +617,7 @@ extern "C" int nr_adam_multi(const nr_adam_tensor* tensors, int32_t count, float
     }
     AdamEntry& e = a.e[a.count];
     e.p = d.param; e.g = d.grad; e.m = d.exp_avg; e.v = d.exp_avg_sq; e.n = d.n;
-    e.step_dev = d.step_dev; e.lr_dev = d.lr_dev; e.lr = d.lr;
+    e.step_dev = const_cast<int64_t*>(d.step_dev); e.lr_dev = d.lr_dev; e.lr = d.lr;
     const double st = (double)(d.step < 1 ? 1 : d.step);   // bias corrections in double, as torch's Python floats
     e.step = (int64_t)st;
     e.step_size = (float)((double)d.lr / (1.0 - pow((double)beta1, st)));
@@ -553,4 +627,16 @@ extern "C" int nr_adam_multi(const nr_adam_tensor* tensors, int32_t count, float
     ++a.count;
   }
   return adam_multi_launch(a, blocks, stream);
+}
+}  // namespace
+
+extern "C" int nr_adam_multi(const nr_adam_tensor* tensors, int32_t count, float beta1, float beta2, float eps,
+                             float weight_decay, float grad_scale, hipStream_t stream) {
+  return adam_multi_impl(tensors, count, beta1, beta2, eps, weight_decay, grad_scale, nullptr, stream);
+}
+
+extern "C" int nr_adam_multi_step(const nr_adam_tensor* tensors, int32_t count, float beta1, float beta2, float eps,
+                                  float weight_decay, float grad_scale, int32_t* ticket, hipStream_t stream) {
+  if (!ticket) return NR_EINVAL(4);
+  return adam_multi_impl(tensors, count, beta1, beta2, eps, weight_decay, grad_scale, ticket, stream);
 }

@@ -53,7 +53,12 @@ _SIGS = {
     "nr_gemm_f32_dyn_cus": [c_i64, c_i64, c_i64, ctypes.POINTER(nr_operand), ctypes.POINTER(nr_operand),
                             c_ptr, c_i64, c_ptr, c_i32, ctypes.POINTER(nr_operand), c_i64, c_i32, c_ptr, c_ptr, c_i32,
                             c_i32, c_ptr],
-    "nr_score_nll_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_i32, c_ptr, c_ptr, c_ptr],
+    "nr_gemm_f32_ws": [c_i64, c_i64, c_i64, ctypes.POINTER(nr_operand), ctypes.POINTER(nr_operand),
+                       c_ptr, c_i64, c_ptr, c_i32, ctypes.POINTER(nr_operand), c_i64, c_i32, c_ptr, c_ptr, c_i32,
+                       c_i32, c_ptr, c_i64, c_ptr, ctypes.POINTER(c_i32), c_ptr],
+    "nr_gemm_splitk_workspace": [],
+    "nr_score_nll_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
+    "nr_score_nll_workspace": [c_i64],
     "nr_score_nll_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_i32, c_i32, c_ptr, c_i64,
                          c_ptr, c_i64, c_ptr],
     "nr_unique_rows": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
@@ -91,6 +96,7 @@ _SIGS = {
     "nr_embedding_fwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr],
     "nr_embedding_bwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_ptr],
     "nr_colsum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr],
+    "nr_colsum_ws": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr],
     "nr_colsum_workspace": [c_i64, c_i64],
     "nr_mha_pool_fwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_f32,
                         c_u64, c_u64, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i32,
@@ -123,15 +129,18 @@ _SIGS = {
                          c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr],
     "nr_tanh_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr],
     "nr_adam_multi": [ctypes.POINTER(nr_adam_tensor), c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_ptr],
+    "nr_adam_multi_step": [ctypes.POINTER(nr_adam_tensor), c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_ptr,
+                           c_ptr],
     "nr_build_hash": [],
 }
 
 _RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_unique_rows_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64,
-             "nr_colsum_workspace": c_i64,
+             "nr_colsum_workspace": c_i64, "nr_score_nll_workspace": c_i64,
+             "nr_gemm_splitk_workspace": c_i64,
              "nr_build_hash": ctypes.c_char_p}
 
 # enum nr_batch_flags / nr_metric_flags
-BATCH_REVERSE_HISTORY, BATCH_SHUFFLE_POS = 1, 2
+BATCH_REVERSE_HISTORY, BATCH_SHUFFLE_POS, BATCH_CURSOR = 1, 2, 4
 METRIC_ONE_CLASS, METRIC_NONBINARY = 1, 2
 
 _lib = None

@@ -84,9 +84,11 @@ def _proj_wgrad(dY, X_op, dW, db, M_rows):
     the layer input with MN-contiguous layout (rows = token index)."""
     n_out = dW.shape[0]
     k_in = dW.shape[1]
-    K.gemm(n_out, k_in, M_rows, K.operand(dY, L.MNCONTIG), X_op, dW, epilogue=L.EPI_ATOMIC,
-           split_k=_split_k(n_out, k_in, M_rows))
-    if db is not None:
+    # db folds into the GEMM on its split-K workspace path (the first column tile's units sum the dY
+    # tiles they load); other routings leave it to the two-pass column sum
+    folded = K.gemm(n_out, k_in, M_rows, K.operand(dY, L.MNCONTIG), X_op, dW, epilogue=L.EPI_ATOMIC,
+                    split_k=_split_k(n_out, k_in, M_rows), colsum=db)
+    if db is not None and not folded:
         K.colsum(dY, M_rows, n_out, db)
 
 

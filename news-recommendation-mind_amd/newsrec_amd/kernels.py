@@ -4,6 +4,7 @@ Each wrapper validates shapes/dtypes on the host BEFORE launching (a wrong shape
 device is a memory fault, not an exception), then calls the kernel on the current stream.
 """
 import contextlib
+import ctypes
 import os
 import threading
 
@@ -68,14 +69,38 @@ def _prec(prec):
 
 
 def gemm(M, N, K, A, B, C, ldc=None, bias=None, epilogue=L.EPI_STORE, c_rows=None,
-         pad_row=-1, split_k=1, prec=None):
+         pad_row=-1, split_k=1, prec=None, colsum=None):
     """C (op)= A(m,k) B(k,n); A, B, c_rows are nr_operand structs built by ``operand``; ``prec``:
-    the GEMM arithmetic (None: the thread default, ``get_gemm_precision``)."""
-    _f32(C, bias)
+    the GEMM arithmetic (None: the thread default, ``get_gemm_precision``).  ``colsum`` (split-K
+    weight gradients with an MN-contiguous A): colsum[m] += Σ_k A[k][m] folded into the GEMM where
+    the library can (nr_gemm_f32_ws); returns True then, False when the caller must reduce it."""
+    _f32(C, bias, colsum)
     if bias is not None and bias.numel() < N:
         raise L.HipError("gemm: bias has %d < N=%d entries" % (bias.numel(), N))
+    if colsum is not None and (colsum.numel() < M or not colsum.is_contiguous()):
+        raise L.HipError("gemm: colsum must be a contiguous [M] float tensor")
+    if epilogue == L.EPI_ATOMIC and split_k > 1 and colsum is not None:
+        # the workspace path only where it carries the bias gradient: alone (plain partial stores +
+        # one reduction) it measured slower than the atomic epilogue on the NRMS weight gradient
+        # (292-301 vs 277 µs) and equal on the BERT ones; with the column sums folded in it saves
+        # the two colsum launches (BERT FFN: 401 µs vs 409 + colsum)
+        work = _splitk_work(C)
+        folded = ctypes.c_int32(0)
+        L.call("nr_gemm_f32_ws", M, N, K, A, B, L.ptr(C), ldc if ldc is not None else C.stride(0),
+               L.ptr(bias), epilogue, c_rows, pad_row, split_k, None, None, _prec(prec), 0, L.ptr(work),
+               work.numel(), L.ptr(colsum), ctypes.byref(folded) if colsum is not None else None,
+               L.stream_ptr(C))
+        return bool(folded.value)
     L.call("nr_gemm_f32", M, N, K, A, B, L.ptr(C), ldc if ldc is not None else C.stride(0),
            L.ptr(bias), epilogue, c_rows, pad_row, split_k, _prec(prec), L.stream_ptr(C))
+    return False
+
+
+def _splitk_work(like):
+    """Workspace of a split-K weight-gradient GEMM with its bias gradient folded in (nr_gemm_f32_ws:
+    partial tiles and column sums through plain stores and one reduction); from the caching
+    allocator, so it is reused from call to call (and from the graph pool inside a capture)."""
+    return torch.empty(int(L.load().nr_gemm_splitk_workspace()), device=like.device, dtype=torch.float32)
 
 
 def gemm_dyn(M, N, K, A, B, C, m_dev=None, k_dev=None, ldc=None, bias=None, epilogue=L.EPI_STORE,
@@ -105,6 +130,29 @@ def _ceil32(n):
     return (n + 31) // 32 * 32
 
 
+_SELF_CLEANING = {}
+_RETIRED = []   # outgrown buffers stay allocated: a captured graph may still address them
+
+
+def self_cleaning_workspace(dev, name, n):
+    """A persistent zeroed int32 device buffer of at least ``n`` words per (device, name) for the
+    kernels whose counters start at zero and that leave them zero again (nr_unique_rows,
+    nr_score_nll_fwd): no zero-fill launch per call.
+
+    Created (or grown) by an eager call, never inside a graph capture: a buffer first zero-filled
+    during a capture would only be zero once that graph had replayed.  Steps run one at a time on
+    a device, so one buffer per (device, name) serves every stream."""
+    key = (torch.device(dev), name)
+    ws = _SELF_CLEANING.get(key)
+    if ws is None or ws.numel() < n:
+        if torch.cuda.is_current_stream_capturing():
+            raise L.HipError(f"{name} workspace must be created by an eager call before graph capture")
+        if ws is not None:
+            _RETIRED.append(ws)
+        ws = _SELF_CLEANING[key] = torch.zeros(max(int(n), 4), device=dev, dtype=torch.int32)
+    return ws
+
+
 class UniqueRows:
     """Distinct ids of a token batch (``nr_unique_rows``), sizes left on the device.
 
@@ -120,7 +168,7 @@ class UniqueRows:
         self.T, self.vocab = T, vocab
         self.cap = max(32, _ceil32(min(T, vocab)))
         i32 = dict(device=dev, dtype=torch.int32)
-        work = torch.empty(int(L.load().nr_unique_rows_workspace(vocab)), **i32)
+        work = self_cleaning_workspace(dev, f"nr_unique_rows/{vocab}", L.load().nr_unique_rows_workspace(vocab))
         self.uids = torch.empty(self.cap, device=dev, dtype=torch.int64)
         self.inv = torch.empty(T, device=dev, dtype=torch.int64)
         self.seg_off = torch.empty(self.cap + 1, **i32)
@@ -449,8 +497,9 @@ def score_nll_fwd(cdd, user, label, B, C, H, logits, loss):
     _check_rows(label, None, "label")
     if label.numel() != B or not logits.is_contiguous() or logits.numel() < B * C:
         raise L.HipError("score_nll_fwd: label [B] int64, logits contiguous [B, C]")
+    work = self_cleaning_workspace(user.device, "nr_score_nll_fwd", L.load().nr_score_nll_workspace(B))
     L.call("nr_score_nll_fwd", L.ptr(cdd), cdd.stride(0), L.ptr(user), user.stride(0), L.ptr(label), B, C, H,
-           L.ptr(logits), L.ptr(loss), L.stream_ptr(user))
+           L.ptr(logits), L.ptr(loss), L.ptr(work), L.stream_ptr(user))
 
 
 def score_nll_bwd(cdd, user, logits, label, dloss, dlogits, B, C, H, dcdd, duser):
@@ -482,10 +531,11 @@ def adam(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, 
            weight_decay, step, L.ptr(step_dev), grad_scale, L.stream_ptr(param))
 
 
-def adam_multi(entries, beta1, beta2, eps, weight_decay, grad_scale=1.0):
+def adam_multi(entries, beta1, beta2, eps, weight_decay, grad_scale=1.0, advance_steps=False):
     """entries: [(param, grad, exp_avg, exp_avg_sq, lr, step)] with ``step`` an int or an int64 CUDA
     scalar and ``lr`` a float or a float32 CUDA scalar (read on the device); one nr_adam_multi call
-    (a launch per <= 40 tensors)."""
+    (a launch per <= 40 tensors).  ``advance_steps``: the device step counts hold the count BEFORE
+    this step and the launch itself adds 1 to each (nr_adam_multi_step)."""
     if not entries:
         return
     arr = (L.nr_adam_tensor * len(entries))()
@@ -506,6 +556,11 @@ def adam_multi(entries, beta1, beta2, eps, weight_decay, grad_scale=1.0):
             ld, lr = lr.data_ptr(), 0.0
         arr[i] = L.nr_adam_tensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, float(lr), int(step), sd,
                                   ld)
+    if advance_steps:
+        ticket = self_cleaning_workspace(entries[0][0].device, "nr_adam_multi_step", 4)
+        L.call("nr_adam_multi_step", arr, len(entries), beta1, beta2, eps, weight_decay, grad_scale,
+               L.ptr(ticket), L.stream_ptr(entries[0][0]))
+        return
     L.call("nr_adam_multi", arr, len(entries), beta1, beta2, eps, weight_decay, grad_scale,
            L.stream_ptr(entries[0][0]))
 
@@ -536,7 +591,8 @@ def colsum(x, rows, cols, out):
         raise L.HipError("colsum: out too small")
     nbytes = L.load().nr_colsum_workspace(rows, cols)
     work = torch.empty(max(1, nbytes // 4), device=x.device, dtype=torch.float32)
-    L.call("nr_colsum", L.ptr(x), x.stride(0), rows, cols, L.ptr(out), L.ptr(work), L.stream_ptr(x))
+    tick = self_cleaning_workspace(x.device, "nr_colsum", (cols + 63) // 64)
+    L.call("nr_colsum_ws", L.ptr(x), x.stride(0), rows, cols, L.ptr(out), L.ptr(work), L.ptr(tick), L.stream_ptr(x))
 
 
 MHA_POOL_SHAPES = {(64, 32, 384), (64, 64, 768), (64, 32, 256), (32, 32, 384)}

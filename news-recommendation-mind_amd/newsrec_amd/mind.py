@@ -219,14 +219,17 @@ class MINDStore:
                 m for b, m in ((1, "sample index out of range"), (2, "news id out of range"),
                                (4, "candidate/user row out of range")) if s & b))
 
-    def train_batch(self, sample_idx, out=None, device_rng=False):
+    def train_batch(self, sample_idx, out=None, device_rng=False, epoch_batch=None):
         """Collated MIND.__getitem__ train outputs for the samples sample_idx (int64 [B],
         device or host).
 
         out: a dict from an earlier call to fill in place (a captured graph's static inputs).
         device_rng: draw from the device-resident (seed, offset) pair ``rng_state`` and advance
         it on the device (graph-capturable: every replay draws fresh negatives) instead of the
-        host-side offset."""
+        host-side offset.
+        epoch_batch = B (with device_rng): sample_idx is a whole epoch order on the device and each
+        call forms its next batch of B from it (the cursor lives in ``rng_state`` and the launch
+        advances it: a replayed graph walks the epoch with no copy per step)."""
         if self.mode != "train":
             raise ValueError("train_batch on a %s split" % self.mode)
         dev = self.device
@@ -236,7 +239,12 @@ class MINDStore:
                 raise IndexError("sample index out of range [0, %d)" % self.n_samples)
             idx = idx.to(dev, non_blocking=True)
         idx = idx.contiguous()
-        B, C, NH, Ls = idx.numel(), self.npratio + 1, self.his_size, self.signal_length
+        if epoch_batch is not None and not device_rng:
+            raise ValueError("epoch_batch needs device_rng (the cursor lives in rng_state)")
+        B = idx.numel() if epoch_batch is None else int(epoch_batch)
+        if epoch_batch is not None and not 0 < B <= idx.numel():
+            raise ValueError("epoch_batch must be in (0, len(order)]")
+        C, NH, Ls = self.npratio + 1, self.his_size, self.signal_length
         shapes = {"user_id": ((B,), torch.int64), "cdd_id": ((B, C), torch.int64), "his_id": ((B, NH), torch.int64),
                   "cdd_encoded_index": ((B, C, Ls), torch.int64), "his_encoded_index": ((B, NH, Ls), torch.int64),
                   "cdd_attn_mask": ((B, C, Ls), torch.int64), "his_attn_mask": ((B, NH, Ls), torch.int64),
@@ -259,19 +267,24 @@ class MINDStore:
         rng = None
         if device_rng:
             if getattr(self, "rng_state", None) is None:
-                self.rng_state = torch.tensor([self.seed, self.offset], dtype=torch.int64, device=dev)
+                # {seed, offset, ticket, cursor, n_order, 0}: nr_form_train_batch advances the offset
+                # (and, walking an epoch order, the cursor) itself
+                self.rng_state = torch.tensor([self.seed, self.offset, 0, 0, 0, 0], dtype=torch.int64, device=dev)
+                self._rng_order = None
+            if epoch_batch is not None and getattr(self, "_rng_order", None) != idx.numel():
+                self.rng_state[3:5] = torch.tensor([0, idx.numel()], dtype=torch.int64)
+                self._rng_order = idx.numel()
             rng = self.rng_state
         seed, off = self.seed, self.offset
         self.offset += B * 4 * C
         P = L.ptr
         L.call("nr_form_train_batch", P(idx), B, P(self.imprs), self.n_samples, P(self.his_off), P(self.his_ids),
                P(self.neg_off), P(self.neg_ids), P(self.uindex), P(self.tok), P(self.attn), self.n_news, Ls,
-               self.npratio, NH, self.flags, seed, off, P(rng), P(x["cdd_id"]), P(x["his_id"]),
+               self.npratio, NH, self.flags | (L.BATCH_CURSOR if epoch_batch is not None else 0), seed, off, P(rng),
+               P(x["cdd_id"]), P(x["his_id"]),
                P(x["cdd_encoded_index"]), P(x["cdd_attn_mask"]), P(x["his_encoded_index"]), P(x["his_attn_mask"]),
                P(x["cdd_mask"]), P(x["his_mask"]), P(x["user_id"]), P(x["label"]), P(self.status),
                L.stream_ptr(idx))
-        if rng is not None:
-            rng[1:].add_(B * 4 * C)
         return x
 
     def eval_batch(self, chunk0, n_chunks, with_tokens=False):

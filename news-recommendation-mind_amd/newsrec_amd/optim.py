@@ -55,10 +55,8 @@ class FusedAdam(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 todo.append((gi, group, p, st))
-        if self.capturable:
-            steps = [st["step"] for _, _, _, st in todo]
-            if steps:
-                torch._foreach_add_(steps, 1)
+        # capturable: the device step counts are advanced by the Adam launch itself
+        # (nr_adam_multi_step: the bias corrections use count + 1, the last workgroup adds 1)
         # one nr_adam_multi call per (betas, eps, weight_decay) combination: every tensor of the
         # step in a few launches instead of one launch per parameter
         batches = {}
@@ -70,5 +68,5 @@ class FusedAdam(torch.optim.Optimizer):
             lr = self._lr_dev[gi] if self.capturable else group["lr"]
             batches.setdefault(key, []).append((p, g, st["exp_avg"], st["exp_avg_sq"], lr, st["step"]))
         for (betas, eps, wd), entries in batches.items():
-            K.adam_multi(entries, betas[0], betas[1], eps, wd, grad_scale)
+            K.adam_multi(entries, betas[0], betas[1], eps, wd, grad_scale, advance_steps=self.capturable)
         return loss

@@ -19,7 +19,9 @@ def _ids(T, V, seed, pad_frac=0.4):
     return ids
 
 
-@pytest.mark.parametrize("T,V", [(1, 5), (37, 7), (1000, 30522), (52800, 30522), (4096, 100)])
+# V <= 65536: count + fused scan (one launch); 200000: the multi-tile scan (two more launches)
+@pytest.mark.parametrize("T,V", [(1, 5), (37, 7), (1000, 30522), (52800, 30522), (4096, 100), (60000, 200000),
+                                 (20000, 65536)])
 def test_unique_rows(T, V):
     ids = _ids(T, V, T + V)
     ur = K.UniqueRows(ids.cuda(), V, fill_row=0)
@@ -64,12 +66,36 @@ def test_unique_rows_grad_mask_segments():
     torch.testing.assert_close(dst[:Up].double(), ref[:Up], rtol=1e-5, atol=1e-5)   # empty segments: 0
 
 
-def test_unique_rows_flags_bad_ids():
-    ids = torch.tensor([0, 3, 9, 2], dtype=torch.int64)
-    ur = K.UniqueRows(ids.cuda(), 5)
+@pytest.mark.parametrize("V", [5, 100000])
+def test_unique_rows_flags_bad_ids(V):
+    ids = torch.tensor([0, 3, V + 4, 2], dtype=torch.int64)
+    ur = K.UniqueRows(ids.cuda(), V)
     torch.cuda.synchronize()
     U, Up, bad, Tc = ur.counts.tolist()
     assert bad == 1 and U == 3 and Tc == 3
+    # the workspace is self-cleaning: the next call on the same buffer starts from zero counters
+    ur2 = K.UniqueRows(torch.tensor([1, 1, 2], dtype=torch.int64).cuda(), V)
+    torch.cuda.synchronize()
+    assert ur2.counts.tolist() == [2, 32, 0, 3]
+
+
+@pytest.mark.parametrize("V", [30522, 100000])
+def test_unique_rows_repeated_calls_and_empty(V):
+    """Back-to-back calls on the one persistent workspace (its counters and control words must come
+    back zero after every call), an empty batch among them."""
+    for i, T in enumerate([5000, 0, 1, 30000, 5000]):
+        ids = _ids(T, V, 1000 + i)
+        ur = K.UniqueRows(ids.cuda(), V, fill_row=0)
+        torch.cuda.synchronize()
+        U, Up, bad, Tc = ur.counts.tolist()
+        ref = np.unique(ids.numpy())
+        assert (U, Up, bad, Tc) == (len(ref), (len(ref) + 31) // 32 * 32, 0, T)
+        assert (ur.uids[:U].cpu().numpy() == ref).all()
+        if T:
+            assert (ur.uids.cpu().numpy()[ur.inv.cpu().numpy()] == ids.numpy()).all()
+    ws = K._SELF_CLEANING[(torch.device("cuda", 0), f"nr_unique_rows/{V}")]
+    V4 = (V + 3) // 4 * 4
+    assert int(ws[:4 + 2 * V4].abs().sum()) == 0   # ctrl words + both counters back to zero
 
 
 @pytest.mark.parametrize("T,V,W", [(300, 50, 1152), (52800, 30522, 1152), (33, 4, 4)])

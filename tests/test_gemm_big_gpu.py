@@ -100,9 +100,8 @@ def test_big_dgrad_store_and_scatter_store(prec):
 @pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("gather,N", [(False, 1152), (True, 1152), (True, 1100), (True, 1200)])
 def test_big_wgrad_split_k(prec, gather, N):
-    """dW = dYᵀ X over K = rows (MN_PLAIN x MN_PLAIN / MN_GATHER), split-K atomics, device-resident K.
-    N = 1152 / 1100: the last row of 256-row tiles holds <= 128 live rows -> balanced splits (its waves
-    4-7 skip their MFMAs, its units carry twice the k range); N = 1200: uniform splits."""
+    """dW = dYᵀ X over K = rows (MN_PLAIN x MN_PLAIN / MN_GATHER), split-K atomics, device-resident K.  N = 1152 / 1100: the last row of 256-row
+    tiles holds <= 128 live rows (its waves 4-7 skip their MFMAs); N = 1200: every tile row full."""
     g = torch.Generator().manual_seed(5 + gather)
     R, E, V = 24576, 768, 30000
     dY = torch.randn(R, N, generator=g)
@@ -118,6 +117,48 @@ def test_big_wgrad_split_k(prec, gather, N):
     Kr = R - 4096
     want = _ref(dY[:Kr].t(), X[:Kr], prec)
     assert _err(dW, want) <= _tol(dY, X, Kr, prec)
+
+
+@pytest.mark.parametrize("kd", [24576, 20000, 992, 0])
+def test_big_wgrad_split_k_workspace_accumulates(kd):
+    """nr_gemm_f32_ws' workspace path: the split-K reduction ADDS into C (the atomic epilogue's
+    contract), skips the splits whose k range starts past the device K (k_dev = 992: 16 of 17 splits
+    hold rows; a device K is a multiple of 32), sums the splits in a fixed order (two runs bitwise
+    equal), and matches the atomic path (no workspace) to rounding."""
+    g = torch.Generator().manual_seed(11)
+    R, N, E = 24576, 1152, 768
+    dY = torch.randn(R, N, generator=g)
+    X = torch.randn(R, E, generator=g)
+    C0 = torch.randn(N, E, generator=g)
+    k_dev = torch.tensor([kd], dtype=torch.int32, device="cuda")
+    A, B = K.operand(dY.cuda(), L.MNCONTIG), K.operand(X.cuda(), L.MNCONTIG)
+    outs = []
+    for _ in range(2):   # the C ABI's workspace form (K.gemm_dyn itself keeps the atomic epilogue here)
+        dW = C0.cuda()
+        work = K._splitk_work(dW)
+        L.call("nr_gemm_f32_ws", N, E, R, A, B, L.ptr(dW), dW.stride(0), None, L.EPI_ATOMIC, None, -1, 9, None,
+               L.ptr(k_dev), L.GEMM_BF16X6, 0, L.ptr(work), work.numel(), None, None, L.stream_ptr(dW))
+        outs.append(dW)
+    want = C0.double() + _ref(dY[:kd].t(), X[:kd], L.GEMM_BF16X6)
+    assert _err(outs[0], want) <= _tol(dY, X, max(kd, 1), L.GEMM_BF16X6)
+    assert torch.equal(outs[0], outs[1])
+    at = C0.cuda()   # the atomic epilogue (the C ABI without a workspace)
+    L.call("nr_gemm_f32_dyn", N, E, R, A, B, L.ptr(at), at.stride(0), None, L.EPI_ATOMIC, None, -1, 9, None,
+           L.ptr(k_dev), L.GEMM_BF16X6, L.stream_ptr(at))
+    assert _err(at, want) <= _tol(dY, X, max(kd, 1), L.GEMM_BF16X6)
+
+
+@pytest.mark.parametrize("prec", PRECS)
+def test_big_wgrad_split_k_static(prec):
+    """A BERT-shaped weight gradient through the static entry (K.gemm -> nr_gemm_f32_ws)."""
+    g = torch.Generator().manual_seed(12)
+    R, N, E = 8192, 3072, 768
+    G = torch.randn(R, N, generator=g)
+    X = torch.randn(R, E, generator=g)
+    dW = torch.zeros(N, E, device="cuda")
+    K.gemm(N, E, R, K.operand(G.cuda(), L.MNCONTIG), K.operand(X.cuda(), L.MNCONTIG), dW, epilogue=L.EPI_ATOMIC,
+           split_k=8, prec=prec)
+    assert _err(dW, _ref(G.t(), X, prec)) <= _tol(G, X, R, prec)
 
 
 @pytest.mark.parametrize("prec", PRECS)
@@ -143,3 +184,38 @@ def test_big_dgrad_scatter_zeroed_tail(prec, U, u_dev):
     full[rows[:m]] = want
     full[0] = 0
     assert _err(dt, full) <= _tol(dY, W, N, prec)
+
+
+@pytest.mark.parametrize("kd", [None, 20000])
+def test_big_wgrad_folds_bias_colsum(kd):
+    """K.gemm(..., colsum=db): on the split-K workspace path the weight gradient's bias gradient
+    db += Σ_k dY[k] is summed from the dY tiles the first column tile's units load (fp32, per split,
+    then the reduction) -> True; device-resident K honoured.  A shape that stays off that path
+    returns False and leaves db alone."""
+    g = torch.Generator().manual_seed(13)
+    R, N, E = 20832, 3072, 768
+    dY = torch.randn(R, N, generator=g)
+    X = torch.randn(R, E, generator=g)
+    db0 = torch.randn(N, generator=g)
+    dW = torch.zeros(N, E, device="cuda")
+    db = db0.cuda()
+    A, B = K.operand(dY.cuda(), L.MNCONTIG), K.operand(X.cuda(), L.MNCONTIG)
+    if kd is None:
+        folded = K.gemm(N, E, R, A, B, dW, epilogue=L.EPI_ATOMIC, split_k=8, colsum=db)
+        kr = R
+    else:
+        K.gemm_dyn(N, E, R, A, B, dW, k_dev=torch.tensor([kd], dtype=torch.int32, device="cuda"),
+                   epilogue=L.EPI_ATOMIC, split_k=8)   # (gemm_dyn takes no colsum: the weights only)
+        folded = K.gemm(N, E, kd, A, B, torch.zeros(N, E, device="cuda"), epilogue=L.EPI_ATOMIC, split_k=8,
+                        colsum=db)
+        kr = kd
+    assert folded
+    want = db0.double() + dY[:kr].double().sum(0)
+    assert _err(db, want) <= 1e-5 * kr ** 0.5 * dY.abs().max().item() + 1e-5
+    assert _err(dW, _ref(dY[:kr].t(), X[:kr], L.GEMM_BF16X6)) <= _tol(dY, X, kr, L.GEMM_BF16X6)
+    # a small contraction runs on the 64 x 64 kernel: not folded, db untouched
+    small = db0.cuda()
+    f2 = K.gemm(64, 64, 256, K.operand(dY[:256, :64].contiguous().cuda(), L.MNCONTIG),
+                K.operand(X[:256, :64].contiguous().cuda(), L.MNCONTIG), torch.zeros(64, 64, device="cuda"),
+                epilogue=L.EPI_ATOMIC, split_k=2, colsum=small[:64])
+    assert not f2 and torch.equal(small.cpu(), db0)

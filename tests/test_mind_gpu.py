@@ -57,6 +57,51 @@ def test_train_batch_bit_exact(data, shuffle, desc):
         assert x["his_mask"].shape == (40, st.his_size, 1) and x["cdd_mask"].shape == (40, st.npratio + 1, 1)
 
 
+def test_train_batch_device_rng_advances_in_kernel(data):
+    """device_rng: the launch draws from the device words {seed, offset} and advances the offset by
+    B * 4C itself (the last workgroup, ticket back to zero) -- three batches in a row, each equal
+    to the oracle at the offset the previous launch left; no host bookkeeping read."""
+    st = _store(data, "train", shuffle_pos=True, seed=31)
+    B = 40
+    idx = torch.arange(B) % len(st)
+    C = st.npratio + 1
+    out = None
+    for rep in range(3):
+        off = 12345 + rep * B * 4 * C if rep else 12345
+        if rep == 0:
+            st.offset = 12345
+        out = st.train_batch(idx.to(DEV), out=out, device_rng=True)
+        torch.cuda.synchronize()
+        st.check_status()
+        want = R.mind_train_batch(store_arrays(st), idx.tolist(), 31, off, st.npratio, st.his_size, False, True)
+        for k, v in want.items():
+            np.testing.assert_array_equal(out[k].cpu().numpy().reshape(v.shape), v, err_msg=k)
+        rs = st.rng_state.cpu().tolist()
+        assert rs[1] == off + B * 4 * C and rs[2] == 0
+
+
+def test_train_batch_epoch_cursor(data):
+    """epoch_batch: the launch takes batch (cursor mod len(order) // B) of a device epoch order and
+    advances the cursor itself (with the RNG offset); a 2.5-batch order wraps after two batches."""
+    st = _store(data, "train", seed=8)
+    B = 16
+    order = torch.randperm(len(st), generator=torch.Generator().manual_seed(2))[:B * 5 // 2]
+    st.offset = 500
+    out = None
+    C = st.npratio + 1
+    for rep, start in enumerate([0, B, 0]):
+        out = st.train_batch(order.to(DEV), out=out, device_rng=True, epoch_batch=B)
+        torch.cuda.synchronize()
+        st.check_status()
+        idx = order[start:start + B].tolist()
+        want = R.mind_train_batch(store_arrays(st), idx, 8, 500 + rep * B * 4 * C, st.npratio, st.his_size, False,
+                                  False)
+        for k, v in want.items():
+            np.testing.assert_array_equal(out[k].cpu().numpy().reshape(v.shape), v, err_msg=k)
+    rs = st.rng_state.cpu().tolist()
+    assert rs[2] == 0 and rs[3] == 3 and rs[4] == len(order)
+
+
 def test_train_batch_sampling_distribution(data):
     """One impression with >= npratio negatives drawn many times: distinct picks, each negative
     with frequency npratio / n (uniform subsets, as random.sample)."""

@@ -180,3 +180,53 @@ def test_forward_loss_fused_head(cfg):
             continue
         scale = max(p.grad.abs().max().item(), 1e-6)
         torch.testing.assert_close(gf[n], p.grad, rtol=0, atol=1e-5 * scale, msg=n)
+
+
+@pytest.mark.parametrize("B,C,H", [(1, 5, 150), (32, 5, 150), (300, 5, 150), (64, 20, 400), (7, 1, 3)])
+def test_score_nll_kernel_vs_torch(B, C, H):
+    """nr_score_nll_fwd / _bwd against torch (scores, log_softmax, nll_loss mean): one workgroup per
+    impression, the last arrival sums the loss terms; run three times on the one self-cleaning
+    ticket (a stale ticket would leave the loss unwritten)."""
+    from newsrec_amd import kernels as K
+    g = torch.Generator().manual_seed(B * 31 + C)
+    cdd = torch.randn(B * C, H, generator=g).cuda()
+    user = torch.randn(B, H, generator=g).cuda()
+    label = torch.randint(0, C, (B,), generator=g).cuda()
+    cr, ur = cdd.clone().requires_grad_(), user.clone().requires_grad_()
+    lg = torch.log_softmax((cr.view(B, C, H) * ur[:, None]).sum(-1) / H ** 0.5, -1)
+    lref = torch.nn.functional.nll_loss(lg, label)
+    lref.backward()
+    for _ in range(3):
+        logits = torch.full((B, C), float("nan"), device="cuda")
+        loss = torch.full((1,), float("nan"), device="cuda")
+        K.score_nll_fwd(cdd, user, label, B, C, H, logits, loss)
+        dcdd, duser = torch.empty_like(cdd), torch.empty_like(user)
+        K.score_nll_bwd(cdd, user, logits, label, torch.ones(1, device="cuda"), None, B, C, H, dcdd, duser)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(logits, lg.detach(), rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(loss[0], lref.detach(), rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(dcdd, cr.grad, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(duser, ur.grad, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("rows,cols,ld", [(1600, 1152, 1152), (52800, 150, 152), (7, 3, 4), (20832, 3072, 3072),
+                                          (4000, 700, 768)])
+def test_colsum_one_launch(rows, cols, ld):
+    """K.colsum (nr_colsum_ws: the last workgroup per 64-column chunk sums the partial rows) against
+    fp64 and against the two-launch nr_colsum; out is accumulated into (+=); three calls in a row on
+    the one self-cleaning counter array."""
+    from newsrec_amd import _lib as L
+    from newsrec_amd import kernels as K
+    g = torch.Generator().manual_seed(rows + cols)
+    x = torch.randn(rows, ld, generator=g)[:, :cols].cuda()
+    base = torch.randn(cols, generator=g)
+    want = base.double() + x.cpu().double().sum(0)
+    for _ in range(3):
+        out = base.cuda()
+        K.colsum(x, rows, cols, out)
+        torch.cuda.synchronize()
+        assert (out.cpu().double() - want).abs().max().item() <= 1e-5 * rows ** 0.5 + 1e-5
+    two = base.cuda()
+    work = torch.empty(max(1, L.load().nr_colsum_workspace(rows, cols) // 4), device="cuda")
+    L.call("nr_colsum", L.ptr(x), x.stride(0), rows, cols, L.ptr(two), L.ptr(work), L.stream_ptr(x))
+    torch.testing.assert_close(out, two, rtol=1e-6, atol=1e-5)

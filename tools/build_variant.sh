@@ -1,6 +1,6 @@
 #!/bin/bash
-# Build libnewsrec_hip.so with extra -D flags on gemm_fast.hip into ab/<name>/ (A/B timing with
-# NR_LIB_PATH).  Usage: tools/build_variant.sh NAME [-DFLAG ...]
+# Build libnewsrec_hip.so with extra -D flags on the GEMM translation units (gemm_*.hip) into
+# ab/<name>/ (A/B timing with NR_LIB_PATH).  Usage: tools/build_variant.sh NAME [-DFLAG ...]
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 NAME=$1; shift
@@ -8,7 +8,14 @@ OUT=$ROOT/ab/$NAME
 mkdir -p $OUT
 PKG=$ROOT/news-recommendation-mind_amd
 OBJ=$PKG/newsrec_amd/lib/obj
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -munsafe-fp-atomics -I$ROOT/include "$@" -c $PKG/csrc/gemm_fast.hip -o $OUT/gemm_fast.o
-objs=$(ls $OBJ/*.o | grep -v "/gemm_fast.hip\.")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libnewsrec_hip.so $objs $OUT/gemm_fast.o
+pids=()
+for src in $PKG/csrc/gemm_*.hip; do
+  b=$(basename $src)
+  extra=$(python3 -c "import sys; sys.path.insert(0, '$PKG'); import build; print(' '.join(build.EXTRA.get('$b', [])))")
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -munsafe-fp-atomics -I$ROOT/include $extra "$@" -c $src -o $OUT/$b.o &
+  pids+=($!)
+done
+for p in "${pids[@]}"; do wait $p; done
+objs=$(ls $OBJ/*.o | grep -v "/gemm_[a-z0-9_]*\.hip\.")
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libnewsrec_hip.so $objs $OUT/gemm_*.hip.o
 echo $OUT/libnewsrec_hip.so

@@ -31,7 +31,7 @@ x = torch.randn(T, 768, device=dev); wqkv = torch.randn(2304, 768, device=dev) /
 qkv = torch.empty(T, 2304, device=dev); wi = torch.randn(3072, 768, device=dev) / 30
 G = torch.empty(T, 3072, device=dev); Ub = torch.empty(T, 3072, device=dev)
 wo2 = torch.randn(768, 3072, device=dev) / 50; o = torch.empty(T, 768, device=dev)
-dWi = torch.zeros(3072, 768, device=dev)
+dWi = torch.zeros(3072, 768, device=dev); dbi = torch.zeros(3072, device=dev)
 P = torch.empty(U, 480, device=dev); w3 = torch.randn(480, E, device=dev)
 uids = torch.randperm(V - 1, device=dev)[:24600] + 1; dT = torch.zeros(V, E, device=dev)
 dYc = torch.randn(52800, 1152, device=dev); WT = W.t().contiguous()
@@ -54,6 +54,9 @@ cases = {
  "bert_ffn1_gelu": (2*T*768*3072, lambda p: K.gemm(T, 3072, 768, K.operand(x, L.KCONTIG), K.operand(wi, L.KCONTIG), G, epilogue=L.EPI_STORE_GELU, c_rows=K.operand(Ub, L.KCONTIG), prec=p)),
  "bert_ffn2": (2*T*768*3072, lambda p: K.gemm(T, 768, 3072, K.operand(G, L.KCONTIG), K.operand(wo2, L.KCONTIG), o, prec=p)),
  "bert_ffn1_wgrad": (2*T*768*3072, lambda p: K.gemm(3072, 768, T, K.operand(G, L.MNCONTIG), K.operand(x, L.MNCONTIG), dWi, epilogue=L.EPI_ATOMIC, split_k=F._split_k(3072, 768, T), prec=p)),
+ "bert_ffn1_wgrad_cs": (2*T*768*3072, lambda p: K.gemm(3072, 768, T, K.operand(G, L.MNCONTIG), K.operand(x, L.MNCONTIG), dWi, epilogue=L.EPI_ATOMIC, split_k=F._split_k(3072, 768, T), prec=p, colsum=dbi)),
+ "bert_ffn1_wgrad_atomic": (2*T*768*3072, lambda p: L.call("nr_gemm_f32", 3072, 768, T, K.operand(G, L.MNCONTIG), K.operand(x, L.MNCONTIG), L.ptr(dWi), 768, None, L.EPI_ATOMIC, None, -1, F._split_k(3072, 768, T), p, L.stream_ptr(dWi))),
+ "nrms_proj_wgrad_atomic": (2*U*E*1152, lambda p: L.call("nr_gemm_f32_dyn", 1152, E, U, K.operand(dY, L.MNCONTIG), K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), L.ptr(dW), E, None, L.EPI_ATOMIC, None, -1, F._split_k(1152, E, U), None, None, p, L.stream_ptr(dW))),
 }
 out = {}
 import os
@@ -87,8 +90,9 @@ def main():
             res[m] = {"error": r.stderr[-2000:]}
             print(json.dumps({m: res[m]}), flush=True)
             break
-        res[m] = json.loads(r.stdout.strip().splitlines()[-1])
-        print(json.dumps({m: res[m]}), flush=True)
+        key = m if m not in res else "%s#%d" % (m, len(res))
+        res[key] = json.loads(r.stdout.strip().splitlines()[-1])
+        print(json.dumps({key: res[key]}), flush=True)
     print(json.dumps(res))
 
 

@@ -1,4 +1,5 @@
-"""Run bench.config_legs alone (profiling helper): python tools/legs_only.py [leg ...] [--steps K]."""
+"""Run bench.config_legs alone (profiling helper): python tools/legs_only.py [leg ...] [--steps K];
+``xformer`` alone runs bench.xformer_leg."""
 import argparse
 import json
 import os
@@ -12,5 +13,8 @@ ap.add_argument("legs", nargs="*")
 ap.add_argument("--steps", type=int, default=20)
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
-feed = bench.DeviceFeed(dev, 1, 0)
-print(json.dumps(bench.config_legs(dev, feed, steps=a.steps, only=a.legs or None)))
+if a.legs == ["xformer"]:
+    print(json.dumps(bench.xformer_leg(dev, steps=a.steps)))
+else:
+    feed = bench.DeviceFeed(dev, 1, 0)
+    print(json.dumps(bench.config_legs(dev, feed, steps=a.steps, only=a.legs or None)))
