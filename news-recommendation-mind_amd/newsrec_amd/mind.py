@@ -260,9 +260,11 @@ class MINDStore:
                 x[b] = buf[B * C * Ls:].view(B, NH, Ls)
         else:
             x = out
+            want_dev = torch.device(dev)
             for k, (sh, dt) in shapes.items():
                 t = x[k]
-                if tuple(t.shape) != sh or t.dtype != dt or not t.is_contiguous() or t.device != dev:
+                same_dev = t.device.type == want_dev.type and (want_dev.index is None or t.device.index == want_dev.index)
+                if tuple(t.shape) != sh or t.dtype != dt or not t.is_contiguous() or not same_dev:
                     raise ValueError("out[%r]: expected contiguous %s %s on %s" % (k, sh, dt, dev))
         rng = None
         if device_rng:

@@ -229,4 +229,5 @@ def test_colsum_one_launch(rows, cols, ld):
     two = base.cuda()
     work = torch.empty(max(1, L.load().nr_colsum_workspace(rows, cols) // 4), device="cuda")
     L.call("nr_colsum", L.ptr(x), x.stride(0), rows, cols, L.ptr(two), L.ptr(work), L.stream_ptr(x))
-    torch.testing.assert_close(out, two, rtol=1e-6, atol=1e-5)
+    # both orders of the fp32 sums within the same bound of fp64
+    assert (two.cpu().double() - want).abs().max().item() <= 1e-5 * rows ** 0.5 + 1e-5
