@@ -23,10 +23,13 @@
 namespace nrfast {
 
 constexpr int BIG_BM = 256;
-// k-tile depth: bf16x6 (three planes) 16, bf16 (one plane) 32 -- one barrier per k-tile either way,
-// so the one-product form gets as many MFMAs between barriers as its LDS budget allows
-template <int NP>
-constexpr int big_bk() { return NP == 1 ? 32 : 16; }
+// k-tile depth: bf16x6 (three planes) 16; bf16 (one plane) 32 when both operands are K-contiguous --
+// twice the MFMAs between barriers in the same LDS budget -- else 16: the MN-contiguous loaders'
+// stores at 32 cost more than the extra MFMAs per barrier buy (one-box A/B, bf16, µs: BERT FFN-in
+// weight gradient 657 -> 387, NRMS table dgrad 208 -> 141, CNN conv weight gradient 144 -> 115;
+// the K-contiguous forward shapes keep 32: BERT FFN-out 152 vs 187 at 16)
+template <int NP, int AM, int BMODE>
+constexpr int big_bk() { return NP == 1 && is_kc(AM) && is_kc(BMODE) ? 32 : 16; }
 // bf16 per LDS row: BK k + 8 pad (48 / 80 B: odd multiples of 16 B, conflict-free ds_read_b128)
 template <int BK>
 constexpr int big_sr() { return BK + 8; }
@@ -241,7 +244,7 @@ __device__ __forceinline__ void tail_scatter_tr(const Args& g, f32x16 (&acc)[TI]
 template <int AM, int BMODE, bool TR, int NP, int BN>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
   constexpr int BM = BIG_BM;
-  constexpr int BK = big_bk<NP>(), SR = big_sr<BK>(), KS = BK / 16;   // KS: 16-deep MFMA steps per k-tile
+  constexpr int BK = big_bk<NP, AM, BMODE>(), SR = big_sr<BK>(), KS = BK / 16;   // KS: 16-deep MFMA steps per k-tile
   using LA = BigLoader<BM, AM, BK>;
   using LB = BigLoader<BN, BMODE, BK>;
   constexpr int PA = BM * SR, PB = BN * SR;   // one plane
@@ -300,9 +303,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
   f32x16 acc[TI][TJ];
   LA la;
   LB lb;
-#ifdef NR_AB_PRIO_STATIC   // A/B build knob (tools/build_variant.sh): the younger half at priority 1
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
 
   // persistent over this block's units (virtual ids blockIdx.x + j * gridDim.x); each unit runs its
   // own two-deep pipeline, so the k-loop carries no unit bookkeeping (a pipeline refill per unit
@@ -378,6 +378,9 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
     // one k-tile (KS MFMA steps of 16): MFMAs from stage st; behind the first row blocks the wave
     // splits k-tile kt+1 (set (kt+1) % 2 = NS) into the other stage, then reuses that set for k-tile
     // kt+3's loads
+    // (waves 4-7 splitting behind their last two row blocks instead -- a stagger of the VALU
+    // clumps of the two waves on a SIMD -- measured slower: projection fwd 270-280 vs 257-260 µs)
+    constexpr int ia = 0, ib = KS == 1 ? 1 : 0;
     auto ktile = [&](auto nset, int kt, int st) {
       constexpr int NS = decltype(nset)::value;
       const bool stage_next = kt + 1 < nt;
@@ -399,9 +402,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
 #pragma unroll
         for (int p = 0; p < NP; ++p)
           a[p] = *reinterpret_cast<const bf16x8*>(a_s + p * PA + (wm + 32 * i + c) * SR + 16 * kk + 8 * h);
-#ifdef NR_AB_PRIO_CLUSTER
-        __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
 #define NR_MF(X, Y)                                                                                    \
@@ -417,19 +417,16 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
           NR_MF(0, 0);
 #undef NR_MF
         }
-#ifdef NR_AB_PRIO_CLUSTER
-        __builtin_amdgcn_s_setprio(0);
-#endif
         }
         // split-stores of the next stage: A behind step 0's first row block, B (then the loads of
         // k-tile kt+3 into the freed register set) behind step KS/2's second (KS = 1) or first row block
-        if (kk == 0 && i == 0 && stage_next) {
+        if (kk == 0 && i == ia && stage_next) {
           if constexpr (CS_OK) {
             if (do_cs) la.template add_colsum<NS>(cs, tid);
           }
           la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid);
         }
-        if (kk == KS / 2 && i == (KS == 1 ? 1 : 0) && stage_next) {
+        if (kk == KS / 2 && i == ib && stage_next) {
           lb.template store<NS, NP>(Bs + (st ^ 1) * NP * PB, tid);
           if (kt + 3 < nt) issue(nset, kt + 3);
         }

@@ -30,20 +30,13 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
 __device__ __forceinline__ float pk_lo(uint32_t p) { return __uint_as_float(p << 16); }
 __device__ __forceinline__ float pk_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
 // a, b -> the packed (h, m, l) terms of both: 3 conversions, 4 bit ops, 4 subtractions per pair
-#ifdef NR_AB_ASM_SUB   // A/B build knob: the subtractions as scalar v_sub_f32 (no SLP packing)
-__device__ __forceinline__ float nr_sub(float a, float b) {
-  float r;
-  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-#else
-__device__ __forceinline__ float nr_sub(float a, float b) { return a - b; }
-#endif
+// (the bf16x6 GEMM units build without SLP vectorisation so these subtractions stay scalar
+// v_sub_f32 beside the MFMAs: build.py EXTRA)
 __device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
   h = pk_bf16(a, b);
-  const float ra = nr_sub(a, pk_lo(h)), rb = nr_sub(b, pk_hi(h));   // exact
+  const float ra = a - pk_lo(h), rb = b - pk_hi(h);   // exact
   m = pk_bf16(ra, rb);
-  l = pk_bf16(nr_sub(ra, pk_lo(m)), nr_sub(rb, pk_hi(m)));
+  l = pk_bf16(ra - pk_lo(m), rb - pk_hi(m));
 }
 __device__ __forceinline__ void split4(float a, float b, float c, float d, uint2& p0, uint2& p1, uint2& p2) {
   split2(a, b, p0.x, p1.x, p2.x);

@@ -360,9 +360,9 @@ constexpr int kColsumBlocks = 1024;
 
 // tick (nr_colsum_ws): per 64-column chunk arrival counters, zero on entry; the chunk's last
 // workgroup to arrive sums the chunk's partial rows in row-block order and resets its counter, so the
-// final pass needs no launch of its own (cdna_hip_programming.md §6 Guideline 16's counter form:
-// plain partial stores, every storing wave's vmcnt drain, barrier, lane-0 agent release + ticket;
-// the last arriver's acquire, then plain loads)
+// final pass needs no launch of its own (cdna_hip_programming.md §6 Guideline 16's counter form with
+// write-through partials: sc1 stores need no release fence -- the storing wave's vmcnt drain, the
+// barrier, lane 0's agent-scope ticket; the last arriver's acquire, then plain loads)
 __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows,
                                                           int64_t cols, int64_t rb_rows, float* __restrict__ part,
                                                           int32_t* __restrict__ tick, float* __restrict__ out) {
@@ -384,14 +384,18 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restric
   }
   red[w][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
   __syncthreads();
-  if (w == 0 && c < cols) part[(int64_t)blockIdx.y * cols + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-  if (!tick) return;
+  if (!tick) {
+    if (w == 0 && c < cols) part[(int64_t)blockIdx.y * cols + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    return;
+  }
+  if (w == 0 && c < cols)
+    __hip_atomic_store(&part[(int64_t)blockIdx.y * cols + c], (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = atomicAdd(&tick[blockIdx.x], 1) == (int)gridDim.y - 1;
+    last = __hip_atomic_fetch_add(&tick[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (int)gridDim.y - 1;
     if (last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -435,10 +439,12 @@ __global__ __launch_bounds__(1024) void colsum_final_kernel(const float* __restr
   }
 }
 
-void colsum_grid(int64_t rows, int64_t cols, int64_t* nrb, int64_t* rb_rows) {
+// blocks: total workgroups to aim for; min_rows: rows per workgroup at least
+void colsum_grid(int64_t rows, int64_t cols, int64_t* nrb, int64_t* rb_rows, int64_t blocks = kColsumBlocks,
+                 int64_t min_rows = 32) {
   const int64_t cc = (cols + 63) / 64;
-  int64_t n = kColsumBlocks / cc;
-  const int64_t by_rows = (rows + 31) / 32;   // at least 32 rows per block
+  int64_t n = blocks / cc;
+  const int64_t by_rows = (rows + min_rows - 1) / min_rows;
   if (n > by_rows) n = by_rows;
   if (n < 1) n = 1;
   *rb_rows = (rows + n - 1) / n;
@@ -572,8 +578,9 @@ extern "C" int nr_colsum_ws(const float* x, int64_t ldx, int64_t rows, int64_t c
   if (rows < 0 || cols < 0 || ldx < cols) return NR_EINVAL(0);
   if (!x || !out || (rows > 0 && cols > 0 && (!work || !tick))) return NR_EINVAL(1);
   if (rows == 0 || cols == 0) return NR_OK;
+  // one round of workgroups (fewer, longer partials: the last arriver of a chunk reads them all)
   int64_t nrb, rb_rows;
-  colsum_grid(rows, cols, &nrb, &rb_rows);
+  colsum_grid(rows, cols, &nrb, &rb_rows, 512, 128);
   hipLaunchKernelGGL(colsum_part_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)nrb), dim3(256), 0, stream, x,
                      ldx, rows, cols, rb_rows, work, tick, out);
   NR_LAUNCH_CHECK();

@@ -352,6 +352,8 @@ class CNNNewsFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, table, ids, mask, w3, conv_b, wq, bq, query, seq_len, pad_row):
+        # the token output C is rarely consumed: an unused one must not cost a zero-filled gradient
+        ctx.set_materialize_grads(False)
         ctx.prec = K.get_gemm_precision()
         T = ids.numel()
         n = T // seq_len
@@ -379,6 +381,8 @@ class CNNNewsFn(torch.autograd.Function):
         n = T // seq_len
         V, E = table.shape
         H = w3.shape[0]
+        if dnews is None:   # (grads not materialised) the pooled output unused
+            dnews = torch.zeros(n, H, device=table.device)
         dev = table.device
         dnews = dnews.contiguous()
         # dC with its columns padded to a multiple of 32 (zeros): the table dgrad below contracts
@@ -463,6 +467,9 @@ class CNNNewsRowsFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, table, ids, mask, w3t, conv_b, wq, bq, query, seq_len, pad_row, H):
+        # the token output C is rarely consumed: an unused one must not cost a zero-filled gradient
+        # (and a padded copy of it) per step
+        ctx.set_materialize_grads(False)
         ctx.prec = K.get_gemm_precision()
         T = ids.numel()
         n = T // seq_len
@@ -496,6 +503,8 @@ class CNNNewsRowsFn(torch.autograd.Function):
         ur = ctx.ur
         T = ids.numel()
         n = T // seq_len
+        if dnews is None:   # (grads not materialised) the pooled output unused
+            dnews = torch.zeros(n, H, device=table.device)
         V, E = table.shape
         Hp = w3t.shape[0] // 3
         dev = table.device
