@@ -1,8 +1,8 @@
-# full -m gpu suite + the default bench line + kernel traces of the NRMS step and the CNN legs
+# full -m gpu suite + the default bench line + kernel traces of the NRMS step, the CNN legs and XFormer
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r03e
+O=gpurun_out/${1:-pass}
 mkdir -p $O
-echo tests; timeout -k 10 900 python -u -m pytest tests/test_model_gpu.py tests -m gpu -x -q --timeout 500 --timeout-method thread > $O/tests.log 2>&1 || exit 1
+echo tests; timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 500 --timeout-method thread > $O/tests.log 2>&1 || exit 1
 echo bench; timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 2
 B="python bench.py --steps 3 --warmup 2 --eval-impr 0 --config-legs 0 --xformer-steps 0 --no-cpu-baseline"
 echo trace; timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- $B > $O/kt.log 2>&1 || exit 3
