@@ -1,0 +1,429 @@
+// Fused word-attention head of the CNN news encoder (models/Encoders/CNN.py:18-24,44-46 over the
+// conv output C of CNN.py:41-42), one workgroup per title of L <= 32 tokens:
+//
+//   K   = tanh(C Wqᵀ + bq)                     wordQueryProject + Tanh (CNN.py:46)
+//   s_l = q · K_l / sqrt(H),  p = XSoftmax(s, mask),  news = Σ_l p_l C_l
+//                                              scaled_dp_attention (Attention.py:5-30)
+//
+// and its whole backward in ONE pass over C per title: the key projection is recomputed (never
+// stored), dp_l = dnews · C_l, ds = p (dp - Σ p dp) / sqrt(H), dK = ds q (1 - K²),
+// dC = p dnews + dK Wq (+ dz) gated by ReLU'(C) (the conv pre-activation gradient), and the
+// parameter gradients dWq = Σ dKᵀ C, dbq = Σ dK, dq = Σ ds K, dconv_b = Σ gated dC accumulate in
+// registers across the titles of a persistent workgroup; each workgroup stores one partial and
+// cnn_keypool_reduce_kernel adds the partials in workgroup order (deterministic, no atomics).
+// This replaces the T x Hp key GEMM + tanh epilogue, the word pooling, its backward, the key
+// dgrad / wgrad GEMMs and two bias column sums: seven launches and four T x Hp round trips.
+//
+// Layout: Hp = 32 NB <= 160 (the conv width padded; the backward's per-wave dWq accumulators, 16 NB
+// registers, spill past NB = 5, C / Wq / bq / q exactly zero past H); wave w of the
+// NB waves owns output column block w of K, of dC and of dWq's rows.  Products on the matrix
+// cores in the caller's GEMM arithmetic (mfma_planes.h: 0 = f32 MFMA, 3 = bf16x6, 1 = bf16), each
+// 32 x 32 output block over 16-value per-lane fragments, lane (c, h) holding k = 32 chunk + 16 h +
+// 0..15 (the same k order in both operands).  Operand sources: C and dK tiles from LDS (row reads
+// as ds_read_b128, column reads as ds_read_b32 -- both conflict-free at a row stride of Hp + 4
+// floats); Wq rows / columns straight from L2 (100 KB at H = 150, shared by every workgroup).
+#include "common.h"
+#include "../../include/newsrec_hip.h"
+#include "mfma_planes.h"
+
+namespace {
+
+struct KPArgs {
+  const float* c; int64_t ldc;        // [T][Hp] conv output after ReLU (zero past H)
+  const float* wq;                    // [Hp][Hp] padded key projection (row j = output, col k = input)
+  const float* bq;                    // [Hp]
+  const float* q; int qn;             // query [qn] (qn = H), zero past qn
+  const void* mask; int mask_dt;      // [nseq][L] (forward)
+  int64_t nseq; int L; float scale;
+  float* news; int64_t ldn;           // fwd: [nseq][Hp]
+  float* probs;                       // fwd out / bwd in: [T]
+  const float* dnews; int64_t lddn;   // bwd: [nseq][>= qn]
+  const float* dz; int64_t lddz;      // bwd (optional): gradient of the token output C, [T][>= H]
+  int H;
+  float* dc; int64_t lddc;            // bwd out: [T][Hp] gated dC (zero past H)
+  float* ws;                          // bwd: [gridDim.x][nws] partials: dwq | dbq | dq | dconv_b
+  int64_t nws;
+};
+
+template <int NB>
+struct KPShared {
+  static constexpr int HP = 32 * NB, SW = HP + 4;
+  float ct[32][SW];   // C tile (rows >= L zero)
+  float dk[32][SW];   // bwd: dK tile; fwd: K_j q_j products
+  float p[32], ds[32];
+  float dn[HP], qv[HP], bq[HP];
+};
+
+template <int NB>
+__device__ __forceinline__ void stage_tile(const KPArgs& g, int64_t seq, KPShared<NB>& sm) {
+  constexpr int Q4 = 8 * NB;   // float4 per row
+  const int nt = 64 * NB;
+  for (int i = threadIdx.x; i < 32 * Q4; i += nt) {
+    const int r = i / Q4, c4 = i - r * Q4;
+    float4 v = *reinterpret_cast<const float4*>(g.c + (seq * g.L + (r < g.L ? r : 0)) * g.ldc + 4 * c4);
+    if (r >= g.L) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    *reinterpret_cast<float4*>(&sm.ct[r][4 * c4]) = v;
+  }
+}
+
+// acc = C Wqᵀ for output columns 32 w .. 32 w + 31 (rows = the title's 32 token slots).  B (Wq rows)
+// either from registers held across titles (bw, the forward) or from L2 one chunk ahead of its
+// MFMAs (the backward, whose registers hold the dWq accumulators).
+template <int NB>
+__device__ __forceinline__ void load_wrow(const KPArgs& g, int w, int c, int h, int ch, float (&b)[16]) {
+  constexpr int HP = 32 * NB;
+  const float* wrow = g.wq + (int64_t)(32 * w + c) * HP + 16 * h + 32 * ch;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float4 y = *reinterpret_cast<const float4*>(wrow + 4 * u);
+    b[4 * u] = y.x; b[4 * u + 1] = y.y; b[4 * u + 2] = y.z; b[4 * u + 3] = y.w;
+  }
+}
+
+template <int NB>
+__device__ __forceinline__ void load_crow(const KPShared<NB>& sm, int c, int h, int ch, float (&a)[16]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float4 x = *reinterpret_cast<const float4*>(&sm.ct[c][32 * ch + 16 * h + 4 * u]);
+    a[4 * u] = x.x; a[4 * u + 1] = x.y; a[4 * u + 2] = x.z; a[4 * u + 3] = x.w;
+  }
+}
+
+template <int NB, int NP>
+__device__ __forceinline__ void key_block_regs(const KPShared<NB>& sm, int c, int h, const float (&bw)[NB][16],
+                                               f32x16& acc) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int ch = 0; ch < NB; ++ch) {
+    float a[16];
+    load_crow<NB>(sm, c, h, ch, a);
+    mfma16<NP>(acc, a, bw[ch]);
+  }
+}
+
+template <int NB, int NP>
+__device__ __forceinline__ void key_block(const KPArgs& g, const KPShared<NB>& sm, int w, int c, int h, f32x16& acc) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float bn[16];
+  load_wrow<NB>(g, w, c, h, 0, bn);
+#pragma unroll 1
+  for (int ch = 0; ch < NB; ++ch) {   // one chunk's fragments live at a time, the next one's B in flight
+    float a[16], b[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) b[s] = bn[s];
+    if (ch + 1 < NB) load_wrow<NB>(g, w, c, h, ch + 1, bn);
+    load_crow<NB>(sm, c, h, ch, a);
+    mfma16<NP>(acc, a, b);
+  }
+}
+
+template <int NB>
+__device__ __forceinline__ void stage_vectors(const KPArgs& g, KPShared<NB>& sm) {
+  constexpr int HP = 32 * NB;
+  for (int k = threadIdx.x; k < HP; k += 64 * NB) {
+    sm.qv[k] = k < g.qn ? g.q[k] : 0.f;
+    sm.bq[k] = g.bq[k];
+  }
+}
+
+template <int NB, int NP>
+__global__ __launch_bounds__(64 * NB) void cnn_keypool_fwd_kernel(KPArgs g) {
+  constexpr int HP = 32 * NB;
+  __shared__ KPShared<NB> sm;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
+  stage_vectors<NB>(g, sm);
+  float bw[NB][16];   // this wave's Wq rows, every chunk: loaded once, used by every title
+#pragma unroll
+  for (int ch = 0; ch < NB; ++ch) load_wrow<NB>(g, w, c, h, ch, bw[ch]);
+  for (int64_t seq = blockIdx.x; seq < g.nseq; seq += gridDim.x) {
+    __syncthreads();   // the previous title's pooling reads of ct are done
+    stage_tile<NB>(g, seq, sm);
+    __syncthreads();
+    {
+      f32x16 acc;
+      key_block_regs<NB, NP>(sm, c, h, bw, acc);
+      const int j = 32 * w + c;
+      const float bj = sm.bq[j], qj = sm.qv[j];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sm.dk[crow(r, h)][j] = tanhf(acc[r] + bj) * qj;
+    }
+    __syncthreads();
+    if (w == 0) {   // scores and the masked softmax, lane l = token l
+      const int l = lane & 31;
+      float s = 0.f;
+#pragma unroll 4
+      for (int k4 = 0; k4 < HP / 4; ++k4) {
+        const float4 v = *reinterpret_cast<const float4*>(&sm.dk[l][4 * k4]);
+        s += (v.x + v.y) + (v.z + v.w);
+      }
+      const bool keep = lane < g.L && nr_mask_at(g.mask, g.mask_dt, seq * g.L + lane);
+      const float v = keep ? s * g.scale : -INFINITY;
+      const float mx = nr_wave_max(v);
+      const float e = keep ? __expf(v - mx) : 0.f;
+      const float sum = nr_wave_sum(e);
+      const float p = sum > 0.f ? e / sum : 0.f;
+      if (lane < 32) sm.p[lane] = p;
+      if (lane < g.L) g.probs[seq * g.L + lane] = p;
+    }
+    __syncthreads();
+    for (int k = tid; k < HP; k += 64 * NB) {   // news = Σ_l p_l C_l
+      float acc = 0.f;
+      for (int l = 0; l < g.L; ++l) acc = fmaf(sm.p[l], sm.ct[l][k], acc);
+      g.news[seq * g.ldn + k] = acc;
+    }
+  }
+}
+
+template <int NB, int NP>
+__global__ __launch_bounds__(64 * NB) void cnn_keypool_bwd_kernel(KPArgs g) {
+  constexpr int HP = 32 * NB;
+  __shared__ KPShared<NB> sm;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
+  stage_vectors<NB>(g, sm);
+  f32x16 accw[NB];   // dWq rows 32 w .. + 31, column block kb
+#pragma unroll
+  for (int kb = 0; kb < NB; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accw[kb][r] = 0.f;
+  float dq_acc = 0.f, dbq_acc = 0.f, dcb_acc = 0.f;
+  const int j = 32 * w + c;   // this lane's column of K / dK / dC
+  for (int64_t seq = blockIdx.x; seq < g.nseq; seq += gridDim.x) {
+    __syncthreads();   // the previous title's reads of ct / dk are done
+    stage_tile<NB>(g, seq, sm);
+    if (tid < 32) sm.p[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
+    for (int k = tid; k < HP; k += 64 * NB) sm.dn[k] = k < g.qn ? g.dnews[seq * g.lddn + k] : 0.f;
+    __syncthreads();
+    float kr[16];
+    {
+      f32x16 acc;
+      key_block<NB, NP>(g, sm, w, c, h, acc);
+      const float bj = sm.bq[j];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) kr[r] = tanhf(acc[r] + bj);
+    }
+    if (w == 0) {   // dp_l = dnews · C_l; ds = p (dp - Σ p dp) scale
+      const int l = lane & 31;
+      float dp = 0.f;
+#pragma unroll 4
+      for (int k4 = 0; k4 < HP / 4; ++k4) {
+        const float4 x = *reinterpret_cast<const float4*>(&sm.ct[l][4 * k4]);
+        const float4 d = *reinterpret_cast<const float4*>(&sm.dn[4 * k4]);
+        dp = fmaf(x.x, d.x, dp); dp = fmaf(x.y, d.y, dp);
+        dp = fmaf(x.z, d.z, dp); dp = fmaf(x.w, d.w, dp);
+      }
+      const float pl = lane < 32 ? sm.p[l] : 0.f;
+      const float rs = nr_wave_sum(pl * dp);
+      if (lane < 32) sm.ds[lane] = pl * (dp - rs) * g.scale;
+    }
+    __syncthreads();
+    {
+      const float qj = sm.qv[j];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int tok = crow(r, h);
+        const float dsr = sm.ds[tok];
+        dq_acc = fmaf(dsr, kr[r], dq_acc);
+        const float dkv = dsr * qj * (1.f - kr[r] * kr[r]);
+        dbq_acc += dkv;
+        sm.dk[tok][j] = dkv;
+      }
+    }
+    __syncthreads();
+    {   // dC block w = dK Wq (+ p dnews + dz), gated by ReLU'(C)
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const float* wcol = g.wq + (int64_t)(16 * h) * HP + j;
+#pragma unroll 1
+      for (int ch = 0; ch < NB; ++ch) {
+        float a[16], b[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) b[s] = wcol[(int64_t)(32 * ch + s) * HP];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 x = *reinterpret_cast<const float4*>(&sm.dk[c][32 * ch + 16 * h + 4 * u]);
+          a[4 * u] = x.x; a[4 * u + 1] = x.y; a[4 * u + 2] = x.z; a[4 * u + 3] = x.w;
+        }
+        mfma16<NP>(acc, a, b);
+      }
+      const float dnj = sm.dn[j];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int tok = crow(r, h);
+        float v = fmaf(sm.p[tok], dnj, acc[r]);
+        if (tok < g.L) {
+          if (g.dz && j < g.H) v += g.dz[(seq * g.L + tok) * g.lddz + j];
+          const float gated = sm.ct[tok][j] > 0.f ? v : 0.f;
+          g.dc[(seq * g.L + tok) * g.lddc + j] = gated;
+          dcb_acc += gated;
+        }
+      }
+    }
+    {   // dWq rows of block w += dKᵀ C over the title's tokens
+      float a[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) a[s] = sm.dk[16 * h + s][j];
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb) {
+        float b[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) b[s] = sm.ct[16 * h + s][32 * kb + c];
+        mfma16<NP>(accw[kb], a, b);
+        __builtin_amdgcn_sched_barrier(0);   // keep the next block's fragment reads out of this one
+      }
+    }
+  }
+  // this workgroup's partials (every slot written, also by a workgroup without titles)
+  float* wsb = g.ws + (int64_t)blockIdx.x * g.nws;
+#pragma unroll
+  for (int kb = 0; kb < NB; ++kb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) wsb[(int64_t)(32 * w + crow(r, h)) * HP + 32 * kb + c] = accw[kb][r];
+  dq_acc += __shfl_xor(dq_acc, 32, 64);
+  dbq_acc += __shfl_xor(dbq_acc, 32, 64);
+  dcb_acc += __shfl_xor(dcb_acc, 32, 64);
+  if (h == 0) {
+    wsb[(int64_t)HP * HP + j] = dbq_acc;
+    wsb[(int64_t)HP * HP + HP + j] = dq_acc;
+    wsb[(int64_t)HP * HP + 2 * HP + j] = dcb_acc;
+  }
+}
+
+// outputs: dwq [Hp][Hp], dbq [Hp], dq [qn], dconv_b [H] (stored), each the sum of the partials.  A block
+// takes 64 columns; its four waves sum every fourth partial, then wave 0 adds the four in order
+// (deterministic)
+__global__ __launch_bounds__(256) void cnn_keypool_reduce_kernel(const float* __restrict__ ws, int64_t nws, int G,
+                                                                 int HP, int qn, int H, float* __restrict__ dwq,
+                                                                 float* __restrict__ dbq, float* __restrict__ dq,
+                                                                 float* __restrict__ dcb) {
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t ic = i < nws ? i : nws - 1;
+  float s = 0.f;
+  int gi = wv;
+  for (; gi + 28 < G; gi += 32) {   // eight loads in flight
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ws[(int64_t)(gi + 4 * u) * nws + ic];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; gi < G; gi += 4) s += ws[(int64_t)gi * nws + ic];
+  part[wv][lane] = s;
+  __syncthreads();
+  if (wv != 0 || i >= nws) return;
+  s = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+  const int64_t hh = (int64_t)HP * HP;
+  if (i < hh) {
+    dwq[i] = s;
+  } else if (i < hh + HP) {
+    dbq[i - hh] = s;
+  } else if (i < hh + 2 * HP) {
+    if (i - hh - HP < qn) dq[i - hh - HP] = s;
+  } else if (i - hh - 2 * HP < H) {
+    dcb[i - hh - 2 * HP] = s;
+  }
+}
+
+int g_cus = 0;
+int cu_count() {
+  if (g_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      g_cus = n;
+    if (g_cus <= 0) g_cus = 256;
+  }
+  return g_cus;
+}
+
+constexpr int KP_WG_PER_CU = 2;
+
+int64_t kp_groups(int64_t nseq) {
+  const int64_t cap = (int64_t)cu_count() * KP_WG_PER_CU;
+  return nseq < cap ? (nseq > 0 ? nseq : 1) : cap;
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+#define NR_KP_LAUNCH(KERN)                                                                                  \
+  template <int NB>                                                                                         \
+  int launch_##KERN(int np, const KPArgs& g, int64_t grid, hipStream_t s) {                               \
+    if (np == 0) hipLaunchKernelGGL((KERN<NB, 0>), dim3((unsigned)grid), dim3(64 * NB), 0, s, g);         \
+    else if (np == 1) hipLaunchKernelGGL((KERN<NB, 1>), dim3((unsigned)grid), dim3(64 * NB), 0, s, g);    \
+    else hipLaunchKernelGGL((KERN<NB, 3>), dim3((unsigned)grid), dim3(64 * NB), 0, s, g);                 \
+    NR_LAUNCH_CHECK();                                                                                      \
+    return NR_OK;                                                                                           \
+  }
+NR_KP_LAUNCH(cnn_keypool_fwd_kernel)
+NR_KP_LAUNCH(cnn_keypool_bwd_kernel)
+#undef NR_KP_LAUNCH
+
+int np_of(int prec) { return prec == NR_GEMM_F32 ? 0 : prec == NR_GEMM_BF16 ? 1 : 3; }
+
+}  // namespace
+
+extern "C" int64_t nr_cnn_keypool_workspace(int64_t nseq, int32_t Hp) {
+  if (nseq < 0 || Hp < 32 || Hp > 160 || (Hp & 31)) return -1;
+  return kp_groups(nseq) * ((int64_t)Hp * Hp + 3 * (int64_t)Hp);
+}
+
+extern "C" int nr_cnn_keypool_fwd(const float* C, int64_t ldc, const float* wq, const float* bq, const float* q,
+                                  int32_t qn, const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L,
+                                  int32_t Hp, float scale, int32_t prec, float* news, int64_t ldn, float* probs,
+                                  hipStream_t stream) {
+  if (Hp < 32 || Hp > 160 || (Hp & 31) || L < 1 || L > 32 || qn < 1 || qn > Hp || nseq < 0 || ldc < Hp ||
+      (ldc & 3) || ldn < Hp)
+    return NR_EINVAL(0);
+  if (!C || !wq || !bq || !q || !mask || !news || !probs) return NR_EINVAL(1);
+  if (!al16(C) || !al16(wq)) return NR_EINVAL(2);
+  if (nseq == 0) return NR_OK;
+  KPArgs g{};
+  g.c = C; g.ldc = ldc; g.wq = wq; g.bq = bq; g.q = q; g.qn = qn; g.mask = mask; g.mask_dt = mask_dtype;
+  g.nseq = nseq; g.L = L; g.scale = scale; g.news = news; g.ldn = ldn; g.probs = probs; g.H = qn;
+  const int64_t grid = kp_groups(nseq);
+  const int np = np_of(prec);
+  switch (Hp / 32) {
+    case 1: return launch_cnn_keypool_fwd_kernel<1>(np, g, grid, stream);
+    case 2: return launch_cnn_keypool_fwd_kernel<2>(np, g, grid, stream);
+    case 3: return launch_cnn_keypool_fwd_kernel<3>(np, g, grid, stream);
+    case 4: return launch_cnn_keypool_fwd_kernel<4>(np, g, grid, stream);
+    default: return launch_cnn_keypool_fwd_kernel<5>(np, g, grid, stream);
+  }
+}
+
+extern "C" int nr_cnn_keypool_bwd(const float* C, int64_t ldc, const float* wq, const float* bq, const float* q,
+                                  int32_t qn, int64_t nseq, int32_t L, int32_t Hp, int32_t H, float scale,
+                                  int32_t prec, const float* probs, const float* dnews, int64_t lddn, const float* dz,
+                                  int64_t lddz, float* dc, int64_t lddc, float* dwq, float* dbq, float* dq,
+                                  float* dconv_b, float* ws, int64_t ws_floats, hipStream_t stream) {
+  if (Hp < 32 || Hp > 160 || (Hp & 31) || L < 1 || L > 32 || qn < 1 || qn > Hp || H < 1 || H > Hp || nseq < 0 ||
+      ldc < Hp || (ldc & 3) || lddn < qn || lddc < Hp || (dz && lddz < H))
+    return NR_EINVAL(0);
+  if (!C || !wq || !bq || !q || !probs || !dnews || !dc || !dwq || !dbq || !dq || !dconv_b || !ws) return NR_EINVAL(1);
+  if (!al16(C) || !al16(wq)) return NR_EINVAL(2);
+  const int64_t nws = (int64_t)Hp * Hp + 3 * (int64_t)Hp;
+  const int64_t grid = kp_groups(nseq);
+  if (ws_floats < grid * nws) return NR_EINVAL(3);
+  KPArgs g{};
+  g.c = C; g.ldc = ldc; g.wq = wq; g.bq = bq; g.q = q; g.qn = qn;
+  g.nseq = nseq; g.L = L; g.scale = scale; g.probs = const_cast<float*>(probs);
+  g.dnews = dnews; g.lddn = lddn; g.dz = dz; g.lddz = lddz; g.H = H; g.dc = dc; g.lddc = lddc;
+  g.ws = ws; g.nws = nws;
+  const int np = np_of(prec);
+  int rc;
+  switch (Hp / 32) {
+    case 1: rc = launch_cnn_keypool_bwd_kernel<1>(np, g, grid, stream); break;
+    case 2: rc = launch_cnn_keypool_bwd_kernel<2>(np, g, grid, stream); break;
+    case 3: rc = launch_cnn_keypool_bwd_kernel<3>(np, g, grid, stream); break;
+    case 4: rc = launch_cnn_keypool_bwd_kernel<4>(np, g, grid, stream); break;
+    default: rc = launch_cnn_keypool_bwd_kernel<5>(np, g, grid, stream); break;
+  }
+  if (rc != NR_OK) return rc;
+  hipLaunchKernelGGL(cnn_keypool_reduce_kernel, dim3((unsigned)((nws + 63) / 64)), dim3(256), 0, stream, ws, nws,
+                     (int)grid, Hp, qn, H, dwq, dbq, dq, dconv_b);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}

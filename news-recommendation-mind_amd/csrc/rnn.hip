@@ -244,6 +244,16 @@ __global__ __launch_bounds__(((G * H + 63) / 64) * 64) void rnn_fwd_reg_kernel(R
   __syncthreads();
   const int len = seq_len(g, b, &red);
   if (len == 0 && tid < H) g.hout[b * g.ldho + tid] = h[tid];   // all-zero mask row: h0
+  // the input projections of step t + 1 are loaded during step t: the load latency (L2 / HBM, ~1 us)
+  // otherwise sits on the sequential critical path of every step
+  float xn[G];
+  auto load_x = [&](int t) {
+    const int tt = g.reverse ? g.N - 1 - t : t;
+    const float* xs = g.gx + (b * g.N + tt) * g.ldgx + tid;
+#pragma unroll
+    for (int i = 0; i < G; ++i) xn[i] = xs[i * H];
+  };
+  if (tid < H && len > 0) load_x(0);
   for (int t = 0; t < g.N; ++t) {
     const int tt = g.reverse ? g.N - 1 - t : t;
     const int64_t row = b * g.N + tt;
@@ -255,6 +265,10 @@ __global__ __launch_bounds__(((G * H + 63) / 64) * 64) void rnn_fwd_reg_kernel(R
       }
       continue;
     }
+    float xc[G];
+#pragma unroll
+    for (int i = 0; i < G; ++i) xc[i] = xn[i];
+    if (tid < H && t + 1 < len) load_x(t + 1);
     if (tid < GH) {
       float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll
@@ -266,31 +280,39 @@ __global__ __launch_bounds__(((G * H + 63) / 64) * 64) void rnn_fwd_reg_kernel(R
         if (k + 3 < KR) a3 = fmaf(w[k + 3], hv.w, a3);
         if ((k & 15) == 12) __builtin_amdgcn_sched_barrier(0);   // keep the h reads from all hoisting
       }
-#pragma unroll 10
-      for (int k = KR; k < H; ++k) a0 = fmaf(wl[(k - KR) * GH + tid], h[k], a0);
+      if constexpr (KL > 0) {
+        static_assert(KR % 4 == 0, "the LDS part of a row starts float4-aligned in h");
+#pragma unroll 4
+        for (int k = KR; k < H; k += 4) {   // h read as float4 (padded with zeros past H)
+          const float4 hv = *reinterpret_cast<const float4*>(&h[k]);
+          a0 = fmaf(wl[(k - KR) * GH + tid], hv.x, a0);
+          if (k + 1 < H) a1 = fmaf(wl[(k + 1 - KR) * GH + tid], hv.y, a1);
+          if (k + 2 < H) a2 = fmaf(wl[(k + 2 - KR) * GH + tid], hv.z, a2);
+          if (k + 3 < H) a3 = fmaf(wl[(k + 3 - KR) * GH + tid], hv.w, a3);
+        }
+      }
       gh[tid] = bias + ((a0 + a1) + (a2 + a3));
     }
     __syncthreads();
     float hn = 0.f, cn = 0.f;
     if (tid < H) {
       const int u = tid;
-      const float* xs = g.gx + row * g.ldgx;
       float* gs = g.gates + row * 4 * H;
       g.hprev[row * H + u] = h[u];
       if (G == 4) {
-        const float ig = sigm(xs[u] + gh[u]);
-        const float fg = sigm(xs[H + u] + gh[H + u]);
-        const float gg = tanhf(xs[2 * H + u] + gh[2 * H + u]);
-        const float og = sigm(xs[3 * H + u] + gh[3 * H + u]);
+        const float ig = sigm(xc[0] + gh[u]);
+        const float fg = sigm(xc[1] + gh[H + u]);
+        const float gg = tanhf(xc[2] + gh[2 * H + u]);
+        const float og = sigm(xc[3] + gh[3 * H + u]);
         const float cc = fmaf(fg, c[u], ig * gg);
         g.cprev[row * H + u] = c[u];
         gs[u] = ig; gs[H + u] = fg; gs[2 * H + u] = gg; gs[3 * H + u] = og;
         cn = cc;
         hn = og * tanhf(cc);
       } else {
-        const float rg = sigm(xs[u] + gh[u]);
-        const float zg = sigm(xs[H + u] + gh[H + u]);
-        const float ng = tanhf(fmaf(rg, gh[2 * H + u], xs[2 * H + u]));
+        const float rg = sigm(xc[0] + gh[u]);
+        const float zg = sigm(xc[1] + gh[H + u]);
+        const float ng = tanhf(fmaf(rg, gh[2 * H + u], xc[2 % G]));
         gs[u] = rg; gs[H + u] = zg; gs[2 * H + u] = ng; gs[3 * H + u] = gh[2 * H + u];
         hn = fmaf(zg, h[u] - ng, ng);
       }
@@ -337,17 +359,32 @@ __global__ __launch_bounds__(((G * H + 63) / 64) * 64) void rnn_bwd_reg_kernel(R
       if (g.dgh) g.dgh[row * g.lddg + r] = 0.f;
     }
   }
+  // the saved gates (and c_{t-1} / h_{t-1}) of step t - 1 are loaded during step t (off the
+  // sequential critical path)
+  float gn[4], pn = 0.f;
+  auto load_g = [&](int t) {
+    const int tt = g.reverse ? g.N - 1 - t : t;
+    const int64_t row = b * g.N + tt;
+    const float* gs = g.gates + row * 4 * H + tid;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gn[i] = gs[i * H];
+    pn = G == 4 ? g.cprev[row * H + tid] : g.hprev[row * H + tid];
+  };
+  if (tid < H && len > 0) load_g(len - 1);
   for (int t = len - 1; t >= 0; --t) {
     const int tt = g.reverse ? g.N - 1 - t : t;
     const int64_t row = b * g.N + tt;
+    float gc[4], pc = pn;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gc[i] = gn[i];
+    if (tid < H && t > 0) load_g(t - 1);
     if (tid < H) {
       const int u = tid;
-      const float* gs = g.gates + row * 4 * H;
       float* dgi = g.dgi + row * g.lddg;
       float* dgh = g.dgh ? g.dgh + row * g.lddg : nullptr;
       if (G == 4) {
-        const float ig = gs[u], fg = gs[H + u], gg = gs[2 * H + u], og = gs[3 * H + u];
-        const float cp = g.cprev[row * H + u];
+        const float ig = gc[0], fg = gc[1], gg = gc[2], og = gc[3];
+        const float cp = pc;
         const float cc = fmaf(fg, cp, ig * gg);
         const float tc = tanhf(cc);
         const float dcc = dc[u] + dh[u] * og * (1.f - tc * tc);
@@ -360,8 +397,8 @@ __global__ __launch_bounds__(((G * H + 63) / 64) * 64) void rnn_bwd_reg_kernel(R
         dg[u] = di; dg[H + u] = df; dg[2 * H + u] = dgg; dg[3 * H + u] = dog;
         dc[u] = dcc * fg;
       } else {
-        const float rg = gs[u], zg = gs[H + u], ng = gs[2 * H + u], ghn = gs[3 * H + u];
-        const float hp = g.hprev[row * H + u];
+        const float rg = gc[0], zg = gc[1], ng = gc[2], ghn = gc[3];
+        const float hp = pc;
         const float dn = dh[u] * (1.f - zg) * (1.f - ng * ng);
         const float dz = dh[u] * (hp - ng) * zg * (1.f - zg);
         const float dr = dn * ghn * rg * (1.f - rg);

@@ -71,6 +71,12 @@ _SIGS = {
                                   c_i64, c_ptr],
     "nr_cnn_pack_weights": [c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
     "nr_cnn_unpack_grads": [c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
+    "nr_cnn_keypool_fwd": [c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i32, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_i32,
+                           c_ptr, c_i64, c_ptr, c_ptr],
+    "nr_cnn_keypool_workspace": [c_i64, c_i32],
+    "nr_cnn_keypool_bwd": [c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_f32, c_i32,
+                           c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
+                           c_ptr],
     "nr_conv3_rows_fwd": [c_ptr, c_i64, c_i32, c_i32, c_ptr, c_i64, c_i32, c_ptr, c_i32, c_ptr, c_i64, c_ptr],
     "nr_mha_attn_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
                         c_f32, c_ptr, c_i64, c_ptr],
@@ -136,7 +142,7 @@ _SIGS = {
 
 _RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_unique_rows_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64,
              "nr_colsum_workspace": c_i64, "nr_score_nll_workspace": c_i64,
-             "nr_gemm_splitk_workspace": c_i64,
+             "nr_gemm_splitk_workspace": c_i64, "nr_cnn_keypool_workspace": c_i64,
              "nr_build_hash": ctypes.c_char_p}
 
 # enum nr_batch_flags / nr_metric_flags

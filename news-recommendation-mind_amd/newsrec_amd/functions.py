@@ -139,6 +139,11 @@ DEDUP_ROWS = True
 # Training forward saves the attention output; the backward runs split (False: the fused backward
 # that recomputes the attention).
 SPLIT_BWD = True
+# CNN word attention (tanh key projection + learned-query pooling) fused per title, forward and
+# backward (nr_cnn_keypool_*; False: the key GEMM + pooling kernels the parity tests compare with).
+FUSED_KEYPOOL = True
+
+
 class _TableGradHook:
     """Optional callback ``hook(table_param, dtable) -> bool`` run inside a news-tower backward
     as soon as the dense word-table gradient exists (before the weight-gradient GEMMs).  When it
@@ -483,14 +488,21 @@ class CNNNewsRowsFn(torch.autograd.Function):
         PROBE.add("conv_fwd", ev0, PROBE.record(), ur)
         C = _empty(T, Hp, table)
         K.conv3_rows_fwd(P, Hp, H, ur.inv, seq_len, conv_b, C, relu=True)
-        Kq = _empty(T, Hp, table)
-        K.gemm(T, Hp, Hp, K.operand(C, L.KCONTIG), K.operand(wq, L.KCONTIG), Kq, bias=bq, epilogue=L.EPI_STORE_TANH)
-        # pooling over the padded width: C and Kq are exactly zero past H, and so is the padded query
         news = _empty(n, Hp, table)
         probs = torch.empty(T, device=table.device)
-        K.seq_pool_fwd(C, query, mask, n, seq_len, Hp, news, probs, key=Kq, qn=H)
-        ctx.save_for_backward(table, ids, mask, w3t, wq, query, C, Kq, probs)
-        ctx.cfg = (seq_len, pad_row, H)
+        fused = FUSED_KEYPOOL and K.cnn_keypool_supported(Hp, seq_len)
+        if fused:
+            # key projection + tanh + pooling per title: the key matrix never reaches HBM
+            K.cnn_keypool_fwd(C, wq, bq, query, mask, n, seq_len, news, probs, qn=H, prec=ctx.prec)
+            Kq = None
+        else:
+            Kq = _empty(T, Hp, table)
+            K.gemm(T, Hp, Hp, K.operand(C, L.KCONTIG), K.operand(wq, L.KCONTIG), Kq, bias=bq,
+                   epilogue=L.EPI_STORE_TANH)
+            # pooling over the padded width: C and Kq are exactly zero past H, and so is the padded query
+            K.seq_pool_fwd(C, query, mask, n, seq_len, Hp, news, probs, key=Kq, qn=H)
+        ctx.save_for_backward(table, ids, mask, w3t, wq, bq, query, C, Kq, probs)
+        ctx.cfg = (seq_len, pad_row, H, fused)
         ctx.table_ref = table
         ctx.ur = ur
         return news[:, :H], C[:, :H]
@@ -498,8 +510,8 @@ class CNNNewsRowsFn(torch.autograd.Function):
     @staticmethod
     @_gemm_backward
     def backward(ctx, dnews, dC_out):
-        table, ids, mask, w3t, wq, query, C, Kq, probs = ctx.saved_tensors
-        seq_len, pad_row, H = ctx.cfg
+        table, ids, mask, w3t, wq, bq, query, C, Kq, probs = ctx.saved_tensors
+        seq_len, pad_row, H, fused = ctx.cfg
         ur = ctx.ur
         T = ids.numel()
         n = T // seq_len
@@ -509,21 +521,28 @@ class CNNNewsRowsFn(torch.autograd.Function):
         Hp = w3t.shape[0] // 3
         dev = table.device
         dC = _empty(T, Hp, table)
-        dKq = _empty(T, Hp, table)
         dwq, dbq, dconv_b, dw3t, dq = _zeros_views(dev, (Hp, Hp), (Hp,), (H,), (3 * Hp, E), (H,))
-        # dC = p dnews (+ dC_out), dKq = ds q (1 - Kq²) over the padded width: exactly zero past H
-        # (dnews and the query count as zero there)
-        dz = torch.nn.functional.pad(dC_out, (0, Hp - H)) if dC_out is not None else None
         if dnews.stride(-1) != 1:
             dnews = dnews.contiguous()
-        K.seq_pool_bwd(C, query, mask, n, seq_len, Hp, probs, dnews, dC, dq, key=Kq, dk=dKq, key_tanh=True, dz=dz,
-                       qn=H)
-        # key projection: dWq = dKqᵀ C, dbq = colsum(dKq); dC = ReLU'(C) ⊙ (dC + dKq Wq) (padded
-        # columns of C are zero, so the gate also zeroes dC's padding)
-        _proj_wgrad(dKq, K.operand(C, L.MNCONTIG), dwq, dbq, T)
-        K.gemm(T, Hp, Hp, K.operand(dKq, L.KCONTIG), K.operand(wq, L.MNCONTIG), dC, epilogue=L.EPI_ACCUM_GATE,
-               c_rows=K.aux_operand(C))
-        K.colsum(dC, T, H, dconv_b)
+        if fused:
+            # one pass per title: key recomputed, pooling / tanh / key-projection backward, ReLU gate,
+            # dWq / dbq / dq / dconv_b summed over per-workgroup partials
+            dz = dC_out if dC_out is None or dC_out.stride(-1) == 1 else dC_out.contiguous()
+            K.cnn_keypool_bwd(C, wq, bq, query, n, seq_len, H, probs, dnews, dC, dwq, dbq, dq, dconv_b, dz=dz,
+                              prec=ctx.prec)
+        else:
+            dKq = _empty(T, Hp, table)
+            # dC = p dnews (+ dC_out), dKq = ds q (1 - Kq²) over the padded width: exactly zero past H
+            # (dnews and the query count as zero there)
+            dz = torch.nn.functional.pad(dC_out, (0, Hp - H)) if dC_out is not None else None
+            K.seq_pool_bwd(C, query, mask, n, seq_len, Hp, probs, dnews, dC, dq, key=Kq, dk=dKq, key_tanh=True,
+                           dz=dz, qn=H)
+            # key projection: dWq = dKqᵀ C, dbq = colsum(dKq); dC = ReLU'(C) ⊙ (dC + dKq Wq) (padded
+            # columns of C are zero, so the gate also zeroes dC's padding)
+            _proj_wgrad(dKq, K.operand(C, L.MNCONTIG), dwq, dbq, T)
+            K.gemm(T, Hp, Hp, K.operand(dKq, L.KCONTIG), K.operand(wq, L.MNCONTIG), dC, epilogue=L.EPI_ACCUM_GATE,
+                   c_rows=K.aux_operand(C))
+            K.colsum(dC, T, H, dconv_b)
         S = _empty(ur.cap, 3 * Hp, table)
         ur.segment_sum_conv3(dC, S, Hp, seq_len)
         dtable = None

@@ -228,6 +228,57 @@ def conv3_rows_fwd(P, tap_width, H, inv, seq_len, bias, out, relu=True):
            int(relu), L.ptr(out), out.stride(0), L.stream_ptr(P))
 
 
+def cnn_keypool_supported(Hp, seq_len):
+    return Hp % 32 == 0 and 32 <= Hp <= 160 and 1 <= seq_len <= 32
+
+
+def cnn_keypool_fwd(C, wq, bq, query, mask, nseq, seq_len, news, probs, qn, prec=None):
+    """nr_cnn_keypool_fwd: K = tanh(C wqᵀ + bq), p = XSoftmax(q·K / sqrt(qn), mask), news = Σ p C per
+    title.  C [nseq*L, Hp] (zero past qn), wq [Hp, Hp], bq [Hp] padded, query [>= qn]; news [nseq, >= Hp]."""
+    _f32(C, wq, bq, query, news, probs)
+    Hp = wq.shape[0]
+    if not cnn_keypool_supported(Hp, seq_len):
+        raise L.HipError("cnn_keypool: Hp %% 32 == 0, Hp <= 160, L <= 32 required (Hp=%d, L=%d)" % (Hp, seq_len))
+    _al(C, "cnn_keypool C")
+    _rows_ok(C, nseq * seq_len, Hp, "cnn_keypool C")
+    if not wq.is_contiguous() or wq.shape != (Hp, Hp) or bq.numel() < Hp or query.numel() < qn:
+        raise L.HipError("cnn_keypool: wq [Hp, Hp] contiguous, bq [Hp], query [qn] required")
+    _rows_ok(news, nseq, Hp, "cnn_keypool news")
+    if probs.numel() < nseq * seq_len:
+        raise L.HipError("cnn_keypool: probs needs nseq*L floats")
+    mp, mdt = mask_arg(mask, nseq * seq_len)
+    prec = get_gemm_precision() if prec is None else prec
+    L.call("nr_cnn_keypool_fwd", L.ptr(C), C.stride(0), L.ptr(wq), L.ptr(bq), L.ptr(query), qn, mp, mdt, nseq, seq_len,
+           Hp, 1.0 / float(qn) ** 0.5, prec, L.ptr(news), news.stride(0), L.ptr(probs), L.stream_ptr(C))
+
+
+def cnn_keypool_bwd(C, wq, bq, query, nseq, seq_len, H, probs, dnews, dc, dwq, dbq, dq, dconv_b, dz=None, prec=None):
+    """Backward of cnn_keypool_fwd: dc [T, >= Hp] = ReLU'(C) (p dnews + dK wq + dz); dwq [Hp, Hp], dbq [Hp],
+    dq [qn], dconv_b [H] are STORED.  dnews [nseq, >= qn] (row stride any), dz [T, >= H] optional."""
+    _f32(C, wq, bq, query, probs, dnews, dc, dwq, dbq, dq, dconv_b, dz)
+    Hp = wq.shape[0]
+    qn = dq.numel()
+    if not cnn_keypool_supported(Hp, seq_len):
+        raise L.HipError("cnn_keypool: Hp %% 32 == 0, Hp <= 160, L <= 32 required (Hp=%d, L=%d)" % (Hp, seq_len))
+    _al(C, "cnn_keypool C")
+    _rows_ok(C, nseq * seq_len, Hp, "cnn_keypool C")
+    _rows_ok(dc, nseq * seq_len, Hp, "cnn_keypool dc")
+    if not (dwq.is_contiguous() and dwq.numel() == Hp * Hp and dbq.numel() >= Hp and dconv_b.numel() >= H
+            and query.numel() >= qn and wq.is_contiguous()):
+        raise L.HipError("cnn_keypool_bwd: dwq [Hp, Hp] contiguous, dbq [Hp], dconv_b [H] required")
+    if dnews.stride(-1) != 1 or dnews.shape[0] < nseq:
+        raise L.HipError("cnn_keypool_bwd: dnews rows must be unit-stride")
+    if dz is not None and (dz.stride(-1) != 1 or dz.shape[0] < nseq * seq_len or dz.shape[1] < H):
+        raise L.HipError("cnn_keypool_bwd: dz [T, >= H] with unit column stride required")
+    nws = int(L.load().nr_cnn_keypool_workspace(nseq, Hp))
+    ws = torch.empty(max(nws, 1), device=C.device)
+    prec = get_gemm_precision() if prec is None else prec
+    L.call("nr_cnn_keypool_bwd", L.ptr(C), C.stride(0), L.ptr(wq), L.ptr(bq), L.ptr(query), qn, nseq, seq_len, Hp, H,
+           1.0 / float(qn) ** 0.5, prec, L.ptr(probs), L.ptr(dnews), dnews.stride(0), L.ptr(dz),
+           dz.stride(0) if dz is not None else 0, L.ptr(dc), dc.stride(0), L.ptr(dwq), L.ptr(dbq), L.ptr(dq),
+           L.ptr(dconv_b), L.ptr(ws), ws.numel(), L.stream_ptr(C))
+
+
 def operand(t, layout, rows=None, mapping=L.ROWS_PLAIN, seq_len=1, seg=1, ld=None):
     """Describe a stored matrix ``t`` (2-D, row-major, ld % 4 == 0, 16-B aligned)."""
     _f32(t)
