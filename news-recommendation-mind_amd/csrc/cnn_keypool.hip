@@ -54,21 +54,8 @@ struct KPShared {
   float dn[HP], qv[HP], bq[HP];
 };
 
-template <int NB>
-__device__ __forceinline__ void stage_tile(const KPArgs& g, int64_t seq, KPShared<NB>& sm) {
-  constexpr int Q4 = 8 * NB;   // float4 per row
-  const int nt = 64 * NB;
-  for (int i = threadIdx.x; i < 32 * Q4; i += nt) {
-    const int r = i / Q4, c4 = i - r * Q4;
-    float4 v = *reinterpret_cast<const float4*>(g.c + (seq * g.L + (r < g.L ? r : 0)) * g.ldc + 4 * c4);
-    if (r >= g.L) v = make_float4(0.f, 0.f, 0.f, 0.f);
-    *reinterpret_cast<float4*>(&sm.ct[r][4 * c4]) = v;
-  }
-}
-
-// acc = C Wqᵀ for output columns 32 w .. 32 w + 31 (rows = the title's 32 token slots).  B (Wq rows)
-// either from registers held across titles (bw, the forward) or from L2 one chunk ahead of its
-// MFMAs (the backward, whose registers hold the dWq accumulators).
+// acc = C Wqᵀ for output columns 32 w .. 32 w + 31 (rows = the title's 32 token slots); B (Wq rows)
+// from L2, one chunk ahead of its MFMAs.
 template <int NB>
 __device__ __forceinline__ void load_wrow(const KPArgs& g, int w, int c, int h, int ch, float (&b)[16]) {
   constexpr int HP = 32 * NB;
@@ -86,19 +73,6 @@ __device__ __forceinline__ void load_crow(const KPShared<NB>& sm, int c, int h, 
   for (int u = 0; u < 4; ++u) {
     const float4 x = *reinterpret_cast<const float4*>(&sm.ct[c][32 * ch + 16 * h + 4 * u]);
     a[4 * u] = x.x; a[4 * u + 1] = x.y; a[4 * u + 2] = x.z; a[4 * u + 3] = x.w;
-  }
-}
-
-template <int NB, int NP>
-__device__ __forceinline__ void key_block_regs(const KPShared<NB>& sm, int c, int h, const float (&bw)[NB][16],
-                                               f32x16& acc) {
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-  for (int ch = 0; ch < NB; ++ch) {
-    float a[16];
-    load_crow<NB>(sm, c, h, ch, a);
-    mfma16<NP>(acc, a, bw[ch]);
   }
 }
 
@@ -134,16 +108,32 @@ __global__ __launch_bounds__(64 * NB) void cnn_keypool_fwd_kernel(KPArgs g) {
   __shared__ KPShared<NB> sm;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
   stage_vectors<NB>(g, sm);
-  float bw[NB][16];   // this wave's Wq rows, every chunk: loaded once, used by every title
+  constexpr int Q4 = 8 * NB;
+  constexpr int TPF = (32 * Q4 + 64 * NB - 1) / (64 * NB);   // C-tile float4 per thread
+  float4 cn[TPF];   // the next title's C tile travels in registers while this one computes
+  auto fetch = [&](int64_t seq) {
 #pragma unroll
-  for (int ch = 0; ch < NB; ++ch) load_wrow<NB>(g, w, c, h, ch, bw[ch]);
+    for (int u = 0; u < TPF; ++u) {
+      const int i = tid + u * 64 * NB;
+      const int r = i / Q4, c4 = i - r * Q4;
+      const bool ok = i < 32 * Q4 && r < g.L;
+      cn[u] = *reinterpret_cast<const float4*>(g.c + (seq * g.L + (ok ? r : 0)) * g.ldc + 4 * (ok ? c4 : 0));
+      if (!ok) cn[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  if ((int64_t)blockIdx.x < g.nseq) fetch(blockIdx.x);
   for (int64_t seq = blockIdx.x; seq < g.nseq; seq += gridDim.x) {
     __syncthreads();   // the previous title's pooling reads of ct are done
-    stage_tile<NB>(g, seq, sm);
+#pragma unroll
+    for (int u = 0; u < TPF; ++u) {
+      const int i = tid + u * 64 * NB;
+      if (i < 32 * Q4) *reinterpret_cast<float4*>(&sm.ct[i / Q4][4 * (i % Q4)]) = cn[u];
+    }
     __syncthreads();
+    if (seq + gridDim.x < g.nseq) fetch(seq + gridDim.x);
     {
       f32x16 acc;
-      key_block_regs<NB, NP>(sm, c, h, bw, acc);
+      key_block<NB, NP>(g, sm, w, c, h, acc);
       const int j = 32 * w + c;
       const float bj = sm.bq[j], qj = sm.qv[j];
 #pragma unroll
@@ -176,49 +166,99 @@ __global__ __launch_bounds__(64 * NB) void cnn_keypool_fwd_kernel(KPArgs g) {
   }
 }
 
+// Backward: KP_BW = 8 waves (one workgroup per CU, two waves per SIMD).  Waves 0 .. NB-1 are COLUMN
+// waves (key block, dK block and dC block w); the other 8 - NB are dWq waves, each owning a fixed
+// round-robin share of dWq's NB² 32 x 32 blocks, accumulated across the workgroup's titles in LDS
+// ([block][register][lane]: conflict-free, 100 KB at NB = 5 -- in registers they would cost every
+// wave 144 VGPRs and spill) and computed while the column waves run the dC products; the first dWq
+// wave also forms dp / ds.  With NB = 5 each SIMD carries 18-20
+// fragment products per title (five column waves on four SIMDs alone would leave one SIMD with
+// twice the others' work).
+constexpr int KP_BW = 8;
+
+template <int NB>
+constexpr int kp_maxb() { return (NB * NB + (KP_BW - NB) - 1) / (KP_BW - NB); }
+
 template <int NB, int NP>
-__global__ __launch_bounds__(64 * NB) void cnn_keypool_bwd_kernel(KPArgs g) {
+__global__ __launch_bounds__(64 * KP_BW) void cnn_keypool_bwd_kernel(KPArgs g) {
+  static_assert(NB >= 1 && NB < KP_BW, "column waves + at least one dWq wave");
   constexpr int HP = 32 * NB;
+  constexpr int ND = KP_BW - NB;        // dWq waves
+  constexpr int MAXB = kp_maxb<NB>();   // dWq blocks per dWq wave
+  constexpr int Q4 = 8 * NB;            // float4 per C row
+  constexpr int TPF = (32 * Q4 + 64 * KP_BW - 1) / (64 * KP_BW);   // C-tile float4 per thread
   __shared__ KPShared<NB> sm;
+  __shared__ float wacc[NB * NB][16][64];   // dWq block b: rows 32 jb + crow(r, h), columns 32 kb + c
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
-  stage_vectors<NB>(g, sm);
-  f32x16 accw[NB];   // dWq rows 32 w .. + 31, column block kb
-#pragma unroll
-  for (int kb = 0; kb < NB; ++kb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) accw[kb][r] = 0.f;
+  const bool colw = w < NB;
+  const int d = w - NB;                 // dWq wave index (when !colw)
+  for (int k = tid; k < HP; k += 64 * KP_BW) {
+    sm.qv[k] = k < g.qn ? g.q[k] : 0.f;
+    sm.bq[k] = g.bq[k];
+  }
+  for (int i = tid; i < NB * NB * 16 * 64; i += 64 * KP_BW) (&wacc[0][0][0])[i] = 0.f;
   float dq_acc = 0.f, dbq_acc = 0.f, dcb_acc = 0.f;
-  const int j = 32 * w + c;   // this lane's column of K / dK / dC
+  const int j = 32 * (colw ? w : 0) + c;   // a column wave lane's column of K / dK / dC
+  // a column wave's Wq column fragments (the dC products: 32 w + c, every chunk) for every title; the
+  // row fragments of the key products come from L2 one chunk ahead (both sets would spill)
+  constexpr bool WC_REGS = NP != 3;   // bf16x6: the operand split needs those registers (it would spill)
+  float wc[WC_REGS ? NB : 1][16];
+  if (WC_REGS && colw) {
+#pragma unroll
+    for (int ch = 0; ch < NB; ++ch)
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) wc[ch][s2] = g.wq[(int64_t)(32 * ch + 16 * h + s2) * HP + j];
+  }
+  // the next title's C tile / probabilities / dnews travel in registers while this one computes
+  float4 cn[TPF];
+  float pn = 0.f, dnn = 0.f;
+  auto fetch = [&](int64_t seq) {
+#pragma unroll
+    for (int u = 0; u < TPF; ++u) {
+      const int i = tid + u * 64 * KP_BW;
+      const int r = i / Q4, c4 = i - r * Q4;
+      const bool ok = i < 32 * Q4 && r < g.L;
+      cn[u] = *reinterpret_cast<const float4*>(g.c + (seq * g.L + (ok ? r : 0)) * g.ldc + 4 * (ok ? c4 : 0));
+      if (!ok) cn[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (tid < 32) pn = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
+    if (tid >= 64 && tid < 64 + HP) dnn = tid - 64 < g.qn ? g.dnews[seq * g.lddn + tid - 64] : 0.f;
+  };
+  if ((int64_t)blockIdx.x < g.nseq) fetch(blockIdx.x);
   for (int64_t seq = blockIdx.x; seq < g.nseq; seq += gridDim.x) {
-    __syncthreads();   // the previous title's reads of ct / dk are done
-    stage_tile<NB>(g, seq, sm);
-    if (tid < 32) sm.p[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
-    for (int k = tid; k < HP; k += 64 * NB) sm.dn[k] = k < g.qn ? g.dnews[seq * g.lddn + k] : 0.f;
+    __syncthreads();   // the previous title's reads of ct / dk / p / dn are done
+#pragma unroll
+    for (int u = 0; u < TPF; ++u) {
+      const int i = tid + u * 64 * KP_BW;
+      if (i < 32 * Q4) *reinterpret_cast<float4*>(&sm.ct[i / Q4][4 * (i % Q4)]) = cn[u];
+    }
+    if (tid < 32) sm.p[tid] = pn;
+    if (tid >= 64 && tid < 64 + HP) sm.dn[tid - 64] = dnn;
     __syncthreads();
+    if (seq + gridDim.x < g.nseq) fetch(seq + gridDim.x);
     float kr[16];
-    {
+    if (colw) {
       f32x16 acc;
       key_block<NB, NP>(g, sm, w, c, h, acc);
       const float bj = sm.bq[j];
 #pragma unroll
       for (int r = 0; r < 16; ++r) kr[r] = tanhf(acc[r] + bj);
-    }
-    if (w == 0) {   // dp_l = dnews · C_l; ds = p (dp - Σ p dp) scale
+    } else if (d == 0) {   // dp_l = dnews · C_l; ds = p (dp - Σ p dp) scale
       const int l = lane & 31;
       float dp = 0.f;
 #pragma unroll 4
       for (int k4 = 0; k4 < HP / 4; ++k4) {
         const float4 x = *reinterpret_cast<const float4*>(&sm.ct[l][4 * k4]);
-        const float4 d = *reinterpret_cast<const float4*>(&sm.dn[4 * k4]);
-        dp = fmaf(x.x, d.x, dp); dp = fmaf(x.y, d.y, dp);
-        dp = fmaf(x.z, d.z, dp); dp = fmaf(x.w, d.w, dp);
+        const float4 dv = *reinterpret_cast<const float4*>(&sm.dn[4 * k4]);
+        dp = fmaf(x.x, dv.x, dp); dp = fmaf(x.y, dv.y, dp);
+        dp = fmaf(x.z, dv.z, dp); dp = fmaf(x.w, dv.w, dp);
       }
       const float pl = lane < 32 ? sm.p[l] : 0.f;
       const float rs = nr_wave_sum(pl * dp);
       if (lane < 32) sm.ds[lane] = pl * (dp - rs) * g.scale;
     }
     __syncthreads();
-    {
+    if (colw) {
       const float qj = sm.qv[j];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -231,22 +271,42 @@ __global__ __launch_bounds__(64 * NB) void cnn_keypool_bwd_kernel(KPArgs g) {
       }
     }
     __syncthreads();
-    {   // dC block w = dK Wq (+ p dnews + dz), gated by ReLU'(C)
+    if (colw) {   // dC block w = dK Wq (+ p dnews + dz), gated by ReLU'(C)
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const float* wcol = g.wq + (int64_t)(16 * h) * HP + j;
-#pragma unroll 1
-      for (int ch = 0; ch < NB; ++ch) {
-        float a[16], b[16];
+      if constexpr (WC_REGS) {
 #pragma unroll
-        for (int s = 0; s < 16; ++s) b[s] = wcol[(int64_t)(32 * ch + s) * HP];
+        for (int ch = 0; ch < NB; ++ch) {
+          float a[16];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float4 x = *reinterpret_cast<const float4*>(&sm.dk[c][32 * ch + 16 * h + 4 * u]);
-          a[4 * u] = x.x; a[4 * u + 1] = x.y; a[4 * u + 2] = x.z; a[4 * u + 3] = x.w;
+          for (int u = 0; u < 4; ++u) {
+            const float4 x = *reinterpret_cast<const float4*>(&sm.dk[c][32 * ch + 16 * h + 4 * u]);
+            a[4 * u] = x.x; a[4 * u + 1] = x.y; a[4 * u + 2] = x.z; a[4 * u + 3] = x.w;
+          }
+          mfma16<NP>(acc, a, wc[ch]);
         }
-        mfma16<NP>(acc, a, b);
+      } else {
+        const float* wcol = g.wq + (int64_t)(16 * h) * HP + j;
+        float bn[16];
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) bn[s2] = wcol[(int64_t)s2 * HP];
+#pragma unroll 1
+        for (int ch = 0; ch < NB; ++ch) {   // the next chunk's Wq column fragment in flight
+          float a[16], b[16];
+#pragma unroll
+          for (int s2 = 0; s2 < 16; ++s2) b[s2] = bn[s2];
+          if (ch + 1 < NB) {
+#pragma unroll
+            for (int s2 = 0; s2 < 16; ++s2) bn[s2] = wcol[(int64_t)(32 * (ch + 1) + s2) * HP];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float4 x = *reinterpret_cast<const float4*>(&sm.dk[c][32 * ch + 16 * h + 4 * u]);
+            a[4 * u] = x.x; a[4 * u + 1] = x.y; a[4 * u + 2] = x.z; a[4 * u + 3] = x.w;
+          }
+          mfma16<NP>(acc, a, b);
+        }
       }
       const float dnj = sm.dn[j];
 #pragma unroll
@@ -260,34 +320,46 @@ __global__ __launch_bounds__(64 * NB) void cnn_keypool_bwd_kernel(KPArgs g) {
           dcb_acc += gated;
         }
       }
-    }
-    {   // dWq rows of block w += dKᵀ C over the title's tokens
-      float a[16];
+    } else {   // dWq blocks of this wave += dKᵀ C over the title's tokens
 #pragma unroll
-      for (int s = 0; s < 16; ++s) a[s] = sm.dk[16 * h + s][j];
+      for (int i = 0; i < MAXB; ++i) {
+        const int b = d + i * ND;
+        if (b < NB * NB) {
+          const int jb = b / NB, kb = b - jb * NB;
+          float a[16], bb[16];
 #pragma unroll
-      for (int kb = 0; kb < NB; ++kb) {
-        float b[16];
+          for (int s2 = 0; s2 < 16; ++s2) {
+            a[s2] = sm.dk[16 * h + s2][32 * jb + c];
+            bb[s2] = sm.ct[16 * h + s2][32 * kb + c];
+          }
+          f32x16 acc;
 #pragma unroll
-        for (int s = 0; s < 16; ++s) b[s] = sm.ct[16 * h + s][32 * kb + c];
-        mfma16<NP>(accw[kb], a, b);
+          for (int r = 0; r < 16; ++r) acc[r] = wacc[b][r][lane];
+          mfma16<NP>(acc, a, bb);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) wacc[b][r][lane] = acc[r];
+        }
         __builtin_amdgcn_sched_barrier(0);   // keep the next block's fragment reads out of this one
       }
     }
   }
   // this workgroup's partials (every slot written, also by a workgroup without titles)
+  __syncthreads();
   float* wsb = g.ws + (int64_t)blockIdx.x * g.nws;
-#pragma unroll
-  for (int kb = 0; kb < NB; ++kb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) wsb[(int64_t)(32 * w + crow(r, h)) * HP + 32 * kb + c] = accw[kb][r];
-  dq_acc += __shfl_xor(dq_acc, 32, 64);
-  dbq_acc += __shfl_xor(dbq_acc, 32, 64);
-  dcb_acc += __shfl_xor(dcb_acc, 32, 64);
-  if (h == 0) {
-    wsb[(int64_t)HP * HP + j] = dbq_acc;
-    wsb[(int64_t)HP * HP + HP + j] = dq_acc;
-    wsb[(int64_t)HP * HP + 2 * HP + j] = dcb_acc;
+  if (colw) {
+    dq_acc += __shfl_xor(dq_acc, 32, 64);
+    dbq_acc += __shfl_xor(dbq_acc, 32, 64);
+    dcb_acc += __shfl_xor(dcb_acc, 32, 64);
+    if (h == 0) {
+      wsb[(int64_t)HP * HP + j] = dbq_acc;
+      wsb[(int64_t)HP * HP + HP + j] = dq_acc;
+      wsb[(int64_t)HP * HP + 2 * HP + j] = dcb_acc;
+    }
+  }
+  for (int i = tid; i < NB * NB * 16 * 64; i += 64 * KP_BW) {   // dWq blocks, coalesced along columns
+    const int b = i / (16 * 64), r = (i / 64) % 16, ln = i % 64;
+    const int jb = b / NB, kb = b - jb * NB;
+    wsb[(int64_t)(32 * jb + crow(r, ln >> 5)) * HP + 32 * kb + (ln & 31)] = wacc[b][r][ln];
   }
 }
 
@@ -339,26 +411,26 @@ int cu_count() {
   return g_cus;
 }
 
-constexpr int KP_WG_PER_CU = 2;
-
-int64_t kp_groups(int64_t nseq) {
-  const int64_t cap = (int64_t)cu_count() * KP_WG_PER_CU;
+// persistent workgroups per CU: the forward (NB waves, 44 KB of LDS) three, the backward (8 waves,
+// 147 KB of LDS) one
+int64_t kp_groups(int64_t nseq, int per_cu) {
+  const int64_t cap = (int64_t)cu_count() * per_cu;
   return nseq < cap ? (nseq > 0 ? nseq : 1) : cap;
 }
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-#define NR_KP_LAUNCH(KERN)                                                                                  \
+#define NR_KP_LAUNCH(KERN, NT)                                                                              \
   template <int NB>                                                                                         \
   int launch_##KERN(int np, const KPArgs& g, int64_t grid, hipStream_t s) {                               \
-    if (np == 0) hipLaunchKernelGGL((KERN<NB, 0>), dim3((unsigned)grid), dim3(64 * NB), 0, s, g);         \
-    else if (np == 1) hipLaunchKernelGGL((KERN<NB, 1>), dim3((unsigned)grid), dim3(64 * NB), 0, s, g);    \
-    else hipLaunchKernelGGL((KERN<NB, 3>), dim3((unsigned)grid), dim3(64 * NB), 0, s, g);                 \
+    if (np == 0) hipLaunchKernelGGL((KERN<NB, 0>), dim3((unsigned)grid), dim3(NT), 0, s, g);              \
+    else if (np == 1) hipLaunchKernelGGL((KERN<NB, 1>), dim3((unsigned)grid), dim3(NT), 0, s, g);         \
+    else hipLaunchKernelGGL((KERN<NB, 3>), dim3((unsigned)grid), dim3(NT), 0, s, g);                      \
     NR_LAUNCH_CHECK();                                                                                      \
     return NR_OK;                                                                                           \
   }
-NR_KP_LAUNCH(cnn_keypool_fwd_kernel)
-NR_KP_LAUNCH(cnn_keypool_bwd_kernel)
+NR_KP_LAUNCH(cnn_keypool_fwd_kernel, 64 * NB)
+NR_KP_LAUNCH(cnn_keypool_bwd_kernel, 64 * KP_BW)
 #undef NR_KP_LAUNCH
 
 int np_of(int prec) { return prec == NR_GEMM_F32 ? 0 : prec == NR_GEMM_BF16 ? 1 : 3; }
@@ -367,7 +439,7 @@ int np_of(int prec) { return prec == NR_GEMM_F32 ? 0 : prec == NR_GEMM_BF16 ? 1 
 
 extern "C" int64_t nr_cnn_keypool_workspace(int64_t nseq, int32_t Hp) {
   if (nseq < 0 || Hp < 32 || Hp > 160 || (Hp & 31)) return -1;
-  return kp_groups(nseq) * ((int64_t)Hp * Hp + 3 * (int64_t)Hp);
+  return kp_groups(nseq, 1) * ((int64_t)Hp * Hp + 3 * (int64_t)Hp);
 }
 
 extern "C" int nr_cnn_keypool_fwd(const float* C, int64_t ldc, const float* wq, const float* bq, const float* q,
@@ -383,7 +455,7 @@ extern "C" int nr_cnn_keypool_fwd(const float* C, int64_t ldc, const float* wq, 
   KPArgs g{};
   g.c = C; g.ldc = ldc; g.wq = wq; g.bq = bq; g.q = q; g.qn = qn; g.mask = mask; g.mask_dt = mask_dtype;
   g.nseq = nseq; g.L = L; g.scale = scale; g.news = news; g.ldn = ldn; g.probs = probs; g.H = qn;
-  const int64_t grid = kp_groups(nseq);
+  const int64_t grid = kp_groups(nseq, 3);
   const int np = np_of(prec);
   switch (Hp / 32) {
     case 1: return launch_cnn_keypool_fwd_kernel<1>(np, g, grid, stream);
@@ -405,7 +477,7 @@ extern "C" int nr_cnn_keypool_bwd(const float* C, int64_t ldc, const float* wq, 
   if (!C || !wq || !bq || !q || !probs || !dnews || !dc || !dwq || !dbq || !dq || !dconv_b || !ws) return NR_EINVAL(1);
   if (!al16(C) || !al16(wq)) return NR_EINVAL(2);
   const int64_t nws = (int64_t)Hp * Hp + 3 * (int64_t)Hp;
-  const int64_t grid = kp_groups(nseq);
+  const int64_t grid = kp_groups(nseq, 1);
   if (ws_floats < grid * nws) return NR_EINVAL(3);
   KPArgs g{};
   g.c = C; g.ldc = ldc; g.wq = wq; g.bq = bq; g.q = q; g.qn = qn;
