@@ -192,6 +192,53 @@ class _SparseGradHook:
 SPARSE_GRAD_HOOK = _SparseGradHook()
 
 
+class _LocalRowGrad:
+    """Single-process gradient of a row-sparse table (LSTUR's user table: B rows of 876,957 per step)
+    when no SPARSE_GRAD_HOOK owns it: a dense buffer zeroed ONCE and installed as ``table.grad``; each
+    step re-zeroes only the rows the previous step wrote, then scatter-adds this step's rows (instead
+    of a 526 MB zero fill per step).  Used only when ``table.grad`` is None at backward time
+    (zero_grad(set_to_none=True), as Manager._train and bench do), so gradient accumulation across
+    backward passes keeps torch's dense semantics."""
+
+    def __init__(self):
+        self.buf, self.prev = {}, {}
+
+    def __call__(self, table, rows, grads):
+        if not _is_param_leaf(table):
+            return False
+        key = id(table)
+        buf = self.buf.get(key)
+        if table.grad is not None:
+            # torch's dense accumulation into the existing gradient; if that is our buffer, it now
+            # holds rows this class does not track: zero it whole before its next use
+            if buf is not None and table.grad.data_ptr() == buf.data_ptr():
+                self.prev[key] = None
+            return False
+        if buf is None or buf.shape != table.shape or buf.device != table.device:
+            buf = self.buf[key] = torch.zeros_like(table)
+            self.prev.pop(key, None)
+        elif key in self.prev and self.prev[key] is None:
+            buf.zero_()
+            del self.prev[key]
+        prev = self.prev.get(key)
+        if prev is not None:
+            buf.index_fill_(0, prev, 0.0)
+        K.embedding_bwd(grads, rows, buf, padding_idx=None)
+        if prev is not None and prev.numel() == rows.numel():
+            prev.copy_(rows.reshape(-1))      # in place: a captured step replays the same buffer
+        else:
+            self.prev[key] = rows.reshape(-1).clone()
+        table.grad = buf
+        return True
+
+    def clear(self):
+        self.buf.clear()
+        self.prev.clear()
+
+
+LOCAL_ROW_GRAD = _LocalRowGrad()
+
+
 class _WgradDeferHook:
     """Optional callback ``hook(run, out) -> bool`` for the news tower's projection weight-gradient
     GEMM (the longest kernel of the backward, issued after the word-table gradient).  ``run(max_cus)``
@@ -690,7 +737,7 @@ class RNNUserFn(torch.autograd.Function):
         _proj_wgrad(dgh_, K.operand(hprev, L.MNCONTIG), dw_hh, db_hh, B * N)
         dtab = None
         if user_table is not None and ctx.needs_input_grad[5]:
-            if not SPARSE_GRAD_HOOK(ctx.table_ref, h0_idx, dh0):
+            if not SPARSE_GRAD_HOOK(ctx.table_ref, h0_idx, dh0) and not LOCAL_ROW_GRAD(ctx.table_ref, h0_idx, dh0):
                 dtab = torch.zeros_like(user_table)
                 K.embedding_bwd(dh0, h0_idx, dtab, padding_idx=None)
         return dx, dw_ih, dw_hh, db_ih, db_hh, dtab, None, None, None, None, None, None
