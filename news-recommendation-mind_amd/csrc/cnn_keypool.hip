@@ -9,8 +9,8 @@
 // stored), dp_l = dnews · C_l, ds = p (dp - Σ p dp) / sqrt(H), dK = ds q (1 - K²),
 // dC = p dnews + dK Wq (+ dz) gated by ReLU'(C) (the conv pre-activation gradient), and the
 // parameter gradients dWq = Σ dKᵀ C, dbq = Σ dK, dq = Σ ds K, dconv_b = Σ gated dC accumulate in
-// registers across the titles of a persistent workgroup; each workgroup stores one partial and
-// cnn_keypool_reduce_kernel adds the partials in workgroup order (deterministic, no atomics).
+// registers / LDS across the titles of a persistent workgroup; each workgroup stores one partial and
+// two reduce kernels add the partials in a fixed order (deterministic, no atomics).
 // This replaces the T x Hp key GEMM + tanh epilogue, the word pooling, its backward, the key
 // dgrad / wgrad GEMMs and two bias column sums: seven launches and four T x Hp round trips.
 //
@@ -363,31 +363,43 @@ __global__ __launch_bounds__(64 * KP_BW) void cnn_keypool_bwd_kernel(KPArgs g) {
   }
 }
 
-// outputs: dwq [Hp][Hp], dbq [Hp], dq [qn], dconv_b [H] (stored), each the sum of the partials.  A block
-// takes 64 columns; its four waves sum every fourth partial, then wave 0 adds the four in order
-// (deterministic)
-__global__ __launch_bounds__(256) void cnn_keypool_reduce_kernel(const float* __restrict__ ws, int64_t nws, int G,
-                                                                 int HP, int qn, int H, float* __restrict__ dwq,
-                                                                 float* __restrict__ dbq, float* __restrict__ dq,
-                                                                 float* __restrict__ dcb) {
-  __shared__ float part[4][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
-  const int64_t ic = i < nws ? i : nws - 1;
+// Partials -> outputs in two deterministic stages: stage 1 sums slice y of the G workgroup
+// partials (G / KP_SLICES each, eight loads in flight per thread) into part[y]; stage 2 adds the
+// KP_SLICES slices in order and scatters to dwq [Hp][Hp], dbq [Hp], dq [qn], dconv_b [H] (stored).
+// One pass over all G partials with one thread per column left the reads latency-bound.
+constexpr int KP_SLICES = 8;
+
+__global__ __launch_bounds__(256) void cnn_keypool_reduce1_kernel(const float* __restrict__ ws, int64_t nws, int G,
+                                                                  float* __restrict__ part) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nws) return;
+  const int y = blockIdx.y;
+  const int g0 = (int)((int64_t)G * y / KP_SLICES), g1 = (int)((int64_t)G * (y + 1) / KP_SLICES);
   float s = 0.f;
-  int gi = wv;
-  for (; gi + 28 < G; gi += 32) {   // eight loads in flight
+  int g = g0;
+  for (; g + 8 <= g1; g += 8) {
     float v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = ws[(int64_t)(gi + 4 * u) * nws + ic];
+    for (int u = 0; u < 8; ++u) v[u] = ws[(int64_t)(g + u) * nws + i];
 #pragma unroll
     for (int u = 0; u < 8; ++u) s += v[u];
   }
-  for (; gi < G; gi += 4) s += ws[(int64_t)gi * nws + ic];
-  part[wv][lane] = s;
-  __syncthreads();
-  if (wv != 0 || i >= nws) return;
-  s = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+  for (; g < g1; ++g) s += ws[(int64_t)g * nws + i];
+  part[(int64_t)y * nws + i] = s;
+}
+
+__global__ __launch_bounds__(256) void cnn_keypool_reduce2_kernel(const float* __restrict__ part, int64_t nws,
+                                                                  int HP, int qn, int H, float* __restrict__ dwq,
+                                                                  float* __restrict__ dbq, float* __restrict__ dq,
+                                                                  float* __restrict__ dcb) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nws) return;
+  float v[KP_SLICES];
+#pragma unroll
+  for (int y = 0; y < KP_SLICES; ++y) v[y] = part[(int64_t)y * nws + i];
+  float s = 0.f;
+#pragma unroll
+  for (int y = 0; y < KP_SLICES; ++y) s += v[y];
   const int64_t hh = (int64_t)HP * HP;
   if (i < hh) {
     dwq[i] = s;
@@ -439,7 +451,7 @@ int np_of(int prec) { return prec == NR_GEMM_F32 ? 0 : prec == NR_GEMM_BF16 ? 1 
 
 extern "C" int64_t nr_cnn_keypool_workspace(int64_t nseq, int32_t Hp) {
   if (nseq < 0 || Hp < 32 || Hp > 160 || (Hp & 31)) return -1;
-  return kp_groups(nseq, 1) * ((int64_t)Hp * Hp + 3 * (int64_t)Hp);
+  return (kp_groups(nseq, 1) + KP_SLICES) * ((int64_t)Hp * Hp + 3 * (int64_t)Hp);
 }
 
 extern "C" int nr_cnn_keypool_fwd(const float* C, int64_t ldc, const float* wq, const float* bq, const float* q,
@@ -478,7 +490,7 @@ extern "C" int nr_cnn_keypool_bwd(const float* C, int64_t ldc, const float* wq, 
   if (!al16(C) || !al16(wq)) return NR_EINVAL(2);
   const int64_t nws = (int64_t)Hp * Hp + 3 * (int64_t)Hp;
   const int64_t grid = kp_groups(nseq, 1);
-  if (ws_floats < grid * nws) return NR_EINVAL(3);
+  if (ws_floats < (grid + KP_SLICES) * nws) return NR_EINVAL(3);
   KPArgs g{};
   g.c = C; g.ldc = ldc; g.wq = wq; g.bq = bq; g.q = q; g.qn = qn;
   g.nseq = nseq; g.L = L; g.scale = scale; g.probs = const_cast<float*>(probs);
@@ -494,8 +506,12 @@ extern "C" int nr_cnn_keypool_bwd(const float* C, int64_t ldc, const float* wq, 
     default: rc = launch_cnn_keypool_bwd_kernel<5>(np, g, grid, stream); break;
   }
   if (rc != NR_OK) return rc;
-  hipLaunchKernelGGL(cnn_keypool_reduce_kernel, dim3((unsigned)((nws + 63) / 64)), dim3(256), 0, stream, ws, nws,
-                     (int)grid, Hp, qn, H, dwq, dbq, dq, dconv_b);
+  float* part = ws + grid * nws;
+  hipLaunchKernelGGL(cnn_keypool_reduce1_kernel, dim3((unsigned)((nws + 255) / 256), KP_SLICES), dim3(256), 0, stream,
+                     ws, nws, (int)grid, part);
+  NR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(cnn_keypool_reduce2_kernel, dim3((unsigned)((nws + 255) / 256)), dim3(256), 0, stream, part, nws,
+                     Hp, qn, H, dwq, dbq, dq, dconv_b);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

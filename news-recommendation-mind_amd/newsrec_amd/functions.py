@@ -28,6 +28,10 @@ def _gemm_backward(fn):
     return wrapper
 
 
+def _ceil32(n):
+    return (n + 31) // 32 * 32
+
+
 def _pad4(n):
     return (n + 3) // 4 * 4
 
@@ -703,7 +707,15 @@ class RNNUserFn(torch.autograd.Function):
         G = 4 if cell == L.CELL_LSTM else 3
         dev = x.device
         gx = _empty(B * N, G * H, x)
-        K.gemm(B * N, G * H, H, K.operand(x, L.KCONTIG), K.operand(w_ih, L.KCONTIG), gx, bias=b_ih)
+        # the input projection contracts over H: padded to a multiple of 32 with zero columns (a 1 MB
+        # copy of x, 0.4 MB of w_ih) it runs on the fast GEMM path instead of the generic one
+        Hp = _ceil32(H)
+        if Hp != H:
+            x = torch.nn.functional.pad(x, (0, Hp - H))
+            w_k = torch.nn.functional.pad(w_ih.detach(), (0, Hp - H))
+        else:
+            w_k = w_ih
+        K.gemm(B * N, G * H, Hp, K.operand(x, L.KCONTIG), K.operand(w_k, L.KCONTIG), gx, bias=b_ih)
         gates = torch.empty(B * N, 4 * H, device=dev)
         hprev = torch.empty(B * N, H, device=dev)
         cprev = torch.empty(B * N, H, device=dev) if cell == L.CELL_LSTM else None
@@ -721,20 +733,36 @@ class RNNUserFn(torch.autograd.Function):
     def backward(ctx, dh):
         x, w_ih, w_hh, gates, hprev, cprev, mask, h0_idx, user_table = ctx.saved_tensors
         cell, B, N, reverse = ctx.cfg
-        H = x.shape[1]
+        H = w_ih.shape[1]
+        Hp = x.shape[1]            # x saved zero-padded to a multiple of 32 columns (forward)
         G = 4 if cell == L.CELL_LSTM else 3
+        GH = G * H
+        GHp = _ceil32(GH) if Hp != H else GH
         dev = x.device
-        dgi = torch.empty(B * N, G * H, device=dev)
-        dgh = torch.empty(B * N, G * H, device=dev) if cell == L.CELL_GRU else None
+        # the gate gradients with zero columns up to GHp (the dx GEMM contracts over them) and the
+        # padded operands below keep the three GEMMs on the fast path (K % 32 == 0, float4 rows)
+        dgi_b = torch.empty(B * N, GHp, device=dev)
+        dgh_b = torch.empty(B * N, GHp, device=dev) if cell == L.CELL_GRU else None
+        for t in (dgi_b, dgh_b):
+            if t is not None and GHp != GH:
+                t[:, GH:].zero_()
+        dgi = dgi_b[:, :GH]
+        dgh = dgh_b[:, :GH] if dgh_b is not None else None
         dh0 = torch.empty(B, H, device=dev) if user_table is not None else None
         K.rnn_bwd(cell, w_hh.contiguous(), gates, hprev, cprev, B, N, H, dh.contiguous(), dgi, dgh=dgh, dh0=dh0,
                   mask=mask, reverse=reverse)
         dgh_ = dgi if dgh is None else dgh
         dx = _empty(B * N, H, x)
-        K.gemm(B * N, H, G * H, K.operand(dgi, L.KCONTIG), K.operand(w_ih, L.MNCONTIG), dx)
-        dw_ih, db_ih, dw_hh, db_hh = _zeros_views(dev, (G * H, H), (G * H,), (G * H, H), (G * H,))
+        if Hp != H:
+            w_k = torch.nn.functional.pad(w_ih.detach(), (0, Hp - H, 0, GHp - GH))
+            K.gemm(B * N, H, GHp, K.operand(dgi_b, L.KCONTIG), K.operand(w_k, L.MNCONTIG), dx)
+            h_k = torch.nn.functional.pad(hprev, (0, Hp - H))
+        else:
+            K.gemm(B * N, H, GH, K.operand(dgi, L.KCONTIG), K.operand(w_ih, L.MNCONTIG), dx)
+            h_k = hprev
+        dw_ih, db_ih, dw_hh, db_hh = _zeros_views(dev, (GH, H), (GH,), (GH, H), (GH,))
         _proj_wgrad(dgi, K.operand(x, L.MNCONTIG), dw_ih, db_ih, B * N)
-        _proj_wgrad(dgh_, K.operand(hprev, L.MNCONTIG), dw_hh, db_hh, B * N)
+        _proj_wgrad(dgh_, K.operand(h_k, L.MNCONTIG), dw_hh, db_hh, B * N)
         dtab = None
         if user_table is not None and ctx.needs_input_grad[5]:
             if not SPARSE_GRAD_HOOK(ctx.table_ref, h0_idx, dh0) and not LOCAL_ROW_GRAD(ctx.table_ref, h0_idx, dh0):
