@@ -48,14 +48,15 @@ int big_bn(int64_t M, int64_t N, int64_t K, int splits, bool resplit, bool m_dyn
   const int64_t gm = (M + 255) / 256;
   if (!resplit && gm * splits < 8) return 0;
   if (resplit) return (N % 256 == 0 || N >= 1024) ? 256 : 128;
-  // device-resident M (distinct-row counts): the host M is only a bound, so the round efficiency is
-  // unknown; the persistent grid absorbs the actual count -- take the big tiles for wide N
-  if (m_dyn) return N >= 1024 ? 256 : 0;
   // padded-N MFMA work counts against a tile width too; measured on the step's shapes, the
   // 256 x 256 core is ~15 % faster per unit of work than the 128 x 128 kernel, 256 x 128 is not
   const double e256 = round_eff(gm * ((N + 255) / 256) * splits, 256) * (double)N / (double)((N + 255) / 256 * 256);
   const double e_old = round_eff(((M + 127) / 128) * ((N + 127) / 128) * splits, 512) * (double)N /
                        (double)((N + 127) / 128 * 128);
+  // device-resident M (distinct-row counts): the host M is only a bound and the persistent grid
+  // absorbs the actual count -- the big tiles for wide N, else the round efficiencies at the bound
+  // (the CNN tap projection, N = 480: 141 -> see DESIGN §4.1)
+  if (m_dyn) return (N >= 1024 || e256 >= 0.87 * e_old) ? 256 : 0;
   return e256 >= 0.87 * e_old ? 256 : 0;
 }
 // Split-K slabs -> C: C[m][n] += sum over the valid splits of slab[s][m][n], in split order
