@@ -24,7 +24,10 @@
 namespace {
 
 constexpr int SEG_RANGE = 64;   // CSR positions per segment-sum workgroup
-constexpr int SEG_BATCH = 16;   // row loads in flight per thread (8: 70 us per NRMS step, waits 0.66 of wave cycles)
+#ifndef NR_SEG_BATCH   // A/B builds only (tools/build_variant.sh)
+#define NR_SEG_BATCH 16
+#endif
+constexpr int SEG_BATCH = NR_SEG_BATCH;   // row loads in flight per thread (8: waits 0.66 of wave cycles)
 constexpr int CNT_THREADS = 1024;
 constexpr int HASH_SLOTS = 2048;
 

@@ -143,6 +143,8 @@ DEDUP_ROWS = True
 # Training forward saves the attention output; the backward runs split (False: the fused backward
 # that recomputes the attention).
 SPLIT_BWD = True
+# Split-K factor of the MHA user encoder's input gradient (dx = dY [Wk; Wv], K = 1152)
+USER_DGRAD_SPLIT = 1
 # CNN word attention (tanh key projection + learned-query pooling) fused per title, forward and
 # backward (nr_cnn_keypool_*; False: the key GEMM + pooling kernels the parity tests compare with).
 FUSED_KEYPOOL = True
@@ -686,8 +688,16 @@ class MHAFn(torch.autograd.Function):
             dO = dO.contiguous()
         dY = _empty(rows, NY, x)
         K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, nseq, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
-        dx = _empty(rows, D, x)
-        K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx)
+        split = USER_DGRAD_SPLIT if NY >= 512 * USER_DGRAD_SPLIT else 1
+        if split > 1:
+            # few output tiles (1600 x 384 for the NRMS user encoder) over a long contraction (1152): split
+            # K and add the pieces atomically into a zeroed dx
+            dx = torch.zeros(rows, D, device=dev)
+            K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx, epilogue=L.EPI_ATOMIC,
+                   split_k=split)
+        else:
+            dx = _empty(rows, D, x)
+            K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx)
         dw, db = _zeros_views(dev, (NY, D), (NY,))
         _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows)
         return dx, None, dw, db, None, None, None, None, None

@@ -1,0 +1,52 @@
+"""functions.USER_DGRAD_SPLIT: the MHA user encoder's input gradient (dx = dY [Wk; Wv], K = 1152,
+models/Modules/Attention.py:107-108) split along K with the pieces added atomically into a zeroed dx.
+Every gradient of an NRMS step must match the unsplit contraction to fp32 rounding."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from newsrec_amd import functions as F
+from newsrec_amd.manager import build_model
+
+
+def _batch(dev, b=32, c=5, nh=50, l=30, vocab=30522):
+    g = torch.Generator().manual_seed(11)
+
+    def titles(n):
+        tok = torch.randint(1000, vocab, (n, l), generator=g)
+        lens = torch.randint(5, l + 1, (n,), generator=g)
+        mask = (torch.arange(l)[None] < lens[:, None]).long()
+        return (tok * mask).view(-1, l), mask
+
+    ct, cm = titles(b * c)
+    ht, hm = titles(b * nh)
+    x = {"cdd_encoded_index": ct.view(b, c, l), "cdd_attn_mask": cm.view(b, c, l),
+         "his_encoded_index": ht.view(b, nh, l), "his_attn_mask": hm.view(b, nh, l),
+         "his_mask": torch.ones(b, nh, 1, dtype=torch.float64), "user_id": torch.randint(1, 50, (b,), generator=g),
+         "label": torch.zeros(b, dtype=torch.long)}
+    return {k: v.to(dev) for k, v in x.items()}
+
+
+@pytest.mark.parametrize("split", [2, 3])
+def test_user_dgrad_split_matches_unsplit(split):
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(3)
+    model = build_model("mha", "mha", 384, vocab=30522, device=dev, user_num=50, dropout_p=0.0)
+    x = _batch(dev)
+    grads = {}
+    old = F.USER_DGRAD_SPLIT
+    try:
+        for s in (1, split):
+            F.USER_DGRAD_SPLIT = s
+            model.zero_grad(set_to_none=True)
+            _, loss = model.forward_loss(x)
+            loss.backward()
+            torch.cuda.synchronize()
+            grads[s] = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    finally:
+        F.USER_DGRAD_SPLIT = old
+    for n, g1 in grads[1].items():
+        g2 = grads[split][n]
+        err = (g2 - g1).abs().max().item()
+        assert err <= 1e-4 * max(1e-8, g1.abs().max().item()), (n, err)

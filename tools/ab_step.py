@@ -29,7 +29,8 @@ def main():
     for v in a.variants:
         for kv in v.split(","):
             k, val = kv.split("=")
-            setattr(F, k, bool(int(val)))
+            cur = getattr(F, k)
+            setattr(F, k, bool(int(val)) if isinstance(cur, bool) else int(val))
         model = bench.build(dev)
         model.train()
         opt = bench.make_optim(model, capturable=True)
