@@ -28,7 +28,7 @@ def _batch(dev, b=32, c=5, nh=50, l=30, vocab=30522):
     return {k: v.to(dev) for k, v in x.items()}
 
 
-@pytest.mark.parametrize("split", [2, 3])
+@pytest.mark.parametrize("split", [2])
 def test_user_dgrad_split_matches_unsplit(split):
     dev = torch.device("cuda", 0)
     torch.manual_seed(3)
