@@ -147,6 +147,11 @@ SPLIT_BWD = True
 # >= 512 k per piece.  One-box A/B of the NRMS step, interleaved rounds: unsplit 1.4206-1.4275 ms,
 # two pieces 1.4292 ms -- kept unsplit
 USER_DGRAD_SPLIT = 1
+# CNN conv weight gradient: split-K partials through a workspace + one ordered reduction instead of
+# fp32 atomics.  bf16 (one product per k-step leaves the atomic epilogue exposed): one-box A/B of the
+# configs[1] bf16 step 0.741 -> 0.700 ms.  bf16x6: WGRAD_WS_BF16X6
+WGRAD_WS_BF16 = True
+WGRAD_WS_BF16X6 = False
 # CNN word attention (tanh key projection + learned-query pooling) fused per title, forward and
 # backward (nr_cnn_keypool_*; False: the key GEMM + pooling kernels the parity tests compare with).
 FUSED_KEYPOOL = True
@@ -613,7 +618,9 @@ class CNNNewsRowsFn(torch.autograd.Function):
         K.gemm_dyn(3 * Hp, E, ur.cap, K.operand(S, L.MNCONTIG),
                    K.operand(table, L.MNCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER), dw3t, k_dev=ur.u_pad,
                    epilogue=L.EPI_ATOMIC, split_k=_split_k(3 * Hp, E, ur.cap),
-                   max_cus=WGRAD_DEFER_HOOK.max_cus if inflight else 0)
+                   max_cus=WGRAD_DEFER_HOOK.max_cus if inflight else 0,
+                   workspace=(WGRAD_WS_BF16 and ctx.prec == L.GEMM_BF16) or
+                   (WGRAD_WS_BF16X6 and ctx.prec == L.GEMM_BF16X6))
         return (dtable, None, None, dw3t, dconv_b, dwq, dbq, dq.view_as(query), None, None, None)
 
 

@@ -104,10 +104,12 @@ def _splitk_work(like):
 
 
 def gemm_dyn(M, N, K, A, B, C, m_dev=None, k_dev=None, ldc=None, bias=None, epilogue=L.EPI_STORE,
-             c_rows=None, pad_row=-1, split_k=1, prec=None, max_cus=0):
+             c_rows=None, pad_row=-1, split_k=1, prec=None, max_cus=0, workspace=False):
     """``gemm`` with device-resident extents: M, K are upper bounds, the kernel reads the actual
     M / K from the int32 CUDA scalars ``m_dev`` / ``k_dev`` (e.g. ``UniqueRows.counts[1:2]``).
-    ``max_cus`` > 0 limits the persistent grid to that many CUs (nr_gemm_f32_dyn_cus)."""
+    ``max_cus`` > 0 limits the persistent grid to that many CUs (nr_gemm_f32_dyn_cus).
+    ``workspace`` (split-K NR_EPI_ATOMIC): partial tiles through plain stores into a workspace and
+    one ordered reduction instead of fp32 atomics (nr_gemm_f32_ws)."""
     _f32(C, bias)
     for t in (m_dev, k_dev):
         if t is not None and (t.dtype != torch.int32 or not t.is_cuda):
@@ -116,6 +118,12 @@ def gemm_dyn(M, N, K, A, B, C, m_dev=None, k_dev=None, ldc=None, bias=None, epil
         raise L.HipError("gemm_dyn: bias has %d < N=%d entries" % (bias.numel(), N))
     if K % 32:
         raise L.HipError("gemm_dyn: K must be a multiple of 32")
+    if workspace and epilogue == L.EPI_ATOMIC and split_k > 1:
+        work = _splitk_work(C)
+        L.call("nr_gemm_f32_ws", M, N, K, A, B, L.ptr(C), ldc if ldc is not None else C.stride(0),
+               L.ptr(bias), epilogue, c_rows, pad_row, split_k, L.ptr(m_dev), L.ptr(k_dev), _prec(prec),
+               int(max_cus), L.ptr(work), work.numel(), L.ptr(None), None, L.stream_ptr(C))
+        return
     if max_cus:
         L.call("nr_gemm_f32_dyn_cus", M, N, K, A, B, L.ptr(C), ldc if ldc is not None else C.stride(0),
                L.ptr(bias), epilogue, c_rows, pad_row, split_k, L.ptr(m_dev), L.ptr(k_dev), _prec(prec),

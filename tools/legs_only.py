@@ -11,7 +11,12 @@ import torch  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("legs", nargs="*")
 ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--set", action="append", default=[], help="NAME=INT: a newsrec_amd.functions switch (A/B)")
 a = ap.parse_args()
+from newsrec_amd import functions as F  # noqa: E402
+for kv in a.set:
+    k, v = kv.split("=")
+    setattr(F, k, bool(int(v)) if isinstance(getattr(F, k), bool) else int(v))
 dev = torch.device("cuda", 0)
 if a.legs == ["xformer"]:
     print(json.dumps(bench.xformer_leg(dev, steps=a.steps)))
