@@ -148,10 +148,12 @@ SPLIT_BWD = True
 # two pieces 1.4292 ms -- kept unsplit
 USER_DGRAD_SPLIT = 1
 # CNN conv weight gradient: split-K partials through a workspace + one ordered reduction instead of
-# fp32 atomics.  bf16 (one product per k-step leaves the atomic epilogue exposed): one-box A/B of the
-# configs[1] bf16 step 0.741 -> 0.700 ms.  bf16x6: WGRAD_WS_BF16X6
+# fp32 atomics (one-box A/B, graphed steps): configs[1] bf16 0.741 -> 0.700 ms; bf16x6 CNN + attention
+# 0.899 -> 0.860 ms, CNN + GRU 1.171 -> 1.126 ms
 WGRAD_WS_BF16 = True
-WGRAD_WS_BF16X6 = False
+WGRAD_WS_BF16X6 = True
+# the NRMS projection weight gradient on the same workspace path (A/B switch)
+PROJ_WGRAD_WS = False
 # CNN word attention (tanh key projection + learned-query pooling) fused per title, forward and
 # backward (nr_cnn_keypool_*; False: the key GEMM + pooling kernels the parity tests compare with).
 FUSED_KEYPOOL = True
@@ -390,7 +392,8 @@ class MHANewsFn(torch.autograd.Function):
             def wgrad(max_cus=0):
                 K.gemm_dyn(NY, E, ur.cap, K.operand(dYu, L.MNCONTIG),
                            K.operand(table, L.MNCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER), dw, k_dev=ur.u_pad,
-                           epilogue=L.EPI_ATOMIC, split_k=_split_k(NY, E, ur.cap), prec=prec, max_cus=max_cus)
+                           epilogue=L.EPI_ATOMIC, split_k=_split_k(NY, E, ur.cap), prec=prec, max_cus=max_cus,
+                           workspace=PROJ_WGRAD_WS)
             if not WGRAD_DEFER_HOOK(wgrad, dw):
                 ev0 = PROBE.record()
                 wgrad(WGRAD_DEFER_HOOK.max_cus if inflight else 0)
