@@ -152,8 +152,9 @@ USER_DGRAD_SPLIT = 1
 # 0.899 -> 0.860 ms, CNN + GRU 1.171 -> 1.126 ms
 WGRAD_WS_BF16 = True
 WGRAD_WS_BF16X6 = True
-# the NRMS projection weight gradient on the same workspace path (A/B switch)
-PROJ_WGRAD_WS = False
+# the NRMS projection weight gradient on the same workspace path: one process, interleaved rounds,
+# 1.459 -> 1.446 ms per NRMS step (round 2 measured it slower, before the bf16x6 units lost SLP)
+PROJ_WGRAD_WS = True
 # CNN word attention (tanh key projection + learned-query pooling) fused per title, forward and
 # backward (nr_cnn_keypool_*; False: the key GEMM + pooling kernels the parity tests compare with).
 FUSED_KEYPOOL = True
