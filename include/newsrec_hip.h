@@ -432,6 +432,11 @@ typedef struct nr_adam_tensor {
   int64_t step;
   const int64_t* step_dev;
   const float* lr_dev;
+  /* optional: one byte per row of row_len elements, 0 = the row's gradient is all zero (a row-sparse
+   * table gradient, e.g. LSTUR's user table): its gradient is not read (the update uses g = 0, the
+   * same arithmetic as reading the zeros).  NULL: every element's gradient is read. */
+  const uint8_t* row_touched;
+  int64_t row_len;
 } nr_adam_tensor;
 int nr_adam_multi(const nr_adam_tensor* tensors, int32_t count, float beta1, float beta2, float eps,
                   float weight_decay, float grad_scale, hipStream_t stream);

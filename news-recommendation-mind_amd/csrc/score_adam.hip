@@ -236,7 +236,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 
 // ---- multi-tensor Adam: up to kAdamMulti tensors per launch, their descriptors passed by value
 // (graph-capturable: no device-side pointer table), blocks assigned to tensors by a prefix sum
-constexpr int kAdamMulti = 40;
+constexpr int kAdamMulti = 32;   // the descriptors travel as kernel arguments (< 4 KB)
 constexpr int kAdamChunk = 4096;   // elements per block (256 threads x 4 float4)
 
 struct AdamEntry {
@@ -248,6 +248,8 @@ struct AdamEntry {
   float bc2_sqrt;            // sqrt(1 - beta2^t) when step_dev is null
   float lr;
   int64_t step;              // host step count
+  const uint8_t* rt;         // optional per-row "gradient non-zero" flags (rows of rlen elements)
+  int64_t rlen;
 };
 
 struct AdamMulti {
@@ -294,7 +296,10 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
     for (int u = 0; u < 4; ++u) {
       const int64_t i = base / 4 + u * 256 + threadIdx.x;
       pp[u] = reinterpret_cast<const float4*>(e.p)[i];
-      gg[u] = reinterpret_cast<const float4*>(e.g)[i];
+      // rows flagged untouched hold zeros: skip their gradient read (a float4 that reaches into a
+      // touched row is read whole -- the untouched part reads as the zeros it holds)
+      const bool rd = !e.rt || e.rt[(4 * i) / e.rlen] || e.rt[(4 * i + 3) / e.rlen];
+      gg[u] = rd ? reinterpret_cast<const float4*>(e.g)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
       mm[u] = reinterpret_cast<const float4*>(e.m)[i];
       vv[u] = reinterpret_cast<const float4*>(e.v)[i];
     }
@@ -312,7 +317,8 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
   } else {
     for (int64_t i = base + threadIdx.x; i < end; i += 256) {
       float pp = e.p[i], mm = e.m[i], vv = e.v[i];
-      adam_elem(pp, e.g[i], mm, vv, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
+      const float gv = (!e.rt || e.rt[i / e.rlen]) ? e.g[i] : 0.f;
+      adam_elem(pp, gv, mm, vv, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
       e.p[i] = pp;
       e.m[i] = mm;
       e.v[i] = vv;
@@ -606,6 +612,7 @@ int adam_multi_impl(const nr_adam_tensor* tensors, int32_t count, float beta1, f
     if (d.n < 0 || (d.step < 1 && !d.step_dev)) return NR_EINVAL(1);
     if (d.n > 0 && (!d.param || !d.grad || !d.exp_avg || !d.exp_avg_sq)) return NR_EINVAL(2);
     if ((d.n + kAdamChunk - 1) / kAdamChunk > 0x3fffffff) return NR_EINVAL(3);
+    if (d.row_touched && d.row_len < 1) return NR_EINVAL(5);
   }
   AdamMulti a;
   a.b1 = beta1; a.b2 = beta2; a.eps = eps; a.wd = weight_decay; a.gscale = grad_scale;
@@ -625,6 +632,7 @@ int adam_multi_impl(const nr_adam_tensor* tensors, int32_t count, float beta1, f
     AdamEntry& e = a.e[a.count];
     e.p = d.param; e.g = d.grad; e.m = d.exp_avg; e.v = d.exp_avg_sq; e.n = d.n;
     e.step_dev = const_cast<int64_t*>(d.step_dev); e.lr_dev = d.lr_dev; e.lr = d.lr;
+    e.rt = d.row_touched; e.rlen = d.row_touched ? d.row_len : 1;
     const double st = (double)(d.step < 1 ? 1 : d.step);   // bias corrections in double, as torch's Python floats
     e.step = (int64_t)st;
     e.step_size = (float)((double)d.lr / (1.0 - pow((double)beta1, st)));

@@ -40,7 +40,8 @@ class nr_operand(ctypes.Structure):
 class nr_adam_tensor(ctypes.Structure):
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
                 ("exp_avg_sq", ctypes.c_void_p), ("n", c_i64), ("lr", c_f32), ("step", c_i64),
-                ("step_dev", ctypes.c_void_p), ("lr_dev", ctypes.c_void_p)]
+                ("step_dev", ctypes.c_void_p), ("lr_dev", ctypes.c_void_p),
+                ("row_touched", ctypes.c_void_p), ("row_len", c_i64)]
 
 
 # name -> argtypes (restype int32 unless listed in _RESTYPES)

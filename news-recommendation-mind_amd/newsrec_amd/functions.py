@@ -217,7 +217,7 @@ class _LocalRowGrad:
     backward passes keeps torch's dense semantics."""
 
     def __init__(self):
-        self.buf, self.prev = {}, {}
+        self.buf, self.prev, self.flags = {}, {}, {}
 
     def __call__(self, table, rows, grads):
         if not _is_param_leaf(table):
@@ -229,27 +229,36 @@ class _LocalRowGrad:
             # holds rows this class does not track: zero it whole before its next use
             if buf is not None and table.grad.data_ptr() == buf.data_ptr():
                 self.prev[key] = None
+            table._nr_row_touched = None
             return False
+        flags = self.flags.get(key)
         if buf is None or buf.shape != table.shape or buf.device != table.device:
             buf = self.buf[key] = torch.zeros_like(table)
+            # per-row "may be non-zero" flags for Adam (it skips reading the rows flagged zero)
+            flags = self.flags[key] = torch.zeros(table.shape[0], dtype=torch.uint8, device=table.device)
             self.prev.pop(key, None)
         elif key in self.prev and self.prev[key] is None:
             buf.zero_()
+            flags.zero_()
             del self.prev[key]
         prev = self.prev.get(key)
         if prev is not None:
             buf.index_fill_(0, prev, 0.0)
+            flags.index_fill_(0, prev, 0)
         K.embedding_bwd(grads, rows, buf, padding_idx=None)
+        flags.index_fill_(0, rows.reshape(-1), 1)
         if prev is not None and prev.numel() == rows.numel():
             prev.copy_(rows.reshape(-1))      # in place: a captured step replays the same buffer
         else:
             self.prev[key] = rows.reshape(-1).clone()
         table.grad = buf
+        table._nr_row_touched = (buf, flags)
         return True
 
     def clear(self):
         self.buf.clear()
         self.prev.clear()
+        self.flags.clear()
 
 
 LOCAL_ROW_GRAD = _LocalRowGrad()

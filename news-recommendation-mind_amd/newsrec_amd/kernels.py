@@ -593,13 +593,20 @@ def adam(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, 
 def adam_multi(entries, beta1, beta2, eps, weight_decay, grad_scale=1.0, advance_steps=False):
     """entries: [(param, grad, exp_avg, exp_avg_sq, lr, step)] with ``step`` an int or an int64 CUDA
     scalar and ``lr`` a float or a float32 CUDA scalar (read on the device); one nr_adam_multi call
-    (a launch per <= 40 tensors).  ``advance_steps``: the device step counts hold the count BEFORE
+    (a launch per <= 32 tensors).  ``advance_steps``: the device step counts hold the count BEFORE
     this step and the launch itself adds 1 to each (nr_adam_multi_step)."""
     if not entries:
         return
     arr = (L.nr_adam_tensor * len(entries))()
-    for i, (p, g, m, v, lr, step) in enumerate(entries):
+    for i, ent in enumerate(entries):
+        p, g, m, v, lr, step = ent[:6]
+        rt = ent[6] if len(ent) > 6 else None   # optional uint8 per-row "gradient non-zero" flags
         _f32(p, g, m, v)
+        rlen = 0
+        if rt is not None:
+            if rt.dtype != torch.uint8 or not rt.is_cuda or rt.numel() < 1 or p.numel() % rt.numel():
+                raise L.HipError("adam_multi: row flags must be a uint8 CUDA tensor dividing the parameter")
+            rlen = p.numel() // rt.numel()
         n = p.numel()
         for t in (p, g, m, v):
             if not t.is_contiguous() or t.numel() != n:
@@ -614,7 +621,7 @@ def adam_multi(entries, beta1, beta2, eps, weight_decay, grad_scale=1.0, advance
                 raise L.HipError("adam_multi: a device learning rate must be a float32 CUDA scalar")
             ld, lr = lr.data_ptr(), 0.0
         arr[i] = L.nr_adam_tensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, float(lr), int(step), sd,
-                                  ld)
+                                  ld, rt.data_ptr() if rt is not None else 0, rlen)
     if advance_steps:
         ticket = self_cleaning_workspace(entries[0][0].device, "nr_adam_multi_step", 4)
         L.call("nr_adam_multi_step", arr, len(entries), beta1, beta2, eps, weight_decay, grad_scale,

@@ -66,7 +66,13 @@ class FusedAdam(torch.optim.Optimizer):
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
             key = (tuple(group["betas"]), group["eps"], group["weight_decay"])
             lr = self._lr_dev[gi] if self.capturable else group["lr"]
-            batches.setdefault(key, []).append((p, g, st["exp_avg"], st["exp_avg_sq"], lr, st["step"]))
+            ent = (p, g, st["exp_avg"], st["exp_avg_sq"], lr, st["step"])
+            # a row-sparse table gradient (functions.LOCAL_ROW_GRAD) carries per-row "touched" flags:
+            # the kernel skips reading the rows known to be zero
+            rt = getattr(p, "_nr_row_touched", None)
+            if rt is not None and p.grad.data_ptr() == rt[0].data_ptr():
+                ent = ent + (rt[1],)
+            batches.setdefault(key, []).append(ent)
         for (betas, eps, wd), entries in batches.items():
             K.adam_multi(entries, betas[0], betas[1], eps, wd, grad_scale, advance_steps=self.capturable)
         return loss

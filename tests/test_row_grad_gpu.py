@@ -42,3 +42,29 @@ def test_local_row_grad_steps():
     table.grad = None
     assert h(table, rows3, g3)
     torch.testing.assert_close(table.grad, _dense(V, E, rows3, g3), rtol=0, atol=1e-6)
+
+
+def test_adam_skips_untouched_rows_exactly():
+    """nr_adam_multi with the handler's per-row flags: bitwise the same parameters and moments as the
+    dense update (the flagged-zero rows' gradients are zeros; the kernel only skips reading them),
+    including a row width that float4 groups straddle (150)."""
+    from newsrec_amd import kernels as K
+    torch.manual_seed(1)
+    V, E = 3001, 150
+    table = torch.nn.Parameter(torch.randn(V, E, device="cuda"))
+    h = F._LocalRowGrad()
+    rows = torch.randint(0, V, (32,), device="cuda")
+    assert h(table, rows, torch.randn(32, E, device="cuda"))
+    buf, flags = table._nr_row_touched
+    assert int(flags.sum()) == len(set(rows.tolist()))
+    m0 = torch.randn(V, E, device="cuda").abs() * 0.01
+    v0 = torch.randn(V, E, device="cuda").abs() * 0.001
+    outs = []
+    for use_flags in (True, False):
+        p, m, v = table.detach().clone(), m0.clone(), v0.clone()
+        ent = (p, buf, m, v, 1e-3, 3) + ((flags,) if use_flags else ())
+        K.adam_multi([ent], 0.9, 0.999, 1e-8, 0.0, 1.0)
+        torch.cuda.synchronize()
+        outs.append((p, m, v))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
