@@ -152,6 +152,9 @@ USER_DGRAD_SPLIT = 1
 # 0.899 -> 0.860 ms, CNN + GRU 1.171 -> 1.126 ms
 WGRAD_WS_BF16 = True
 WGRAD_WS_BF16X6 = True
+# CNN table dgrad with the conv weights transposed to k-contiguous (one 1.5 MB copy per step):
+# one-box A/B of the graphed legs, bf16 0.698 -> 0.657 ms, fp32-class 0.851 -> 0.842 ms
+CNN_DGRAD_KC = True
 # the NRMS projection weight gradient on the same workspace path: one process, interleaved rounds,
 # 1.459 -> 1.446 ms per NRMS step (round 2 measured it slower, before the bf16x6 units lost SLP)
 PROJ_WGRAD_WS = True
@@ -622,7 +625,11 @@ class CNNNewsRowsFn(torch.autograd.Function):
         inflight = False
         if ctx.needs_input_grad[0]:
             dtable = torch.zeros(V, E, device=dev)
-            K.gemm_dyn(ur.cap, E, 3 * Hp, K.operand(S, L.KCONTIG), K.operand(w3t, L.MNCONTIG), dtable,
+            if CNN_DGRAD_KC:   # the weights transposed once (1.5 MB) so both operands are k-contiguous
+                w_b = K.operand(w3t.t().contiguous(), L.KCONTIG)
+            else:
+                w_b = K.operand(w3t, L.MNCONTIG)
+            K.gemm_dyn(ur.cap, E, 3 * Hp, K.operand(S, L.KCONTIG), w_b, dtable,
                        m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(ur.uids, L.ROWS_GATHER),
                        pad_row=pad_row)
             if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
