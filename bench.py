@@ -307,6 +307,9 @@ def xformer_leg(dev, steps=5, warmup=2, b=B):
 
 # algorithmic train FLOPs per impression (token-wise count, fwd x 3) and the
 # parameter count of the dense Adam per configuration (H = 150, V = 30522)
+LEG_FLOPS_BASIS = ("token-wise algorithmic FLOPs (the reference's Conv1d and key projection over every token, "
+                   "fwd x 3); the distinct-row CNN encoder executes about half of them (the tap projection and its "
+                   "two gradient GEMMs over the batch's U distinct word rows instead of T tokens)")
 LEG_FLOPS = {"cnn_attn": 3.65e9, "cnn_attn_bf16": 3.65e9, "cnn_lstur": 3.70e9, "cnn_gru": 3.60e9}
 
 
@@ -324,7 +327,8 @@ def _leg_floor(name, model, ms):
     floor = max(t_mfma, t_hbm)
     return {"bound": "mfma" if t_mfma >= t_hbm else "hbm", "floor_ms": round(floor, 4),
             "frac": round(floor / ms, 4), "achieved_tflops": round(flops / (ms * 1e-3) / 1e12, 1),
-            "peak_tflops": round(peak_tf, 1), "adam_params": n_params, "hbm_bytes_floor": bytes_,
+            "peak_tflops": round(peak_tf, 1), "flop_basis": LEG_FLOPS_BASIS, "adam_params": n_params,
+            "hbm_bytes_floor": bytes_,
             "gemm_arithmetic": "bf16 (operands rounded to bf16, fp32 accumulate)" if bf16 else "bf16x6 (fp32-class)"}
 
 
@@ -540,19 +544,27 @@ def main():
     el = time.perf_counter() - t0
     if a.data == "device":
         feed.store.check_status()
+    from newsrec_amd import kernels as Kn
+    if Kn.score_nll_status(dev):
+        raise RuntimeError("the training head saw a label outside [0, C) (NaN loss)")
 
-    # per-launch timing of the dominant kernel (the fused gather + key/value projection GEMM),
-    # HIP events on its stream, over a few eager steps (events cannot sit inside a replay)
-    F.PROBE.enable()
-    for i in range(3):
-        feed.feed(a.steps + i)
-        train_step(model, opt, feed.form(), sync)
-    probe = F.PROBE.collect()
-    F.PROBE.disable()
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    # data parallel: every rank must hold the same parameters and Adam moments after the timed steps
+    in_sync = dp_check(model, opt, world, dev) if world > 1 else None
+    if in_sync is not None and not in_sync["dp_in_sync"]:
+        print("bench.py: ranks diverged after the timed steps: %s" % json.dumps(in_sync), file=sys.stderr)
+
+    # per-launch timing of the step's projection GEMMs: the launches of one eager step kept as
+    # closures over their real operands, each replayed back to back between HIP events on its stream
+    # (events cannot sit inside a graph replay; rocprofv3's trace of the graphed step agrees)
+    F.PROBE.enable()
+    feed.feed(a.steps)
+    train_step(model, opt, feed.form(), sync)
+    probe = F.PROBE.time(reps=20)
+    F.PROBE.disable()
 
     # eval (a): forward in eval mode (sigmoid) over train-shaped batches -> candidates scored/s
     model.eval()
@@ -584,14 +596,15 @@ def main():
         split = Kn.get_gemm_precision() == Lb.GEMM_BF16X6
         # bf16x6: six bf16 MFMAs per fp32 multiply-add -> fp32-equivalent peak = bf16 dense peak / 6
         peak = BF16_MFMA_PEAK_TF / 6 if split else FP32_MFMA_PEAK_TF
-        # the news tower's three projection GEMMs, each timed per launch with HIP events on its
-        # stream: forward (gathered table rows x [Wk; Wv]^T), table dgrad (dY W -> distinct table
-        # rows), weight gradient (dY^T x gathered rows).  Each is 2 x rows x 768 x 1152 FLOP with
-        # rows = the batch's distinct word rows (device-side count read back after the timed region)
+        # the news tower's three projection GEMMs, each timed per launch (F.PROBE.time): forward
+        # (gathered table rows x [Wk; Wv]^T), table dgrad (dY W -> distinct table rows), weight
+        # gradient (dY^T x gathered rows: the split-K GEMM + its ordered reduction, one unit).  Each
+        # is 2 x rows x 768 x 1152 FLOP with rows = the batch's distinct word rows U_pad (read back
+        # from the device)
         gemms = {}
         for name, what in (("proj_fwd", "forward: gathered rows x [Wk;Wv]^T"),
                            ("proj_dgrad", "table dgrad: dY x [Wk;Wv] -> distinct table rows"),
-                           ("proj_wgrad", "weight gradient: dY^T x gathered rows (split-K)")):
+                           ("proj_wgrad", "weight gradient: dY^T x gathered rows (split-K GEMM + splitk_reduce)")):
             g_ms = probe.get(name + "_ms")
             if not g_ms:
                 continue
@@ -604,7 +617,9 @@ def main():
                 tr = json.load(open(pmc)).get("hbm_bytes_per_launch")
             gemms[name] = {"what": what, "launch_ms": round(g_ms, 4), "rows_per_launch": rows,
                            "flops_per_launch": fl, "achieved": round(ach, 2), "frac": round(ach / peak, 4),
-                           "traffic": tr}
+                           "traffic": tr, "traffic_source": ("profiles/pmc_%s.json (rocprofv3 --pmc passes of "
+                                                             "this build: FETCH_SIZE x 2 + WRITE_SIZE)" % name)
+                           if tr else None}
         # the roofline line names the DOMINANT kernel of the step: the longest of the three
         dom = max(gemms, key=lambda k: gemms[k]["launch_ms"]) if gemms else None
         gd = gemms.get(dom, {})
@@ -641,8 +656,12 @@ def main():
                          "frac_of_fp32_peak": round(achieved / FP32_MFMA_PEAK_TF, 4) if achieved else None,
                          "traffic": traffic, "launch_ms": round(gemm_ms, 4) if gemm_ms else None,
                          "flops_per_launch": gemm_flops, "rows_per_launch": gemm_rows,
-                         "tokens_per_launch": B * (C + NH) * L, "projection_gemms": gemms},
+                         "tokens_per_launch": B * (C + NH) * L,
+                         "timing": "per-launch average of 20 back-to-back replays of the step's own launch "
+                                   "(HIP events on its stream)", "projection_gemms": gemms},
         }
+        if in_sync is not None:
+            out.update(in_sync)
         if xf is not None:
             out["xformer"] = xf
         if legs is not None:
@@ -655,6 +674,32 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if in_sync is not None and not in_sync["dp_in_sync"]:
+        sys.exit(3)
+
+
+def dp_check(model, opt, world, dev):
+    """After the timed data-parallel steps: each rank's float64 checksums (sum and sum of squares) of
+    every parameter and both Adam moments, all-gathered over the process group and compared with
+    rank 0's.  DDP semantics (twotower.py:49-50, Manager.py:167) keep the replicas identical: every
+    rank applies the same all-reduced gradients through the same Adam, so the sums agree bitwise."""
+    sums = []
+    with torch.no_grad():
+        for p in model.parameters():
+            ts = [p] + [opt.state[p][k] for k in ("exp_avg", "exp_avg_sq") if k in opt.state.get(p, {})]
+            for t in ts:
+                d = t.detach().double()
+                sums.append(d.sum())
+                sums.append((d * d).sum())
+    vec = torch.stack(sums)
+    allv = torch.empty(world, vec.numel(), dtype=vec.dtype, device=dev)
+    dist.all_gather_into_tensor(allv.view(-1), vec)
+    ref = allv[0]
+    diff = (allv - ref).abs() / ref.abs().clamp_min(1e-30)
+    rel = float(diff.max().item())
+    exact = bool((allv == ref).all().item())
+    return {"dp_in_sync": rel <= 1e-9, "dp_bitwise_equal": exact, "dp_max_rel_diff": rel,
+            "dp_checksums": int(vec.numel()), "dp_world_size": dist.get_world_size()}
 
 
 if __name__ == "__main__":

@@ -384,19 +384,24 @@ int nr_score_fwd(const float* cdd, int64_t ldc, const int64_t* cdd_idx, const fl
 
 /* The training head with its loss: logits = log_softmax(cdd_row(b,c) · user[b] / sqrt(H)) as
  * nr_score_fwd (NR_SCORE_LOG_SOFTMAX) AND loss[0] = mean_b -logits[b][label[b]] -- Manager.py:641's
- * NLLLoss (reduction 'mean') on TwoTowerBaseModel.forward's output, in one launch (no separate loss
- * kernels, no zero fill): one workgroup per impression, the last to finish sums the B loss terms
- * in a fixed order.  work: nr_score_nll_workspace(B) int32, all zero before the first call; every
- * call leaves its first word zero again (the rest is scratch), so one buffer serves every call on
- * a stream. */
+ * NLLLoss (torch.nn.NLLLoss() defaults: reduction 'mean', ignore_index -100) on
+ * TwoTowerBaseModel.forward's output, in one launch (no separate loss kernels, no zero fill): one
+ * workgroup per impression, the last to finish forms the mean over the labels in [0, C) in a fixed
+ * order (labels -100 are ignored: no term, not counted; all ignored -> NaN, torch's 0/0).  A label
+ * outside [0, C) other than -100 (torch raises) makes the loss NaN and sets work[1] to 1 -- a sticky
+ * status the caller reads and clears itself.  work: nr_score_nll_workspace(B) int32,
+ * all zero before the first call; every call leaves work[0] zero again (work[1] is the status, the
+ * rest scratch), so one buffer serves every call on a stream.  Calls on one buffer must not run
+ * concurrently. */
 int nr_score_nll_fwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
                      const int64_t* label, int64_t B, int32_t C, int32_t H, float* logits, float* loss,
                      int32_t* work, hipStream_t stream);
 /* int32 elements of nr_score_nll_fwd's work buffer for B impressions */
 int64_t nr_score_nll_workspace(int64_t B);
 
-/* Backward of nr_score_nll_fwd: the gradient of the loss (dloss, a device scalar, or NULL) plus an
- * optional gradient of the logits themselves (dlogits [B][C] or NULL). */
+/* Backward of nr_score_nll_fwd: the gradient of the loss (dloss, a device scalar, or NULL; spread
+ * over the labels in [0, C) as 1/count each) plus an optional gradient of the logits themselves
+ * (dlogits [B][C] or NULL). */
 int nr_score_nll_bwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
                      const float* logits, const int64_t* label, const float* dloss,
                      const float* dlogits, int64_t B, int32_t C, int32_t H, float* dcdd, int64_t lddc,

@@ -10,7 +10,8 @@
 //   * 256 x BN tile (BN = 256 or 128), 8 waves (512 threads), wave tile 128x64 or 64x64: each loaded
 //     element feeds twice the MFMAs, halving the split work per MFMA;
 //   * 16-deep k-tiles, LDS DOUBLE-buffered ([stage][plane][row][24] bf16, 48-B rows: ds_read_b128
-//     fragments conflict-free), ONE barrier per k-tile: while the waves run k-tile P's MFMAs from
+//     fragments conflict-free; the K-contiguous split-stores conflict-free by their row order,
+//     BigKC), ONE barrier per k-tile: while the waves run k-tile P's MFMAs from
 //     one stage, the same waves split k-tile P+1 (already in registers) into the other stage and
 //     issue the global loads of P+2, so the VALU / LDS-store / load work is interleaved with the
 //     MFMA stream of the same wave instead of being serialised between barriers;
@@ -34,20 +35,33 @@ constexpr int big_bk() { return NP == 1 && is_kc(AM) && is_kc(BMODE) ? 32 : 16; 
 template <int BK>
 constexpr int big_sr() { return BK + 8; }
 
-// K-contiguous operand, R rows x BK k: 512 threads x (R BK / 2048) float4 (row f / (BK / 4), k
-// quad f % (BK / 4))
+// K-contiguous operand, R rows x BK k: 512 threads x (R BK / 2048) float4.  Float4 f holds k quad
+// quad_of(f) of tile row row_of(f); each 64-float4 block covers 64 / QPR consecutive rows.  The
+// split-stores are ds_write_b64 (one 4-k bf16 quad per plane), serviced in four 16-lane groups over
+// 32 banks (MI355X_MICROARCH.md §LDS): a group must cover 32 distinct banks.  With rows of SR bf16
+// (12 dwords at BK = 16, 20 at BK = 32) a group of consecutive rows wraps onto itself (rows 0 and 3
+// share banks 4-7 at BK = 16; rows 0 and 1 banks 0-3 at BK = 32: the 2-way conflicts the round-3
+// PMC counted, ~2 extra cycles per LDS instruction), so a group takes rows 12 dwords x {0, 2, 4, 6}
+// = {0, 24, 16, 8} mod 32 apart (BK = 16: rows of one parity) or 20 x {0, 4} = {0, 16} (BK = 32).
 template <int R, int MODE, int BK>
 struct BigKC {
   static constexpr int QPR = BK / 4;           // float4 per row
   static constexpr int NV = R * QPR / 512;
   static constexpr int SR = big_sr<BK>();
+  static_assert(QPR == 4 || QPR == 8, "BigKC: 16- or 32-deep k-tiles");
   float4 v[2][NV];   // two register sets: k-tile t lives in set t % 2 (loads issued 3 tiles ahead)
   const float* rowp[NV];
+  __device__ __forceinline__ static int row_of(int f) {
+    const int l = f & 63, g = l >> 4;
+    return QPR == 4 ? 16 * (f >> 6) + 8 * (g >> 1) + (g & 1) + 2 * ((l >> 2) & 3)
+                    : 8 * (f >> 6) + g + 4 * ((l >> 3) & 1);
+  }
+  __device__ __forceinline__ static int quad_of(int f) { return f & (QPR - 1); }
   __device__ __forceinline__ void init(const Op& d, int64_t r0, int64_t rlim, int tid) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int f = tid + 512 * i;
-      int64_t row = r0 + f / QPR;
+      int64_t row = r0 + row_of(f);
       row = row < rlim ? row : rlim - 1;   // clamp: rows >= M are computed and discarded
       rowp[i] = MODE == KC_GATHER ? d.base + d.idx[row] * d.ld : d.base + row * d.ld;
     }
@@ -59,7 +73,7 @@ struct BigKC {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int f = tid + 512 * i;
-      v[S][i] = *reinterpret_cast<const float4*>(rowp[i] + k0 + 4 * (f % QPR));
+      v[S][i] = *reinterpret_cast<const float4*>(rowp[i] + k0 + 4 * quad_of(f));
     }
   }
   template <int S, int NP>
@@ -68,7 +82,7 @@ struct BigKC {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int f = tid + 512 * i;
-      uint16_t* q = lds + (f / QPR) * SR + 4 * (f % QPR);
+      uint16_t* q = lds + row_of(f) * SR + 4 * quad_of(f);
       const float4 x = v[S][i];
       if constexpr (NP == 1) {
         *reinterpret_cast<uint2*>(q) = hi4(x.x, x.y, x.z, x.w);

@@ -108,6 +108,14 @@ inline int capped_slots(int slots, int max_cus) {
   return per * max_cus;
 }
 
+// K-contiguous 32-deep tile: float4 f (of R x 8) holds k quad kc_quad(f) of row kc_row(f).  Each
+// 64-float4 block covers 8 rows; the lanes of one 16-lane ds_write_b64 group take rows g and g + 4
+// (SROW = 20 dwords: 0 and 16 mod 32), so the split-stores hit 32 distinct banks (consecutive rows
+// 0 and 1 would share banks 0-3; MI355X_MICROARCH.md §LDS).  Each 8-lane group is one whole row, so
+// the fp32 image's ds_write_b128 stays conflict-free too.
+__device__ __forceinline__ int kc_row(int f) { return 8 * (f >> 6) + ((f & 63) >> 4) + 4 * ((f >> 3) & 1); }
+__device__ __forceinline__ int kc_quad(int f) { return f & 7; }
+
 // Register-staged tile loader for an operand of R rows (the M or N extent) x 32 k.
 template <int R, int MODE>
 struct Loader {
@@ -129,7 +137,7 @@ struct Loader {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         const int f = tid + 256 * i;
-        int64_t row = r0 + (f >> 3);
+        int64_t row = r0 + kc_row(f);
         row = row < rlim ? row : rlim - 1;                  // clamp: rows >= M are discarded
         if (MODE == KC_PLAIN) rowp[i] = d.base + row * d.ld;
         if (MODE == KC_GATHER) rowp[i] = d.base + d.idx[row] * d.ld;
@@ -171,7 +179,7 @@ struct Loader {
     for (int i = 0; i < NV; ++i) {
       const int f = tid + 256 * i;
       if (KC) {
-        const int kq = f & 7;
+        const int kq = kc_quad(f);
         const int64_t k = k0 + 4 * kq;
         const float* p = rowp[i] + k;
         const bool ok = MODE != KC_CONV3 || ((okbits >> i) & 1u);
@@ -225,7 +233,7 @@ struct Loader {
     for (int i = 0; i < NV; ++i) {
       const int f = tid + 256 * i;
       if (KC) {
-        *reinterpret_cast<float4*>(&lds[(f >> 3) * 36 + 4 * (f & 7)]) = v[i];
+        *reinterpret_cast<float4*>(&lds[kc_row(f) * 36 + 4 * kc_quad(f)]) = v[i];
       } else {
         constexpr int CPR = R / 4;
         *reinterpret_cast<float4*>(&lds[(f / CPR) * S + 4 * (f % CPR)]) = v[i];
@@ -241,7 +249,7 @@ struct Loader {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         const int f = tid + 256 * i;
-        uint16_t* q = lds + (f >> 3) * SROW + 4 * (f & 7);
+        uint16_t* q = lds + kc_row(f) * SROW + 4 * kc_quad(f);
         if constexpr (NP == 1) {
           *reinterpret_cast<uint2*>(q) = hi4(v[i].x, v[i].y, v[i].z, v[i].w);
         } else {

@@ -84,11 +84,17 @@ __global__ __launch_bounds__(256) void score_bwd_kernel(const float* cdd, int64_
   }
 }
 
-// Training head + NLLLoss (Manager.py:641, reduction 'mean') in one launch: workgroup b forms the C
-// scores of impression b (one wave per candidate dot product), their log-softmax and its loss term
-// part[b]; the workgroup that arrives last (agent-scope release + ticket, acquire:
-// cdna_hip_programming.md §6 Guideline 16's counter form) sums the B terms in a fixed order
-// (deterministic) and resets the ticket, so `work` is zero again on return.
+// Training head + NLLLoss (Manager.py:641, torch.nn.NLLLoss(): reduction 'mean', ignore_index -100)
+// in one launch: workgroup b forms the C scores of impression b (one wave per candidate dot product),
+// their log-softmax, its loss term part[b] and its weight wt[b] (1 for a label in [0, C), 0 for the
+// ignored label -100, NaN for any other label); the workgroup that arrives last (agent-scope release +
+// ticket, acquire: cdna_hip_programming.md §6 Guideline 16's counter form) forms sum(part) / sum(wt)
+// in a fixed order (deterministic: torch's weighted mean -- NaN when every label is ignored, as 0/0 --
+// and NaN for an out-of-range label, where torch raises) and resets the ticket.  work[0] is the ticket
+// (zero again on return), work[1] a sticky status: non-zero once a label outside [0, C) other than
+// -100 was seen (read and cleared by the host, nr_score_nll_workspace's layout).
+constexpr int64_t kIgnoreIndex = -100;
+
 __global__ __launch_bounds__(1024) void score_nll_fwd_kernel(const float* cdd, int64_t ldc, const float* user,
                                                              int64_t ldu, const int64_t* label, int B, int C, int H,
                                                              float scale, float* logits, float* loss,
@@ -97,6 +103,7 @@ __global__ __launch_bounds__(1024) void score_nll_fwd_kernel(const float* cdd, i
   __shared__ int last;
   const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6;
   float* part = reinterpret_cast<float*>(work + 4);
+  float* wt = part + B;
   const float* u = user + (int64_t)b * ldu;
   for (int c = w; c < C; c += nw) {
     const float* x = cdd + ((int64_t)b * C + c) * ldc;
@@ -116,7 +123,10 @@ __global__ __launch_bounds__(1024) void score_nll_fwd_kernel(const float* cdd, i
     for (int c = lane; c < C; c += 64) logits[(int64_t)b * C + c] = sc[c] - lse;
     if (lane == 0) {
       const int64_t y = label[b];
-      part[b] = (y >= 0 && y < C) ? -(sc[y] - lse) : 0.f;   // out-of-range labels: no term
+      const bool ok = y >= 0 && y < C;
+      part[b] = ok ? -(sc[y] - lse) : 0.f;
+      wt[b] = ok ? 1.f : (y == kIgnoreIndex ? 0.f : __int_as_float(0x7fc00000));
+      if (!ok && y != kIgnoreIndex) __hip_atomic_store(&work[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -133,17 +143,22 @@ __global__ __launch_bounds__(1024) void score_nll_fwd_kernel(const float* cdd, i
   }
   __syncthreads();
   if (!last || w != 0) return;
-  float s = 0.f;   // fixed-order sum of the B terms
-  for (int r = lane; r < B; r += 64) s += part[r];
+  float s = 0.f, n = 0.f;   // fixed-order sums of the B terms and weights
+  for (int r = lane; r < B; r += 64) {
+    s += part[r];
+    n += wt[r];
+  }
   s = nr_wave_sum(s);
+  n = nr_wave_sum(n);
   if (lane == 0) {
-    loss[0] = s / (float)B;
+    loss[0] = s / n;
     __hip_atomic_store(&work[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-// Backward of score_nll_fwd_kernel: d logits = dlogits (optional) - dloss / B at the label, then the
-// log-softmax and dot-product backward (as score_bwd_kernel), one workgroup per impression.
+// Backward of score_nll_fwd_kernel: d logits = dlogits (optional) - dloss / n at the label (n = the
+// labels in [0, C), counted by each workgroup; ignored labels get no term), then the log-softmax
+// and dot-product backward (as score_bwd_kernel), one workgroup per impression.
 __global__ __launch_bounds__(256) void score_nll_bwd_kernel(const float* cdd, int64_t ldc, const float* user,
                                                             int64_t ldu, const float* logits, const int64_t* label,
                                                             const float* dloss, const float* dlogits, int B, int C,
@@ -153,7 +168,15 @@ __global__ __launch_bounds__(256) void score_nll_bwd_kernel(const float* cdd, in
   const int b = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   if (w == 0) {
     const int64_t y = label[b];
-    const float gl = dloss ? -dloss[0] / (float)B : 0.f;
+    float gl = 0.f;
+    if (dloss) {
+      float n = 0.f;
+      for (int r = lane; r < B; r += 64) {
+        const int64_t yr = label[r];
+        n += (yr >= 0 && yr < C) ? 1.f : 0.f;
+      }
+      gl = -dloss[0] / nr_wave_sum(n);
+    }
     float sg = 0.f;
     for (int c = lane; c < C; c += 64) {
       const int64_t o = (int64_t)b * C + c;
@@ -297,8 +320,11 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
       const int64_t i = base / 4 + u * 256 + threadIdx.x;
       pp[u] = reinterpret_cast<const float4*>(e.p)[i];
       // rows flagged untouched hold zeros: skip their gradient read (a float4 that reaches into a
-      // touched row is read whole -- the untouched part reads as the zeros it holds)
-      const bool rd = !e.rt || e.rt[(4 * i) / e.rlen] || e.rt[(4 * i + 3) / e.rlen];
+      // touched row is read whole -- the untouched part reads as the zeros it holds).  The float4
+      // spans rows (4i) / rlen .. (4i + 3) / rlen: all of them when rows are shorter than 4
+      bool rd = !e.rt;
+      if (!rd)
+        for (int64_t r = (4 * i) / e.rlen; r <= (4 * i + 3) / e.rlen && !rd; ++r) rd = e.rt[r] != 0;
       gg[u] = rd ? reinterpret_cast<const float4*>(e.g)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
       mm[u] = reinterpret_cast<const float4*>(e.m)[i];
       vv[u] = reinterpret_cast<const float4*>(e.v)[i];
@@ -497,7 +523,7 @@ extern "C" int nr_score_nll_fwd(const float* cdd, int64_t ldc, const float* user
   return NR_OK;
 }
 
-extern "C" int64_t nr_score_nll_workspace(int64_t B) { return 4 + (B < 0 ? 0 : B); }
+extern "C" int64_t nr_score_nll_workspace(int64_t B) { return 4 + 2 * (B < 0 ? 0 : B); }
 
 extern "C" int nr_score_nll_bwd(const float* cdd, int64_t ldc, const float* user, int64_t ldu,
                                 const float* logits, const int64_t* label, const float* dloss,
@@ -596,6 +622,8 @@ extern "C" int nr_colsum_ws(const float* x, int64_t ldx, int64_t rows, int64_t c
 namespace {
 int adam_multi_launch(AdamMulti& a, int64_t blocks, hipStream_t stream) {
   if (a.count == 0) return NR_OK;
+  // only empty tensors (ticket launches): one block with no elements advances their step counts
+  if (blocks == 0) blocks = 1;
   a.blk_off[a.count] = (int32_t)blocks;
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a);
   NR_LAUNCH_CHECK();
@@ -621,7 +649,10 @@ int adam_multi_impl(const nr_adam_tensor* tensors, int32_t count, float beta1, f
   int64_t blocks = 0;
   for (int32_t t = 0; t < count; ++t) {
     const nr_adam_tensor& d = tensors[t];
-    if (d.n == 0) continue;
+    // an empty tensor has no work; with a ticket it still takes an entry (no blocks) so that the
+    // launch advances its device step count, as torch's capturable Adam does for every parameter
+    // with a gradient
+    if (d.n == 0 && !(ticket && d.step_dev)) continue;
     const int64_t nb = (d.n + kAdamChunk - 1) / kAdamChunk;
     if (a.count == kAdamMulti || blocks + nb > 0x7fffffff) {
       const int rc = adam_multi_launch(a, blocks, stream);

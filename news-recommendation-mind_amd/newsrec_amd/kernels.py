@@ -161,6 +161,40 @@ def self_cleaning_workspace(dev, name, n):
     return ws
 
 
+def self_cleaning_check(dev=None, reset=False):
+    """Debug check of the self-cleaning workspaces: every kernel using one leaves its counters zero,
+    so after a synchronize they must all read zero (the score_nll buffer's word 1, a sticky label
+    status, excepted).  A launch that never completed, or two launches on one buffer from concurrent
+    streams, leaves a counter set and silently corrupts later calls: -> the names of the buffers found
+    non-zero; ``reset``: zero them again (after an error)."""
+    torch.cuda.synchronize()
+    bad = []
+    for (d, name), ws in _SELF_CLEANING.items():
+        if dev is not None and d != torch.device(dev):
+            continue
+        w = ws.clone()
+        if name == "nr_score_nll_fwd":
+            w[1] = 0
+        if bool((w != 0).any().item()):
+            bad.append(name)
+            if reset:
+                ws.zero_()
+    return bad
+
+
+def score_nll_status(dev, clear=True):
+    """The sticky label status of nr_score_nll_fwd on ``dev`` (True: some call since the last check
+    saw a label outside [0, C) other than the ignored -100 and returned a NaN loss, where
+    torch.nn.functional.nll_loss raises).  Reads the device (synchronises)."""
+    ws = _SELF_CLEANING.get((torch.device(dev), "nr_score_nll_fwd"))
+    if ws is None:
+        return False
+    bad = bool(ws[1].item() != 0)
+    if bad and clear:
+        ws[1].zero_()
+    return bad
+
+
 class UniqueRows:
     """Distinct ids of a token batch (``nr_unique_rows``), sizes left on the device.
 

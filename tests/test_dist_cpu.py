@@ -238,3 +238,108 @@ def test_grad_sync_deferred_wgrad_gloo_world2():
         assert set(g) == set(want), (set(g), set(want))
         for n in want:
             torch.testing.assert_close(torch.from_numpy(g[n]), want[n], rtol=1e-6, atol=1e-6)
+
+
+def _dense_rows_worker(rank, world, port, q):
+    """GradSync(sparse_tables=False): the row-sparse user-table gradient goes through the dense
+    all-reduce, so functions.LOCAL_ROW_GRAD (the single-process row buffer + Adam row flags) must
+    stand aside -- its flags would miss the rows other ranks touched."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    D.setup(rank, world, backend="gloo", master_port=str(port))
+    try:
+        model = Tiny()
+        x = torch.tensor([rank, rank + 3, 7])
+        sync = D.GradSync(model, bucket_mb=1e-4, sparse_tables=False)
+
+        class UserRows(torch.autograd.Function):   # RNNUserFn's table gradient order of hooks
+            @staticmethod
+            def forward(ctx, table, idx):
+                ctx.save_for_backward(idx)
+                ctx.table_ref = table
+                return table[idx]
+
+            @staticmethod
+            def backward(ctx, g):
+                (idx,) = ctx.saved_tensors
+                if F.SPARSE_GRAD_HOOK(ctx.table_ref, idx, g) or F.LOCAL_ROW_GRAD(ctx.table_ref, idx, g):
+                    return None, None
+                return torch.zeros_like(ctx.table_ref).index_add_(0, idx, g), None
+        model.zero_grad(set_to_none=True)
+        u = torch.tensor([int(x[0]) * 7 % 50, 3, 3])
+        out = model.lin2(model.lin(model.table[x] + UserRows.apply(model.users, u)))
+        (out ** 2).sum().backward()
+        assert getattr(model.users, "_nr_row_touched", None) is None
+        scale = sync()
+        sync.close()
+        q.put((rank, None, {n: (p.grad * scale).numpy().copy() for n, p in model.named_parameters()}))
+    except Exception as e:
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e), None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_local_row_grad_stands_aside_under_dense_sync_gloo_world2():
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_dense_rows_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    want = {}
+    for r in range(world):
+        m = Tiny()
+        _grads(m, torch.tensor([r, r + 3, 7]), use_hook=False)
+        for n, p in m.named_parameters():
+            want[n] = want.get(n, 0) + p.grad / world
+    for rank, err, g in res:
+        assert err is None, err
+        for n in want:
+            torch.testing.assert_close(torch.from_numpy(g[n]), want[n], rtol=1e-6, atol=1e-6)
+
+
+def _dp_check_worker(rank, world, port, q, diverge):
+    """bench.dp_check: float64 checksums of parameters and Adam moments compared across ranks."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    D.setup(rank, world, backend="gloo", master_port=str(port))
+    try:
+        model = Tiny()
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+        for p in model.parameters():
+            p.grad = torch.ones_like(p)
+        opt.step()
+        if diverge and rank == 1:
+            with torch.no_grad():
+                model.lin.bias[0] += 1e-3
+        q.put((rank, None, bench.dp_check(model, opt, world, torch.device("cpu"))))
+    except Exception as e:
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e), None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("diverge", [False, True])
+def test_bench_dp_check_gloo_world2(diverge):
+    world, port = 2, _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_dp_check_worker, args=(r, world, port, q, diverge)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, err, out in res:
+        assert err is None, err
+        assert out["dp_world_size"] == 2
+        assert out["dp_in_sync"] is (not diverge)
+        assert out["dp_bitwise_equal"] is (not diverge)

@@ -4,7 +4,10 @@ history, 30-token titles — the bench's exact kernels (the 256x256 persistent b
 distinct-row projection, the fused attention kernels, the split backward, Adam) — against the fp32 CPU oracle
 (oracle/restatement.py, which tests/test_oracle_golden.py pins to the reference's goldens):
 
-* logits within the north star's 1e-3 (models/TwoTowerBaseModel.py:65-75), the loss;
+* logits within the north star's 1e-3 (models/TwoTowerBaseModel.py:65-75), the loss — through the
+  head bench.py times (``TwoTowerBaseModel.forward_loss``: scorer + log-softmax + NLLLoss fused,
+  nr_score_nll_*), on a host-fed ragged batch AND on a batch formed on the device by
+  bench.DeviceFeed (nr_form_train_batch, the timed step's own input path);
 * the word-table, projection and every other gradient within 1e-3 of each one's max magnitude;
 * every parameter after one Adam step (Manager.py:404-413,647);
 * the same step replayed as a HIP graph (bench.GraphedStep) against eager steps;
@@ -57,6 +60,17 @@ def _batch(seed):
     return x
 
 
+def _device_batch(dev):
+    """One batch formed on the device exactly as the timed steps form theirs (bench.DeviceFeed:
+    nr_form_train_batch over a resident MIND-shaped train split, negatives from the device RNG);
+    -> (device batch, host copy for the oracle)."""
+    import bench
+    feed = bench.DeviceFeed(dev, 1, 0, n_impr=4096)
+    x = {k: v.clone() for k, v in feed.form().items()}
+    feed.store.check_status()
+    return x, {k: v.cpu() for k, v in x.items()}
+
+
 def _oracle_params(model):
     return {n: p.detach().cpu().clone().requires_grad_(True) for n, p in model.named_parameters()}
 
@@ -73,19 +87,25 @@ def _close_grads(model, P, names=None, rel=1e-3):
         assert err <= rel * scale, (n, err, scale)
 
 
-def test_nrms_fullsize_step_vs_oracle():
+@pytest.mark.parametrize("feed", ["host", "device"])
+def test_nrms_fullsize_step_vs_oracle(feed):
+    """bench.forward_backward's path: forward_loss (fused scorer + log-softmax + NLL) and backward."""
+    import bench
     from newsrec_amd.manager import get_optim
     dev = torch.device("cuda", 0)
     model = _nrms(dev)
     model.train()
-    x = _batch(1)
-    xg = {k: v.to(dev) for k, v in x.items()}
+    if feed == "host":
+        x = _batch(1)
+        xg = {k: v.to(dev) for k, v in x.items()}
+    else:
+        xg, x = _device_batch(dev)
     P = _oracle_params(model)
     opt = get_optim(model)
+    # bench.forward_backward, keeping the logits
     opt.zero_grad(set_to_none=True)
-    logits, _ = model(xg)
-    loss = F.nll_loss(logits, xg["label"])
-    loss.backward()
+    logits, loss = model.forward_loss(xg)
+    loss.backward(bench._one(loss))
     opt.step()
     torch.cuda.synchronize()
     want_loss, want_logits, _ = R.train_step(P, x, "mha", "mha")

@@ -68,3 +68,77 @@ def test_adam_skips_untouched_rows_exactly():
         outs.append((p, m, v))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("rlen", [1, 2, 3, 5])
+def test_adam_row_flags_short_rows(rlen):
+    """Rows shorter than a float4: a float4 of the gradient spans up to four rows and is
+    read when ANY of them is flagged -- bitwise the dense update, one touched row in four."""
+    from newsrec_amd import kernels as K
+    torch.manual_seed(2)
+    rows = 4096
+    flags = torch.zeros(rows, dtype=torch.uint8, device="cuda")
+    flags[1::4] = 1
+    g = torch.randn(rows, rlen, device="cuda") * flags[:, None].float()
+    p0 = torch.randn(rows, rlen, device="cuda")
+    m0 = torch.randn(rows, rlen, device="cuda").abs() * 0.01
+    v0 = torch.randn(rows, rlen, device="cuda").abs() * 0.001
+    outs = []
+    for use_flags in (True, False):
+        p, m, v = p0.clone(), m0.clone(), v0.clone()
+        K.adam_multi([(p, g, m, v, 1e-3, 2) + ((flags,) if use_flags else ())], 0.9, 0.999, 1e-8, 0.0, 1.0)
+        torch.cuda.synchronize()
+        outs.append((p, m, v))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_adam_step_advances_empty_tensors():
+    """nr_adam_multi_step (capturable Adam): the device step count of an EMPTY parameter advances
+    too, as torch's capturable Adam increments every parameter with a gradient; a launch
+    of only empty tensors advances theirs."""
+    from newsrec_amd import kernels as K
+    p = torch.randn(1000, device="cuda")
+    g = torch.randn(1000, device="cuda")
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    e = torch.empty(0, device="cuda")
+    s_full = torch.zeros((), dtype=torch.int64, device="cuda")
+    s_empty = torch.zeros((), dtype=torch.int64, device="cuda")
+    lr = torch.full((), 1e-3, device="cuda")
+    for _ in range(3):
+        K.adam_multi([(p, g, m, v, lr, s_full), (e, e, e.clone(), e.clone(), lr, s_empty)], 0.9, 0.999, 1e-8,
+                     0.0, 1.0, advance_steps=True)
+    s_only = torch.zeros((), dtype=torch.int64, device="cuda")
+    K.adam_multi([(e, e, e.clone(), e.clone(), lr, s_only)], 0.9, 0.999, 1e-8, 0.0, 1.0, advance_steps=True)
+    torch.cuda.synchronize()
+    assert int(s_full) == 3 and int(s_empty) == 3 and int(s_only) == 1
+    assert K.self_cleaning_check("cuda") == []
+
+
+def test_score_nll_label_semantics():
+    """The fused head's loss follows torch.nn.NLLLoss: label -100 is ignored (no term, not
+    in the mean's count, no gradient), the mean divides by the counted labels; an out-of-range label
+    gives a NaN loss and sets the sticky status (torch raises)."""
+    from newsrec_amd import kernels as K
+    from newsrec_amd.functions import ScoreNLLFn
+    torch.manual_seed(3)
+    B, C, H = 8, 5, 64
+    cdd = torch.randn(B * C, H, device="cuda", requires_grad=True)
+    user = torch.randn(B, H, device="cuda", requires_grad=True)
+    label = torch.tensor([0, 1, -100, 4, 0, -100, 2, 3], device="cuda")
+    logits, loss = ScoreNLLFn.apply(cdd, user, B, C, label)
+    loss.backward()
+    c2 = cdd.detach().clone().requires_grad_(True)
+    u2 = user.detach().clone().requires_grad_(True)
+    s = (c2.view(B, C, H) * u2[:, None]).sum(-1) / H ** 0.5
+    want = torch.nn.functional.nll_loss(torch.log_softmax(s, -1), label)
+    want.backward()
+    torch.testing.assert_close(loss, want, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(cdd.grad, c2.grad, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(user.grad, u2.grad, rtol=1e-4, atol=1e-6)
+    assert not K.score_nll_status("cuda")
+    _, bad = ScoreNLLFn.apply(cdd.detach(), user.detach(), B, C, torch.tensor([0, 1, 7, 0, 0, 0, 0, 0], device="cuda"))
+    assert torch.isnan(bad).item()
+    assert K.score_nll_status("cuda")            # seen, and cleared by the read
+    assert not K.score_nll_status("cuda")
+    assert K.self_cleaning_check("cuda") == []
