@@ -277,11 +277,12 @@ int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows, const voi
 
 /* Backward of nr_mha_pool_fwd: writes dy [T][heads*(dk+dv)] and ATOMICALLY ACCUMULATES dbias
  * (= column sums of dy), dq, dgamma, dbeta (caller zeroes).  dy stays per token (row t) when
- * yrows is given; rows of masked tokens are exactly zero.  With o (the forward's oout) the
+ * yrows is given; rows of masked tokens are exactly zero.  With o (the forward's oout) and dob the
  * backward runs split: a per-title pooling/LN pass writes dO into dob [T][heads*dv] (caller's
- * workspace), then a per-(title, head) attention pass at high occupancy; without o one fused
- * kernel recomputes the attention.
- * ws (optional, split form only): ws_copies x ceil4(3*heads*dv + heads*(dk+dv)) floats, ZERO on entry
+ * workspace), then a per-(title, head) attention pass at high occupancy; with o and dob NULL one
+ * fused kernel per title loads the saved O, keeps dO in LDS and runs every head's attention
+ * backward; without o the fused kernel recomputes the attention.
+ * ws (optional, forms with o only): ws_copies x ceil4(3*heads*dv + heads*(dk+dv)) floats, ZERO on entry
  * and left zero on return -- workgroups spread their dgamma / dbeta / dq / dbias atomics over the
  * copies (one address per title would serialise them at L2) and a last kernel adds the copy sums
  * into the outputs. */

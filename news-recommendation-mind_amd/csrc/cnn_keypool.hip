@@ -45,8 +45,12 @@ struct KPArgs {
   int64_t nws;
 };
 
+// 16-B aligned: without it hipcc cannot prove the float4 row reads / writes aligned and splits each
+// into ds_read2_b32 / ds_write2_b32, whose 32-bank addressing puts the 32 rows of one column (row
+// stride Hp + 4 = 164 dwords, 4 mod 32) on 8 banks: the 7.45 (fwd) / 3.49 (bwd) extra LDS cycles per
+// instruction of the round-3 PMC (profiles/r03_l_pmc_keypool_*.json)
 template <int NB>
-struct KPShared {
+struct alignas(16) KPShared {
   static constexpr int HP = 32 * NB, SW = HP + 4;
   float ct[32][SW];   // C tile (rows >= L zero)
   float dk[32][SW];   // bwd: dK tile; fwd: K_j q_j products
@@ -188,7 +192,7 @@ __global__ __launch_bounds__(64 * KP_BW) void cnn_keypool_bwd_kernel(KPArgs g) {
   constexpr int Q4 = 8 * NB;            // float4 per C row
   constexpr int TPF = (32 * Q4 + 64 * KP_BW - 1) / (64 * KP_BW);   // C-tile float4 per thread
   __shared__ KPShared<NB> sm;
-  __shared__ float wacc[NB * NB][16][64];   // dWq block b: rows 32 jb + crow(r, h), columns 32 kb + c
+  __shared__ __attribute__((aligned(16))) float wacc[NB * NB][16][64];   // dWq block b: rows 32 jb + crow(r, h), columns 32 kb + c
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
   const bool colw = w < NB;
   const int d = w - NB;                 // dWq wave index (when !colw)

@@ -76,24 +76,33 @@ struct BigKC {
       v[S][i] = *reinterpret_cast<const float4*>(rowp[i] + k0 + 4 * quad_of(f));
     }
   }
+  // float4 i of register set S -> its plane slots
+  template <int S, int NP>
+  __device__ __forceinline__ void store_one(uint16_t* lds, int tid, int i) const {
+    constexpr int PL = R * SR;   // one plane
+    const int f = tid + 512 * i;
+    uint16_t* q = lds + row_of(f) * SR + 4 * quad_of(f);
+    const float4 x = v[S][i];
+    if constexpr (NP == 1) {
+      *reinterpret_cast<uint2*>(q) = hi4(x.x, x.y, x.z, x.w);
+    } else {
+      uint2 p0, p1, p2;
+      split4(x.x, x.y, x.z, x.w, p0, p1, p2);
+      *reinterpret_cast<uint2*>(q) = p0;
+      *reinterpret_cast<uint2*>(q + PL) = p1;
+      *reinterpret_cast<uint2*>(q + 2 * PL) = p2;
+    }
+  }
   template <int S, int NP>
   __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
-    constexpr int PL = R * SR;   // one plane
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int f = tid + 512 * i;
-      uint16_t* q = lds + row_of(f) * SR + 4 * quad_of(f);
-      const float4 x = v[S][i];
-      if constexpr (NP == 1) {
-        *reinterpret_cast<uint2*>(q) = hi4(x.x, x.y, x.z, x.w);
-      } else {
-        uint2 p0, p1, p2;
-        split4(x.x, x.y, x.z, x.w, p0, p1, p2);
-        *reinterpret_cast<uint2*>(q) = p0;
-        *reinterpret_cast<uint2*>(q + PL) = p1;
-        *reinterpret_cast<uint2*>(q + 2 * PL) = p2;
-      }
-    }
+    for (int i = 0; i < NV; ++i) store_one<S, NP>(lds, tid, i);
+  }
+  // piece p of PIECES equal parts of store() (the interleaved k-tile spreads them between MFMAs)
+  static constexpr int PIECES = NV;
+  template <int S, int NP>
+  __device__ __forceinline__ void store_piece(uint16_t* lds, int tid, int p) const {
+    store_one<S, NP>(lds, tid, p);
   }
 };
 
@@ -197,25 +206,39 @@ struct BigMN {
   // 2-way conflict on every write).  Column groups with cg ^ (cg >> 1) odd write their rows in the
   // order 2, 3, 0, 1 instead, which puts the four windows 8 banks apart: conflict-free.  (The float4
   // halves are swapped to match: 4 selects per float4.)
+  // chunk j's rows 2 half .. 2 half + 1 (half 0: rows 0, 1 or 2, 3 per the rotation below)
+  template <int S, int NP>
+  __device__ __forceinline__ void store_half(uint16_t* lds, int tid, int j, int half) const {
+    if (tid >= ACT) return;
+    const int c = tid + 512 * j;
+    const int cg = cg_of(c);
+    const bool rot = BK == 16 && ((cg ^ (cg >> 1)) & 1) != 0;
+    uint16_t* q = lds + (4 * cg) * SR + 2 * kp_of(c);
+    const float4 a = v[S][j][0], b = v[S][j][1];
+    if (half == 0) {
+      uint16_t* qa = q + (rot ? 2 * SR : 0);   // rows 0, 1 (or 2, 3)
+      put<NP>(qa, rot ? a.z : a.x, rot ? b.z : b.x);
+      put<NP>(qa + SR, rot ? a.w : a.y, rot ? b.w : b.y);
+    } else {
+      uint16_t* qb = q + (rot ? 0 : 2 * SR);   // rows 2, 3 (or 0, 1)
+      put<NP>(qb, rot ? a.x : a.z, rot ? b.x : b.z);
+      put<NP>(qb + SR, rot ? a.y : a.w, rot ? b.y : b.w);
+    }
+  }
+  // Chunk (column group cg, k pair kp) writes its four rows 4cg .. 4cg + 3 as four ds_write_b32 per
+  // plane (see store_half for the order).
   template <int S, int NP>
   __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
-    if (tid >= ACT) return;
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-      const int c = tid + 512 * j;
-      const int cg = cg_of(c);
-      const bool rot = BK == 16 && ((cg ^ (cg >> 1)) & 1) != 0;
-      uint16_t* q = lds + (4 * cg) * SR + 2 * kp_of(c);
-      uint16_t* qa = q + (rot ? 2 * SR : 0);   // rows 0, 1 (or 2, 3)
-      uint16_t* qb = q + (rot ? 0 : 2 * SR);   // rows 2, 3 (or 0, 1)
-      const float4 a = v[S][j][0], b = v[S][j][1];
-      const float a0 = rot ? a.z : a.x, a1 = rot ? a.w : a.y, a2 = rot ? a.x : a.z, a3 = rot ? a.y : a.w;
-      const float b0 = rot ? b.z : b.x, b1 = rot ? b.w : b.y, b2 = rot ? b.x : b.z, b3 = rot ? b.y : b.w;
-      put<NP>(qa, a0, b0);
-      put<NP>(qa + SR, a1, b1);
-      put<NP>(qb, a2, b2);
-      put<NP>(qb + SR, a3, b3);
+      store_half<S, NP>(lds, tid, j, 0);
+      store_half<S, NP>(lds, tid, j, 1);
     }
+  }
+  static constexpr int PIECES = 2 * NC;
+  template <int S, int NP>
+  __device__ __forceinline__ void store_piece(uint16_t* lds, int tid, int p) const {
+    store_half<S, NP>(lds, tid, p >> 1, p & 1);
   }
 };
 
@@ -360,19 +383,23 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
     lb.init(g.B, u.n0, g.N, tid);
     // k-tile t is loaded into register set t % 2, three tiles ahead of its MFMAs: tile kt+3's loads
     // are issued during k-tile kt and stored to LDS during kt+2 (two MFMA phases of latency cover:
-    // the gathered rows come from the Infinity Cache / HBM)
+    // the gathered rows come from the Infinity Cache / HBM).  Past the unit's last tile the loads
+    // re-read that tile (clamped, never used): the k-tile body stays one basic block.
     auto issue = [&](auto set, int kt) {
       constexpr int S = decltype(set)::value;
+      kt = kt < nt ? kt : nt - 1;
       const int64_t k = u.kbeg + (int64_t)kt * BK;
       la.template load<S>(g.A, u.m0, g.M, k, tid);
       lb.template load<S>(g.B, u.n0, g.N, k, tid);
-      if (IDX_AHEAD && kt + 2 < nt) {   // ids of the set's next tile (kt + 2)
+      if (IDX_AHEAD) {   // ids of the set's next tile (kt + 2; clamped to K inside)
         la.template prefetch_idx<S>(g.A, k + 2 * BK, g.K, tid);
         lb.template prefetch_idx<S>(g.B, k + 2 * BK, g.K, tid);
       }
     };
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
+    using LiveT = std::integral_constant<bool, true>;
+    using DeadT = std::integral_constant<bool, false>;
     if (IDX_AHEAD) {
       la.template prefetch_idx<0>(g.A, u.kbeg, g.K, tid);
       lb.template prefetch_idx<0>(g.B, u.kbeg, g.K, tid);
@@ -381,77 +408,163 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
     }
     __syncthreads();   // the previous unit's last stage reads are done before stage 0 is rewritten
     issue(S0{}, 0);
-    if (nt > 1) issue(S1{}, 1);
+    issue(S1{}, 1);
     if constexpr (CS_OK) {
       if (do_cs) la.template add_colsum<0>(cs, tid);
     }
     la.template store<0, NP>(As, tid);
     lb.template store<0, NP>(Bs, tid);
-    if (nt > 2) issue(S0{}, 2);
+    issue(S0{}, 2);
     __syncthreads();
     // one k-tile (KS MFMA steps of 16): MFMAs from stage st; behind the first row blocks the wave
     // splits k-tile kt+1 (set (kt+1) % 2 = NS) into the other stage, then reuses that set for k-tile
-    // kt+3's loads
+    // kt+3's loads.  The A fragments of row block i+1 are read while row block i's MFMAs run (two
+    // fragment register sets), and nothing in a live wave's k-tile branches: the split VALU, the
+    // LDS traffic and the MFMAs of one tile form a single scheduling region.  After the unit's last
+    // tile the split-stores write the other stage with values nobody reads (the next unit starts
+    // behind a barrier and rewrites stage 0).
     // (waves 4-7 splitting behind their last two row blocks instead -- a stagger of the VALU
     // clumps of the two waves on a SIMD -- measured slower: projection fwd 270-280 vs 257-260 µs)
     constexpr int ia = 0, ib = KS == 1 ? 1 : 0;
-    auto ktile = [&](auto nset, int kt, int st) {
+    auto ktile = [&](auto live_t, auto nset, int kt, int st) {
+      constexpr bool LIVE = decltype(live_t)::value;
       constexpr int NS = decltype(nset)::value;
-      const bool stage_next = kt + 1 < nt;
+#ifdef NR_BIG_ILV
+      constexpr bool ILV = LIVE && NP == 3 && KS == 1 && TJ == 2 && LA::PIECES == 2 && LB::PIECES == 2;
+#else
+      constexpr bool ILV = false;
+#endif
       const uint16_t* a_s = As + st * NP * PA;
       const uint16_t* b_s = Bs + st * NP * PB;
+      // after MFMA m (of 12) of row block i: A pieces behind row block ia's MFMAs 2 and 5 (j = 0),
+      // B pieces behind row block ib's, the loads of k-tile kt+3 behind its last
+      auto ilv_hook = [&](int i, int m) {
+        const int piece = m == 2 ? 0 : m == 5 ? 1 : m == 8 ? 2 : 3;
+        __builtin_amdgcn_sched_barrier(0);
+        if (i == ia && piece < 2) {
+          if constexpr (CS_OK) {
+            if (piece == 0 && do_cs) la.template add_colsum<NS>(cs, tid);
+          }
+          la.template store_piece<NS, NP>(As + (st ^ 1) * NP * PA, tid, piece);
+        }
+        if (i == ib && piece < 2) lb.template store_piece<NS, NP>(Bs + (st ^ 1) * NP * PB, tid, piece);
+        if (i == ib && piece == 3) issue(nset, kt + 3);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      (void)ilv_hook;
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
       bf16x8 b[TJ][NP];
-      if (live)
+      bf16x8 a[2][NP];
+      if constexpr (LIVE) {
 #pragma unroll
-      for (int j = 0; j < TJ; ++j)
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int p = 0; p < NP; ++p)
+            b[j][p] = *reinterpret_cast<const bf16x8*>(b_s + p * PB + (wn + 32 * j + c) * SR + 16 * kk + 8 * h);
 #pragma unroll
         for (int p = 0; p < NP; ++p)
-          b[j][p] = *reinterpret_cast<const bf16x8*>(b_s + p * PB + (wn + 32 * j + c) * SR + 16 * kk + 8 * h);
+          a[0][p] = *reinterpret_cast<const bf16x8*>(a_s + p * PA + (wm + c) * SR + 16 * kk + 8 * h);
+      }
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
-        if (live) {
-        bf16x8 a[NP];
+        if constexpr (LIVE) {
+          if (i + 1 < TI)
 #pragma unroll
-        for (int p = 0; p < NP; ++p)
-          a[p] = *reinterpret_cast<const bf16x8*>(a_s + p * PA + (wm + 32 * i + c) * SR + 16 * kk + 8 * h);
+            for (int p = 0; p < NP; ++p)
+              a[(i + 1) & 1][p] =
+                  *reinterpret_cast<const bf16x8*>(a_s + p * PA + (wm + 32 * (i + 1) + c) * SR + 16 * kk + 8 * h);
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) {
-#define NR_MF(X, Y)                                                                                    \
-  acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][Y], a[X], acc[i][j], 0, 0, 0) \
-                 : __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[X], b[j][Y], acc[i][j], 0, 0, 0)
-          if constexpr (NP == 3) {   // smallest terms first
-            NR_MF(2, 0);
-            NR_MF(1, 1);
-            NR_MF(0, 2);
-            NR_MF(1, 0);
-            NR_MF(0, 1);
-          }
-          NR_MF(0, 0);
+          for (int j = 0; j < TJ; ++j) {
+#define NR_MF(X, Y)                                                                                                    \
+  acc[i][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][Y], a[i & 1][X], acc[i][j], 0, 0, 0) \
+                 : __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i & 1][X], b[j][Y], acc[i][j], 0, 0, 0)
+            if constexpr (ILV) {
+              // interleaved: the split-stores of the next stage go in pieces between this row block's
+              // MFMAs (a piece's ~22 VALU + its LDS writes behind every third MFMA) instead of as one
+              // VALU clump between row blocks, which left the matrix pipe idle when both waves of a
+              // SIMD reached it together
+              static_assert(NP == 3, "interleave: bf16x6 only");
+              NR_MF(2, 0);
+              NR_MF(1, 1);
+              NR_MF(0, 2);
+              ilv_hook(i, 6 * j + 2);
+              NR_MF(1, 0);
+              NR_MF(0, 1);
+              NR_MF(0, 0);
+              ilv_hook(i, 6 * j + 5);
+            } else {
+              if constexpr (NP == 3) {   // smallest terms first
+                NR_MF(2, 0);
+                NR_MF(1, 1);
+                NR_MF(0, 2);
+                NR_MF(1, 0);
+                NR_MF(0, 1);
+              }
+              NR_MF(0, 0);
+            }
 #undef NR_MF
-        }
+          }
+          if constexpr (ILV) continue;
         }
         // split-stores of the next stage: A behind step 0's first row block, B (then the loads of
         // k-tile kt+3 into the freed register set) behind step KS/2's second (KS = 1) or first row block
-        if (kk == 0 && i == ia && stage_next) {
+        if (kk == 0 && i == ia) {
           if constexpr (CS_OK) {
             if (do_cs) la.template add_colsum<NS>(cs, tid);
           }
           la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid);
         }
-        if (kk == KS / 2 && i == ib && stage_next) {
+        if (kk == KS / 2 && i == ib) {
           lb.template store<NS, NP>(Bs + (st ^ 1) * NP * PB, tid);
-          if (kt + 3 < nt) issue(nset, kt + 3);
+          issue(nset, kt + 3);
         }
       }
       }
+#ifdef NR_BIG_SGB
+      if constexpr (LIVE && NP == 3 && KS == 1 && TI == 4 && TJ == 2) {
+        // A/B experiment: pin the interleave of the tile's 48 MFMAs with the next row block's fragment
+        // reads, the two operand splits (VALU + LDS writes) and the loads (masks: MFMA 0x8, VALU 0x2,
+        // DS read 0x100, DS write 0x200, VMEM read 0x20)
+        __builtin_amdgcn_sched_group_barrier(0x100, 9, 0);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+          for (int u = 0; u < 3; ++u) {
+            __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x2, 2, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < 9; ++u) {
+            __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x2, 5, 0);
+            if (u % 2 == 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+          }
+          if (q == 1) __builtin_amdgcn_sched_group_barrier(0x20, 4, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x8, 21, 0);
+      }
+#endif
       __syncthreads();   // stage st fully read; stage st^1 fully written
     };
-    for (int kt = 0; kt < nt; kt += 2) {   // unrolled by two: the register sets alternate statically
-      ktile(S1{}, kt, 0);
-      if (kt + 1 < nt) ktile(S0{}, kt + 1, 1);
-    }
+    // unrolled by two: the register sets alternate statically; a wave with no live rows / columns
+    // runs the same loads, splits, stores and barriers without fragment reads or MFMAs
+    auto kloop = [&](auto live_t) {
+      for (int kt = 0; kt < nt; kt += 2) {
+        ktile(live_t, S1{}, kt, 0);
+        if (kt + 1 < nt) ktile(live_t, S0{}, kt + 1, 1);
+      }
+    };
+    if (live)
+      kloop(LiveT{});
+    else
+      kloop(DeadT{});
     if (!tail_unit) {
       if constexpr (CS_OK) {
         if (do_cs)

@@ -436,9 +436,9 @@ __device__ __forceinline__ void pool_ln_bwd(const MPArgs& g, int64_t seq, float*
       b += red[(ww * 3 + 1) * H + d];
       q += red[(ww * 3 + 2) * H + d];
     }
-    atomicAdd(&g.dgamma[d], a);
-    atomicAdd(&g.dbeta[d], b);
-    atomicAdd(&g.dq[d], q);
+    atomicAdd(g.ws ? grad_slot(g, d) : &g.dgamma[d], a);
+    atomicAdd(g.ws ? grad_slot(g, H + d) : &g.dbeta[d], b);
+    atomicAdd(g.ws ? grad_slot(g, 2 * H + d) : &g.dq[d], q);
   }
   __syncthreads();   // red may alias later scratch
 }
@@ -593,9 +593,11 @@ __device__ __forceinline__ void flush_dbias(const MPArgs& g, int head, float (&c
   }
 }
 
-// Fused backward (no saved O): recompute the attention into LDS, pooling/LN backward in
-// place, then the attention backward of every head with dO from LDS.
-template <int DK, int DV, int NH64, int NP>
+// Fused backward: the attention output O into LDS -- recomputed from the projections, or (SAVED)
+// the rows the training forward saved -- then the pooling/LN backward in place and the attention
+// backward of every head with dO from LDS.  SAVED keeps dO on chip (the split form writes it to HBM
+// and reads it back, 2 x 81 MB per NRMS step).
+template <int DK, int DV, int NH64, int NP, bool SAVED>
 __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
   if (g.rng) g.dkey = nr_dropout_key(g.rng[0], g.rng[1] + g.offset);   // graph-replay RNG
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -613,7 +615,18 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
   const int tid = threadIdx.x, w = tid >> 6;
   const uint64_t bits = token_bits(g, seq);
   stage_rows(g, seq);
-  attention_to_lds<DK, DV, NP>(g, seq, bits, os, SO);
+  if constexpr (SAVED) {
+    constexpr int H4 = NH64 * 16;   // float4 per O row
+    for (int i = tid; i < 32 * H4; i += blockDim.x) {
+      const int l = i / H4, c4 = i - l * H4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (l < g.L) v = *reinterpret_cast<const float4*>(g.o + (seq * g.L + l) * g.ldo + 4 * c4);
+      float* d = os + l * SO + 4 * c4;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+  } else {
+    attention_to_lds<DK, DV, NP>(g, seq, bits, os, SO);
+  }
   if (tid < 32) {
     ps[tid] = tid < g.L ? g.probs[seq * g.L + tid] : 0.f;
     st[2 * tid] = tid < g.L ? g.stats[2 * (seq * g.L + tid)] : 0.f;
@@ -849,11 +862,22 @@ int launch_np(const MPArgs& g, Pass pass, hipStream_t s) {
     hipLaunchKernelGGL((mha_pool_fwd_kernel<DK, DV, NH64, NP>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
   } else if (pass == BWD_FUSED) {
     // one wave per two heads (its per-head state needs ~200 VGPRs, more than a 12-wave
-    // workgroup can give a wave)
+    // workgroup can give a wave); with the saved O (g.o) the O rows are loaded, not recomputed
     const int nw = (g.heads + 1) / 2 < 4 ? 4 : (g.heads + 1) / 2;
     const size_t sz = bwd_smem(H, nw);
-    allow_smem(mha_pool_bwd_kernel<DK, DV, NH64, NP>, sz);
-    hipLaunchKernelGGL((mha_pool_bwd_kernel<DK, DV, NH64, NP>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
+    if (g.o) {
+      allow_smem(mha_pool_bwd_kernel<DK, DV, NH64, NP, true>, sz);
+      hipLaunchKernelGGL((mha_pool_bwd_kernel<DK, DV, NH64, NP, true>), dim3((unsigned)g.nseq), dim3(64 * nw), sz,
+                         s, g);
+    } else {
+      allow_smem(mha_pool_bwd_kernel<DK, DV, NH64, NP, false>, sz);
+      hipLaunchKernelGGL((mha_pool_bwd_kernel<DK, DV, NH64, NP, false>), dim3((unsigned)g.nseq), dim3(64 * nw), sz,
+                         s, g);
+    }
+    if (g.ws) {
+      const int NY = g.heads * (DK + DV);
+      hipLaunchKernelGGL(copies_reduce_kernel, dim3((unsigned)((3 * H + NY + 63) / 64)), dim3(64), 0, s, g, H, NY);
+    }
   } else {
     hipLaunchKernelGGL((mha_ln_bwd_kernel<NH64>), dim3((unsigned)g.nseq), dim3(256), 0, s, g);
     MPArgs g2 = g;
@@ -942,7 +966,8 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
   g.probs = const_cast<float*>(probs); g.dz = dz; g.lddz = lddz; g.dy = dy; g.lddy = lddy; g.dbias = dbias;
   g.dq = dq; g.dgamma = dgamma; g.dbeta = dbeta;
   g.o = const_cast<float*>(o); g.ldo = ldo; g.dob = dob; g.lddob = lddob;
-  if (o && (!dob || lddob < (int64_t)heads * dv || ldo < (int64_t)heads * dv || (ldo & 3) || !al16(o)))
+  // o with dob: the split backward (dO through dob); o without dob: the fused backward on the saved O
+  if (o && ((dob && lddob < (int64_t)heads * dv) || ldo < (int64_t)heads * dv || (ldo & 3) || !al16(o)))
     return NR_EINVAL(3);
   // backward: the six-product form measured slower than exact f32 MFMA products here (the split
   // VALU work lands on a latency-bound kernel: head pass 170 -> 189 us), so bf16x6 callers get the
@@ -951,5 +976,5 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
   if (ws && (!o || ws_copies < 1 || ws_copies > 1024)) return NR_EINVAL(5);
   g.ws = ws; g.ws_copies = ws_copies;
   g.ws_ld = ((int64_t)3 * heads * dv + (int64_t)heads * (dk + dv) + 3) & ~int64_t(3);
-  return dispatch(g, dk, dv, o ? BWD_SPLIT : BWD_FUSED, stream);
+  return dispatch(g, dk, dv, o && dob ? BWD_SPLIT : BWD_FUSED, stream);
 }

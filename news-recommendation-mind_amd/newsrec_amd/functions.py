@@ -150,6 +150,9 @@ DEDUP_ROWS = True
 # Training forward saves the attention output; the backward runs split (False: the fused backward
 # that recomputes the attention).
 SPLIT_BWD = True
+# With the saved attention output: one fused kernel per title (LN backward + every head's attention
+# backward, dO kept in LDS) instead of the split pair (dO through HBM)
+FUSED_SAVED_BWD = False
 # Split-K factor of the MHA user encoder's input gradient (dx = dY [Wk; Wv], K = 1152); a split keeps
 # >= 512 k per piece.  One-box A/B of the NRMS step, interleaved rounds: unsplit 1.4206-1.4275 ms,
 # two pieces 1.4292 ms -- kept unsplit
@@ -387,7 +390,7 @@ class MHANewsFn(torch.autograd.Function):
         dz = dtok.contiguous() if dtok is not None else None
         ur = ctx.ur
         if fused:
-            dob = _empty(T, H, table) if O is not None else None
+            dob = _empty(T, H, table) if O is not None and not FUSED_SAVED_BWD else None
             ws = _grad_copies(table.device, 3 * H + NY) if O is not None else None
             K.mha_pool_bwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, stats, probs, dnews, dY, db, dq,
                            dgamma, dbeta, p_drop=p_drop, seed=seed, offset=0 if ctx.rng is not None else offset,

@@ -738,9 +738,10 @@ def mha_pool_fwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, news, st
 def mha_pool_bwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, dbias, dq,
                  dgamma, dbeta, p_drop=0.0, seed=0, offset=0, dz=None, yrows=None, rng=None, o=None, dob=None,
                  prec=None, ws=None, ws_copies=0):
-    """``o`` (the forward's ``oout``) selects the split backward; ``dob`` [T, heads*dv] is its
-    dO workspace; ``ws`` (split form) a zeroed [ws_copies, >= 3*heads*dv + heads*(dk+dv)] buffer
-    that spreads the parameter-gradient atomics (left zero)."""
+    """``o`` (the forward's ``oout``) with ``dob`` [T, heads*dv] (its dO workspace) selects the split
+    backward, ``o`` without ``dob`` the fused backward on the saved O (dO kept in LDS); ``ws`` (forms
+    with ``o``) a zeroed [ws_copies, >= 3*heads*dv + heads*(dk+dv)] buffer that spreads the
+    parameter-gradient atomics (left zero)."""
     _rng_ok(rng)
     H = heads * dv
     _f32(y, gamma, beta, q, stats, probs, dnews, dy, dbias, dq, dgamma, dbeta, dz)
@@ -754,7 +755,7 @@ def mha_pool_bwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, stats, p
         _f32(ws)
         w = (3 * heads * dv + heads * (dk + dv) + 3) // 4 * 4
         if o is None or ws_copies < 1 or ws.numel() < ws_copies * w or not ws.is_contiguous():
-            raise L.HipError("mha_pool_bwd: ws needs the split form and ws_copies x %d contiguous floats" % w)
+            raise L.HipError("mha_pool_bwd: ws needs the saved O and ws_copies x %d contiguous floats" % w)
     mp, mdt = mask_arg(mask, nseq * seq_len)
     L.call("nr_mha_pool_bwd", L.ptr(y), y.stride(0), L.ptr(yrows), mp, mdt, nseq, seq_len, heads, dk, dv, L.ptr(gamma),
            L.ptr(beta), p_drop, seed, offset, L.ptr(rng), L.ptr(q), L.ptr(stats), L.ptr(probs), L.ptr(dnews), dnews.stride(0),

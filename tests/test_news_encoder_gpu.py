@@ -87,10 +87,12 @@ def _fused_mha_news_encoder(p_drop):
                                    msg=k)
 
 
+@pytest.mark.parametrize("mode", ["split", "fused_saved", "fused_saved_ws"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.2])
-def test_mha_pool_split_backward_matches_fused(p_drop):
-    """The split backward (forward saves O; pooling/LN pass + per-head attention pass) against
-    the fused one (recomputes the attention) on the same inputs."""
+def test_mha_pool_split_backward_matches_fused(p_drop, mode):
+    """The backward forms with the saved attention output O -- split (pooling/LN pass, dO through
+    HBM, per-head attention pass) and fused on the saved O (dO kept in LDS; with and without the
+    parameter-gradient copies) -- against the fused one that recomputes the attention."""
     from newsrec_amd import kernels as K
     torch.manual_seed(11)
     n, Lq, heads, dk, dv = 97, 30, 12, 64, 32
@@ -104,19 +106,24 @@ def test_mha_pool_split_backward_matches_fused(p_drop):
     q = torch.randn(H, device="cuda")
     dnews = torch.randn(n, H, device="cuda")
     outs = []
-    for split in (False, True):
+    for form in ("recompute", mode):
+        saved = form != "recompute"
         news = torch.empty(n, H, device="cuda")
         stats = torch.empty(T, 2, device="cuda")
         probs = torch.empty(T, device="cuda")
-        O = torch.empty(T, H, device="cuda") if split else None
+        O = torch.empty(T, H, device="cuda") if saved else None
         K.mha_pool_fwd(y, mask, n, Lq, heads, dk, dv, gamma, beta, q, news, stats, probs, p_drop=p_drop, seed=9,
                        offset=3, oout=O)
         dy = torch.zeros(T, NY, device="cuda")
         db, dq, dg, dbt = (torch.zeros(NY, device="cuda"), torch.zeros(H, device="cuda"),
                            torch.zeros(H, device="cuda"), torch.zeros(H, device="cuda"))
-        dob = torch.empty(T, H, device="cuda") if split else None
+        dob = torch.empty(T, H, device="cuda") if form == "split" else None
+        ws = torch.zeros(32, (3 * H + NY + 3) // 4 * 4, device="cuda") if form == "fused_saved_ws" else None
         K.mha_pool_bwd(y, mask, n, Lq, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, db, dq, dg, dbt,
-                       p_drop=p_drop, seed=9, offset=3, o=O, dob=dob)
+                       p_drop=p_drop, seed=9, offset=3, o=O, dob=dob, ws=ws, ws_copies=32 if ws is not None else 0)
+        if ws is not None:
+            torch.cuda.synchronize()
+            assert not bool(ws.any().item())   # the copies are left zero
         outs.append((news, dy, db, dq, dg, dbt))
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0])
