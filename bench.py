@@ -456,7 +456,7 @@ def main():
                     help="ranks (one per GPU); without WORLD_SIZE in the environment this process "
                          "spawns them itself (default 1, or WORLD_SIZE under torch.distributed.run)")
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--data", choices=["device", "resident"], default="device",
@@ -657,7 +657,7 @@ def main():
                          "traffic": traffic, "launch_ms": round(gemm_ms, 4) if gemm_ms else None,
                          "flops_per_launch": gemm_flops, "rows_per_launch": gemm_rows,
                          "tokens_per_launch": B * (C + NH) * L,
-                         "timing": "per-launch average of 20 back-to-back replays of the step's own launch "
+                         "timing": "per-launch average of 20 replays of the step's own launch, each after a 512 MB cache-evicting write "
                                    "(HIP events on its stream)", "projection_gemms": gemms},
         }
         if in_sync is not None:

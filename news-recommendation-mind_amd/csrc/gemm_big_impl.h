@@ -429,10 +429,14 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
     auto ktile = [&](auto live_t, auto nset, int kt, int st) {
       constexpr bool LIVE = decltype(live_t)::value;
       constexpr int NS = decltype(nset)::value;
-#ifdef NR_BIG_ILV
-      constexpr bool ILV = LIVE && NP == 3 && KS == 1 && TJ == 2 && LA::PIECES == 2 && LB::PIECES == 2;
-#else
+      // interleaved split-stores for bf16x6, except the dgrad operand pair (K-contiguous A with an
+      // MN-contiguous B): one-box A/B (profiles/r04_a_gemm_ab.json, µs) projection fwd 258 -> 248,
+      // weight gradient 292 -> 273, BERT FFN-out 383 -> 376, table dgrad 258 -> 269 (kept off there)
+#ifdef NR_BIG_NO_ILV
       constexpr bool ILV = false;
+#else
+      constexpr bool ILV = LIVE && NP == 3 && KS == 1 && TJ == 2 && LA::PIECES == 2 && LB::PIECES == 2 &&
+                           !(AM == KC_PLAIN && BMODE == MN_PLAIN);
 #endif
       const uint16_t* a_s = As + st * NP * PA;
       const uint16_t* b_s = Bs + st * NP * PB;
@@ -443,7 +447,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
         __builtin_amdgcn_sched_barrier(0);
         if (i == ia && piece < 2) {
           if constexpr (CS_OK) {
-            if (piece == 0 && do_cs) la.template add_colsum<NS>(cs, tid);
+            if (piece == 0 && do_cs && kt + 1 < nt) la.template add_colsum<NS>(cs, tid);
           }
           la.template store_piece<NS, NP>(As + (st ^ 1) * NP * PA, tid, piece);
         }
@@ -510,8 +514,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
         // split-stores of the next stage: A behind step 0's first row block, B (then the loads of
         // k-tile kt+3 into the freed register set) behind step KS/2's second (KS = 1) or first row block
         if (kk == 0 && i == ia) {
-          if constexpr (CS_OK) {
-            if (do_cs) la.template add_colsum<NS>(cs, tid);
+          if constexpr (CS_OK) {   // (past the unit's last tile the register set holds a re-read tile)
+            if (do_cs && kt + 1 < nt) la.template add_colsum<NS>(cs, tid);
           }
           la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid);
         }

@@ -100,11 +100,13 @@ class _Probe:
     """Per-launch timing of the step's dominant kernels (the news tower's three projection GEMMs).
 
     While enabled, ``run(name, fn, out, ur)`` launches ``fn`` as usual and keeps the first launch of
-    each name as a closure over its real operands.  ``time()`` then replays every kept closure back
-    to back (``reps`` launches between two HIP events on the launch stream) and restores the output
-    it overwrote: the average per-launch duration of exactly the kernels the step runs, free of the
-    eager step's host gaps -- what rocprofv3's kernel trace of the graphed step reports.  A closure
-    is the whole unit of work (the weight gradient = its split-K GEMM + the ordered reduction)."""
+    each name as a closure over its real operands.  ``time()`` then replays every kept closure
+    ``reps`` times, each replay bracketed by HIP events on the launch stream and preceded by a 512 MB
+    write that evicts the L2s and the Infinity Cache (in the step the operands arrive cold: Adam has
+    just streamed 0.7 GB; back-to-back replays with warm operands ran ~8 % faster than the graphed
+    step's launches), and restores the output it overwrote: the average per-launch duration of
+    exactly the kernels the step runs, free of the eager step's host gaps.  A closure is the whole
+    unit of work (the weight gradient = its split-K GEMM + the ordered reduction)."""
 
     def __init__(self):
         self.on = False
@@ -125,18 +127,22 @@ class _Probe:
 
     def time(self, reps=20, warm=2):
         res = {}
+        flush = None
         for name, (fn, out, ur) in self.launches.items():
+            if flush is None:
+                flush = torch.empty(128 << 20, device=out.device)
             saved = out.clone()
             for _ in range(warm):
                 fn()
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            for _ in range(reps):
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+            for s, e in ev:
+                flush.zero_()
+                s.record()
                 fn()
-            e.record()
+                e.record()
             torch.cuda.synchronize()
             out.copy_(saved)
-            res[name + "_ms"] = s.elapsed_time(e) / reps
+            res[name + "_ms"] = sum(s.elapsed_time(e) for s, e in ev) / reps
             if ur is not None:
                 res[name + "_rows"] = int(ur.counts[1].item())
         return res
@@ -165,6 +171,10 @@ WGRAD_WS_BF16X6 = True
 # CNN table dgrad with the conv weights transposed to k-contiguous (one 1.5 MB copy per step):
 # one-box A/B of the graphed legs, bf16 0.698 -> 0.657 ms, fp32-class 0.851 -> 0.842 ms
 CNN_DGRAD_KC = True
+# NRMS table dgrad with the joint projection weight transposed to k-contiguous (one 3.5 MB copy per step),
+# so both operands take the K-contiguous loaders (and the interleaved split-stores) instead of the
+# MN-contiguous weight loader
+PROJ_DGRAD_KC = False
 # the NRMS projection weight gradient on the same workspace path: one process, interleaved rounds,
 # 1.459 -> 1.446 ms per NRMS step (round 2 measured it slower, before the bf16x6 units lost SLP)
 PROJ_WGRAD_WS = True
@@ -412,8 +422,11 @@ class MHANewsFn(torch.autograd.Function):
             if ctx.needs_input_grad[0]:
                 dtable = torch.zeros(V, E, device=table.device)
                 # distinct rows (M = U, not U_pad: no duplicate pad ids): plain row stores
+                wt = w_cat.t().contiguous() if PROJ_DGRAD_KC else None   # kept alive by the closure
+
                 def dgrad():
-                    K.gemm_dyn(ur.cap, E, NY, K.operand(dYu, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dtable,
+                    w_b = K.operand(wt, L.KCONTIG) if wt is not None else K.operand(w_cat, L.MNCONTIG)
+                    K.gemm_dyn(ur.cap, E, NY, K.operand(dYu, L.KCONTIG), w_b, dtable,
                                m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_ZEROED,
                                c_rows=K.rows_map(ur.uids, L.ROWS_GATHER), pad_row=pad_row)
                 PROBE.run("proj_dgrad", dgrad, dtable, ur)

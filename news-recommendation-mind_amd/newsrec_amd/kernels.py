@@ -142,15 +142,20 @@ _SELF_CLEANING = {}
 _RETIRED = []   # outgrown buffers stay allocated: a captured graph may still address them
 
 
-def self_cleaning_workspace(dev, name, n):
+_CLEAN_WORDS = {}   # (device, name) -> leading words the kernels leave zero (the rest is scratch)
+
+
+def self_cleaning_workspace(dev, name, n, clean=None):
     """A persistent zeroed int32 device buffer of at least ``n`` words per (device, name) for the
     kernels whose counters start at zero and that leave them zero again (nr_unique_rows,
-    nr_score_nll_fwd): no zero-fill launch per call.
+    nr_score_nll_fwd): no zero-fill launch per call.  ``clean``: how many leading words are such
+    counters (default all; nr_unique_rows' scan outputs and the NLL head's per-impression terms that
+    follow are scratch), for ``self_cleaning_check``.
 
     Created (or grown) by an eager call, never inside a graph capture: a buffer first zero-filled
     during a capture would only be zero once that graph had replayed.  Steps run one at a time on
     a device, so one buffer per (device, name) serves every stream."""
-    key = (torch.device(dev), name)
+    key = (_dev_key(dev), name)
     ws = _SELF_CLEANING.get(key)
     if ws is None or ws.numel() < n:
         if torch.cuda.is_current_stream_capturing():
@@ -158,27 +163,34 @@ def self_cleaning_workspace(dev, name, n):
         if ws is not None:
             _RETIRED.append(ws)
         ws = _SELF_CLEANING[key] = torch.zeros(max(int(n), 4), device=dev, dtype=torch.int32)
+    _CLEAN_WORDS[key] = int(n if clean is None else clean)
     return ws
+
+
+def _dev_key(dev):
+    """torch.device with an explicit index ("cuda" -> the current device), as the workspaces are keyed."""
+    d = torch.device(dev)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
 
 
 def self_cleaning_check(dev=None, reset=False):
     """Debug check of the self-cleaning workspaces: every kernel using one leaves its counters zero,
-    so after a synchronize they must all read zero (the score_nll buffer's word 1, a sticky label
-    status, excepted).  A launch that never completed, or two launches on one buffer from concurrent
+    so after a synchronize each buffer's counter words (``clean`` of self_cleaning_workspace) must
+    read zero.  A launch that never completed, or two launches on one buffer from concurrent
     streams, leaves a counter set and silently corrupts later calls: -> the names of the buffers found
     non-zero; ``reset``: zero them again (after an error)."""
     torch.cuda.synchronize()
     bad = []
     for (d, name), ws in _SELF_CLEANING.items():
-        if dev is not None and d != torch.device(dev):
+        if dev is not None and d != _dev_key(dev):
             continue
-        w = ws.clone()
-        if name == "nr_score_nll_fwd":
-            w[1] = 0
+        w = ws[:_CLEAN_WORDS.get((d, name), ws.numel())].clone()
         if bool((w != 0).any().item()):
             bad.append(name)
             if reset:
-                ws.zero_()
+                ws[:w.numel()].zero_()
     return bad
 
 
@@ -186,7 +198,7 @@ def score_nll_status(dev, clear=True):
     """The sticky label status of nr_score_nll_fwd on ``dev`` (True: some call since the last check
     saw a label outside [0, C) other than the ignored -100 and returned a NaN loss, where
     torch.nn.functional.nll_loss raises).  Reads the device (synchronises)."""
-    ws = _SELF_CLEANING.get((torch.device(dev), "nr_score_nll_fwd"))
+    ws = _SELF_CLEANING.get((_dev_key(dev), "nr_score_nll_fwd"))
     if ws is None:
         return False
     bad = bool(ws[1].item() != 0)
@@ -210,7 +222,9 @@ class UniqueRows:
         self.T, self.vocab = T, vocab
         self.cap = max(32, _ceil32(min(T, vocab)))
         i32 = dict(device=dev, dtype=torch.int32)
-        work = self_cleaning_workspace(dev, f"nr_unique_rows/{vocab}", L.load().nr_unique_rows_workspace(vocab))
+        # ctrl[4] | cnt_all | cnt_csr are the counters (dedup.hip); cursor | pos | tile totals scratch
+        work = self_cleaning_workspace(dev, f"nr_unique_rows/{vocab}", L.load().nr_unique_rows_workspace(vocab),
+                                       clean=4 + 2 * ((vocab + 3) // 4 * 4))
         self.uids = torch.empty(self.cap, device=dev, dtype=torch.int64)
         self.inv = torch.empty(T, device=dev, dtype=torch.int64)
         self.seg_off = torch.empty(self.cap + 1, **i32)
@@ -590,7 +604,8 @@ def score_nll_fwd(cdd, user, label, B, C, H, logits, loss):
     _check_rows(label, None, "label")
     if label.numel() != B or not logits.is_contiguous() or logits.numel() < B * C:
         raise L.HipError("score_nll_fwd: label [B] int64, logits contiguous [B, C]")
-    work = self_cleaning_workspace(user.device, "nr_score_nll_fwd", L.load().nr_score_nll_workspace(B))
+    # word 0: the ticket; word 1: the sticky label status (not a counter); then per-impression scratch
+    work = self_cleaning_workspace(user.device, "nr_score_nll_fwd", L.load().nr_score_nll_workspace(B), clean=1)
     L.call("nr_score_nll_fwd", L.ptr(cdd), cdd.stride(0), L.ptr(user), user.stride(0), L.ptr(label), B, C, H,
            L.ptr(logits), L.ptr(loss), L.ptr(work), L.stream_ptr(user))
 
