@@ -593,22 +593,27 @@ int nr_bert_add_ln_bwd(const float* x, int64_t ldx, const float* res, int64_t ld
  *   ctx[s*L+i][h*64:] = Σ_j Dropout_p(softmax_j(q_i·k_j / 8 + (1 - m_j) * FLT_MIN_NEG)) v_j
  * with q / k / v at columns h*64, koff + h*64, voff + h*64 of qkv rows (ld ldq).  Fully masked
  * rows are uniform over the L keys (the additive-mask arithmetic).  Saves ml [T][heads][2] =
- * (row max, 1 / row sum) for the backward.  mask: [nseq, L] of enum nr_mask_dtype. */
+ * (row max, 1 / row sum) for the backward.  mask: [nseq, L] of enum nr_mask_dtype.  prec (enum
+ * nr_gemm_precision): the arithmetic of the four products (Q Kᵀ, P V and their backward) --
+ * NR_GEMM_F32 the f32 MFMA, NR_GEMM_BF16X6 the fp32-class bf16 split form, NR_GEMM_BF16 one bf16
+ * product; the softmax, its statistics and the dropout stay fp32.  Replaces the self-attention core
+ * of transformers' BertSelfAttention.forward as models/XFormer.py:68,94 call it. */
 int nr_bert_attn_fwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
                      int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, float p_drop,
                      uint64_t seed, uint64_t offset, const uint64_t* rng, float* ctx, int64_t ldc,
-                     float* ml, hipStream_t stream);
+                     float* ml, int32_t prec, hipStream_t stream);
 
 /* Bytes of `work` nr_bert_attn_bwd needs. */
 int64_t nr_bert_attn_bwd_workspace(int64_t nseq, int32_t L, int32_t heads);
 
 /* Backward of nr_bert_attn_fwd: writes dQ, dK, dV into dqkv at the columns of qkv (every column
- * of the 3 * heads * 64 block is stored).  Deterministic (no atomics). */
+ * of the 3 * heads * 64 block is stored).  Deterministic (no atomics).  prec as in the forward
+ * (the two may differ; ml is the forward's either way). */
 int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
                      int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, float p_drop,
                      uint64_t seed, uint64_t offset, const uint64_t* rng, const float* ctx, int64_t ldc,
                      const float* ml, const float* dctx, int64_t ldd, float* work, float* dqkv,
-                     int64_t lddq, hipStream_t stream);
+                     int64_t lddq, int32_t prec, hipStream_t stream);
 
 /* dx = dy * (1 - y^2): the pooler's tanh backward (BertPooler). */
 int nr_tanh_bwd(const float* y, int64_t ldy, const float* dy, int64_t lddy, int64_t rows, int32_t cols,

@@ -6,7 +6,8 @@
 //   nr_bert_embed_fwd / _bwd   word + position + token-type rows -> LayerNorm -> dropout
 //   nr_bert_add_ln_fwd / _bwd  LayerNorm(dropout(dense) + residual)     (BertSelfOutput/BertOutput)
 //   nr_bert_attn_fwd           softmax(Q Kᵀ / 8 + additive key mask) -> dropout -> · V per
-//                              (sequence, head), online softmax, f32 MFMA, L <= any
+//                              (sequence, head), online softmax, any L; products on the f32
+//                              MFMA or the bf16 MFMA (bf16x6 / bf16, per the caller's precision)
 //   nr_bert_attn_bwd           dQ, dK, dV from the saved per-query (max, 1/sum)
 //   nr_tanh_bwd                pooler tanh backward
 //
@@ -20,9 +21,8 @@
 // head dims uses dim 32h + s in k-step s (the order is free), so every operand fragment is 32
 // consecutive floats of one row.
 #include "common.h"
+#include "mfma_planes.h"
 #include "../../include/newsrec_hip.h"
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
@@ -43,9 +43,6 @@ __device__ __forceinline__ float xhalf_max(float v) {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
-
-// row of 32x32 C tile held by accumulator register r in lane half h
-__device__ __forceinline__ int crow(int r, int h) { return 8 * (r >> 2) + 4 * h + (r & 3); }
 
 // ------------------------------------------------------------------------------------ LayerNorm rows
 // One wave per row of H floats (H % 4 == 0, H <= 256 * NV); lane owns float4 chunks lane + 64 j.
@@ -654,6 +651,401 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(AttnArgs g) {
   }
 }
 
+// ---- attention products on the bf16 MFMA (prec = NR_GEMM_BF16X6 / NR_GEMM_BF16) -----------------
+// The f32 kernels above run v_mfma_f32_32x32x2_f32; these run the same products on
+// v_mfma_f32_32x32x16_bf16 in the caller's GEMM arithmetic (mfma_planes.h: NP = 3 is bf16x6, the
+// fp32-class six-product form at 2.7x the f32 MFMA's rate; NP = 1 plain bf16).  One 16-deep step
+// feeds lane (c, h) eight k-slots 8h .. 8h + 7:
+//   * head-dim contractions (S = Q Kᵀ, dP = dctx Vᵀ): step t gives slot 8h + u the dim 32h + 8t + u,
+//     the f32 form's per-lane half-row -- the wave's own rows are split once into planes, the tile's
+//     rows come split from LDS (row-major plane image, rowfrag);
+//   * tile-row contractions (O = P V, dV = Pᵀ dctx, dK = dSᵀ Q, dQ = dS K): step t gives slot u of
+//     lane (c, h) the tile row crow(8t + u, h) -- the row the accumulator value the lane already
+//     holds belongs to -- so the tile is staged TRANSPOSED (dims x rows) and read as two 4-row runs
+//     per plane (colfrag).
+// Every staged element is split once per tile by the staging threads, not once per wave.
+constexpr int kKR = kHD + 8;   // row-major plane row: 64 dims + 8 pad (144 B: ds_read_b128 conflict-free)
+constexpr int kVR = 36;        // transposed plane row: 32 rows + 4 pad (72 B: ds_read_b64 conflict-free)
+
+template <int NP>
+__device__ __forceinline__ void put4(uint16_t (*P)[32][kKR], int r, int cc, float4 a) {
+  if constexpr (NP == 1) {
+    *reinterpret_cast<uint2*>(&P[0][r][cc]) = make_uint2(nrfast::pk_bf16(a.x, a.y), nrfast::pk_bf16(a.z, a.w));
+  } else {
+    uint2 p0, p1, p2;
+    nrfast::split4(a.x, a.y, a.z, a.w, p0, p1, p2);
+    *reinterpret_cast<uint2*>(&P[0][r][cc]) = p0;
+    *reinterpret_cast<uint2*>(&P[1][r][cc]) = p1;
+    *reinterpret_cast<uint2*>(&P[2][r][cc]) = p2;
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ void put2(uint16_t (*T)[kHD][kVR], int d, int k, float a, float b) {
+  if constexpr (NP == 1) {
+    *reinterpret_cast<uint32_t*>(&T[0][d][k]) = nrfast::pk_bf16(a, b);
+  } else {
+    uint32_t h2, m2, l2;
+    nrfast::split2(a, b, h2, m2, l2);
+    *reinterpret_cast<uint32_t*>(&T[0][d][k]) = h2;
+    *reinterpret_cast<uint32_t*>(&T[1][d][k]) = m2;
+    *reinterpret_cast<uint32_t*>(&T[2][d][k]) = l2;
+  }
+}
+
+// Stage rows j0 .. j0 + 31 (zeros at and past L) of one 64-wide column block, split into planes,
+// row-major into P and/or transposed into T; the whole workgroup takes part.
+template <int NP>
+__device__ __forceinline__ void stage_planes(uint16_t (*P)[32][kKR], uint16_t (*T)[kHD][kVR], const float* base,
+                                             int64_t ld, int64_t row0, int j0, int L, int64_t col) {
+  const int tid = threadIdx.x;
+  if (P) {
+    for (int f = tid; f < 512; f += blockDim.x) {
+      const int r = f >> 4, cc = (f & 15) * 4;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (j0 + r < L) a = ld4(base + (row0 + j0 + r) * ld + col + cc);
+      put4<NP>(P, r, cc, a);
+    }
+  }
+  if (T) {
+    for (int f = tid; f < 256; f += blockDim.x) {
+      const int kp = f & 15, dq = f >> 4;   // rows 2 kp, 2 kp + 1; dims 4 dq .. 4 dq + 3
+      const int j = j0 + 2 * kp;
+      const float* vb = base + (row0 + j) * ld + col + 4 * dq;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if (j < L) a = ld4(vb);
+      if (j + 1 < L) b = ld4(vb + ld);
+      put2<NP>(T, 4 * dq, 2 * kp, a.x, b.x);
+      put2<NP>(T, 4 * dq + 1, 2 * kp, a.y, b.y);
+      put2<NP>(T, 4 * dq + 2, 2 * kp, a.z, b.z);
+      put2<NP>(T, 4 * dq + 3, 2 * kp, a.w, b.w);
+    }
+  }
+}
+
+// head-dim step t of tile row c: dims 32 h + 8 t .. + 7 of a row-major plane image
+template <int NP>
+__device__ __forceinline__ Planes<NP> rowfrag(const uint16_t (*P)[32][kKR], int c, int h, int t) {
+  Planes<NP> r;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) r.v[p] = *reinterpret_cast<const bf16x8*>(&P[p][c][32 * h + 8 * t]);
+  return r;
+}
+
+// tile-row step t of dim d: rows crow(8t + u, h), u = 0..7 = runs 16t + 4h .. +3 and 16t + 8 + 4h .. +3
+template <int NP>
+__device__ __forceinline__ Planes<NP> colfrag(const uint16_t (*T)[kHD][kVR], int d, int h, int t) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  Planes<NP> r;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const uint2 a0 = *reinterpret_cast<const uint2*>(&T[p][d][16 * t + 4 * h]);
+    const uint2 a1 = *reinterpret_cast<const uint2*>(&T[p][d][16 * t + 8 + 4 * h]);
+    r.v[p] = __builtin_bit_cast(bf16x8, (u32x4){a0.x, a0.y, a1.x, a1.y});
+  }
+  return r;
+}
+
+// a wave's own 32-value half-row (dims 32 h .. 32 h + 31 of one row, times `scale`) as four
+// head-dim steps of planes; zeros when the row does not exist
+template <int NP>
+__device__ __forceinline__ void own_rows(Planes<NP> (&out)[4], const float* p, bool ok, float scale) {
+  float f[32];
+  if (ok) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 x = ld4(p + 4 * j);
+      f[4 * j] = x.x * scale; f[4 * j + 1] = x.y * scale; f[4 * j + 2] = x.z * scale; f[4 * j + 3] = x.w * scale;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 32; ++j) f[j] = 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) out[t] = planes8<NP>(f + 8 * t);
+}
+
+template <int NP, bool DROP>
+__global__ void __launch_bounds__(256) attn_fwd_mp_kernel(AttnArgs g) {
+  __shared__ __attribute__((aligned(16))) uint16_t Kp[NP][32][kKR];
+  __shared__ __attribute__((aligned(16))) uint16_t Vt[NP][kHD][kVR];
+  __shared__ float kadd[32];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, hh = lane >> 5;
+  const int nw = blockDim.x >> 6;
+  int64_t bid = blockIdx.x;
+  const int qc = (int)(bid % g.chunks);
+  bid /= g.chunks;
+  const int head = (int)(bid % g.heads);
+  const int64_t seq = bid / g.heads;
+  const int L = g.L;
+  const int64_t row0 = seq * L;
+  const int q0 = (qc * nw + wave) * 32;
+  const bool active = q0 < L;
+  const int q = q0 + c;
+  const uint32_t dkey = DROP ? attn_key(g, seq, head) : 0u;
+
+  Planes<NP> qp[4];   // B operand of Sᵀ = K Qᵀ: Q[q][32 hh + 8 t + u] / 8 (exact power-of-two scale)
+  own_rows<NP>(qp, g.qkv + (row0 + q) * g.ldq + head * kHD + 32 * hh, active && q < L, 0.125f);
+  f32x16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o0[r] = o1[r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int nkb = (L + 31) / 32;
+  for (int kb = 0; kb < nkb; ++kb) {
+    __syncthreads();
+    stage_planes<NP>(Kp, nullptr, g.qkv, g.ldq, row0, kb * 32, L, g.koff + head * kHD);
+    stage_planes<NP>(nullptr, Vt, g.qkv, g.ldq, row0, kb * 32, L, g.voff + head * kHD);
+    if (threadIdx.x < 32) {
+      const int j = kb * 32 + threadIdx.x;
+      kadd[threadIdx.x] = j >= L ? -INFINITY : (nr_mask_at(g.mask, g.mdt, row0 + j) ? 0.f : kNegMax);
+    }
+    __syncthreads();
+    if (!active) continue;
+    f32x16 s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) mfma_x<NP>(s, rowfrag<NP>(Kp, c, hh, t), qp[t]);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[r] = s[r] + kadd[crow(r, hh)];
+      mx = fmaxf(mx, s[r]);
+    }
+    mx = xhalf_max(mx);
+    const float mn = fmaxf(m, mx);
+    const float alpha = __expf(m - mn);
+    float ps = 0.f;
+    float pe[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      pe[r] = __expf(s[r] - mn);
+      ps += pe[r];
+    }
+    ps = xhalf_sum(ps);
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      o0[r] *= alpha;
+      o1[r] *= alpha;
+    }
+    if (DROP) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const uint32_t e = (uint32_t)q * (uint32_t)L + (uint32_t)(kb * 32 + crow(r, hh));
+        pe[r] = nr_dropout_keep(dkey, e, g.thresh) ? pe[r] * g.pscale : 0.f;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const Planes<NP> pp = planes8<NP>(pe + 8 * t);
+      mfma_x<NP>(o0, colfrag<NP>(Vt, c, hh, t), pp);
+      mfma_x<NP>(o1, colfrag<NP>(Vt, 32 + c, hh, t), pp);
+    }
+  }
+  if (!active || q >= L) return;
+  const float inv = 1.f / l;
+  float* op = g.ctx + (row0 + q) * g.ldc + head * kHD;
+#pragma unroll
+  for (int gq = 0; gq < 4; ++gq) {
+    const int d = 8 * gq + 4 * hh;
+    st4(op + d, make_float4(o0[4 * gq] * inv, o0[4 * gq + 1] * inv, o0[4 * gq + 2] * inv, o0[4 * gq + 3] * inv));
+    st4(op + 32 + d, make_float4(o1[4 * gq] * inv, o1[4 * gq + 1] * inv, o1[4 * gq + 2] * inv, o1[4 * gq + 3] * inv));
+  }
+  if (hh == 0) {
+    float* mp = g.ml + ((row0 + q) * g.heads + head) * 2;
+    mp[0] = m;
+    mp[1] = inv;
+  }
+}
+
+// dK, dV (attn_bwd_kv_kernel's products): a wave owns 32 keys, split once; per query tile the Q and
+// dctx rows are staged split, row-major (S, dP) and transposed (dV, dK).
+template <int NP, bool DROP>
+__global__ void __launch_bounds__(256) attn_bwd_kv_mp_kernel(AttnArgs g) {
+  __shared__ __attribute__((aligned(16))) uint16_t Qp[NP][32][kKR];
+  __shared__ __attribute__((aligned(16))) uint16_t Op[NP][32][kKR];
+  __shared__ __attribute__((aligned(16))) uint16_t Qt[NP][kHD][kVR];
+  __shared__ __attribute__((aligned(16))) uint16_t Ot[NP][kHD][kVR];
+  __shared__ float qm[32], qi[32], qd[32];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, hh = lane >> 5;
+  const int nw = blockDim.x >> 6;
+  int64_t bid = blockIdx.x;
+  const int kc = (int)(bid % g.chunks);
+  bid /= g.chunks;
+  const int head = (int)(bid % g.heads);
+  const int64_t seq = bid / g.heads;
+  const int L = g.L;
+  const int64_t row0 = seq * L;
+  const int k0 = (kc * nw + wave) * 32;
+  const bool active = k0 < L;
+  const int key = k0 + c;
+  const bool own = active && key < L;
+  const uint32_t dkey = DROP ? attn_key(g, seq, head) : 0u;
+
+  Planes<NP> kp4[4], vp4[4];
+  own_rows<NP>(kp4, g.qkv + (row0 + key) * g.ldq + g.koff + head * kHD + 32 * hh, own, 0.125f);
+  own_rows<NP>(vp4, g.qkv + (row0 + key) * g.ldq + g.voff + head * kHD + 32 * hh, own, 1.f);
+  const float kadd = own ? (nr_mask_at(g.mask, g.mdt, row0 + key) ? 0.f : kNegMax) : -INFINITY;
+  f32x16 dk0, dk1, dv0, dv1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dk0[r] = dk1[r] = dv0[r] = dv1[r] = 0.f;
+  const int nqb = (L + 31) / 32;
+  for (int qb = 0; qb < nqb; ++qb) {
+    __syncthreads();
+    stage_planes<NP>(Qp, Qt, g.qkv, g.ldq, row0, qb * 32, L, head * kHD);
+    stage_planes<NP>(Op, Ot, g.dctx, g.ldd, row0, qb * 32, L, head * kHD);
+    if (threadIdx.x < 32) {
+      const int j = qb * 32 + threadIdx.x;
+      if (j < L) {
+        const float* mp = g.ml + ((row0 + j) * g.heads + head) * 2;
+        qm[threadIdx.x] = mp[0];
+        qi[threadIdx.x] = mp[1];
+        qd[threadIdx.x] = g.Dq[(row0 + j) * g.heads + head];
+      } else {
+        qm[threadIdx.x] = INFINITY;   // exp(s - inf) = 0: no such query
+        qi[threadIdx.x] = 0.f;
+        qd[threadIdx.x] = 0.f;
+      }
+    }
+    __syncthreads();
+    if (!active) continue;
+    f32x16 s, dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      mfma_x<NP>(s, rowfrag<NP>(Qp, c, hh, t), kp4[t]);
+      mfma_x<NP>(dp, rowfrag<NP>(Op, c, hh, t), vp4[t]);
+    }
+    // S rows = queries crow(r, hh) of the tile, column = this lane's key
+    float pd[16], ds[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qr = crow(r, hh);
+      const float pr = __expf(s[r] + kadd - qm[qr]) * qi[qr];
+      float d = dp[r];
+      float pdr = pr;
+      if (DROP) {
+        const uint32_t e = (uint32_t)(qb * 32 + qr) * (uint32_t)L + (uint32_t)key;
+        const bool kp = nr_dropout_keep(dkey, e, g.thresh);
+        d = kp ? d * g.pscale : 0.f;
+        pdr = kp ? pr * g.pscale : 0.f;
+      }
+      pd[r] = pdr;
+      ds[r] = pr * (d - qd[qr]);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const Planes<NP> pp = planes8<NP>(pd + 8 * t), sp = planes8<NP>(ds + 8 * t);
+      mfma_x<NP>(dv0, colfrag<NP>(Ot, c, hh, t), pp);
+      mfma_x<NP>(dv1, colfrag<NP>(Ot, 32 + c, hh, t), pp);
+      mfma_x<NP>(dk0, colfrag<NP>(Qt, c, hh, t), sp);
+      mfma_x<NP>(dk1, colfrag<NP>(Qt, 32 + c, hh, t), sp);
+    }
+  }
+  if (!own) return;
+  float* kp = g.dqkv + (row0 + key) * g.lddq + g.koff + head * kHD;
+  float* vp = g.dqkv + (row0 + key) * g.lddq + g.voff + head * kHD;
+#pragma unroll
+  for (int gq = 0; gq < 4; ++gq) {
+    const int d = 8 * gq + 4 * hh;
+    st4(kp + d, make_float4(dk0[4 * gq] * 0.125f, dk0[4 * gq + 1] * 0.125f, dk0[4 * gq + 2] * 0.125f,
+                            dk0[4 * gq + 3] * 0.125f));
+    st4(kp + 32 + d, make_float4(dk1[4 * gq] * 0.125f, dk1[4 * gq + 1] * 0.125f, dk1[4 * gq + 2] * 0.125f,
+                                 dk1[4 * gq + 3] * 0.125f));
+    st4(vp + d, make_float4(dv0[4 * gq], dv0[4 * gq + 1], dv0[4 * gq + 2], dv0[4 * gq + 3]));
+    st4(vp + 32 + d, make_float4(dv1[4 * gq], dv1[4 * gq + 1], dv1[4 * gq + 2], dv1[4 * gq + 3]));
+  }
+}
+
+// dQ (attn_bwd_q_kernel's products): a wave owns 32 queries (Q and dctx split once); per key tile
+// K and V staged split row-major (S, dP) and K transposed (dQ = dS K).
+template <int NP, bool DROP>
+__global__ void __launch_bounds__(256) attn_bwd_q_mp_kernel(AttnArgs g) {
+  __shared__ __attribute__((aligned(16))) uint16_t Kp[NP][32][kKR];
+  __shared__ __attribute__((aligned(16))) uint16_t Vp[NP][32][kKR];
+  __shared__ __attribute__((aligned(16))) uint16_t Kt[NP][kHD][kVR];
+  __shared__ float kadd[32];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, hh = lane >> 5;
+  const int nw = blockDim.x >> 6;
+  int64_t bid = blockIdx.x;
+  const int qc = (int)(bid % g.chunks);
+  bid /= g.chunks;
+  const int head = (int)(bid % g.heads);
+  const int64_t seq = bid / g.heads;
+  const int L = g.L;
+  const int64_t row0 = seq * L;
+  const int q0 = (qc * nw + wave) * 32;
+  const bool active = q0 < L;
+  const int q = q0 + c;
+  const bool own = active && q < L;
+  const uint32_t dkey = DROP ? attn_key(g, seq, head) : 0u;
+
+  Planes<NP> qp4[4], dp4[4];
+  own_rows<NP>(qp4, g.qkv + (row0 + q) * g.ldq + head * kHD + 32 * hh, own, 0.125f);
+  own_rows<NP>(dp4, g.dctx + (row0 + q) * g.ldd + head * kHD + 32 * hh, own, 1.f);
+  float mq = INFINITY, iq = 0.f, dq = 0.f;
+  if (own) {
+    const float* mp = g.ml + ((row0 + q) * g.heads + head) * 2;
+    mq = mp[0];
+    iq = mp[1];
+    dq = g.Dq[(row0 + q) * g.heads + head];
+  }
+  f32x16 a0, a1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) a0[r] = a1[r] = 0.f;
+  const int nkb = (L + 31) / 32;
+  for (int kb = 0; kb < nkb; ++kb) {
+    __syncthreads();
+    stage_planes<NP>(Kp, Kt, g.qkv, g.ldq, row0, kb * 32, L, g.koff + head * kHD);
+    stage_planes<NP>(Vp, nullptr, g.qkv, g.ldq, row0, kb * 32, L, g.voff + head * kHD);
+    if (threadIdx.x < 32) {
+      const int j = kb * 32 + threadIdx.x;
+      kadd[threadIdx.x] = j >= L ? -INFINITY : (nr_mask_at(g.mask, g.mdt, row0 + j) ? 0.f : kNegMax);
+    }
+    __syncthreads();
+    if (!active) continue;
+    f32x16 s, dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      mfma_x<NP>(s, rowfrag<NP>(Kp, c, hh, t), qp4[t]);
+      mfma_x<NP>(dp, rowfrag<NP>(Vp, c, hh, t), dp4[t]);
+    }
+    float ds[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kr = crow(r, hh);
+      const float pr = __expf(s[r] + kadd[kr] - mq) * iq;
+      float d = dp[r];
+      if (DROP) {
+        const uint32_t e = (uint32_t)q * (uint32_t)L + (uint32_t)(kb * 32 + kr);
+        d = nr_dropout_keep(dkey, e, g.thresh) ? d * g.pscale : 0.f;
+      }
+      ds[r] = pr * (d - dq);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const Planes<NP> sp = planes8<NP>(ds + 8 * t);
+      mfma_x<NP>(a0, colfrag<NP>(Kt, c, hh, t), sp);
+      mfma_x<NP>(a1, colfrag<NP>(Kt, 32 + c, hh, t), sp);
+    }
+  }
+  if (!own) return;
+  float* op = g.dqkv + (row0 + q) * g.lddq + head * kHD;
+#pragma unroll
+  for (int gq = 0; gq < 4; ++gq) {
+    const int d = 8 * gq + 4 * hh;
+    st4(op + d, make_float4(a0[4 * gq] * 0.125f, a0[4 * gq + 1] * 0.125f, a0[4 * gq + 2] * 0.125f,
+                            a0[4 * gq + 3] * 0.125f));
+    st4(op + 32 + d, make_float4(a1[4 * gq] * 0.125f, a1[4 * gq + 1] * 0.125f, a1[4 * gq + 2] * 0.125f,
+                                 a1[4 * gq + 3] * 0.125f));
+  }
+}
+
 __global__ void __launch_bounds__(256) tanh_bwd_kernel(const float* y, int64_t ldy, const float* dy, int64_t lddy,
                                                        int64_t rows, int cols, float* dx, int64_t lddx) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -679,6 +1071,8 @@ int attn_setup(AttnArgs& g, const float* qkv, int64_t ldq, int64_t koff, int64_t
   g.key = nr_dropout_key(seed, offset); g.rng = rng; g.offset = offset; g.ml = ml;
   return NR_OK;
 }
+
+bool prec_ok(int32_t prec) { return prec == NR_GEMM_F32 || prec == NR_GEMM_BF16X6 || prec == NR_GEMM_BF16; }
 
 // waves per workgroup: enough to cover L with 32-row waves, at most 4
 int attn_waves(int L) {
@@ -757,18 +1151,30 @@ extern "C" int nr_bert_add_ln_bwd(const float* x, int64_t ldx, const float* res,
 extern "C" int nr_bert_attn_fwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
                                 int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, float p_drop,
                                 uint64_t seed, uint64_t offset, const uint64_t* rng, float* ctx, int64_t ldc,
-                                float* ml, hipStream_t stream) {
+                                float* ml, int32_t prec, hipStream_t stream) {
   AttnArgs g{};
   int rc = attn_setup(g, qkv, ldq, koff, voff, mask, mask_dtype, nseq, L, heads, p_drop, seed, offset, rng, ml);
   if (rc) return rc;
   if (!ctx || !al16(ctx) || (ldc & 3)) return NR_EINVAL(4);
+  if (!prec_ok(prec)) return NR_EINVAL(6);
   if (nseq == 0) return NR_OK;
   g.ctx = ctx; g.ldc = ldc;
   const int nw = attn_waves(L);
   g.chunks = (L + 32 * nw - 1) / (32 * nw);
-  const dim3 grid((unsigned)(nseq * heads * g.chunks));
-  if (p_drop > 0.f) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(64 * nw), 0, stream, g);
-  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(64 * nw), 0, stream, g);
+  const dim3 grid((unsigned)(nseq * heads * g.chunks)), block(64 * nw);
+  const bool drop = p_drop > 0.f;
+#define NR_FWD(KER) hipLaunchKernelGGL(KER, grid, block, 0, stream, g)
+  if (prec == NR_GEMM_F32) {
+    if (drop) NR_FWD(attn_fwd_kernel<true>);
+    else NR_FWD(attn_fwd_kernel<false>);
+  } else if (prec == NR_GEMM_BF16) {
+    if (drop) NR_FWD((attn_fwd_mp_kernel<1, true>));
+    else NR_FWD((attn_fwd_mp_kernel<1, false>));
+  } else {
+    if (drop) NR_FWD((attn_fwd_mp_kernel<3, true>));
+    else NR_FWD((attn_fwd_mp_kernel<3, false>));
+  }
+#undef NR_FWD
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
@@ -781,13 +1187,14 @@ extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int
                                 int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, float p_drop,
                                 uint64_t seed, uint64_t offset, const uint64_t* rng, const float* ctx, int64_t ldc,
                                 const float* ml, const float* dctx, int64_t ldd, float* work, float* dqkv,
-                                int64_t lddq, hipStream_t stream) {
+                                int64_t lddq, int32_t prec, hipStream_t stream) {
   AttnArgs g{};
   int rc = attn_setup(g, qkv, ldq, koff, voff, mask, mask_dtype, nseq, L, heads, p_drop, seed, offset, rng,
                       const_cast<float*>(ml));
   if (rc) return rc;
   if (!ctx || !dctx || !work || !dqkv) return NR_EINVAL(4);
   if (!al16(ctx) || !al16(dctx) || !al16(dqkv) || ((ldc | ldd | lddq) & 3)) return NR_EINVAL(5);
+  if (!prec_ok(prec)) return NR_EINVAL(6);
   if (nseq == 0) return NR_OK;
   const int64_t T = nseq * L;
   hipLaunchKernelGGL(attn_dsum_kernel, dim3((unsigned)((T * heads + 255) / 256)), dim3(256), 0, stream, dctx, ldd, ctx,
@@ -796,14 +1203,24 @@ extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int
   g.dctx = dctx; g.ldd = ldd; g.Dq = work; g.dqkv = dqkv; g.lddq = lddq;
   const int nw = attn_waves(L);
   g.chunks = (L + 32 * nw - 1) / (32 * nw);
-  const dim3 grid((unsigned)(nseq * heads * g.chunks));
-  if (p_drop > 0.f) {
-    hipLaunchKernelGGL(attn_bwd_kv_kernel<true>, grid, dim3(64 * nw), 0, stream, g);
-    hipLaunchKernelGGL(attn_bwd_q_kernel<true>, grid, dim3(64 * nw), 0, stream, g);
+  const dim3 grid((unsigned)(nseq * heads * g.chunks)), block(64 * nw);
+  const bool drop = p_drop > 0.f;
+#define NR_BWD(KV, Q)                                          \
+  do {                                                         \
+    hipLaunchKernelGGL(KV, grid, block, 0, stream, g);         \
+    hipLaunchKernelGGL(Q, grid, block, 0, stream, g);          \
+  } while (0)
+  if (prec == NR_GEMM_F32) {
+    if (drop) NR_BWD(attn_bwd_kv_kernel<true>, attn_bwd_q_kernel<true>);
+    else NR_BWD(attn_bwd_kv_kernel<false>, attn_bwd_q_kernel<false>);
+  } else if (prec == NR_GEMM_BF16) {
+    if (drop) NR_BWD((attn_bwd_kv_mp_kernel<1, true>), (attn_bwd_q_mp_kernel<1, true>));
+    else NR_BWD((attn_bwd_kv_mp_kernel<1, false>), (attn_bwd_q_mp_kernel<1, false>));
   } else {
-    hipLaunchKernelGGL(attn_bwd_kv_kernel<false>, grid, dim3(64 * nw), 0, stream, g);
-    hipLaunchKernelGGL(attn_bwd_q_kernel<false>, grid, dim3(64 * nw), 0, stream, g);
+    if (drop) NR_BWD((attn_bwd_kv_mp_kernel<3, true>), (attn_bwd_q_mp_kernel<3, true>));
+    else NR_BWD((attn_bwd_kv_mp_kernel<3, false>), (attn_bwd_q_mp_kernel<3, false>));
   }
+#undef NR_BWD
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

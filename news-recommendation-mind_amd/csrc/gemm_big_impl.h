@@ -116,29 +116,34 @@ struct BigMN {
   static constexpr int KP = BK / 2;                            // k pairs per tile
   static constexpr int CH = (R / 4) * KP;                      // chunks per tile
   static constexpr int NC = CH >= 512 ? CH / 512 : 1;          // chunks per thread
-  static constexpr int ACT = CH >= 512 ? 512 : CH;             // active threads
+  // active threads.  The guards below test ACT < 512 first: with every thread active a runtime
+  // `tid >= 512` (never true under __launch_bounds__(512), but not provable) put an exec-mask branch
+  // around each load / split-store and broke the k-tile into blocks, with a vmcnt(0) at the top of
+  // every tile -- the weight-gradient GEMMs ran 20 % slower than round 3 (profiles/r04_f_gemm_ab.json)
+  static constexpr int ACT = CH >= 512 ? 512 : CH;
   static constexpr int SR = big_sr<BK>();
   static_assert(CH % 512 == 0 || CH < 512, "BigMN: whole chunks per thread");
   float4 v[2][NC][2];     // [register set][chunk][k of the pair]
   int64_t kid[2][NC][2];  // MN_GATHER: stored-row ids of a set's next tile (prefetched one load ahead)
   __device__ __forceinline__ void init(const Op&, int64_t, int64_t, int) {}
-  // column sums of register set S's tile (both k of each pair) into cs (the fused bias gradient)
+  // column sums of register set S's tile (both k of each pair), times f (0 or 1), into cs (the fused
+  // bias gradient)
   template <int S>
-  __device__ __forceinline__ void add_colsum(float (&cs)[NC][4], int tid) const {
-    if (tid >= ACT) return;
+  __device__ __forceinline__ void add_colsum(float (&cs)[NC][4], int tid, float f = 1.f) const {
+    if (ACT < 512 && tid >= ACT) return;
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-      cs[j][0] += v[S][j][0].x + v[S][j][1].x;
-      cs[j][1] += v[S][j][0].y + v[S][j][1].y;
-      cs[j][2] += v[S][j][0].z + v[S][j][1].z;
-      cs[j][3] += v[S][j][0].w + v[S][j][1].w;
+      cs[j][0] += f * (v[S][j][0].x + v[S][j][1].x);
+      cs[j][1] += f * (v[S][j][0].y + v[S][j][1].y);
+      cs[j][2] += f * (v[S][j][0].z + v[S][j][1].z);
+      cs[j][3] += f * (v[S][j][0].w + v[S][j][1].w);
     }
   }
   // the per-thread sums of the KP threads of one column group (adjacent lanes) combined; the
   // group's first lane stores its four columns' sums (columns past M skipped)
   __device__ __forceinline__ void put_colsum(float (&cs)[NC][4], int64_t r0, int64_t rlim, float* dst,
                                              int tid) const {
-    if (tid >= ACT) return;
+    if (ACT < 512 && tid >= ACT) return;
 #pragma unroll
     for (int j = 0; j < NC; ++j)
 #pragma unroll
@@ -161,7 +166,7 @@ struct BigMN {
   __device__ __forceinline__ static int cg_of(int c) { return c / KP; }
   template <int S>
   __device__ __forceinline__ void prefetch_idx(const Op& d, int64_t k0, int64_t K, int tid) {
-    if (MODE == MN_GATHER && tid < ACT) {
+    if (MODE == MN_GATHER && (ACT == 512 || tid < ACT)) {
 #pragma unroll
       for (int j = 0; j < NC; ++j)
 #pragma unroll
@@ -173,7 +178,7 @@ struct BigMN {
   }
   template <int S>
   __device__ __forceinline__ void load(const Op& d, int64_t r0, int64_t rlim, int64_t k0, int tid) {
-    if (tid >= ACT) return;
+    if (ACT < 512 && tid >= ACT) return;
     const int64_t cmax = ((rlim + 3) & ~int64_t(3)) - 4;
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
@@ -209,7 +214,7 @@ struct BigMN {
   // chunk j's rows 2 half .. 2 half + 1 (half 0: rows 0, 1 or 2, 3 per the rotation below)
   template <int S, int NP>
   __device__ __forceinline__ void store_half(uint16_t* lds, int tid, int j, int half) const {
-    if (tid >= ACT) return;
+    if (ACT < 512 && tid >= ACT) return;
     const int c = tid + 512 * j;
     const int cg = cg_of(c);
     const bool rot = BK == 16 && ((cg ^ (cg >> 1)) & 1) != 0;
@@ -429,14 +434,21 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
     auto ktile = [&](auto live_t, auto nset, int kt, int st) {
       constexpr bool LIVE = decltype(live_t)::value;
       constexpr int NS = decltype(nset)::value;
-      // interleaved split-stores for bf16x6, except the dgrad operand pair (K-contiguous A with an
-      // MN-contiguous B): one-box A/B (profiles/r04_a_gemm_ab.json, µs) projection fwd 258 -> 248,
-      // weight gradient 292 -> 273, BERT FFN-out 383 -> 376, table dgrad 258 -> 269 (kept off there)
+      // the fused column sum runs in every unit of a CS_OK kernel, weighted 0 where the unit does not
+      // sum or the register set holds a re-read tile (past the unit's last tile): a runtime test inside
+      // the k-tile would split its scheduling region (BERT FFN weight gradient 426 -> 520 us with one)
+      const float csf = do_cs && kt + 1 < nt ? 1.f : 0.f;
+      (void)csf;
+      // interleaved split-stores for bf16x6 on the forward operand pairs (both K-contiguous) and the
+      // gathered weight gradient (MN x MN-gathered): one-box A/B (profiles/r04_a_gemm_ab.json, µs)
+      // projection fwd 258 -> 248, NRMS weight gradient 292 -> 273, BERT FFN-out 383 -> 376; off for
+      // the dgrad pair (K-contiguous A x MN-contiguous B: table dgrad 258 -> 269) and the plain weight
+      // gradient (MN x MN: BERT FFN weight gradient 416 -> 447 us, profiles/r04_f_gemm_ab.json)
 #ifdef NR_BIG_NO_ILV
       constexpr bool ILV = false;
 #else
       constexpr bool ILV = LIVE && NP == 3 && KS == 1 && TJ == 2 && LA::PIECES == 2 && LB::PIECES == 2 &&
-                           !(AM == KC_PLAIN && BMODE == MN_PLAIN);
+                           ((is_kc(AM) && is_kc(BMODE)) || (AM == MN_PLAIN && BMODE == MN_GATHER));
 #endif
       const uint16_t* a_s = As + st * NP * PA;
       const uint16_t* b_s = Bs + st * NP * PB;
@@ -447,7 +459,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
         __builtin_amdgcn_sched_barrier(0);
         if (i == ia && piece < 2) {
           if constexpr (CS_OK) {
-            if (piece == 0 && do_cs && kt + 1 < nt) la.template add_colsum<NS>(cs, tid);
+            if (piece == 0) la.template add_colsum<NS>(cs, tid, csf);
           }
           la.template store_piece<NS, NP>(As + (st ^ 1) * NP * PA, tid, piece);
         }
@@ -514,9 +526,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
         // split-stores of the next stage: A behind step 0's first row block, B (then the loads of
         // k-tile kt+3 into the freed register set) behind step KS/2's second (KS = 1) or first row block
         if (kk == 0 && i == ia) {
-          if constexpr (CS_OK) {   // (past the unit's last tile the register set holds a re-read tile)
-            if (do_cs && kt + 1 < nt) la.template add_colsum<NS>(cs, tid);
-          }
+          if constexpr (CS_OK) la.template add_colsum<NS>(cs, tid, csf);
           la.template store<NS, NP>(As + (st ^ 1) * NP * PA, tid);
         }
         if (kk == KS / 2 && i == ib) {

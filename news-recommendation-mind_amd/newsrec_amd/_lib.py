@@ -130,10 +130,10 @@ _SIGS = {
     "nr_bert_add_ln_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_f32, c_u64, c_u64, c_ptr, c_ptr,
                            c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr],
     "nr_bert_attn_fwd": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_u64, c_u64,
-                         c_ptr, c_ptr, c_i64, c_ptr, c_ptr],
+                         c_ptr, c_ptr, c_i64, c_ptr, c_i32, c_ptr],
     "nr_bert_attn_bwd_workspace": [c_i64, c_i32, c_i32],
     "nr_bert_attn_bwd": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_u64, c_u64,
-                         c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr],
+                         c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i32, c_ptr],
     "nr_tanh_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr],
     "nr_adam_multi": [ctypes.POINTER(nr_adam_tensor), c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_ptr],
     "nr_adam_multi_step": [ctypes.POINTER(nr_adam_tensor), c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_ptr,

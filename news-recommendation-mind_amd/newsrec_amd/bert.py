@@ -14,7 +14,7 @@ their rows are concatenated and each GEMM runs once over all of them (only the a
 and the position ids are per segment).  Per layer:
 
   qkv = x [Wq;Wk;Wv]ᵀ + b                 nr_gemm_f32 (one GEMM, N = 3H)
-  ctx = attention(qkv, mask)              nr_bert_attn_fwd (online softmax, f32 MFMA)
+  ctx = attention(qkv, mask)              nr_bert_attn_fwd (online softmax, the GEMM arithmetic)
   h1  = LN(Dropout(ctx Woᵀ + bo) + x)     nr_gemm_f32 + nr_bert_add_ln_fwd
   G   = gelu(h1 Wiᵀ + bi)                 nr_gemm_f32, NR_EPI_STORE_GELU (pre-activation kept)
   h2  = LN(Dropout(G Wo2ᵀ + bo2) + h1)    nr_gemm_f32 + nr_bert_add_ln_fwd

@@ -865,8 +865,9 @@ def _attn_check(qkv, heads, koff, voff, mask, nseq, seq_len):
 
 
 def bert_attn_fwd(qkv, heads, mask, nseq, seq_len, ctx, ml, koff=None, voff=None, p_drop=0.0, seed=0, offset=0,
-                  rng=None):
-    """BertSelfAttention core on a fused [T, 3*heads*64] (Q | K | V) projection."""
+                  rng=None, prec=None):
+    """BertSelfAttention core on a fused [T, 3*heads*64] (Q | K | V) projection.  ``prec``: the
+    attention products' arithmetic (default: this thread's GEMM precision)."""
     koff = heads * 64 if koff is None else koff
     voff = 2 * heads * 64 if voff is None else voff
     mp, mdt = _attn_check(qkv, heads, koff, voff, mask, nseq, seq_len)
@@ -878,11 +879,11 @@ def bert_attn_fwd(qkv, heads, mask, nseq, seq_len, ctx, ml, koff=None, voff=None
         raise L.HipError("bert_attn_fwd: ml too small")
     p, s, o, r = _drop(p_drop, seed, offset, rng)
     L.call("nr_bert_attn_fwd", L.ptr(qkv), qkv.stride(0), koff, voff, mp, mdt, nseq, seq_len, heads, p, s, o, r,
-           L.ptr(ctx), ctx.stride(0), L.ptr(ml), L.stream_ptr(qkv))
+           L.ptr(ctx), ctx.stride(0), L.ptr(ml), _prec(prec), L.stream_ptr(qkv))
 
 
 def bert_attn_bwd(qkv, heads, mask, nseq, seq_len, ctx, ml, dctx, dqkv, koff=None, voff=None, p_drop=0.0, seed=0,
-                  offset=0, rng=None):
+                  offset=0, rng=None, prec=None):
     koff = heads * 64 if koff is None else koff
     voff = 2 * heads * 64 if voff is None else voff
     mp, mdt = _attn_check(qkv, heads, koff, voff, mask, nseq, seq_len)
@@ -896,7 +897,7 @@ def bert_attn_bwd(qkv, heads, mask, nseq, seq_len, ctx, ml, dctx, dqkv, koff=Non
     p, s, o, r = _drop(p_drop, seed, offset, rng)
     L.call("nr_bert_attn_bwd", L.ptr(qkv), qkv.stride(0), koff, voff, mp, mdt, nseq, seq_len, heads, p, s, o, r,
            L.ptr(ctx), ctx.stride(0), L.ptr(ml), L.ptr(dctx), dctx.stride(0), L.ptr(work), L.ptr(dqkv),
-           dqkv.stride(0), L.stream_ptr(qkv))
+           dqkv.stride(0), _prec(prec), L.stream_ptr(qkv))
 
 
 def tanh_bwd(y, dy, dx):

@@ -27,9 +27,18 @@ def _attn_ref(qkv, mask, nseq, L, heads):
     return (p @ v).transpose(1, 2).reshape(nseq * L, H)
 
 
+# attention products' arithmetic -> (forward atol, backward atol relative to max |grad|): f32 and
+# bf16x6 (fp32-class, 2^-24 per product) share the fp32 bars; plain bf16 rounds every operand to
+# 8 bits (2^-9 relative), scaled by the O(1) scores / values here
+ATTN_PRECS = {"f32": (2e-5, 1e-4), "bf16x6": (2e-5, 1e-4), "bf16": (3e-2, 3e-2)}
+
+
+@pytest.mark.parametrize("prec", list(ATTN_PRECS))
 @pytest.mark.parametrize("nseq,L,heads", [(7, 30, 2), (3, 77, 12), (2, 501, 12), (5, 1, 1), (4, 33, 2)])
-def test_attention_fwd_bwd(nseq, L, heads):
-    from newsrec_amd import kernels as K
+def test_attention_fwd_bwd(nseq, L, heads, prec):
+    from newsrec_amd import _lib as Lb, kernels as K
+    mode = {"f32": Lb.GEMM_F32, "bf16x6": Lb.GEMM_BF16X6, "bf16": Lb.GEMM_BF16}[prec]
+    fa, ba = ATTN_PRECS[prec]
     torch.manual_seed(L)
     H = heads * 64
     T = nseq * L
@@ -41,24 +50,27 @@ def test_attention_fwd_bwd(nseq, L, heads):
     mask = mask.reshape(-1).cuda()
     ctx = torch.empty(T, H, device="cuda")
     ml = torch.empty(T * heads * 2, device="cuda")
-    K.bert_attn_fwd(qkv, heads, mask, nseq, L, ctx, ml)
+    K.bert_attn_fwd(qkv, heads, mask, nseq, L, ctx, ml, prec=mode)
     q64 = qkv.detach().cpu().double().requires_grad_()
     want = _attn_ref(q64, mask.cpu(), nseq, L, heads)
-    np.testing.assert_allclose(ctx.cpu().numpy(), want.detach().numpy(), rtol=0, atol=2e-5)
+    np.testing.assert_allclose(ctx.cpu().numpy(), want.detach().numpy(), rtol=0, atol=fa)
     d = torch.randn(T, H, device="cuda")
     dqkv = torch.full((T, 3 * H), float("nan"), device="cuda")
-    K.bert_attn_bwd(qkv, heads, mask, nseq, L, ctx, ml, d, dqkv)
+    K.bert_attn_bwd(qkv, heads, mask, nseq, L, ctx, ml, d, dqkv, prec=mode)
     want.backward(d.cpu().double())
     g = q64.grad.numpy()
-    np.testing.assert_allclose(dqkv.cpu().numpy(), g, rtol=0, atol=1e-4 * max(1.0, np.abs(g).max()))
+    np.testing.assert_allclose(dqkv.cpu().numpy(), g, rtol=0, atol=ba * max(1.0, np.abs(g).max()))
 
 
-def test_attention_dropout_consistent():
+@pytest.mark.parametrize("prec", ["f32", "bf16x6"])
+def test_attention_dropout_consistent(prec, request):
     """Dropout on the probabilities: the backward regenerates the forward's mask (directional
     derivative of <ctx, d> matches finite differences under the same seed); about p of the
     mass is dropped."""
-    from newsrec_amd import kernels as K
+    from newsrec_amd import _lib as Lb, kernels as K
     torch.manual_seed(3)
+    old = K.set_gemm_precision(Lb.GEMM_F32 if prec == "f32" else Lb.GEMM_BF16X6)
+    request.addfinalizer(lambda: K.set_gemm_precision(old))
     nseq, L, heads, p = 3, 45, 2, 0.3
     H, T = heads * 64, nseq * L
     qkv = torch.randn(T, 3 * H, device="cuda")

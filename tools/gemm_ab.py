@@ -32,6 +32,8 @@ qkv = torch.empty(T, 2304, device=dev); wi = torch.randn(3072, 768, device=dev) 
 G = torch.empty(T, 3072, device=dev); Ub = torch.empty(T, 3072, device=dev)
 wo2 = torch.randn(768, 3072, device=dev) / 50; o = torch.empty(T, 768, device=dev)
 dWi = torch.zeros(3072, 768, device=dev); dbi = torch.zeros(3072, device=dev)
+dWo2 = torch.zeros(768, 3072, device=dev); dbo2 = torch.zeros(768, device=dev)
+dWqkv = torch.zeros(2304, 768, device=dev); dbqkv = torch.zeros(2304, device=dev)
 P = torch.empty(U, 480, device=dev); w3 = torch.randn(480, E, device=dev); Pg = torch.randn(U, 480, device=dev); dw3 = torch.zeros(480, E, device=dev)
 uids = torch.randperm(V - 1, device=dev)[:24600] + 1; dT = torch.zeros(V, E, device=dev)
 dYc = torch.randn(52800, 1152, device=dev); WT = W.t().contiguous()
@@ -55,6 +57,8 @@ cases = {
  "bert_ffn2": (2*T*768*3072, lambda p: K.gemm(T, 768, 3072, K.operand(G, L.KCONTIG), K.operand(wo2, L.KCONTIG), o, prec=p)),
  "bert_ffn1_wgrad": (2*T*768*3072, lambda p: K.gemm(3072, 768, T, K.operand(G, L.MNCONTIG), K.operand(x, L.MNCONTIG), dWi, epilogue=L.EPI_ATOMIC, split_k=F._split_k(3072, 768, T), prec=p)),
  "bert_ffn1_wgrad_cs": (2*T*768*3072, lambda p: K.gemm(3072, 768, T, K.operand(G, L.MNCONTIG), K.operand(x, L.MNCONTIG), dWi, epilogue=L.EPI_ATOMIC, split_k=F._split_k(3072, 768, T), prec=p, colsum=dbi)),
+ "bert_ffn2_wgrad_cs": (2*T*768*3072, lambda p: K.gemm(768, 3072, T, K.operand(o, L.MNCONTIG), K.operand(G, L.MNCONTIG), dWo2, epilogue=L.EPI_ATOMIC, split_k=F._split_k(768, 3072, T), prec=p, colsum=dbo2)),
+ "bert_qkv_wgrad_cs": (2*T*768*2304, lambda p: K.gemm(2304, 768, T, K.operand(qkv, L.MNCONTIG), K.operand(x, L.MNCONTIG), dWqkv, epilogue=L.EPI_ATOMIC, split_k=F._split_k(2304, 768, T), prec=p, colsum=dbqkv)),
  "bert_ffn1_wgrad_atomic": (2*T*768*3072, lambda p: L.call("nr_gemm_f32", 3072, 768, T, K.operand(G, L.MNCONTIG), K.operand(x, L.MNCONTIG), L.ptr(dWi), 768, None, L.EPI_ATOMIC, None, -1, F._split_k(3072, 768, T), p, L.stream_ptr(dWi))),
  "cnn_conv_wgrad": (2*U*E*480, lambda p: K.gemm_dyn(480, E, U, K.operand(Pg, L.MNCONTIG), K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dw3, epilogue=L.EPI_ATOMIC, split_k=F._split_k(480, E, U), prec=p)),
  "cnn_table_dgrad": (2*24600*E*480, lambda p: K.gemm_dyn(U, E, 480, K.operand(Pg, L.KCONTIG), K.operand(w3, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
