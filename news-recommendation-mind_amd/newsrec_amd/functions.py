@@ -76,6 +76,136 @@ def _zeros_views(dev, *shapes):
     return [buf[o:o + n].view(sh) for o, n, sh in zip(offs, sizes, shapes)]
 
 
+class _ZeroArena:
+    """One zero fill for the small zero-initialised gradients of a training step.
+
+    A Function's forward reserves the shapes its backward will zero-fill (``reserve``, only when a
+    backward can run); the first backward that takes its views (``take``) zero-fills every
+    reservation made since the previous fill with ONE launch.  The NRMS step had three such fills
+    (the news tower's five parameter gradients, the user encoder's two, the pooling query's), each a
+    launch of its own in the graph.  A token is taken once: a second backward over the same graph
+    (retain_graph) gets fresh zeros, as do reservations past LIMIT floats."""
+
+    LIMIT = 8 << 20
+
+    def __init__(self):
+        self.cur = None
+
+    def reserve(self, dev, *shapes):
+        sizes = [int(torch.Size(sh).numel()) for sh in shapes]
+        need = sum(_pad4(n) for n in sizes)
+        a = self.cur
+        if a is None or a["buf"] is not None or a["dev"] != dev or a["tot"] + need > self.LIMIT:
+            a = self.cur = {"dev": dev, "tot": 0, "buf": None}
+        offs = []
+        for n in sizes:
+            offs.append(a["tot"])
+            a["tot"] += _pad4(n)
+        return {"arena": a, "offs": offs, "sizes": sizes, "shapes": shapes, "taken": False}
+
+    def take(self, tok, dev, *shapes):
+        """The reserved views (zero), or ``_zeros_views(dev, *shapes)`` without a usable token."""
+        if tok is None or tok["taken"] or tuple(tok["shapes"]) != tuple(shapes):
+            return _zeros_views(dev, *shapes)
+        tok["taken"] = True
+        a = tok["arena"]
+        if a["buf"] is None:
+            a["buf"] = torch.zeros(max(a["tot"], 1), device=a["dev"])
+            if self.cur is a:
+                self.cur = None
+        buf = a["buf"]
+        return [buf[o:o + n].view(sh) for o, n, sh in zip(tok["offs"], tok["sizes"], shapes)]
+
+
+ZERO_ARENA = _ZeroArena()
+
+
+def _reserve_zeros(ctx, dev, *shapes):
+    """Forward side of ZERO_ARENA: reserve the backward's zero-initialised gradients (when one can run)."""
+    ctx.zero_tok = ZERO_ARENA.reserve(dev, *shapes) if any(ctx.needs_input_grad) else None
+
+
+def _backward_zeros(ctx, dev, *shapes):
+    return ZERO_ARENA.take(getattr(ctx, "zero_tok", None), dev, *shapes)
+
+
+class _GradDest:
+    """Where a consumer's backward may write the gradient of one of its inputs directly: SplitRowsFn
+    offers the two halves of its joined gradient buffer for its two outputs; a consumer Function
+    (scorer, user encoder) that takes the offer in its forward stores its input gradient there, and
+    SplitRowsFn's backward then finds both halves in place and skips the join copy.  The written
+    values are that consumer's true gradient either way, so a stale or unused offer costs nothing
+    but the copy it fails to save."""
+
+    def __init__(self):
+        self.offers = {}
+
+    @staticmethod
+    def _key(t):
+        return (t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.device)
+
+    def offer(self, t, dest):
+        self.offers[self._key(t)] = dest
+
+    def clear(self):
+        self.offers.clear()
+
+    def take(self, t):
+        if not self.offers:
+            return None
+        d = self.offers.pop(self._key(t), None)
+        if d is None or d.shape != t.shape:
+            return None
+        return d
+
+
+GRAD_DEST = _GradDest()
+
+
+def _grad_out(dest, rows, cols, like):
+    """The backward's output buffer for an input gradient: the offered destination or a new one."""
+    if dest is not None:
+        return dest
+    return _empty(rows, cols, like)
+
+
+class SplitRowsFn(torch.autograd.Function):
+    """``torch.split(x, [n0, rows - n0])`` of a row-major [rows, H] activation (the joint news-encoder
+    output -> candidates | history).  torch's backward joins the two gradients with a copy (a cat);
+    here the joined gradient buffer is allocated in the forward and its halves offered (GRAD_DEST) to
+    the Functions that consume the two outputs, so the join is free when both write in place."""
+
+    stats = {"in_place": 0, "copied": 0}   # backward joins by path (tests)
+
+    @staticmethod
+    def forward(ctx, x, n0):
+        rows, H = x.shape
+        g = _empty(rows, H, x)
+        a, b = x[:n0], x[n0:]
+        GRAD_DEST.clear()
+        GRAD_DEST.offer(a, g[:n0])
+        GRAD_DEST.offer(b, g[n0:])
+        ctx.g, ctx.n0 = g, n0
+        return a, b
+
+    @staticmethod
+    def backward(ctx, da, db):
+        g, n0 = ctx.g, ctx.n0
+        ga, gb = g[:n0], g[n0:]
+        if (da is not None and db is not None and da.data_ptr() == ga.data_ptr() and
+                db.data_ptr() == gb.data_ptr() and da.stride() == ga.stride() and db.stride() == gb.stride()):
+            SplitRowsFn.stats["in_place"] += 1
+            return g, None
+        SplitRowsFn.stats["copied"] += 1
+        out = torch.empty_like(g)
+        for d, o in ((da, out[:n0]), (db, out[n0:])):
+            if d is None:
+                o.zero_()
+            else:
+                o.copy_(d)
+        return out, None
+
+
 def _split_k(m, n, k, slots=512):
     """Split-K factor for a wgrad GEMM: fill the 256 CUs x 2 resident 128x128 blocks in ONE
     wave (a 1.16-wave grid runs as two), keeping >= 512 k per split."""
@@ -377,6 +507,7 @@ class MHANewsFn(torch.autograd.Function):
             K.attn_pool_fwd(O, query, mask, n, seq_len, news, probs, gamma=gamma, beta=beta, stats=stats,
                             p_drop=p_drop, seed=seed, offset=0 if rng is not None else offset, zout=tok, rng=rng)
         ctx.save_for_backward(table, ids, mask, w_cat, gamma, beta, query, Y, O, probs, stats)
+        _reserve_zeros(ctx, table.device, (H,), (H,), (H,), (NY,), (NY, E))
         ctx.cfg = (heads, dk, dv, seq_len, pad_row, p_drop, seed, offset, fused)
         ctx.table_ref = table
         ctx.ur = ur
@@ -395,7 +526,7 @@ class MHANewsFn(torch.autograd.Function):
         NQ = heads * dk
         NY = NQ + H
         dnews = dnews.contiguous()
-        dq, dgamma, dbeta, db, dw = _zeros_views(table.device, (H,), (H,), (H,), (NY,), (NY, E))
+        dq, dgamma, dbeta, db, dw = _backward_zeros(ctx, table.device, (H,), (H,), (H,), (NY,), (NY, E))
         dY = _empty(T, NY, table)
         dz = dtok.contiguous() if dtok is not None else None
         ur = ctx.ur
@@ -609,6 +740,7 @@ class CNNNewsRowsFn(torch.autograd.Function):
             K.seq_pool_fwd(C, query, mask, n, seq_len, Hp, news, probs, key=Kq, qn=H)
         ctx.save_for_backward(table, ids, mask, w3t, wq, bq, query, C, Kq, probs)
         ctx.cfg = (seq_len, pad_row, H, fused)
+        _reserve_zeros(ctx, table.device, (Hp, Hp), (Hp,), (H,), (3 * Hp, E), (H,))
         ctx.table_ref = table
         ctx.ur = ur
         return news[:, :H], C[:, :H]
@@ -627,7 +759,7 @@ class CNNNewsRowsFn(torch.autograd.Function):
         Hp = w3t.shape[0] // 3
         dev = table.device
         dC = _empty(T, Hp, table)
-        dwq, dbq, dconv_b, dw3t, dq = _zeros_views(dev, (Hp, Hp), (Hp,), (H,), (3 * Hp, E), (H,))
+        dwq, dbq, dconv_b, dw3t, dq = _backward_zeros(ctx, dev, (Hp, Hp), (Hp,), (H,), (3 * Hp, E), (H,))
         if dnews.stride(-1) != 1:
             dnews = dnews.contiguous()
         if fused:
@@ -693,19 +825,19 @@ class AttnPoolFn(torch.autograd.Function):
             K.attn_pool_fwd(x, query, mask, B, N, out, probs)
         ctx.save_for_backward(x, query, mask, probs)
         ctx.cfg = (B, N, H, sp)
+        ctx.dx_dest = GRAD_DEST.take(x)
+        _reserve_zeros(ctx, x.device, (H,))
         return out
 
     @staticmethod
     def backward(ctx, dout):
         x, query, mask, probs = ctx.saved_tensors
         B, N, H, sp = ctx.cfg
+        dx = _grad_out(ctx.dx_dest, B * N, H, x)
+        dq, = _backward_zeros(ctx, x.device, (H,))
         if sp:
-            dx = _empty(B * N, H, x)
-            dq = torch.zeros(H, device=x.device)
             K.seq_pool_bwd(x, query, mask, B, N, H, probs, dout if dout.stride(-1) == 1 else dout.contiguous(), dx, dq)
             return dx, dq.view_as(query), None, None, None
-        dx = _empty(B * N, H, x)
-        dq = torch.zeros(H, device=x.device)
         K.attn_pool_bwd(x, query, mask, B, N, probs, dout.contiguous(), dx, dq)
         return dx, dq.view_as(query), None, None, None
 
@@ -731,6 +863,8 @@ class MHAFn(torch.autograd.Function):
         K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:NY], mask, nseq, seq_len, heads, dk, dv, O)
         ctx.save_for_backward(x, mask, w_cat, Y)
         ctx.cfg = (nseq, seq_len, heads, dk, dv)
+        ctx.dx_dest = GRAD_DEST.take(x)
+        _reserve_zeros(ctx, x.device, (NY, D), (NY,))
         return O
 
     @staticmethod
@@ -755,9 +889,9 @@ class MHAFn(torch.autograd.Function):
             K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx, epilogue=L.EPI_ATOMIC,
                    split_k=split)
         else:
-            dx = _empty(rows, D, x)
+            dx = _grad_out(ctx.dx_dest, rows, D, x)
             K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx)
-        dw, db = _zeros_views(dev, (NY, D), (NY,))
+        dw, db = _backward_zeros(ctx, dev, (NY, D), (NY,))
         _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows)
         return dx, None, dw, db, None, None, None, None, None
 
@@ -794,6 +928,8 @@ class RNNUserFn(torch.autograd.Function):
                   h0=user_table if user_table is not None else None, h0_idx=h0_idx, mask=mask, reverse=reverse)
         ctx.save_for_backward(x, w_ih, w_hh, gates, hprev, cprev, mask, h0_idx, user_table)
         ctx.cfg = (cell, B, N, reverse)
+        ctx.dx_dest = GRAD_DEST.take(x) if Hp == H else None
+        _reserve_zeros(ctx, dev, (G * H, H), (G * H,), (G * H, H), (G * H,))
         ctx.table_ref = user_table
         return hout
 
@@ -821,7 +957,7 @@ class RNNUserFn(torch.autograd.Function):
         K.rnn_bwd(cell, w_hh.contiguous(), gates, hprev, cprev, B, N, H, dh.contiguous(), dgi, dgh=dgh, dh0=dh0,
                   mask=mask, reverse=reverse)
         dgh_ = dgi if dgh is None else dgh
-        dx = _empty(B * N, H, x)
+        dx = _grad_out(ctx.dx_dest, B * N, H, x)
         if Hp != H:
             w_k = torch.nn.functional.pad(w_ih.detach(), (0, Hp - H, 0, GHp - GH))
             K.gemm(B * N, H, GHp, K.operand(dgi_b, L.KCONTIG), K.operand(w_k, L.MNCONTIG), dx)
@@ -829,7 +965,7 @@ class RNNUserFn(torch.autograd.Function):
         else:
             K.gemm(B * N, H, GH, K.operand(dgi, L.KCONTIG), K.operand(w_ih, L.MNCONTIG), dx)
             h_k = hprev
-        dw_ih, db_ih, dw_hh, db_hh = _zeros_views(dev, (GH, H), (GH,), (GH, H), (GH,))
+        dw_ih, db_ih, dw_hh, db_hh = _backward_zeros(ctx, dev, (GH, H), (GH,), (GH, H), (GH,))
         _proj_wgrad(dgi, K.operand(x, L.MNCONTIG), dw_ih, db_ih, B * N)
         _proj_wgrad(dgh_, K.operand(h_k, L.MNCONTIG), dw_hh, db_hh, B * N)
         dtab = None
@@ -853,6 +989,7 @@ class ScoreFn(torch.autograd.Function):
         K.score_fwd(cdd, user, B, C, H, mode, logits)
         ctx.save_for_backward(cdd, user, logits)
         ctx.cfg = (B, C, mode)
+        ctx.dcdd_dest = GRAD_DEST.take(cdd)
         return logits
 
     @staticmethod
@@ -860,7 +997,7 @@ class ScoreFn(torch.autograd.Function):
         cdd, user, logits = ctx.saved_tensors
         B, C, mode = ctx.cfg
         H = user.shape[1]
-        dcdd = _empty(B * C, H, user)
+        dcdd = _grad_out(ctx.dcdd_dest, B * C, H, user)
         duser = _empty(B, H, user)
         K.score_bwd(cdd, user, logits, dlogits.contiguous(), B, C, H, mode, dcdd, duser)
         return dcdd, duser, None, None, None
@@ -881,6 +1018,7 @@ class ScoreNLLFn(torch.autograd.Function):
         K.score_nll_fwd(cdd, user, label, B, C, H, logits, loss)
         ctx.save_for_backward(cdd, user, logits, label)
         ctx.cfg = (B, C)
+        ctx.dcdd_dest = GRAD_DEST.take(cdd)
         ctx.set_materialize_grads(False)
         return logits, loss
 
@@ -889,7 +1027,7 @@ class ScoreNLLFn(torch.autograd.Function):
         cdd, user, logits, label = ctx.saved_tensors
         B, C = ctx.cfg
         H = user.shape[1]
-        dcdd = _empty(B * C, H, user)
+        dcdd = _grad_out(ctx.dcdd_dest, B * C, H, user)
         duser = _empty(B, H, user)
         if dlogits is not None and not dlogits.is_contiguous():
             dlogits = dlogits.contiguous()

@@ -15,7 +15,7 @@ from torch import nn
 from . import _lib as L
 from . import kernels as K
 from .attention import _joined_view
-from .functions import ScoreFn, ScoreNLLFn
+from .functions import ScoreFn, ScoreNLLFn, SplitRowsFn
 
 
 class TwoTowerBaseModel(nn.Module):
@@ -179,9 +179,10 @@ class TwoTower(TwoTowerBaseModel):
         if masks is None:
             masks = torch.cat([cdd_m.reshape(B * C, Lq), his_m.reshape(B * N, Lq)], 0)
         news = self.encoderN.encode_tokens(self.embedding.table, tokens, masks)[1]
-        # split, not two slices: the backward joins the two gradients with one copy (two slices'
-        # backwards would zero-fill and copy a full-size gradient each, then add them)
-        cdd, his = torch.split(news, [B * C, B * N])
+        # split, not two slices (two slices' backwards would zero-fill and copy a full-size gradient
+        # each, then add them); SplitRowsFn's consumers write their input gradients straight into
+        # its joined gradient buffer, so the join costs no copy either
+        cdd, his = SplitRowsFn.apply(news, B * C)
         cdd = cdd.reshape(B, C, -1)
         his = his.reshape(B, N, -1)
         return cdd, self._user_from_his(his, x), None

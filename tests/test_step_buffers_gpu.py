@@ -1,0 +1,63 @@
+"""The step's gradient buffers: the candidates | history split joins its two gradients in place
+(SplitRowsFn: the scorer and the user encoder write straight into the joined buffer, no cat), and
+the small zero-initialised parameter gradients of a step come from one fill (functions.ZERO_ARENA)
+-- against the reference goldens, and under a retained graph's second backward (dense accumulation)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from golden_util import Golden
+from model_util import build_model, load_golden_params
+
+
+def _setup(cfg):
+    g = Golden(cfg)
+    model = build_model(g.encN, g.encU, g.hidden, vocab=int(g["meta.vocab"]))
+    load_golden_params(model, g)
+    if g.encU == "lstur":
+        model.encoderU.keep_override = torch.from_numpy(g["in.lstur_keep"])
+    return g, model, g.inputs("cuda")
+
+
+def _check(g, model, mult=1.0):
+    grads = dict(model.named_parameters())
+    for n in g.names:
+        want = mult * g["grad." + n]
+        p = grads.get(n)
+        got = p.grad.cpu().numpy() if (p is not None and p.grad is not None) else np.zeros_like(want)
+        scale = max(float(np.abs(want).max()), 1e-6)
+        np.testing.assert_allclose(got, want, rtol=0, atol=1e-3 * scale, err_msg=n)
+
+
+@pytest.mark.parametrize("cfg", ["nrms", "cnn_attn", "cnn_lstur"])
+@pytest.mark.parametrize("head", ["forward", "forward_loss"])
+def test_split_join_in_place(cfg, head):
+    from newsrec_amd.functions import SplitRowsFn
+    g, model, x = _setup(cfg)
+    model.train()
+    SplitRowsFn.stats.update(in_place=0, copied=0)
+    if head == "forward":
+        logits, _ = model(x)
+        loss = torch.nn.functional.nll_loss(logits, x["label"])
+    else:
+        _, loss = model.forward_loss(x)
+    loss.backward()
+    assert abs(loss.item() - float(g["out.loss"])) < 1e-4
+    assert SplitRowsFn.stats == {"in_place": 1, "copied": 0}, SplitRowsFn.stats
+    _check(g, model)
+
+
+@pytest.mark.parametrize("cfg", ["nrms", "cnn_attn"])
+def test_retained_graph_second_backward(cfg):
+    """Two backward passes over one retained graph accumulate (torch's dense semantics): every
+    gradient is twice the golden one -- the second pass must not reuse the first one's zero arena
+    views or write into the gradient buffers the first pass returned."""
+    g, model, x = _setup(cfg)
+    model.train()
+    logits, _ = model(x)
+    loss = torch.nn.functional.nll_loss(logits, x["label"])
+    loss.backward(retain_graph=True)
+    loss.backward()
+    _check(g, model, mult=2.0)
