@@ -199,10 +199,12 @@ int nr_conv3_rows_fwd(const float* P, int64_t ldp, int32_t tap_width, int32_t H,
 
 /* The distinct-row CNN encoder's weight operands in one launch: w3t [3*Hp][E] (row tap*Hp + h =
  * conv_w[h][:][tap], the Conv1d weight [H][E][3]; rows h >= H zero), wqp [Hp][Hp] and bqp [Hp] (the
- * key projection zero-padded).  nr_cnn_unpack_grads maps the gradients of those operands back to the
- * parameters' layouts (dconv_w [H][E][3], dwq [H][H], dbq [H]; stored, not accumulated). */
+ * key projection zero-padded); optional w3tt [E][3*Hp] = w3t transposed (the K-contiguous weight
+ * operand of the table dgrad; NULL: not written).  nr_cnn_unpack_grads maps the gradients of those
+ * operands back to the parameters' layouts (dconv_w [H][E][3], dwq [H][H], dbq [H]; stored, not
+ * accumulated). */
 int nr_cnn_pack_weights(const float* conv_w, const float* wq, const float* bq, int32_t H, int32_t E,
-                        int32_t Hp, float* w3t, float* wqp, float* bqp, hipStream_t stream);
+                        int32_t Hp, float* w3t, float* wqp, float* bqp, float* w3tt, hipStream_t stream);
 int nr_cnn_unpack_grads(const float* dw3t, const float* dwqp, const float* dbqp, int32_t H, int32_t E,
                         int32_t Hp, float* dconv_w, float* dwq, float* dbq, hipStream_t stream);
 

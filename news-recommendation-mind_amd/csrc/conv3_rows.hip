@@ -71,14 +71,16 @@ namespace {
 __global__ __launch_bounds__(256) void cnn_pack_kernel(const float* __restrict__ cw, const float* __restrict__ wq,
                                                        const float* __restrict__ bq, int H, int E, int Hp,
                                                        float* __restrict__ w3t, float* __restrict__ wqp,
-                                                       float* __restrict__ bqp) {
+                                                       float* __restrict__ bqp, float* __restrict__ w3tt) {
   const int64_t n3 = (int64_t)3 * Hp * E, nq = (int64_t)Hp * Hp;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n3 + nq + Hp;
        i += (int64_t)gridDim.x * blockDim.x) {
-    if (i < n3) {   // w3t[tap*Hp + h][e] = conv.weight[h][e][tap]
+    if (i < n3) {   // w3t[tap*Hp + h][e] = conv.weight[h][e][tap]; w3tt its transpose [e][tap*Hp + h]
       const int64_t r = i / E, e = i - r * E;
       const int tap = (int)(r / Hp), h = (int)(r - (int64_t)tap * Hp);
-      w3t[i] = h < H ? cw[((int64_t)h * E + e) * 3 + tap] : 0.f;
+      const float x = h < H ? cw[((int64_t)h * E + e) * 3 + tap] : 0.f;
+      w3t[i] = x;
+      if (w3tt) w3tt[e * 3 * Hp + r] = x;
     } else if (i < n3 + nq) {
       const int64_t k = i - n3;
       const int r = (int)(k / Hp), c = (int)(k - (int64_t)r * Hp);
@@ -116,10 +118,11 @@ __global__ __launch_bounds__(256) void cnn_unpack_kernel(const float* __restrict
 }  // namespace
 
 extern "C" int nr_cnn_pack_weights(const float* conv_w, const float* wq, const float* bq, int32_t H, int32_t E,
-                                   int32_t Hp, float* w3t, float* wqp, float* bqp, hipStream_t stream) {
+                                   int32_t Hp, float* w3t, float* wqp, float* bqp, float* w3tt, hipStream_t stream) {
   if (H < 1 || E < 1 || Hp < H) return NR_EINVAL(0);
   if (!conv_w || !wq || !bq || !w3t || !wqp || !bqp) return NR_EINVAL(1);
-  hipLaunchKernelGGL(cnn_pack_kernel, dim3(1024), dim3(256), 0, stream, conv_w, wq, bq, H, E, Hp, w3t, wqp, bqp);
+  hipLaunchKernelGGL(cnn_pack_kernel, dim3(1024), dim3(256), 0, stream, conv_w, wq, bq, H, E, Hp, w3t, wqp, bqp,
+                     w3tt);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

@@ -70,7 +70,7 @@ _SIGS = {
     "nr_unique_rows_workspace": [c_i64],
     "nr_segment_rows_sum_conv3": [c_ptr, c_i64, c_i64, c_i32, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr,
                                   c_i64, c_ptr],
-    "nr_cnn_pack_weights": [c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
+    "nr_cnn_pack_weights": [c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
     "nr_cnn_unpack_grads": [c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
     "nr_cnn_keypool_fwd": [c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i32, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_i32,
                            c_ptr, c_i64, c_ptr, c_ptr],

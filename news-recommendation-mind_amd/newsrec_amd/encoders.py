@@ -75,8 +75,7 @@ class CNN_Encoder(nn.Module):
         weight[h, :, tap]) and the key projection zero-padded to Hp = ceil32(H) (K % 32 == 0)."""
         H = self.hidden_dim
         Hp = (H + 31) // 32 * 32
-        w3t, wq, bq = F.CNNWeightsFn.apply(self.cnn.weight, self.wordQueryProject.weight, self.wordQueryProject.bias, Hp)
-        return w3t, wq, bq
+        return F.CNNWeightsFn.apply(self.cnn.weight, self.wordQueryProject.weight, self.wordQueryProject.bias, Hp)
 
     def encode_tokens(self, table, token_ids, attn_mask, pad_row=0):
         lead = token_ids.shape[:-1]
@@ -84,9 +83,9 @@ class CNN_Encoder(nn.Module):
         T = token_ids.numel()
         ids = token_ids.reshape(T)
         if F.DEDUP_ROWS:
-            w3t, wq, bq = self._rows_operands()
+            w3t, wq, bq, w3tt = self._rows_operands()
             news, tok = CNNNewsRowsFn.apply(table, ids, _mask_rows(attn_mask, T), w3t, self.cnn.bias, wq, bq,
-                                            self.query_words, seq_len, pad_row, self.hidden_dim)
+                                            self.query_words, seq_len, pad_row, self.hidden_dim, w3tt)
             return tok.reshape(*lead, seq_len, self.hidden_dim), news.reshape(*lead, self.hidden_dim)
         news, tok = CNNNewsFn.apply(table, ids, _mask_rows(attn_mask, T), self._w3().contiguous(), self.cnn.bias,
                                     self.wordQueryProject.weight, self.wordQueryProject.bias, self.query_words,

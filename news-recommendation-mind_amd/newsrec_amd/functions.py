@@ -659,26 +659,30 @@ class CNNNewsFn(torch.autograd.Function):
 
 class CNNWeightsFn(torch.autograd.Function):
     """The distinct-row CNN encoder's weight operands (nr_cnn_pack_weights): the Conv1d weight
-    [H, E, 3] as w3t [3*Hp, E] (row tap*Hp + h) and the key projection zero-padded to [Hp, Hp] / [Hp],
-    in one launch; the backward maps the three gradients back in one launch."""
+    [H, E, 3] as w3t [3*Hp, E] (row tap*Hp + h), its transpose w3tt [E, 3*Hp] (the table dgrad's
+    K-contiguous weight, CNN_DGRAD_KC; None otherwise) and the key projection zero-padded to
+    [Hp, Hp] / [Hp], in one launch; the backward maps the three gradients back in one launch."""
 
     @staticmethod
     def forward(ctx, conv_w, wq, bq, Hp):
         H, E = conv_w.shape[0], conv_w.shape[1]
         dev = conv_w.device
         w3t = torch.empty(3 * Hp, E, device=dev)
+        w3tt = torch.empty(E, 3 * Hp, device=dev) if CNN_DGRAD_KC else None
         wqp = torch.empty(Hp, Hp, device=dev)
         bqp = torch.empty(Hp, device=dev)
         for t in (conv_w, wq, bq):
             if not t.is_contiguous():
                 raise L.HipError("cnn weights must be contiguous")
         L.call("nr_cnn_pack_weights", L.ptr(conv_w), L.ptr(wq), L.ptr(bq), H, E, Hp, L.ptr(w3t), L.ptr(wqp),
-               L.ptr(bqp), L.stream_ptr(conv_w))
+               L.ptr(bqp), L.ptr(w3tt), L.stream_ptr(conv_w))
         ctx.cfg = (H, E, Hp)
-        return w3t, wqp, bqp
+        if w3tt is not None:
+            ctx.mark_non_differentiable(w3tt)
+        return w3t, wqp, bqp, w3tt
 
     @staticmethod
-    def backward(ctx, dw3t, dwqp, dbqp):
+    def backward(ctx, dw3t, dwqp, dbqp, _dw3tt):
         H, E, Hp = ctx.cfg
         dev = (dw3t if dw3t is not None else dwqp).device
         dw3t = dw3t.contiguous() if dw3t is not None else torch.zeros(3 * Hp, E, device=dev)
@@ -710,7 +714,7 @@ class CNNNewsRowsFn(torch.autograd.Function):
     Returns (news [n, H] view, C [T, H] view)."""
 
     @staticmethod
-    def forward(ctx, table, ids, mask, w3t, conv_b, wq, bq, query, seq_len, pad_row, H):
+    def forward(ctx, table, ids, mask, w3t, conv_b, wq, bq, query, seq_len, pad_row, H, w3tt=None):
         # the token output C is rarely consumed: an unused one must not cost a zero-filled gradient
         # (and a padded copy of it) per step
         ctx.set_materialize_grads(False)
@@ -738,7 +742,7 @@ class CNNNewsRowsFn(torch.autograd.Function):
                    epilogue=L.EPI_STORE_TANH)
             # pooling over the padded width: C and Kq are exactly zero past H, and so is the padded query
             K.seq_pool_fwd(C, query, mask, n, seq_len, Hp, news, probs, key=Kq, qn=H)
-        ctx.save_for_backward(table, ids, mask, w3t, wq, bq, query, C, Kq, probs)
+        ctx.save_for_backward(table, ids, mask, w3t, wq, bq, query, C, Kq, probs, w3tt)
         ctx.cfg = (seq_len, pad_row, H, fused)
         _reserve_zeros(ctx, table.device, (Hp, Hp), (Hp,), (H,), (3 * Hp, E), (H,))
         ctx.table_ref = table
@@ -748,7 +752,7 @@ class CNNNewsRowsFn(torch.autograd.Function):
     @staticmethod
     @_gemm_backward
     def backward(ctx, dnews, dC_out):
-        table, ids, mask, w3t, wq, bq, query, C, Kq, probs = ctx.saved_tensors
+        table, ids, mask, w3t, wq, bq, query, C, Kq, probs, w3tt = ctx.saved_tensors
         seq_len, pad_row, H, fused = ctx.cfg
         ur = ctx.ur
         T = ids.numel()
@@ -787,8 +791,8 @@ class CNNNewsRowsFn(torch.autograd.Function):
         inflight = False
         if ctx.needs_input_grad[0]:
             dtable = torch.zeros(V, E, device=dev)
-            if CNN_DGRAD_KC:   # the weights transposed once (1.5 MB) so both operands are k-contiguous
-                w_b = K.operand(w3t.t().contiguous(), L.KCONTIG)
+            if CNN_DGRAD_KC:   # the weights transposed (1.5 MB, by the pack launch) so both operands are k-contiguous
+                w_b = K.operand(w3tt if w3tt is not None else w3t.t().contiguous(), L.KCONTIG)
             else:
                 w_b = K.operand(w3t, L.MNCONTIG)
             K.gemm_dyn(ur.cap, E, 3 * Hp, K.operand(S, L.KCONTIG), w_b, dtable,
@@ -803,7 +807,7 @@ class CNNNewsRowsFn(torch.autograd.Function):
                    max_cus=WGRAD_DEFER_HOOK.max_cus if inflight else 0,
                    workspace=(WGRAD_WS_BF16 and ctx.prec == L.GEMM_BF16) or
                    (WGRAD_WS_BF16X6 and ctx.prec == L.GEMM_BF16X6))
-        return (dtable, None, None, dw3t, dconv_b, dwq, dbq, dq.view_as(query), None, None, None)
+        return (dtable, None, None, dw3t, dconv_b, dwq, dbq, dq.view_as(query), None, None, None, None)
 
 
 # ---------------------------------------------------------------------- pooling user encoder
@@ -909,6 +913,7 @@ class RNNUserFn(torch.autograd.Function):
         H = x.shape[1]
         G = 4 if cell == L.CELL_LSTM else 3
         dev = x.device
+        ctx.dx_dest = GRAD_DEST.take(x)   # (before x is padded below)
         gx = _empty(B * N, G * H, x)
         # the input projection contracts over H: padded to a multiple of 32 with zero columns (a 1 MB
         # copy of x, 0.4 MB of w_ih) it runs on the fast GEMM path instead of the generic one
@@ -928,7 +933,6 @@ class RNNUserFn(torch.autograd.Function):
                   h0=user_table if user_table is not None else None, h0_idx=h0_idx, mask=mask, reverse=reverse)
         ctx.save_for_backward(x, w_ih, w_hh, gates, hprev, cprev, mask, h0_idx, user_table)
         ctx.cfg = (cell, B, N, reverse)
-        ctx.dx_dest = GRAD_DEST.take(x) if Hp == H else None
         _reserve_zeros(ctx, dev, (G * H, H), (G * H,), (G * H, H), (G * H,))
         ctx.table_ref = user_table
         return hout
