@@ -214,22 +214,25 @@ int nr_cnn_unpack_grads(const float* dw3t, const float* dwqp, const float* dbqp,
  * projection never reaches HBM.  C [nseq*L][Hp] (ldc % 4 == 0, 16-B aligned, exactly zero past the
  * valid width), wq [Hp][Hp] / bq [Hp] zero-padded (nr_cnn_pack_weights), q [qn]; Hp a multiple of
  * 32 up to 160, L <= 32.  prec: enum nr_gemm_precision of the key products.  news [nseq][Hp]
- * (ldn >= Hp), probs [nseq*L]. */
+ * (ldn >= Hp), probs [nseq*L].  kout (optional, [nseq*L][ldk >= Hp]): K stored for the backward (which
+ * then skips the key recompute); NULL keeps the key projection on chip. */
 int nr_cnn_keypool_fwd(const float* C, int64_t ldc, const float* wq, const float* bq, const float* q, int32_t qn,
                        const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L, int32_t Hp, float scale,
-                       int32_t prec, float* news, int64_t ldn, float* probs, hipStream_t stream);
+                       int32_t prec, float* news, int64_t ldn, float* probs, float* kout, int64_t ldk,
+                       hipStream_t stream);
 /* Backward of nr_cnn_keypool_fwd in one pass over C (the key projection recomputed): dc [nseq*L][Hp] =
  * ReLU'(C) ⊙ (p dnews + dK wq + dz) (the conv pre-activation gradient; dz optional, [T][>= H]),
  * dK = ds q ⊙ (1 - K²); dwq [Hp][Hp] = Σ dKᵀ C, dbq [Hp] = Σ dK, dq [qn] = Σ ds K, dconv_b [H] =
  * Σ_t dc[t] -- all STORED (not accumulated), summed deterministically over per-workgroup partials in
- * ws (nr_cnn_keypool_workspace(nseq, Hp) floats).  Replaces the reference's autograd through
- * CNN.py:46 + Attention.py:22-29 and the ReLU of CNN.py:42. */
+ * ws (nr_cnn_keypool_workspace(nseq, Hp) floats).  kin (optional): the forward's kout -- K is read
+ * instead of recomputed.  Replaces the reference's autograd through CNN.py:46 + Attention.py:22-29
+ * and the ReLU of CNN.py:42. */
 int64_t nr_cnn_keypool_workspace(int64_t nseq, int32_t Hp);
 int nr_cnn_keypool_bwd(const float* C, int64_t ldc, const float* wq, const float* bq, const float* q, int32_t qn,
                        int64_t nseq, int32_t L, int32_t Hp, int32_t H, float scale, int32_t prec,
                        const float* probs, const float* dnews, int64_t lddn, const float* dz, int64_t lddz,
                        float* dc, int64_t lddc, float* dwq, float* dbq, float* dq, float* dconv_b, float* ws,
-                       int64_t ws_floats, hipStream_t stream);
+                       int64_t ws_floats, const float* kin, int64_t ldk, hipStream_t stream);
 
 /* ------------------------------------------------------------------ attention */
 

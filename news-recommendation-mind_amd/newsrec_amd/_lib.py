@@ -73,11 +73,11 @@ _SIGS = {
     "nr_cnn_pack_weights": [c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
     "nr_cnn_unpack_grads": [c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_ptr, c_ptr],
     "nr_cnn_keypool_fwd": [c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i32, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_i32,
-                           c_ptr, c_i64, c_ptr, c_ptr],
+                           c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr],
     "nr_cnn_keypool_workspace": [c_i64, c_i32],
     "nr_cnn_keypool_bwd": [c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_f32, c_i32,
                            c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
-                           c_ptr],
+                           c_ptr, c_i64, c_ptr],
     "nr_conv3_rows_fwd": [c_ptr, c_i64, c_i32, c_i32, c_ptr, c_i64, c_i32, c_ptr, c_i32, c_ptr, c_i64, c_ptr],
     "nr_mha_attn_fwd": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32,
                         c_f32, c_ptr, c_i64, c_ptr],

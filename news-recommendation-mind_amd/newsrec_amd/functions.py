@@ -311,6 +311,9 @@ PROJ_WGRAD_WS = True
 # CNN word attention (tanh key projection + learned-query pooling) fused per title, forward and
 # backward (nr_cnn_keypool_*; False: the key GEMM + pooling kernels the parity tests compare with).
 FUSED_KEYPOOL = True
+# The fused key-pool forward stores K = tanh(C Wqᵀ + bq) ([T, Hp], 34 MB at B = 32) and its backward
+# reads it instead of recomputing the key products per title (False: recomputed, K stays on chip)
+KEYPOOL_SAVE_K = True
 
 
 class _TableGradHook:
@@ -733,9 +736,10 @@ class CNNNewsRowsFn(torch.autograd.Function):
         probs = torch.empty(T, device=table.device)
         fused = FUSED_KEYPOOL and K.cnn_keypool_supported(Hp, seq_len)
         if fused:
-            # key projection + tanh + pooling per title: the key matrix never reaches HBM
-            K.cnn_keypool_fwd(C, wq, bq, query, mask, n, seq_len, news, probs, qn=H, prec=ctx.prec)
-            Kq = None
+            # key projection + tanh + pooling per title; with a backward to come K is kept (the backward
+            # reads it instead of recomputing the key products, KEYPOOL_SAVE_K)
+            Kq = _empty(T, Hp, table) if KEYPOOL_SAVE_K and any(ctx.needs_input_grad) else None
+            K.cnn_keypool_fwd(C, wq, bq, query, mask, n, seq_len, news, probs, qn=H, prec=ctx.prec, kout=Kq)
         else:
             Kq = _empty(T, Hp, table)
             K.gemm(T, Hp, Hp, K.operand(C, L.KCONTIG), K.operand(wq, L.KCONTIG), Kq, bias=bq,
@@ -771,7 +775,7 @@ class CNNNewsRowsFn(torch.autograd.Function):
             # dWq / dbq / dq / dconv_b summed over per-workgroup partials
             dz = dC_out if dC_out is None or dC_out.stride(-1) == 1 else dC_out.contiguous()
             K.cnn_keypool_bwd(C, wq, bq, query, n, seq_len, H, probs, dnews, dC, dwq, dbq, dq, dconv_b, dz=dz,
-                              prec=ctx.prec)
+                              prec=ctx.prec, kin=Kq)
         else:
             dKq = _empty(T, Hp, table)
             # dC = p dnews (+ dC_out), dKq = ds q (1 - Kq²) over the padded width: exactly zero past H

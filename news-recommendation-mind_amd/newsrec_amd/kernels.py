@@ -288,9 +288,19 @@ def cnn_keypool_supported(Hp, seq_len):
     return Hp % 32 == 0 and 32 <= Hp <= 160 and 1 <= seq_len <= 32
 
 
-def cnn_keypool_fwd(C, wq, bq, query, mask, nseq, seq_len, news, probs, qn, prec=None):
+def _kp_key(kbuf, rows, Hp, name):
+    if kbuf is None:
+        return None, 0
+    _f32(kbuf)
+    if kbuf.dim() != 2 or kbuf.stride(1) != 1 or kbuf.shape[0] < rows or kbuf.shape[1] < Hp:
+        raise L.HipError("%s: the key buffer must be [T, >= Hp] with unit column stride" % name)
+    return L.ptr(kbuf), kbuf.stride(0)
+
+
+def cnn_keypool_fwd(C, wq, bq, query, mask, nseq, seq_len, news, probs, qn, prec=None, kout=None):
     """nr_cnn_keypool_fwd: K = tanh(C wqᵀ + bq), p = XSoftmax(q·K / sqrt(qn), mask), news = Σ p C per
-    title.  C [nseq*L, Hp] (zero past qn), wq [Hp, Hp], bq [Hp] padded, query [>= qn]; news [nseq, >= Hp]."""
+    title.  C [nseq*L, Hp] (zero past qn), wq [Hp, Hp], bq [Hp] padded, query [>= qn]; news [nseq, >= Hp].
+    ``kout`` [T, >= Hp]: K kept for the backward (``cnn_keypool_bwd(kin=)``)."""
     _f32(C, wq, bq, query, news, probs)
     Hp = wq.shape[0]
     if not cnn_keypool_supported(Hp, seq_len):
@@ -304,13 +314,16 @@ def cnn_keypool_fwd(C, wq, bq, query, mask, nseq, seq_len, news, probs, qn, prec
         raise L.HipError("cnn_keypool: probs needs nseq*L floats")
     mp, mdt = mask_arg(mask, nseq * seq_len)
     prec = get_gemm_precision() if prec is None else prec
+    kp, ldk = _kp_key(kout, nseq * seq_len, Hp, "cnn_keypool_fwd")
     L.call("nr_cnn_keypool_fwd", L.ptr(C), C.stride(0), L.ptr(wq), L.ptr(bq), L.ptr(query), qn, mp, mdt, nseq, seq_len,
-           Hp, 1.0 / float(qn) ** 0.5, prec, L.ptr(news), news.stride(0), L.ptr(probs), L.stream_ptr(C))
+           Hp, 1.0 / float(qn) ** 0.5, prec, L.ptr(news), news.stride(0), L.ptr(probs), kp, ldk, L.stream_ptr(C))
 
 
-def cnn_keypool_bwd(C, wq, bq, query, nseq, seq_len, H, probs, dnews, dc, dwq, dbq, dq, dconv_b, dz=None, prec=None):
+def cnn_keypool_bwd(C, wq, bq, query, nseq, seq_len, H, probs, dnews, dc, dwq, dbq, dq, dconv_b, dz=None, prec=None,
+                    kin=None):
     """Backward of cnn_keypool_fwd: dc [T, >= Hp] = ReLU'(C) (p dnews + dK wq + dz); dwq [Hp, Hp], dbq [Hp],
-    dq [qn], dconv_b [H] are STORED.  dnews [nseq, >= qn] (row stride any), dz [T, >= H] optional."""
+    dq [qn], dconv_b [H] are STORED.  dnews [nseq, >= qn] (row stride any), dz [T, >= H] optional; ``kin``
+    the forward's ``kout`` (K read instead of recomputed)."""
     _f32(C, wq, bq, query, probs, dnews, dc, dwq, dbq, dq, dconv_b, dz)
     Hp = wq.shape[0]
     qn = dq.numel()
@@ -332,7 +345,8 @@ def cnn_keypool_bwd(C, wq, bq, query, nseq, seq_len, H, probs, dnews, dc, dwq, d
     L.call("nr_cnn_keypool_bwd", L.ptr(C), C.stride(0), L.ptr(wq), L.ptr(bq), L.ptr(query), qn, nseq, seq_len, Hp, H,
            1.0 / float(qn) ** 0.5, prec, L.ptr(probs), L.ptr(dnews), dnews.stride(0), L.ptr(dz),
            dz.stride(0) if dz is not None else 0, L.ptr(dc), dc.stride(0), L.ptr(dwq), L.ptr(dbq), L.ptr(dq),
-           L.ptr(dconv_b), L.ptr(ws), ws.numel(), L.stream_ptr(C))
+           L.ptr(dconv_b), L.ptr(ws), ws.numel(), *_kp_key(kin, nseq * seq_len, Hp, "cnn_keypool_bwd"),
+           L.stream_ptr(C))
 
 
 def operand(t, layout, rows=None, mapping=L.ROWS_PLAIN, seq_len=1, seg=1, ld=None):

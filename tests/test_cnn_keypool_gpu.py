@@ -55,7 +55,10 @@ def _ref(pre, wq, bq, q, mask, dnews, dz):
 @pytest.mark.parametrize("prec,tol", [(L.GEMM_F32, 5e-5), (L.GEMM_BF16X6, 5e-5), (L.GEMM_BF16, 3e-2)])
 @pytest.mark.parametrize("nseq,L_,H,with_dz", [(700, 30, 150, False), (37, 32, 150, True), (300, 17, 64, True),
                                                (5, 30, 20, False)])
-def test_cnn_keypool_matches_float64(prec, tol, nseq, L_, H, with_dz):
+@pytest.mark.parametrize("save_k", [False, True])
+def test_cnn_keypool_matches_float64(prec, tol, nseq, L_, H, with_dz, save_k):
+    """save_k: the forward stores K = tanh(C wqᵀ + bq) (checked here too) and the backward reads it
+    instead of recomputing the key products (functions.KEYPOOL_SAVE_K)."""
     Hp = (H + 31) // 32 * 32
     dev = "cuda"
     pre, wq, bq, q, mask, dnews, dz = _case(nseq, L_, H, Hp, nseq + H + L_, with_dz)
@@ -73,7 +76,8 @@ def test_cnn_keypool_matches_float64(prec, tol, nseq, L_, H, with_dz):
     M = mask.to(dev).reshape(-1)
     news = torch.empty(nseq, Hp, device=dev)
     probs = torch.empty(T, device=dev)
-    K.cnn_keypool_fwd(Cd, wqp, bqp, qd, M, nseq, L_, news, probs, qn=H, prec=prec)
+    kbuf = torch.full((T, Hp + 4), float("nan"), device=dev)[:, :Hp] if save_k else None
+    K.cnn_keypool_fwd(Cd, wqp, bqp, qd, M, nseq, L_, news, probs, qn=H, prec=prec, kout=kbuf)
     dc = torch.full((T, Hp), float("nan"), device=dev)
     dwq = torch.full((Hp, Hp), float("nan"), device=dev)
     dbq = torch.full((Hp,), float("nan"), device=dev)
@@ -81,7 +85,7 @@ def test_cnn_keypool_matches_float64(prec, tol, nseq, L_, H, with_dz):
     dcb = torch.full((H,), float("nan"), device=dev)
     dzd = dz.reshape(T, H).float().to(dev) if dz is not None else None
     K.cnn_keypool_bwd(Cd, wqp, bqp, qd, nseq, L_, H, probs, dnews.float().to(dev), dc, dwq, dbq, dq, dcb, dz=dzd,
-                      prec=prec)
+                      prec=prec, kin=kbuf)
     torch.cuda.synchronize()
 
     def close(got, want, name, t=tol):
@@ -90,6 +94,10 @@ def test_cnn_keypool_matches_float64(prec, tol, nseq, L_, H, with_dz):
         err = (got - want).abs().max().item()
         assert err <= t * max(1.0, want.abs().max().item()), (name, err)
 
+    if save_k:
+        k_r = torch.tanh(C.reshape(T, H) @ wq.T + bq)
+        close(kbuf[:, :H], k_r, "K")
+        assert kbuf[:, H:].abs().max().item() < 1e-6   # tanh(0 + 0) past H
     close(news[:, :H], news_r, "news")
     assert news[:, H:].abs().sum().item() == 0.0 and news[0].abs().max().item() == 0.0
     close(probs.view(nseq, L_), p_r, "probs")
