@@ -293,6 +293,26 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p = fmaf(-step, m / den, p);
 }
 
+// A/B knob (tools/build_ab.sh): 1 = nontemporal stores of p / m / v, 2 = nontemporal loads too
+#ifndef NR_ADAM_NT
+#define NR_ADAM_NT 0
+#endif
+typedef float adam_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 adam_ld(const float* base, int64_t i) {
+  if (NR_ADAM_NT >= 2) {
+    const adam_f4 v = __builtin_nontemporal_load(reinterpret_cast<const adam_f4*>(base) + i);
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return reinterpret_cast<const float4*>(base)[i];
+}
+__device__ __forceinline__ void adam_st(float* base, int64_t i, float4 v) {
+  if (NR_ADAM_NT >= 1) {
+    __builtin_nontemporal_store((adam_f4){v.x, v.y, v.z, v.w}, reinterpret_cast<adam_f4*>(base) + i);
+    return;
+  }
+  reinterpret_cast<float4*>(base)[i] = v;
+}
+
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
   const int b = blockIdx.x;
   int t = 0;
@@ -318,16 +338,16 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t i = base / 4 + u * 256 + threadIdx.x;
-      pp[u] = reinterpret_cast<const float4*>(e.p)[i];
+      pp[u] = adam_ld(e.p, i);
       // rows flagged untouched hold zeros: skip their gradient read (a float4 that reaches into a
       // touched row is read whole -- the untouched part reads as the zeros it holds).  The float4
       // spans rows (4i) / rlen .. (4i + 3) / rlen: all of them when rows are shorter than 4
       bool rd = !e.rt;
       if (!rd)
         for (int64_t r = (4 * i) / e.rlen; r <= (4 * i + 3) / e.rlen && !rd; ++r) rd = e.rt[r] != 0;
-      gg[u] = rd ? reinterpret_cast<const float4*>(e.g)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-      mm[u] = reinterpret_cast<const float4*>(e.m)[i];
-      vv[u] = reinterpret_cast<const float4*>(e.v)[i];
+      gg[u] = rd ? adam_ld(e.g, i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      mm[u] = adam_ld(e.m, i);
+      vv[u] = adam_ld(e.v, i);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -336,9 +356,9 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
       adam_elem(pp[u].y, gg[u].y, mm[u].y, vv[u].y, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
       adam_elem(pp[u].z, gg[u].z, mm[u].z, vv[u].z, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
       adam_elem(pp[u].w, gg[u].w, mm[u].w, vv[u].w, a.b1, a.b2, a.eps, a.wd, a.gscale, step, bc2_sqrt);
-      reinterpret_cast<float4*>(e.p)[i] = pp[u];
-      reinterpret_cast<float4*>(e.m)[i] = mm[u];
-      reinterpret_cast<float4*>(e.v)[i] = vv[u];
+      adam_st(e.p, i, pp[u]);
+      adam_st(e.m, i, mm[u]);
+      adam_st(e.v, i, vv[u]);
     }
   } else {
     for (int64_t i = base + threadIdx.x; i < end; i += 256) {

@@ -40,7 +40,12 @@ dYc = torch.randn(52800, 1152, device=dev); WT = W.t().contiguous()
 ux = torch.randn(1600, 384, device=dev); uw = torch.randn(768, 384, device=dev) / 20; ub = torch.randn(768, device=dev)
 uy = torch.empty(1600, 768, device=dev); udy = torch.randn(1600, 768, device=dev); udx = torch.empty(1600, 384, device=dev)
 udw = torch.zeros(768, 384, device=dev); uwT = uw.t().contiguous(); m_dev = torch.tensor([24600], dtype=torch.int32, device=dev)
+adam_p = [torch.randn(30522, 768, device=dev), torch.randn(1152, 768, device=dev), torch.randn(768, 384, device=dev)]
+adam_s = [(q, torch.randn_like(q), torch.zeros_like(q), torch.zeros_like(q)) for q in adam_p]
+def adam_step(p):
+    K.adam_multi([(q, g, m, v, 1e-4, 1) for q, g, m, v in adam_s], 0.9, 0.999, 1e-8, 0.0)
 cases = {
+ "adam_nrms": (0, adam_step),
  "nrms_proj_fwd": (2*U*E*1152, lambda p: K.gemm_dyn(U, 1152, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(W, L.KCONTIG), Y, prec=p)),
  "nrms_proj_dgrad": (2*U*E*1152, lambda p: K.gemm_dyn(U, E, 1152, K.operand(dY, L.KCONTIG), K.operand(W, L.MNCONTIG), dX, prec=p)),
  "nrms_dgrad_table": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), K.operand(W, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
