@@ -64,6 +64,8 @@ cases = {
  "bert_ffn1_wgrad_cs": (2*T*768*3072, lambda p: K.gemm(3072, 768, T, K.operand(G, L.MNCONTIG), K.operand(x, L.MNCONTIG), dWi, epilogue=L.EPI_ATOMIC, split_k=F._split_k(3072, 768, T), prec=p, colsum=dbi)),
  "bert_ffn2_wgrad_cs": (2*T*768*3072, lambda p: K.gemm(768, 3072, T, K.operand(o, L.MNCONTIG), K.operand(G, L.MNCONTIG), dWo2, epilogue=L.EPI_ATOMIC, split_k=F._split_k(768, 3072, T), prec=p, colsum=dbo2)),
  "bert_qkv_wgrad_cs": (2*T*768*2304, lambda p: K.gemm(2304, 768, T, K.operand(qkv, L.MNCONTIG), K.operand(x, L.MNCONTIG), dWqkv, epilogue=L.EPI_ATOMIC, split_k=F._split_k(2304, 768, T), prec=p, colsum=dbqkv)),
+ "bert_ffn2_dgrad": (2*T*768*3072, lambda p: K.gemm(T, 3072, 768, K.operand(o, L.KCONTIG), K.operand(wo2, L.MNCONTIG), Ub, prec=p)),
+ "bert_qkv_dgrad": (2*T*768*2304, lambda p: K.gemm(T, 768, 2304, K.operand(qkv, L.KCONTIG), K.operand(wqkv, L.MNCONTIG), x, prec=p)),
  "bert_ffn1_wgrad_atomic": (2*T*768*3072, lambda p: L.call("nr_gemm_f32", 3072, 768, T, K.operand(G, L.MNCONTIG), K.operand(x, L.MNCONTIG), L.ptr(dWi), 768, None, L.EPI_ATOMIC, None, -1, F._split_k(3072, 768, T), p, L.stream_ptr(dWi))),
  "cnn_conv_wgrad": (2*U*E*480, lambda p: K.gemm_dyn(480, E, U, K.operand(Pg, L.MNCONTIG), K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dw3, epilogue=L.EPI_ATOMIC, split_k=F._split_k(480, E, U), prec=p)),
  "cnn_table_dgrad": (2*24600*E*480, lambda p: K.gemm_dyn(U, E, 480, K.operand(Pg, L.KCONTIG), K.operand(w3, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
