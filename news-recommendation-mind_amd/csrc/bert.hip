@@ -699,6 +699,35 @@ template <int NP>
 __device__ __forceinline__ void stage_planes(uint16_t (*P)[32][kKR], uint16_t (*T)[kHD][kVR], const float* base,
                                              int64_t ld, int64_t row0, int j0, int L, int64_t col) {
   const int tid = threadIdx.x;
+#ifndef NR_ATTN_FUSED_STAGE
+#define NR_ATTN_FUSED_STAGE 0
+#endif
+  if (NR_ATTN_FUSED_STAGE && NP == 3 && P && T) {
+    // both images from one load and one split per element: a thread takes rows 2 kp, 2 kp + 1 and
+    // dims 4 dq .. 4 dq + 3, stores their row-major quads and repacks the same bf16 halves into the
+    // transposed (dim, row pair) words
+    for (int f = tid; f < 256; f += blockDim.x) {
+      const int kp = f & 15, dq = f >> 4;
+      const int j = j0 + 2 * kp;
+      const float* vb = base + (row0 + j) * ld + col + 4 * dq;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if (j < L) a = ld4(vb);
+      if (j + 1 < L) b = ld4(vb + ld);
+      uint2 pa[3], pb[3];
+      nrfast::split4(a.x, a.y, a.z, a.w, pa[0], pa[1], pa[2]);
+      nrfast::split4(b.x, b.y, b.z, b.w, pb[0], pb[1], pb[2]);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        *reinterpret_cast<uint2*>(&P[q][2 * kp][4 * dq]) = pa[q];
+        *reinterpret_cast<uint2*>(&P[q][2 * kp + 1][4 * dq]) = pb[q];
+        *reinterpret_cast<uint32_t*>(&T[q][4 * dq][2 * kp]) = (pa[q].x & 0xffffu) | (pb[q].x << 16);
+        *reinterpret_cast<uint32_t*>(&T[q][4 * dq + 1][2 * kp]) = (pa[q].x >> 16) | (pb[q].x & 0xffff0000u);
+        *reinterpret_cast<uint32_t*>(&T[q][4 * dq + 2][2 * kp]) = (pa[q].y & 0xffffu) | (pb[q].y << 16);
+        *reinterpret_cast<uint32_t*>(&T[q][4 * dq + 3][2 * kp]) = (pa[q].y >> 16) | (pb[q].y & 0xffff0000u);
+      }
+    }
+    return;
+  }
   if (P) {
     for (int f = tid; f < 512; f += blockDim.x) {
       const int r = f >> 4, cc = (f & 15) * 4;
