@@ -336,7 +336,9 @@ constexpr int KP_BW = 8;
 template <int NB>
 constexpr int kp_maxb() { return (NB * NB + (KP_BW - NB) - 1) / (KP_BW - NB); }
 
-template <int NB, int NP>
+// SK: the forward's K is read (g.kin, prefetched with the next title's C tile) instead of recomputed:
+// the key products and their Wq row loads leave the kernel
+template <int NB, int NP, bool SK>
 __global__ __launch_bounds__(64 * KP_BW) void cnn_keypool_bwd_kernel(KPArgs g) {
   static_assert(NB >= 1 && NB < KP_BW, "column waves + at least one dWq wave");
   constexpr int HP = 32 * NB;
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(64 * KP_BW) void cnn_keypool_bwd_kernel(KPArgs g) {
   const int j = 32 * (colw ? w : 0) + c;   // a column wave lane's column of K / dK / dC
   // a column wave's Wq column fragments (the dC products: 32 w + c, every chunk) for every title; the
   // row fragments of the key products come from L2 one chunk ahead (both sets would spill)
-  constexpr bool WC_REGS = NP != 3;   // bf16x6: the operand split needs those registers (it would spill)
+  constexpr bool WC_REGS = NP != 3;   // bf16x6: the operand split needs those registers (51 VGPRs spilled even without the key products)
   float wc[WC_REGS ? NB : 1][16];
   if (WC_REGS && colw) {
 #pragma unroll
@@ -371,7 +373,7 @@ __global__ __launch_bounds__(64 * KP_BW) void cnn_keypool_bwd_kernel(KPArgs g) {
   float pn = 0.f, dnn = 0.f;
   float kn[16];   // with the forward's K: a column wave lane's 16 K values of the next title
   auto fetch = [&](int64_t seq) {
-    if (g.kin && colw) {
+    if (SK && colw) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int tok = crow(r, h);
@@ -400,13 +402,13 @@ __global__ __launch_bounds__(64 * KP_BW) void cnn_keypool_bwd_kernel(KPArgs g) {
     if (tid < 32) sm.p[tid] = pn;
     if (tid >= 64 && tid < 64 + HP) sm.dn[tid - 64] = dnn;
     float kr[16];
-    if (g.kin && colw) {   // (before the next title's fetch reuses kn)
+    if (SK && colw) {   // (before the next title's fetch reuses kn)
 #pragma unroll
       for (int r = 0; r < 16; ++r) kr[r] = kn[r];
     }
     __syncthreads();
     if (seq + gridDim.x < g.nseq) fetch(seq + gridDim.x);
-    if (colw && !g.kin) {
+    if (!SK && colw) {
       f32x16 acc;
       key_block<NB, NP>(g, sm, w, c, h, acc);
       const float bj = sm.bq[j];
@@ -620,7 +622,16 @@ int launch_cnn_keypool_fwd_planes(int np, const KPArgs& g, int64_t grid, hipStre
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
-NR_KP_LAUNCH(cnn_keypool_bwd_kernel, 64 * KP_BW)
+template <int NB>
+int launch_cnn_keypool_bwd_kernel(int np, const KPArgs& g, int64_t grid, hipStream_t s) {
+#define NR_KPB(NP_)                                                                                       \
+  if (g.kin) hipLaunchKernelGGL((cnn_keypool_bwd_kernel<NB, NP_, true>), dim3((unsigned)grid), dim3(64 * KP_BW), 0, s, g); \
+  else hipLaunchKernelGGL((cnn_keypool_bwd_kernel<NB, NP_, false>), dim3((unsigned)grid), dim3(64 * KP_BW), 0, s, g);
+  if (np == 0) { NR_KPB(0) } else if (np == 1) { NR_KPB(1) } else { NR_KPB(3) }
+#undef NR_KPB
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
 #undef NR_KP_LAUNCH
 
 int np_of(int prec) { return prec == NR_GEMM_F32 ? 0 : prec == NR_GEMM_BF16 ? 1 : 3; }
