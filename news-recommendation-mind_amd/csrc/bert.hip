@@ -835,7 +835,57 @@ __device__ __forceinline__ void own_rows(Planes<NP> (&out)[4], const float* p, b
   for (int t = 0; t < 4; ++t) out[t] = planes8<NP>(f + 8 * t);
 }
 
-template <int NP, bool DROP>
+// Register-prefetched staging (workgroups of four waves): thread f holds rows 2 kp, 2 kp + 1 and dims
+// 4 dq .. 4 dq + 3 (kp = f & 15, dq = f >> 4) of the NEXT tile of one tensor, loaded while the current
+// tile's products run, and writes both plane images of it from one split after the barrier.  Without
+// it every tile paid a full load latency between its two barriers (one to three waves per SIMD
+// cannot hide it).
+#ifndef NR_ATTN_PF
+#define NR_ATTN_PF 0
+#endif
+template <int NP>
+struct TileFetch {
+  float4 a, b;
+  __device__ __forceinline__ void fetch(const float* base, int64_t ld, int64_t row0, int j0, int L, int64_t col) {
+    const int f = threadIdx.x, kp = f & 15, dq = f >> 4;
+    const int j = j0 + 2 * kp;
+    const float* vb = base + (row0 + j) * ld + col + 4 * dq;
+    a = make_float4(0.f, 0.f, 0.f, 0.f);
+    b = a;
+    if (j < L) a = ld4(vb);
+    if (j + 1 < L) b = ld4(vb + ld);
+  }
+  __device__ __forceinline__ void store(uint16_t (*P)[32][kKR], uint16_t (*T)[kHD][kVR]) const {
+    const int f = threadIdx.x, kp = f & 15, dq = f >> 4;
+    uint2 pa[NP], pb[NP];
+    if constexpr (NP == 1) {
+      pa[0] = nrfast::hi4(a.x, a.y, a.z, a.w);
+      pb[0] = nrfast::hi4(b.x, b.y, b.z, b.w);
+    } else {
+      nrfast::split4(a.x, a.y, a.z, a.w, pa[0], pa[1], pa[2]);
+      nrfast::split4(b.x, b.y, b.z, b.w, pb[0], pb[1], pb[2]);
+    }
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      if (P) {
+        *reinterpret_cast<uint2*>(&P[q][2 * kp][4 * dq]) = pa[q];
+        *reinterpret_cast<uint2*>(&P[q][2 * kp + 1][4 * dq]) = pb[q];
+      }
+      if (T) {
+        *reinterpret_cast<uint32_t*>(&T[q][4 * dq][2 * kp]) = (pa[q].x & 0xffffu) | (pb[q].x << 16);
+        *reinterpret_cast<uint32_t*>(&T[q][4 * dq + 1][2 * kp]) = (pa[q].x >> 16) | (pb[q].x & 0xffff0000u);
+        *reinterpret_cast<uint32_t*>(&T[q][4 * dq + 2][2 * kp]) = (pa[q].y & 0xffffu) | (pb[q].y << 16);
+        *reinterpret_cast<uint32_t*>(&T[q][4 * dq + 3][2 * kp]) = (pa[q].y >> 16) | (pb[q].y & 0xffff0000u);
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ float key_add(const AttnArgs& g, int64_t row0, int j, int L) {
+  return j >= L ? -INFINITY : (nr_mask_at(g.mask, g.mdt, row0 + j) ? 0.f : kNegMax);
+}
+
+template <int NP, bool DROP, bool PF>
 __global__ void __launch_bounds__(256) attn_fwd_mp_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t Kp[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Vt[NP][kHD][kVR];
@@ -861,13 +911,28 @@ __global__ void __launch_bounds__(256) attn_fwd_mp_kernel(AttnArgs g) {
   for (int r = 0; r < 16; ++r) o0[r] = o1[r] = 0.f;
   float m = -INFINITY, l = 0.f;
   const int nkb = (L + 31) / 32;
+  TileFetch<NP> fk, fv;
+  float kadd_n = 0.f;
+  if constexpr (PF) {
+    fk.fetch(g.qkv, g.ldq, row0, 0, L, g.koff + head * kHD);
+    fv.fetch(g.qkv, g.ldq, row0, 0, L, g.voff + head * kHD);
+    if (threadIdx.x < 32) kadd_n = key_add(g, row0, threadIdx.x, L);
+  }
   for (int kb = 0; kb < nkb; ++kb) {
     __syncthreads();
-    stage_planes<NP>(Kp, nullptr, g.qkv, g.ldq, row0, kb * 32, L, g.koff + head * kHD);
-    stage_planes<NP>(nullptr, Vt, g.qkv, g.ldq, row0, kb * 32, L, g.voff + head * kHD);
-    if (threadIdx.x < 32) {
-      const int j = kb * 32 + threadIdx.x;
-      kadd[threadIdx.x] = j >= L ? -INFINITY : (nr_mask_at(g.mask, g.mdt, row0 + j) ? 0.f : kNegMax);
+    if constexpr (PF) {
+      fk.store(Kp, nullptr);
+      fv.store(nullptr, Vt);
+      if (threadIdx.x < 32) kadd[threadIdx.x] = kadd_n;
+      if (kb + 1 < nkb) {
+        fk.fetch(g.qkv, g.ldq, row0, (kb + 1) * 32, L, g.koff + head * kHD);
+        fv.fetch(g.qkv, g.ldq, row0, (kb + 1) * 32, L, g.voff + head * kHD);
+        if (threadIdx.x < 32) kadd_n = key_add(g, row0, (kb + 1) * 32 + threadIdx.x, L);
+      }
+    } else {
+      stage_planes<NP>(Kp, nullptr, g.qkv, g.ldq, row0, kb * 32, L, g.koff + head * kHD);
+      stage_planes<NP>(nullptr, Vt, g.qkv, g.ldq, row0, kb * 32, L, g.voff + head * kHD);
+      if (threadIdx.x < 32) kadd[threadIdx.x] = key_add(g, row0, kb * 32 + threadIdx.x, L);
     }
     __syncthreads();
     if (!active) continue;
@@ -932,7 +997,7 @@ __global__ void __launch_bounds__(256) attn_fwd_mp_kernel(AttnArgs g) {
 
 // dK, dV (attn_bwd_kv_kernel's products): a wave owns 32 keys, split once; per query tile the Q and
 // dctx rows are staged split, row-major (S, dP) and transposed (dV, dK).
-template <int NP, bool DROP>
+template <int NP, bool DROP, bool PF>
 __global__ void __launch_bounds__(256) attn_bwd_kv_mp_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t Qp[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Op[NP][32][kKR];
@@ -962,22 +1027,45 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_mp_kernel(AttnArgs g) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) dk0[r] = dk1[r] = dv0[r] = dv1[r] = 0.f;
   const int nqb = (L + 31) / 32;
+  // a query row's (max, 1/sum, D); past L: exp(s - inf) = 0, no such query
+  auto qstats = [&](int j, float& a, float& b, float& d) {
+    if (j < L) {
+      const float* mp = g.ml + ((row0 + j) * g.heads + head) * 2;
+      a = mp[0];
+      b = mp[1];
+      d = g.Dq[(row0 + j) * g.heads + head];
+    } else {
+      a = INFINITY;
+      b = 0.f;
+      d = 0.f;
+    }
+  };
+  TileFetch<NP> fq, fo;
+  float qm_n = 0.f, qi_n = 0.f, qd_n = 0.f;
+  if constexpr (PF) {
+    fq.fetch(g.qkv, g.ldq, row0, 0, L, head * kHD);
+    fo.fetch(g.dctx, g.ldd, row0, 0, L, head * kHD);
+    if (threadIdx.x < 32) qstats(threadIdx.x, qm_n, qi_n, qd_n);
+  }
   for (int qb = 0; qb < nqb; ++qb) {
     __syncthreads();
-    stage_planes<NP>(Qp, Qt, g.qkv, g.ldq, row0, qb * 32, L, head * kHD);
-    stage_planes<NP>(Op, Ot, g.dctx, g.ldd, row0, qb * 32, L, head * kHD);
-    if (threadIdx.x < 32) {
-      const int j = qb * 32 + threadIdx.x;
-      if (j < L) {
-        const float* mp = g.ml + ((row0 + j) * g.heads + head) * 2;
-        qm[threadIdx.x] = mp[0];
-        qi[threadIdx.x] = mp[1];
-        qd[threadIdx.x] = g.Dq[(row0 + j) * g.heads + head];
-      } else {
-        qm[threadIdx.x] = INFINITY;   // exp(s - inf) = 0: no such query
-        qi[threadIdx.x] = 0.f;
-        qd[threadIdx.x] = 0.f;
+    if constexpr (PF) {
+      fq.store(Qp, Qt);
+      fo.store(Op, Ot);
+      if (threadIdx.x < 32) {
+        qm[threadIdx.x] = qm_n;
+        qi[threadIdx.x] = qi_n;
+        qd[threadIdx.x] = qd_n;
       }
+      if (qb + 1 < nqb) {
+        fq.fetch(g.qkv, g.ldq, row0, (qb + 1) * 32, L, head * kHD);
+        fo.fetch(g.dctx, g.ldd, row0, (qb + 1) * 32, L, head * kHD);
+        if (threadIdx.x < 32) qstats((qb + 1) * 32 + threadIdx.x, qm_n, qi_n, qd_n);
+      }
+    } else {
+      stage_planes<NP>(Qp, Qt, g.qkv, g.ldq, row0, qb * 32, L, head * kHD);
+      stage_planes<NP>(Op, Ot, g.dctx, g.ldd, row0, qb * 32, L, head * kHD);
+      if (threadIdx.x < 32) qstats(qb * 32 + threadIdx.x, qm[threadIdx.x], qi[threadIdx.x], qd[threadIdx.x]);
     }
     __syncthreads();
     if (!active) continue;
@@ -1032,7 +1120,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_mp_kernel(AttnArgs g) {
 
 // dQ (attn_bwd_q_kernel's products): a wave owns 32 queries (Q and dctx split once); per key tile
 // K and V staged split row-major (S, dP) and K transposed (dQ = dS K).
-template <int NP, bool DROP>
+template <int NP, bool DROP, bool PF>
 __global__ void __launch_bounds__(256) attn_bwd_q_mp_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t Kp[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Vp[NP][32][kKR];
@@ -1067,13 +1155,28 @@ __global__ void __launch_bounds__(256) attn_bwd_q_mp_kernel(AttnArgs g) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) a0[r] = a1[r] = 0.f;
   const int nkb = (L + 31) / 32;
+  TileFetch<NP> fk, fv;
+  float kadd_n = 0.f;
+  if constexpr (PF) {
+    fk.fetch(g.qkv, g.ldq, row0, 0, L, g.koff + head * kHD);
+    fv.fetch(g.qkv, g.ldq, row0, 0, L, g.voff + head * kHD);
+    if (threadIdx.x < 32) kadd_n = key_add(g, row0, threadIdx.x, L);
+  }
   for (int kb = 0; kb < nkb; ++kb) {
     __syncthreads();
-    stage_planes<NP>(Kp, Kt, g.qkv, g.ldq, row0, kb * 32, L, g.koff + head * kHD);
-    stage_planes<NP>(Vp, nullptr, g.qkv, g.ldq, row0, kb * 32, L, g.voff + head * kHD);
-    if (threadIdx.x < 32) {
-      const int j = kb * 32 + threadIdx.x;
-      kadd[threadIdx.x] = j >= L ? -INFINITY : (nr_mask_at(g.mask, g.mdt, row0 + j) ? 0.f : kNegMax);
+    if constexpr (PF) {
+      fk.store(Kp, Kt);
+      fv.store(Vp, nullptr);
+      if (threadIdx.x < 32) kadd[threadIdx.x] = kadd_n;
+      if (kb + 1 < nkb) {
+        fk.fetch(g.qkv, g.ldq, row0, (kb + 1) * 32, L, g.koff + head * kHD);
+        fv.fetch(g.qkv, g.ldq, row0, (kb + 1) * 32, L, g.voff + head * kHD);
+        if (threadIdx.x < 32) kadd_n = key_add(g, row0, (kb + 1) * 32 + threadIdx.x, L);
+      }
+    } else {
+      stage_planes<NP>(Kp, Kt, g.qkv, g.ldq, row0, kb * 32, L, g.koff + head * kHD);
+      stage_planes<NP>(Vp, nullptr, g.qkv, g.ldq, row0, kb * 32, L, g.voff + head * kHD);
+      if (threadIdx.x < 32) kadd[threadIdx.x] = key_add(g, row0, kb * 32 + threadIdx.x, L);
     }
     __syncthreads();
     if (!active) continue;
@@ -1237,12 +1340,20 @@ extern "C" int nr_bert_attn_fwd(const float* qkv, int64_t ldq, int64_t koff, int
   if (prec == NR_GEMM_F32) {
     if (drop) NR_FWD(attn_fwd_kernel<true>);
     else NR_FWD(attn_fwd_kernel<false>);
+  } else if (NR_ATTN_PF && nw == 4) {
+    if (prec == NR_GEMM_BF16) {
+      if (drop) NR_FWD((attn_fwd_mp_kernel<1, true, true>));
+      else NR_FWD((attn_fwd_mp_kernel<1, false, true>));
+    } else {
+      if (drop) NR_FWD((attn_fwd_mp_kernel<3, true, true>));
+      else NR_FWD((attn_fwd_mp_kernel<3, false, true>));
+    }
   } else if (prec == NR_GEMM_BF16) {
-    if (drop) NR_FWD((attn_fwd_mp_kernel<1, true>));
-    else NR_FWD((attn_fwd_mp_kernel<1, false>));
+    if (drop) NR_FWD((attn_fwd_mp_kernel<1, true, false>));
+    else NR_FWD((attn_fwd_mp_kernel<1, false, false>));
   } else {
-    if (drop) NR_FWD((attn_fwd_mp_kernel<3, true>));
-    else NR_FWD((attn_fwd_mp_kernel<3, false>));
+    if (drop) NR_FWD((attn_fwd_mp_kernel<3, true, false>));
+    else NR_FWD((attn_fwd_mp_kernel<3, false, false>));
   }
 #undef NR_FWD
   NR_LAUNCH_CHECK();
@@ -1283,12 +1394,20 @@ extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int
   if (prec == NR_GEMM_F32) {
     if (drop) NR_BWD(attn_bwd_kv_kernel<true>, attn_bwd_q_kernel<true>);
     else NR_BWD(attn_bwd_kv_kernel<false>, attn_bwd_q_kernel<false>);
+  } else if (NR_ATTN_PF && nw == 4) {
+    if (prec == NR_GEMM_BF16) {
+      if (drop) NR_BWD((attn_bwd_kv_mp_kernel<1, true, true>), (attn_bwd_q_mp_kernel<1, true, true>));
+      else NR_BWD((attn_bwd_kv_mp_kernel<1, false, true>), (attn_bwd_q_mp_kernel<1, false, true>));
+    } else {
+      if (drop) NR_BWD((attn_bwd_kv_mp_kernel<3, true, true>), (attn_bwd_q_mp_kernel<3, true, true>));
+      else NR_BWD((attn_bwd_kv_mp_kernel<3, false, true>), (attn_bwd_q_mp_kernel<3, false, true>));
+    }
   } else if (prec == NR_GEMM_BF16) {
-    if (drop) NR_BWD((attn_bwd_kv_mp_kernel<1, true>), (attn_bwd_q_mp_kernel<1, true>));
-    else NR_BWD((attn_bwd_kv_mp_kernel<1, false>), (attn_bwd_q_mp_kernel<1, false>));
+    if (drop) NR_BWD((attn_bwd_kv_mp_kernel<1, true, false>), (attn_bwd_q_mp_kernel<1, true, false>));
+    else NR_BWD((attn_bwd_kv_mp_kernel<1, false, false>), (attn_bwd_q_mp_kernel<1, false, false>));
   } else {
-    if (drop) NR_BWD((attn_bwd_kv_mp_kernel<3, true>), (attn_bwd_q_mp_kernel<3, true>));
-    else NR_BWD((attn_bwd_kv_mp_kernel<3, false>), (attn_bwd_q_mp_kernel<3, false>));
+    if (drop) NR_BWD((attn_bwd_kv_mp_kernel<3, true, false>), (attn_bwd_q_mp_kernel<3, true, false>));
+    else NR_BWD((attn_bwd_kv_mp_kernel<3, false, false>), (attn_bwd_q_mp_kernel<3, false, false>));
   }
 #undef NR_BWD
   NR_LAUNCH_CHECK();

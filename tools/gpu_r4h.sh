@@ -9,8 +9,10 @@ echo tests; timeout -k 10 400 python -u -m pytest tests/test_step_buffers_gpu.py
 echo legs; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_legs -o run -- python tools/legs_only.py cnn_attn cnn_attn_bf16 cnn_lstur cnn_gru --steps 5 > $O/kt_legs.log 2>&1 || exit 5
 echo adam_ab; timeout -k 10 300 python tools/gemm_ab.py --libs base,ab/adamnt1/libnewsrec_hip.so,ab/adamnt2/libnewsrec_hip.so,base,ab/adamnt1/libnewsrec_hip.so,ab/adamnt2/libnewsrec_hip.so --cases adam_nrms > $O/adam_ab.json 2> $O/adam_ab.err || exit 2
 echo gemm_ab; timeout -k 10 400 python tools/gemm_ab.py --libs base,ab/ilv03/libnewsrec_hip.so,base,ab/ilv03/libnewsrec_hip.so --cases nrms_proj_dgrad,nrms_dgrad_table,bert_ffn2_dgrad,bert_qkv_dgrad > $O/gemm_ab.json 2> $O/gemm_ab.err || exit 2
-echo xfboth; NR_LIB_PATH=$PWD/ab/xfboth/libnewsrec_hip.so timeout -k 10 300 python -u -m pytest tests/test_bert_gpu.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/xfboth_tests.log 2>&1 || exit 1
-for i in 1 2; do for v in base fstage lnpf xfboth; do
+for v in attnpf xfall; do
+  echo tests_$v; NR_LIB_PATH=$PWD/ab/$v/libnewsrec_hip.so timeout -k 10 300 python -u -m pytest tests/test_bert_gpu.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/${v}_tests.log 2>&1 || exit 1
+done
+for i in 1 2; do for v in base attnpf lnpf xfall; do
   if [ $v = base ]; then LP=""; else LP=$PWD/ab/$v/libnewsrec_hip.so; fi
   echo xf_$v; NR_LIB_PATH=$LP timeout -k 10 200 python tools/legs_only.py xformer --steps 5 > $O/xf_${v}_$i.json 2> $O/xf_${v}_$i.err || exit 8
 done; done
