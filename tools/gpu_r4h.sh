@@ -12,7 +12,7 @@ echo gemm_ab; timeout -k 10 400 python tools/gemm_ab.py --libs base,ab/ilv03/lib
 for v in attnpf xfall; do
   echo tests_$v; NR_LIB_PATH=$PWD/ab/$v/libnewsrec_hip.so timeout -k 10 300 python -u -m pytest tests/test_bert_gpu.py -m gpu -q -x --timeout 200 --timeout-method thread > $O/${v}_tests.log 2>&1 || exit 1
 done
-for i in 1 2; do for v in base attnpf lnpf xfall; do
+for i in 1; do for v in base attnpf lnpf xfall; do
   if [ $v = base ]; then LP=""; else LP=$PWD/ab/$v/libnewsrec_hip.so; fi
   echo xf_$v; NR_LIB_PATH=$LP timeout -k 10 200 python tools/legs_only.py xformer --steps 5 > $O/xf_${v}_$i.json 2> $O/xf_${v}_$i.err || exit 8
 done; done
@@ -20,5 +20,4 @@ echo all_tests; timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 
 echo bench; timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 3
 B="python bench.py --steps 20 --warmup 3 --eval-impr 0 --config-legs 0 --xformer-steps 0 --no-cpu-baseline"
 echo trace; timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- $B > $O/kt.log 2>&1 || exit 4
-echo pmc_xf; bash tools/pmc_passes.sh $O/pmc_xf python tools/legs_only.py xformer --steps 1 || exit 7
 echo done
