@@ -35,7 +35,7 @@ dWi = torch.zeros(3072, 768, device=dev); dbi = torch.zeros(3072, device=dev)
 dWo2 = torch.zeros(768, 3072, device=dev); dbo2 = torch.zeros(768, device=dev)
 dWqkv = torch.zeros(2304, 768, device=dev); dbqkv = torch.zeros(2304, device=dev)
 P = torch.empty(U, 480, device=dev); w3 = torch.randn(480, E, device=dev); Pg = torch.randn(U, 480, device=dev); dw3 = torch.zeros(480, E, device=dev)
-uids = torch.randperm(V - 1, device=dev)[:24600] + 1; dT = torch.zeros(V, E, device=dev)
+uids = torch.randperm(V - 1, device=dev)[:24600] + 1; dT = torch.zeros(V, E, device=dev); w3T = w3.t().contiguous()
 dYc = torch.randn(52800, 1152, device=dev); WT = W.t().contiguous()
 ux = torch.randn(1600, 384, device=dev); uw = torch.randn(768, 384, device=dev) / 20; ub = torch.randn(768, device=dev)
 uy = torch.empty(1600, 768, device=dev); udy = torch.randn(1600, 768, device=dev); udx = torch.empty(1600, 384, device=dev)
@@ -68,6 +68,7 @@ cases = {
  "bert_qkv_dgrad": (2*T*768*2304, lambda p: K.gemm(T, 768, 2304, K.operand(qkv, L.KCONTIG), K.operand(wqkv, L.MNCONTIG), x, prec=p)),
  "bert_ffn1_wgrad_atomic": (2*T*768*3072, lambda p: L.call("nr_gemm_f32", 3072, 768, T, K.operand(G, L.MNCONTIG), K.operand(x, L.MNCONTIG), L.ptr(dWi), 768, None, L.EPI_ATOMIC, None, -1, F._split_k(3072, 768, T), p, L.stream_ptr(dWi))),
  "cnn_conv_wgrad": (2*U*E*480, lambda p: K.gemm_dyn(480, E, U, K.operand(Pg, L.MNCONTIG), K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dw3, epilogue=L.EPI_ATOMIC, split_k=F._split_k(480, E, U), prec=p)),
+ "cnn_table_dgrad_kc": (2*24600*E*480, lambda p: K.gemm_dyn(U, E, 480, K.operand(Pg, L.KCONTIG), K.operand(w3T, L.KCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
  "cnn_table_dgrad": (2*24600*E*480, lambda p: K.gemm_dyn(U, E, 480, K.operand(Pg, L.KCONTIG), K.operand(w3, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
  "nrms_proj_wgrad_atomic": (2*U*E*1152, lambda p: L.call("nr_gemm_f32_dyn", 1152, E, U, K.operand(dY, L.MNCONTIG), K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), L.ptr(dW), E, None, L.EPI_ATOMIC, None, -1, F._split_k(1152, E, U), None, None, p, L.stream_ptr(dW))),
 }
