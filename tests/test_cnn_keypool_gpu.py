@@ -97,7 +97,8 @@ def test_cnn_keypool_matches_float64(prec, tol, nseq, L_, H, with_dz, save_k):
     if save_k:
         k_r = torch.tanh(C.reshape(T, H) @ wq.T + bq)
         close(kbuf[:, :H], k_r, "K")
-        assert kbuf[:, H:].abs().max().item() < 1e-6   # tanh(0 + 0) past H
+        if Hp > H:
+            assert kbuf[:, H:].abs().max().item() < 1e-6   # tanh(0 + 0) past H
     close(news[:, :H], news_r, "news")
     assert news[:, H:].abs().sum().item() == 0.0 and news[0].abs().max().item() == 0.0
     close(probs.view(nseq, L_), p_r, "probs")
