@@ -152,9 +152,6 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs g) {
   }
 }
 
-#ifndef NR_LN_PREFETCH
-#define NR_LN_PREFETCH 0
-#endif
 template <bool EMBED, int NV>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(LnArgs g) {
   __shared__ float red[4][2][256 * NV];
@@ -164,47 +161,12 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnArgs g) {
 #pragma unroll
   for (int j = 0; j < NV; ++j) ag[j] = ab[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   const float invH = 1.f / (float)g.H;
-  // residual form, A/B knob: the next row's x / res / dout loads issued before this row's math (a wave
-  // walks ~5 rows; without it every row pays a full load latency)
-  constexpr bool PF = NR_LN_PREFETCH && !EMBED;
-  const int64_t stride = (int64_t)gridDim.x * 4;
-  float4 px[PF ? NV : 1], pr[PF ? NV : 1], pd[PF ? NV : 1];
-  auto raw = [&](int64_t t) {
-    if constexpr (PF) {
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        const int c = 4 * (lane + 64 * j);
-        const bool ok = t < g.T && c < g.H;
-        px[j] = ok ? ld4(g.x + t * g.ldx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-        pr[j] = ok ? ld4(g.res + t * g.ldr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-        pd[j] = ok ? ld4(g.dout + t * g.ldd + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    }
-  };
-  raw((int64_t)blockIdx.x * 4 + wave);
-  for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < g.T; t += stride) {
-    float4 v[NV], dcur[PF ? NV : 1];
-    const uint32_t e0 = (uint32_t)(t * g.H);
-    if constexpr (PF) {
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        const int c = 4 * (lane + 64 * j);
-        float4 a = px[j];
-        if (g.p > 0.f) {
-          a.x = nr_dropout_keep(key, e0 + c, g.thresh) ? a.x * g.pscale : 0.f;
-          a.y = nr_dropout_keep(key, e0 + c + 1, g.thresh) ? a.y * g.pscale : 0.f;
-          a.z = nr_dropout_keep(key, e0 + c + 2, g.thresh) ? a.z * g.pscale : 0.f;
-          a.w = nr_dropout_keep(key, e0 + c + 3, g.thresh) ? a.w * g.pscale : 0.f;
-        }
-        v[j] = make_float4(a.x + pr[j].x, a.y + pr[j].y, a.z + pr[j].z, a.w + pr[j].w);
-        dcur[j] = pd[j];
-      }
-      raw(t + stride);
-    } else {
-      load_s<EMBED, NV>(g, t, lane, v, key);
-    }
+  for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < g.T; t += (int64_t)gridDim.x * 4) {
+    float4 v[NV];
+    load_s<EMBED, NV>(g, t, lane, v, key);
     const float mean = g.stats[2 * t], rstd = g.stats[2 * t + 1];
     const float* drow = g.dout + t * g.ldd;
+    const uint32_t e0 = (uint32_t)(t * g.H);
     float4 dy[NV], xh[NV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -214,9 +176,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnArgs g) {
         dy[j] = xh[j] = make_float4(0.f, 0.f, 0.f, 0.f);
         continue;
       }
-      float4 d;
-      if constexpr (PF) d = dcur[j];
-      else d = ld4(drow + c);
+      float4 d = ld4(drow + c);
       if (EMBED && g.p > 0.f) {
         d.x = nr_dropout_keep(key, e0 + c, g.thresh) ? d.x * g.pscale : 0.f;
         d.y = nr_dropout_keep(key, e0 + c + 1, g.thresh) ? d.y * g.pscale : 0.f;
@@ -279,8 +239,7 @@ int launch_ln(const LnArgs& g, hipStream_t s) {
   dim3 grid;
   if (BWD) {
     int64_t nb = (g.T + 3) / 4;
-    const int64_t cap = NR_LN_PREFETCH && !EMBED ? 768 : 1024;   // (the prefetch form: 3 resident workgroups per CU)
-    grid = dim3((unsigned)(nb < cap ? nb : cap));
+    grid = dim3((unsigned)(nb < 1024 ? nb : 1024));
   } else {
     grid = dim3((unsigned)((g.T + 3) / 4));
   }
@@ -740,10 +699,8 @@ template <int NP>
 __device__ __forceinline__ void stage_planes(uint16_t (*P)[32][kKR], uint16_t (*T)[kHD][kVR], const float* base,
                                              int64_t ld, int64_t row0, int j0, int L, int64_t col) {
   const int tid = threadIdx.x;
-#ifndef NR_ATTN_FUSED_STAGE
-#define NR_ATTN_FUSED_STAGE 0
-#endif
-  if (NR_ATTN_FUSED_STAGE && NP == 3 && P && T) {
+  if (NP == 3 && P && T) {
+    // (workgroups of fewer than four waves, e.g. the 30-token titles)
     // both images from one load and one split per element: a thread takes rows 2 kp, 2 kp + 1 and
     // dims 4 dq .. 4 dq + 3, stores their row-major quads and repacks the same bf16 halves into the
     // transposed (dim, row pair) words
@@ -839,10 +796,7 @@ __device__ __forceinline__ void own_rows(Planes<NP> (&out)[4], const float* p, b
 // 4 dq .. 4 dq + 3 (kp = f & 15, dq = f >> 4) of the NEXT tile of one tensor, loaded while the current
 // tile's products run, and writes both plane images of it from one split after the barrier.  Without
 // it every tile paid a full load latency between its two barriers (one to three waves per SIMD
-// cannot hide it).
-#ifndef NR_ATTN_PF
-#define NR_ATTN_PF 0
-#endif
+// cannot hide it): XFormer train step 74.3 -> 71.3 ms (profiles/r04_h_xf_*.json, same box).
 template <int NP>
 struct TileFetch {
   float4 a, b;
@@ -1340,7 +1294,7 @@ extern "C" int nr_bert_attn_fwd(const float* qkv, int64_t ldq, int64_t koff, int
   if (prec == NR_GEMM_F32) {
     if (drop) NR_FWD(attn_fwd_kernel<true>);
     else NR_FWD(attn_fwd_kernel<false>);
-  } else if (NR_ATTN_PF && nw == 4) {
+  } else if (nw == 4) {
     if (prec == NR_GEMM_BF16) {
       if (drop) NR_FWD((attn_fwd_mp_kernel<1, true, true>));
       else NR_FWD((attn_fwd_mp_kernel<1, false, true>));
@@ -1394,7 +1348,7 @@ extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int
   if (prec == NR_GEMM_F32) {
     if (drop) NR_BWD(attn_bwd_kv_kernel<true>, attn_bwd_q_kernel<true>);
     else NR_BWD(attn_bwd_kv_kernel<false>, attn_bwd_q_kernel<false>);
-  } else if (NR_ATTN_PF && nw == 4) {
+  } else if (nw == 4) {
     if (prec == NR_GEMM_BF16) {
       if (drop) NR_BWD((attn_bwd_kv_mp_kernel<1, true, true>), (attn_bwd_q_mp_kernel<1, true, true>));
       else NR_BWD((attn_bwd_kv_mp_kernel<1, false, true>), (attn_bwd_q_mp_kernel<1, false, true>));

@@ -447,12 +447,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
 #ifdef NR_BIG_NO_ILV
       constexpr bool ILV = false;
 #else
-#ifndef NR_AB_ILV03
-#define NR_AB_ILV03 0
-#endif
       constexpr bool ILV = LIVE && NP == 3 && KS == 1 && TJ == 2 && LA::PIECES == 2 && LB::PIECES == 2 &&
-                           ((is_kc(AM) && is_kc(BMODE)) || (AM == MN_PLAIN && BMODE == MN_GATHER) ||
-                            (NR_AB_ILV03 && is_kc(AM) && BMODE == MN_PLAIN));
+                           ((is_kc(AM) && is_kc(BMODE)) || (AM == MN_PLAIN && BMODE == MN_GATHER));
 #endif
       const uint16_t* a_s = As + st * NP * PA;
       const uint16_t* b_s = Bs + st * NP * PB;

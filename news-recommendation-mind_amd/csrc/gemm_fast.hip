@@ -184,10 +184,9 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
     const bool resplit = split_k > 1 && (epilogue == NR_EPI_ATOMIC || epilogue == NR_EPI_SCATTER);
     // shortest contraction the big kernel takes: 512 (32 k-tiles of MFMAs per unit fill), in bf16 too
     // (A/B: the CNN table dgrad, K = 480, ran 94 us on the 128x128 kernel and 114 us on the big one)
-#ifndef NR_AB_KMIN
-#define NR_AB_KMIN 512
-#endif
-    const int kmin = NR_AB_KMIN;
+    // (re-measured in round 4 on the k-contiguous CNN dgrad, bf16: 59 us here, 95 us with kmin = 480,
+    // profiles/r04_h_gemm_ab.json)
+    const int kmin = 512;
     const bool tailed = zeroed && splits == 1 && K >= kmin && N >= 256 && big_bn(M, N, K, 1, false, false, kmin) >= 0;
     // bf16 split-K (atomic) launches take the big kernel too: its fewer, larger units halve the operand
     // re-reads and keep three k-tiles of loads in flight (CNN conv weight gradient 200 -> 138 us)

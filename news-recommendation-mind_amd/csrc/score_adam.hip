@@ -293,24 +293,13 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   p = fmaf(-step, m / den, p);
 }
 
-// A/B knob (tools/build_ab.sh): 1 = nontemporal stores of p / m / v, 2 = nontemporal loads too
-#ifndef NR_ADAM_NT
-#define NR_ADAM_NT 0
-#endif
+// p / m / v are written with nontemporal stores (streamed out, not kept in the L2s): same-box A/B on
+// the NRMS parameter set (24.6 M, 690 MB per step), profiles/r04_h_adam_ab.json: 134 -> 109 us; making
+// the loads nontemporal too measured 120 us
 typedef float adam_f4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 adam_ld(const float* base, int64_t i) {
-  if (NR_ADAM_NT >= 2) {
-    const adam_f4 v = __builtin_nontemporal_load(reinterpret_cast<const adam_f4*>(base) + i);
-    return make_float4(v.x, v.y, v.z, v.w);
-  }
-  return reinterpret_cast<const float4*>(base)[i];
-}
+__device__ __forceinline__ float4 adam_ld(const float* base, int64_t i) { return reinterpret_cast<const float4*>(base)[i]; }
 __device__ __forceinline__ void adam_st(float* base, int64_t i, float4 v) {
-  if (NR_ADAM_NT >= 1) {
-    __builtin_nontemporal_store((adam_f4){v.x, v.y, v.z, v.w}, reinterpret_cast<adam_f4*>(base) + i);
-    return;
-  }
-  reinterpret_cast<float4*>(base)[i] = v;
+  __builtin_nontemporal_store((adam_f4){v.x, v.y, v.z, v.w}, reinterpret_cast<adam_f4*>(base) + i);
 }
 
 __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
