@@ -176,153 +176,6 @@ __global__ __launch_bounds__(64 * NB) void cnn_keypool_fwd_kernel(KPArgs g) {
   }
 }
 
-// Forward on the bf16 MFMA (NP = 3: bf16x6, NP = 1: bf16) with the C tile split ONCE: the staging
-// threads write each C element's bf16 planes to LDS (the f32 form's key products had every column
-// wave split all of C again, NB times per title: ~1.4 K VALU per wave and title, half the kernel's
-// issue), the key products read the A fragments as ds_read_b128 of the planes, the scores are
-// reduced across the wave's 32 columns in registers (no K tile in LDS) and the pooling reads C back
-// as h + m + l (exact: the split's residuals are exact and the last is 8 bits wide) or, for
-// bf16, from the f32 tile kept beside its one plane.
-__device__ __forceinline__ float bf16f(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
-
-template <int NB, int NP>
-struct alignas(16) KPPShared {
-  static constexpr int HP = 32 * NB, SWB = HP + 8, SW = HP + 4;   // 84 dwords per plane row: ds_read_b128 conflict-free
-  uint16_t cp[NP][32][SWB];                 // C tile planes (rows >= L zero)
-  float ct[NP == 1 ? 32 : 1][SW];           // bf16: the f32 C tile for the pooling
-  float ps[NB][32];                         // per column-wave partial scores
-  float p[32];
-  float qv[HP], bq[HP];
-};
-
-template <int NB, int NP>
-__global__ __launch_bounds__(64 * NB) void cnn_keypool_fwd_planes_kernel(KPArgs g) {
-  constexpr int HP = 32 * NB;
-  using SM = KPPShared<NB, NP>;
-  __shared__ SM sm;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
-  for (int k = tid; k < HP; k += 64 * NB) {
-    sm.qv[k] = k < g.qn ? g.q[k] : 0.f;
-    sm.bq[k] = g.bq[k];
-  }
-  constexpr int Q4 = 8 * NB;
-  constexpr int TPF = (32 * Q4 + 64 * NB - 1) / (64 * NB);   // C-tile float4 per thread
-  float4 cn[TPF];   // the next title's C tile travels in registers while this one computes
-  auto fetch = [&](int64_t seq) {
-#pragma unroll
-    for (int u = 0; u < TPF; ++u) {
-      const int i = tid + u * 64 * NB;
-      const int r = i / Q4, c4 = i - r * Q4;
-      const bool ok = i < 32 * Q4 && r < g.L;
-      cn[u] = *reinterpret_cast<const float4*>(g.c + (seq * g.L + (ok ? r : 0)) * g.ldc + 4 * (ok ? c4 : 0));
-      if (!ok) cn[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  const int j = 32 * w + c;   // this lane's output column of K
-  if ((int64_t)blockIdx.x < g.nseq) fetch(blockIdx.x);
-  for (int64_t seq = blockIdx.x; seq < g.nseq; seq += gridDim.x) {
-    __syncthreads();   // the previous title's reads of cp / ct / p are done
-#pragma unroll
-    for (int u = 0; u < TPF; ++u) {
-      const int i = tid + u * 64 * NB;
-      if (i < 32 * Q4) {
-        const int r = i / Q4, k = 4 * (i % Q4);
-        const float4 x = cn[u];
-        if constexpr (NP == 1) {
-          *reinterpret_cast<uint2*>(&sm.cp[0][r][k]) = nrfast::hi4(x.x, x.y, x.z, x.w);
-          *reinterpret_cast<float4*>(&sm.ct[r][k]) = x;
-        } else {
-          uint2 p0, p1, p2;
-          nrfast::split4(x.x, x.y, x.z, x.w, p0, p1, p2);
-          *reinterpret_cast<uint2*>(&sm.cp[0][r][k]) = p0;
-          *reinterpret_cast<uint2*>(&sm.cp[1][r][k]) = p1;
-          *reinterpret_cast<uint2*>(&sm.cp[2][r][k]) = p2;
-        }
-      }
-    }
-    __syncthreads();
-    if (seq + gridDim.x < g.nseq) fetch(seq + gridDim.x);
-    {
-      // acc = C Wqᵀ for output columns 32 w .. 32 w + 31; k order: lane (c, h) step m of chunk ch
-      // holds k = 32 ch + 16 h + 8 m + 0..7 in both operands (A from the planes, B = Wq row j from L2)
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      float bn[16];
-      load_wrow<NB>(g, w, c, h, 0, bn);
-#pragma unroll 1
-      for (int ch = 0; ch < NB; ++ch) {
-        float b[16];
-#pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) b[s2] = bn[s2];
-        if (ch + 1 < NB) load_wrow<NB>(g, w, c, h, ch + 1, bn);
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          Planes<NP> a;
-#pragma unroll
-          for (int pl = 0; pl < NP; ++pl)
-            a.v[pl] = *reinterpret_cast<const bf16x8*>(&sm.cp[pl][c][32 * ch + 16 * h + 8 * m]);
-          mfma_x<NP>(acc, a, planes8<NP>(b + 8 * m));
-        }
-      }
-      // s_l partial over this wave's 32 columns: tanh(acc + bq_j) q_j summed across the 32 lanes of
-      // each half (rows crow(r, h))
-      // (a butterfly: at lane distance 16, 8, 4, 2 each lane keeps the half of its registers its bit
-      // selects and adds the partner's copy of it -- 8 + 4 + 2 + 1 exchanges instead of 16 x 5 -- then
-      // one more at distance 1; lane c then holds row register r = (c >> 1) & 15's full sum)
-      const float bj = sm.bq[j], qj = sm.qv[j];
-      float kv[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float kr = tanhf(acc[r] + bj);
-        if (g.kout && crow(r, h) < g.L) g.kout[(seq * g.L + crow(r, h)) * g.ldk + j] = kr;
-        kv[r] = kr * qj;
-      }
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const int half = 8 >> st, d = 16 >> st;
-        const bool up = (c & d) != 0;
-#pragma unroll
-        for (int i = 0; i < half; ++i) {
-          const float keep = up ? kv[i + half] : kv[i], give = up ? kv[i] : kv[i + half];
-          kv[i] = keep + __shfl_xor(give, d, 64);
-        }
-      }
-      const float tot = kv[0] + __shfl_xor(kv[0], 1, 64);
-      if ((c & 1) == 0) sm.ps[w][crow((c >> 1) & 15, h)] = tot;
-    }
-    __syncthreads();
-    if (w == 0) {   // scores and the masked softmax, lane l = token l
-      const int l = lane & 31;
-      float s = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < NB; ++ww) s += sm.ps[ww][l];
-      const bool keep = lane < g.L && nr_mask_at(g.mask, g.mask_dt, seq * g.L + lane);
-      const float v = keep ? s * g.scale : -INFINITY;
-      const float mx = nr_wave_max(v);
-      const float e = keep ? __expf(v - mx) : 0.f;
-      const float sum = nr_wave_sum(e);
-      const float pr = sum > 0.f ? e / sum : 0.f;
-      if (lane < 32) sm.p[lane] = pr;
-      if (lane < g.L) g.probs[seq * g.L + lane] = pr;
-    }
-    __syncthreads();
-    for (int k = tid; k < HP; k += 64 * NB) {   // news = Σ_l p_l C_l
-      float a = 0.f;
-      for (int l = 0; l < g.L; ++l) {
-        float x;
-        if constexpr (NP == 1) {
-          x = sm.ct[l][k];
-        } else {
-          x = (bf16f(sm.cp[0][l][k]) + bf16f(sm.cp[1][l][k])) + bf16f(sm.cp[2][l][k]);
-        }
-        a = fmaf(sm.p[l], x, a);
-      }
-      g.news[seq * g.ldn + k] = a;
-    }
-  }
-}
-
 // Backward: KP_BW = 8 waves (one workgroup per CU, two waves per SIMD).  Waves 0 .. NB-1 are COLUMN
 // waves (key block, dK block and dC block w); the other 8 - NB are dWq waves, each owning a fixed
 // round-robin share of dWq's NB² 32 x 32 blocks, accumulated across the workgroup's titles in LDS
@@ -615,14 +468,6 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
   }
 NR_KP_LAUNCH(cnn_keypool_fwd_kernel, 64 * NB)
 template <int NB>
-int launch_cnn_keypool_fwd_planes(int np, const KPArgs& g, int64_t grid, hipStream_t s) {
-  if (np == 0) return launch_cnn_keypool_fwd_kernel<NB>(np, g, grid, s);
-  if (np == 1) hipLaunchKernelGGL((cnn_keypool_fwd_planes_kernel<NB, 1>), dim3((unsigned)grid), dim3(64 * NB), 0, s, g);
-  else hipLaunchKernelGGL((cnn_keypool_fwd_planes_kernel<NB, 3>), dim3((unsigned)grid), dim3(64 * NB), 0, s, g);
-  NR_LAUNCH_CHECK();
-  return NR_OK;
-}
-template <int NB>
 int launch_cnn_keypool_bwd_kernel(int np, const KPArgs& g, int64_t grid, hipStream_t s) {
 #define NR_KPB(NP_)                                                                                       \
   if (g.kin) hipLaunchKernelGGL((cnn_keypool_bwd_kernel<NB, NP_, true>), dim3((unsigned)grid), dim3(64 * KP_BW), 0, s, g); \
@@ -661,11 +506,11 @@ extern "C" int nr_cnn_keypool_fwd(const float* C, int64_t ldc, const float* wq, 
   const int64_t grid = kp_groups(nseq, 3);
   const int np = np_of(prec);
   switch (Hp / 32) {
-    case 1: return launch_cnn_keypool_fwd_planes<1>(np, g, grid, stream);
-    case 2: return launch_cnn_keypool_fwd_planes<2>(np, g, grid, stream);
-    case 3: return launch_cnn_keypool_fwd_planes<3>(np, g, grid, stream);
-    case 4: return launch_cnn_keypool_fwd_planes<4>(np, g, grid, stream);
-    default: return launch_cnn_keypool_fwd_planes<5>(np, g, grid, stream);
+    case 1: return launch_cnn_keypool_fwd_kernel<1>(np, g, grid, stream);
+    case 2: return launch_cnn_keypool_fwd_kernel<2>(np, g, grid, stream);
+    case 3: return launch_cnn_keypool_fwd_kernel<3>(np, g, grid, stream);
+    case 4: return launch_cnn_keypool_fwd_kernel<4>(np, g, grid, stream);
+    default: return launch_cnn_keypool_fwd_kernel<5>(np, g, grid, stream);
   }
 }
 
