@@ -211,16 +211,16 @@ int nr_cnn_unpack_grads(const float* dw3t, const float* dwqp, const float* dbqp,
 /* CNN_Encoder's word attention head fused per title (models/Encoders/CNN.py:44-46 with
  * scaled_dp_attention, Modules/Attention.py:5-30, over the conv output C of CNN.py:41-42):
  * K = tanh(C wqᵀ + bq), s_l = scale q·K_l, p = XSoftmax(s, mask), news = Σ_l p_l C_l.  The key
- * projection never reaches HBM.  C [nseq*L][Hp] (ldc % 4 == 0, 16-B aligned, exactly zero past the
+ * projection reaches HBM only through kout.  C [nseq*L][Hp] (ldc % 4 == 0, 16-B aligned, exactly zero past the
  * valid width), wq [Hp][Hp] / bq [Hp] zero-padded (nr_cnn_pack_weights), q [qn]; Hp a multiple of
  * 32 up to 160, L <= 32.  prec: enum nr_gemm_precision of the key products.  news [nseq][Hp]
- * (ldn >= Hp), probs [nseq*L].  kout (optional, [nseq*L][ldk >= Hp]): K stored for the backward (which
- * then skips the key recompute); NULL keeps the key projection on chip. */
+ * (ldn >= Hp), probs [nseq*L].  kout (optional, [nseq*L][ldk >= Hp], ldk % 4 == 0, 16-B aligned): K
+ * stored for the backward (which then skips the key recompute); NULL keeps the key projection on chip. */
 int nr_cnn_keypool_fwd(const float* C, int64_t ldc, const float* wq, const float* bq, const float* q, int32_t qn,
                        const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L, int32_t Hp, float scale,
                        int32_t prec, float* news, int64_t ldn, float* probs, float* kout, int64_t ldk,
                        hipStream_t stream);
-/* Backward of nr_cnn_keypool_fwd in one pass over C (the key projection recomputed): dc [nseq*L][Hp] =
+/* Backward of nr_cnn_keypool_fwd in one pass over C (the key projection read from kin or recomputed): dc [nseq*L][Hp] =
  * ReLU'(C) ⊙ (p dnews + dK wq + dz) (the conv pre-activation gradient; dz optional, [T][>= H]),
  * dK = ds q ⊙ (1 - K²); dwq [Hp][Hp] = Σ dKᵀ C, dbq [Hp] = Σ dK, dq [qn] = Σ ds K, dconv_b [H] =
  * Σ_t dc[t] -- all STORED (not accumulated), summed deterministically over per-workgroup partials in

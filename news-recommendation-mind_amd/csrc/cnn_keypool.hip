@@ -5,8 +5,8 @@
 //   s_l = q · K_l / sqrt(H),  p = XSoftmax(s, mask),  news = Σ_l p_l C_l
 //                                              scaled_dp_attention (Attention.py:5-30)
 //
-// and its whole backward in ONE pass over C per title: the key projection is recomputed (never
-// stored), dp_l = dnews · C_l, ds = p (dp - Σ p dp) / sqrt(H), dK = ds q (1 - K²),
+// and its whole backward in ONE pass over C per title: the key projection is read back from the
+// forward's optional K output (kout / kin) or recomputed, dp_l = dnews · C_l, ds = p (dp - Σ p dp) / sqrt(H), dK = ds q (1 - K²),
 // dC = p dnews + dK Wq (+ dz) gated by ReLU'(C) (the conv pre-activation gradient), and the
 // parameter gradients dWq = Σ dKᵀ C, dbq = Σ dK, dq = Σ ds K, dconv_b = Σ gated dC accumulate in
 // registers / LDS across the titles of a persistent workgroup; each workgroup stores one partial and
@@ -56,7 +56,9 @@ struct alignas(16) KPShared {
   static constexpr int HP = 32 * NB, SW = HP + 4;
   float ct[32][SW];   // C tile (rows >= L zero)
   float dk[32][SW];   // bwd: dK tile; fwd: K_j q_j products
-  float p[32], ds[32];
+  float p[32];
+  float dpp[NB][32];   // bwd: column wave w's partial dp over its 32 columns
+  float dsw[NB][32];   // bwd: ds as column wave w formed it (wave-private)
   float dn[HP], qv[HP], bq[HP];
 };
 
@@ -141,22 +143,27 @@ __global__ __launch_bounds__(64 * NB) void cnn_keypool_fwd_kernel(KPArgs g) {
       f32x16 acc;
       key_block<NB, NP>(g, sm, w, c, h, acc);
       const int j = 32 * w + c;
-      const float bj = sm.bq[j], qj = sm.qv[j];
+      const float bj = sm.bq[j];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float kr = tanhf(acc[r] + bj);
-        if (g.kout && crow(r, h) < g.L) g.kout[(seq * g.L + crow(r, h)) * g.ldk + j] = kr;
-        sm.dk[crow(r, h)][j] = kr * qj;
-      }
+      for (int r = 0; r < 16; ++r) sm.dk[crow(r, h)][j] = tanhf(acc[r] + bj);
     }
     __syncthreads();
+    if (g.kout) {   // K rows < L to HBM as float4 rows from LDS (per-lane column stores from the
+                    // MFMA layout kept 16 64-bit addresses live: 159 VGPRs, two workgroups per CU)
+      for (int i = tid; i < g.L * Q4; i += 64 * NB) {
+        const int r = i / Q4, c4 = i - r * Q4;
+        *reinterpret_cast<float4*>(g.kout + (seq * g.L + r) * g.ldk + 4 * c4) =
+            *reinterpret_cast<const float4*>(&sm.dk[r][4 * c4]);
+      }
+    }
     if (w == 0) {   // scores and the masked softmax, lane l = token l
       const int l = lane & 31;
       float s = 0.f;
 #pragma unroll 4
       for (int k4 = 0; k4 < HP / 4; ++k4) {
         const float4 v = *reinterpret_cast<const float4*>(&sm.dk[l][4 * k4]);
-        s += (v.x + v.y) + (v.z + v.w);
+        const float4 qv = *reinterpret_cast<const float4*>(&sm.qv[4 * k4]);
+        s += (v.x * qv.x + v.y * qv.y) + (v.z * qv.z + v.w * qv.w);
       }
       const bool keep = lane < g.L && nr_mask_at(g.mask, g.mask_dt, seq * g.L + lane);
       const float v = keep ? s * g.scale : -INFINITY;
@@ -172,6 +179,168 @@ __global__ __launch_bounds__(64 * NB) void cnn_keypool_fwd_kernel(KPArgs g) {
       float acc = 0.f;
       for (int l = 0; l < g.L; ++l) acc = fmaf(sm.p[l], sm.ct[l][k], acc);
       g.news[seq * g.ldn + k] = acc;
+    }
+  }
+}
+
+// buffer resource word 3 (gfx9 family: 32-bit data format, raw addressing)
+constexpr int kBufWord3 = 0x00020000;
+
+// Forward on the bf16 MFMA (NP = 3: bf16x6, NP = 1: bf16) with the C tile split ONCE: the staging
+// threads write each C element's bf16 planes to LDS (the f32 form's key products had every column
+// wave split all of C again, NB times per title: ~1.4 K VALU per wave and title, half the kernel's
+// issue), the key products read the A fragments as ds_read_b128 of the planes, the scores are
+// reduced across the wave's 32 columns in registers (no K tile in LDS; the optional K output goes
+// out through buffer stores) and the pooling reads C back
+// as h + m + l (exact: the split's residuals are exact and the last is 8 bits wide) or, for
+// bf16, from the f32 tile kept beside its one plane.
+__device__ __forceinline__ float bf16f(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
+
+template <int NB, int NP>
+struct alignas(16) KPPShared {
+  static constexpr int HP = 32 * NB, SWB = HP + 8, SW = HP + 4;   // 84 dwords per plane row: ds_read_b128 conflict-free
+  uint16_t cp[NP][32][SWB];                 // C tile planes (rows >= L zero)
+  float ct[NP == 1 ? 32 : 1][SW];           // bf16: the f32 C tile for the pooling
+  float ps[NB][32];                         // per column-wave partial scores
+  float p[32];
+  float qv[HP], bq[HP];
+};
+
+template <int NB, int NP>
+__global__ __launch_bounds__(64 * NB) void cnn_keypool_fwd_planes_kernel(KPArgs g) {
+  constexpr int HP = 32 * NB;
+  using SM = KPPShared<NB, NP>;
+  __shared__ SM sm;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
+  for (int k = tid; k < HP; k += 64 * NB) {
+    sm.qv[k] = k < g.qn ? g.q[k] : 0.f;
+    sm.bq[k] = g.bq[k];
+  }
+  constexpr int Q4 = 8 * NB;
+  constexpr int TPF = (32 * Q4 + 64 * NB - 1) / (64 * NB);   // C-tile float4 per thread
+  float4 cn[TPF];   // the next title's C tile travels in registers while this one computes
+  auto fetch = [&](int64_t seq) {
+#pragma unroll
+    for (int u = 0; u < TPF; ++u) {
+      const int i = tid + u * 64 * NB;
+      const int r = i / Q4, c4 = i - r * Q4;
+      const bool ok = i < 32 * Q4 && r < g.L;
+      cn[u] = *reinterpret_cast<const float4*>(g.c + (seq * g.L + (ok ? r : 0)) * g.ldc + 4 * (ok ? c4 : 0));
+      if (!ok) cn[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  const int j = 32 * w + c;   // this lane's output column of K
+  if ((int64_t)blockIdx.x < g.nseq) fetch(blockIdx.x);
+  for (int64_t seq = blockIdx.x; seq < g.nseq; seq += gridDim.x) {
+    __syncthreads();   // the previous title's reads of cp / ct / p are done
+#pragma unroll
+    for (int u = 0; u < TPF; ++u) {
+      const int i = tid + u * 64 * NB;
+      if (i < 32 * Q4) {
+        const int r = i / Q4, k = 4 * (i % Q4);
+        const float4 x = cn[u];
+        if constexpr (NP == 1) {
+          *reinterpret_cast<uint2*>(&sm.cp[0][r][k]) = nrfast::hi4(x.x, x.y, x.z, x.w);
+          *reinterpret_cast<float4*>(&sm.ct[r][k]) = x;
+        } else {
+          uint2 p0, p1, p2;
+          nrfast::split4(x.x, x.y, x.z, x.w, p0, p1, p2);
+          *reinterpret_cast<uint2*>(&sm.cp[0][r][k]) = p0;
+          *reinterpret_cast<uint2*>(&sm.cp[1][r][k]) = p1;
+          *reinterpret_cast<uint2*>(&sm.cp[2][r][k]) = p2;
+        }
+      }
+    }
+    __syncthreads();
+    if (seq + gridDim.x < g.nseq) fetch(seq + gridDim.x);
+    {
+      // acc = C Wqᵀ for output columns 32 w .. 32 w + 31; k order: lane (c, h) step m of chunk ch
+      // holds k = 32 ch + 16 h + 8 m + 0..7 in both operands (A from the planes, B = Wq row j from L2)
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      float bn[16];
+      load_wrow<NB>(g, w, c, h, 0, bn);
+#pragma unroll 1
+      for (int ch = 0; ch < NB; ++ch) {
+        float b[16];
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) b[s2] = bn[s2];
+        if (ch + 1 < NB) load_wrow<NB>(g, w, c, h, ch + 1, bn);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          Planes<NP> a;
+#pragma unroll
+          for (int pl = 0; pl < NP; ++pl)
+            a.v[pl] = *reinterpret_cast<const bf16x8*>(&sm.cp[pl][c][32 * ch + 16 * h + 8 * m]);
+          mfma_x<NP>(acc, a, planes8<NP>(b + 8 * m));
+        }
+      }
+      // s_l partial over this wave's 32 columns: tanh(acc + bq_j) q_j summed across the 32 lanes of
+      // each half (rows crow(r, h))
+      // (a butterfly: at lane distance 16, 8, 4, 2 each lane keeps the half of its registers its bit
+      // selects and adds the partner's copy of it -- 8 + 4 + 2 + 1 exchanges instead of 16 x 5 -- then
+      // one more at distance 1; lane c then holds row register r = (c >> 1) & 15's full sum)
+      const float bj = sm.bq[j], qj = sm.qv[j];
+      float kv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) kv[r] = tanhf(acc[r] + bj);
+      if (g.kout) {
+        // K to HBM through a buffer resource over this title's L rows: one lane offset (row 4 h,
+        // column j) plus a uniform per-register row offset, rows >= L dropped by the range check
+        // (per-lane 64-bit addresses for the 16 stores took the kernel to 159 VGPRs: two workgroups
+        // per CU instead of three)
+        const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc(
+            g.kout + seq * g.L * g.ldk, (short)0, (int)(g.L * g.ldk * 4), kBufWord3);
+        const int vo = (int)((4 * h * g.ldk + j) * 4);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(kv[r]), kr, vo,
+                                                (int)(((r & 3) + 8 * (r >> 2)) * g.ldk * 4), 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) kv[r] *= qj;
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int half = 8 >> st, d = 16 >> st;
+        const bool up = (c & d) != 0;
+#pragma unroll
+        for (int i = 0; i < half; ++i) {
+          const float keep = up ? kv[i + half] : kv[i], give = up ? kv[i] : kv[i + half];
+          kv[i] = keep + __shfl_xor(give, d, 64);
+        }
+      }
+      const float tot = kv[0] + __shfl_xor(kv[0], 1, 64);
+      if ((c & 1) == 0) sm.ps[w][crow((c >> 1) & 15, h)] = tot;
+    }
+    __syncthreads();
+    if (w == 0) {   // scores and the masked softmax, lane l = token l
+      const int l = lane & 31;
+      float s = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NB; ++ww) s += sm.ps[ww][l];
+      const bool keep = lane < g.L && nr_mask_at(g.mask, g.mask_dt, seq * g.L + lane);
+      const float v = keep ? s * g.scale : -INFINITY;
+      const float mx = nr_wave_max(v);
+      const float e = keep ? __expf(v - mx) : 0.f;
+      const float sum = nr_wave_sum(e);
+      const float pr = sum > 0.f ? e / sum : 0.f;
+      if (lane < 32) sm.p[lane] = pr;
+      if (lane < g.L) g.probs[seq * g.L + lane] = pr;
+    }
+    __syncthreads();
+    for (int k = tid; k < HP; k += 64 * NB) {   // news = Σ_l p_l C_l
+      float a = 0.f;
+      for (int l = 0; l < g.L; ++l) {
+        float x;
+        if constexpr (NP == 1) {
+          x = sm.ct[l][k];
+        } else {
+          x = (bf16f(sm.cp[0][l][k]) + bf16f(sm.cp[1][l][k])) + bf16f(sm.cp[2][l][k]);
+        }
+        a = fmaf(sm.p[l], x, a);
+      }
+      g.news[seq * g.ldn + k] = a;
     }
   }
 }
@@ -268,27 +437,34 @@ __global__ __launch_bounds__(64 * KP_BW) void cnn_keypool_bwd_kernel(KPArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) kr[r] = tanhf(acc[r] + bj);
     }
-    if (!colw && d == 0) {   // dp_l = dnews · C_l; ds = p (dp - Σ p dp) scale
-      const int l = lane & 31;
+    if (colw) {   // dp_l = dnews · C_l, this wave's 32 columns: lane (c, h) = token c, columns 32 w + 16 h + 0..15
       float dp = 0.f;
-#pragma unroll 4
-      for (int k4 = 0; k4 < HP / 4; ++k4) {
-        const float4 x = *reinterpret_cast<const float4*>(&sm.ct[l][4 * k4]);
-        const float4 dv = *reinterpret_cast<const float4*>(&sm.dn[4 * k4]);
+#pragma unroll 1
+      for (int u = 0; u < 4; ++u) {
+        const float4 x = *reinterpret_cast<const float4*>(&sm.ct[c][32 * w + 16 * h + 4 * u]);
+        const float4 dv = *reinterpret_cast<const float4*>(&sm.dn[32 * w + 16 * h + 4 * u]);
         dp = fmaf(x.x, dv.x, dp); dp = fmaf(x.y, dv.y, dp);
         dp = fmaf(x.z, dv.z, dp); dp = fmaf(x.w, dv.w, dp);
       }
-      const float pl = lane < 32 ? sm.p[l] : 0.f;
-      const float rs = nr_wave_sum(pl * dp);
-      if (lane < 32) sm.ds[lane] = pl * (dp - rs) * g.scale;
+      dp += __shfl_xor(dp, 32, 64);
+      if (h == 0) sm.dpp[w][c] = dp;
     }
     __syncthreads();
     if (colw) {
+      // ds = p (dp - Σ p dp) scale, formed by every column wave from the same partials in the same
+      // order (identical values) into its own LDS row: no workgroup barrier before the reads
+      float dp = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NB; ++ww) dp += sm.dpp[ww][c];
+      const float pl = sm.p[c];
+      const float rs = nr_wave_sum(h == 0 ? pl * dp : 0.f);
+      if (h == 0) sm.dsw[w][c] = pl * (dp - rs) * g.scale;
+      wave_lds_fence();
       const float qj = sm.qv[j];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int tok = crow(r, h);
-        const float dsr = sm.ds[tok];
+        const float dsr = sm.dsw[w][tok];
         dq_acc = fmaf(dsr, kr[r], dq_acc);
         const float dkv = dsr * qj * (1.f - kr[r] * kr[r]);
         dbq_acc += dkv;
@@ -448,7 +624,7 @@ int cu_count() {
   return g_cus;
 }
 
-// persistent workgroups per CU: the forward (NB waves, 44 KB of LDS) three, the backward (8 waves,
+// persistent workgroups per CU: the forward (NB waves, 44 KB of LDS, <= 128 VGPRs) three, the backward (8 waves,
 // 147 KB of LDS) one
 int64_t kp_groups(int64_t nseq, int per_cu) {
   const int64_t cap = (int64_t)cu_count() * per_cu;
@@ -457,16 +633,38 @@ int64_t kp_groups(int64_t nseq, int per_cu) {
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-#define NR_KP_LAUNCH(KERN, NT)                                                                              \
-  template <int NB>                                                                                         \
-  int launch_##KERN(int np, const KPArgs& g, int64_t grid, hipStream_t s) {                               \
-    if (np == 0) hipLaunchKernelGGL((KERN<NB, 0>), dim3((unsigned)grid), dim3(NT), 0, s, g);              \
-    else if (np == 1) hipLaunchKernelGGL((KERN<NB, 1>), dim3((unsigned)grid), dim3(NT), 0, s, g);         \
-    else hipLaunchKernelGGL((KERN<NB, 3>), dim3((unsigned)grid), dim3(NT), 0, s, g);                      \
-    NR_LAUNCH_CHECK();                                                                                      \
-    return NR_OK;                                                                                           \
+// A persistent grid larger than what is resident leaves a tail of workgroups that start only when
+// others finish: the forward's grid is capped by the instantiation's occupancy (at 159 VGPRs the
+// bf16x6 forward fitted two workgroups per CU, not three, and ran 52 -> 76 us)
+template <typename Kern>
+int resident_per_cu(Kern kern, int nt, int want) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, nt, 0) != hipSuccess || n < 1) n = 1;
+  return n < want ? n : want;
+}
+
+// f32 MFMA: the per-wave fp32 fragments; bf16x6 / bf16: the C tile split once into LDS planes
+template <int NB, int NP>
+void launch_fwd(const KPArgs& g, hipStream_t s) {
+  static int per_cu = 0;   // resident workgroups per CU of this instantiation, queried once
+  if constexpr (NP == 0) {
+    if (per_cu == 0) per_cu = resident_per_cu(cnn_keypool_fwd_kernel<NB, NP>, 64 * NB, 3);
+    hipLaunchKernelGGL((cnn_keypool_fwd_kernel<NB, NP>), dim3((unsigned)kp_groups(g.nseq, per_cu)), dim3(64 * NB), 0, s, g);
+  } else {
+    if (per_cu == 0) per_cu = resident_per_cu(cnn_keypool_fwd_planes_kernel<NB, NP>, 64 * NB, 3);
+    hipLaunchKernelGGL((cnn_keypool_fwd_planes_kernel<NB, NP>), dim3((unsigned)kp_groups(g.nseq, per_cu)), dim3(64 * NB),
+                       0, s, g);
   }
-NR_KP_LAUNCH(cnn_keypool_fwd_kernel, 64 * NB)
+}
+
+template <int NB>
+int launch_cnn_keypool_fwd_kernel(int np, const KPArgs& g, hipStream_t s) {
+  if (np == 0) launch_fwd<NB, 0>(g, s);
+  else if (np == 1) launch_fwd<NB, 1>(g, s);
+  else launch_fwd<NB, 3>(g, s);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
 template <int NB>
 int launch_cnn_keypool_bwd_kernel(int np, const KPArgs& g, int64_t grid, hipStream_t s) {
 #define NR_KPB(NP_)                                                                                       \
@@ -477,7 +675,6 @@ int launch_cnn_keypool_bwd_kernel(int np, const KPArgs& g, int64_t grid, hipStre
   NR_LAUNCH_CHECK();
   return NR_OK;
 }
-#undef NR_KP_LAUNCH
 
 int np_of(int prec) { return prec == NR_GEMM_F32 ? 0 : prec == NR_GEMM_BF16 ? 1 : 3; }
 
@@ -497,20 +694,19 @@ extern "C" int nr_cnn_keypool_fwd(const float* C, int64_t ldc, const float* wq, 
     return NR_EINVAL(0);
   if (!C || !wq || !bq || !q || !mask || !news || !probs) return NR_EINVAL(1);
   if (!al16(C) || !al16(wq)) return NR_EINVAL(2);
-  if (kout && ldk < Hp) return NR_EINVAL(3);
+  if (kout && (ldk < Hp || (ldk & 3) || !al16(kout))) return NR_EINVAL(3);
   if (nseq == 0) return NR_OK;
   KPArgs g{};
   g.c = C; g.ldc = ldc; g.wq = wq; g.bq = bq; g.q = q; g.qn = qn; g.mask = mask; g.mask_dt = mask_dtype;
   g.nseq = nseq; g.L = L; g.scale = scale; g.news = news; g.ldn = ldn; g.probs = probs; g.H = qn;
   g.kout = kout; g.ldk = ldk;
-  const int64_t grid = kp_groups(nseq, 3);
   const int np = np_of(prec);
   switch (Hp / 32) {
-    case 1: return launch_cnn_keypool_fwd_kernel<1>(np, g, grid, stream);
-    case 2: return launch_cnn_keypool_fwd_kernel<2>(np, g, grid, stream);
-    case 3: return launch_cnn_keypool_fwd_kernel<3>(np, g, grid, stream);
-    case 4: return launch_cnn_keypool_fwd_kernel<4>(np, g, grid, stream);
-    default: return launch_cnn_keypool_fwd_kernel<5>(np, g, grid, stream);
+    case 1: return launch_cnn_keypool_fwd_kernel<1>(np, g, stream);
+    case 2: return launch_cnn_keypool_fwd_kernel<2>(np, g, stream);
+    case 3: return launch_cnn_keypool_fwd_kernel<3>(np, g, stream);
+    case 4: return launch_cnn_keypool_fwd_kernel<4>(np, g, stream);
+    default: return launch_cnn_keypool_fwd_kernel<5>(np, g, stream);
   }
 }
 
