@@ -693,6 +693,18 @@ __device__ __forceinline__ void put2(uint16_t (*T)[kHD][kVR], int d, int k, floa
   }
 }
 
+// Staging slot of thread f (0..255): rows 2 kp, 2 kp + 1 and dims 4 dq .. 4 dq + 3 of the tile, with
+// f's bits dealt as kp = {f0, f1, f4, f6}, dq = {f2, f3, f5, f7} so that both images are written
+// conflict-free: a ds_write_b64 group (16 lanes) of the row-major image covers kp mod 4 x dq mod 4 =
+// 16 distinct bank pairs of a 36-dword row stride, a ds_write_b32 group (32 lanes) of the transposed
+// one 8 dq + kp = 32 distinct banks of an 18-dword row stride.  (kp = f & 15 put four lanes of a
+// b64 group on each bank pair: the attention kernels' 2.5 - 3.2 conflict cycles per LDS instruction,
+// profiles/r04_j_pmc_xf_attn_*.json.)
+__device__ __forceinline__ void tile_slot(int f, int& kp, int& dq) {
+  kp = (f & 3) | ((f >> 2) & 4) | ((f >> 3) & 8);
+  dq = ((f >> 2) & 3) | ((f >> 3) & 4) | ((f >> 4) & 8);
+}
+
 // Stage rows j0 .. j0 + 31 (zeros at and past L) of one 64-wide column block, split into planes,
 // row-major into P and/or transposed into T; the whole workgroup takes part.
 template <int NP>
@@ -705,7 +717,8 @@ __device__ __forceinline__ void stage_planes(uint16_t (*P)[32][kKR], uint16_t (*
     // dims 4 dq .. 4 dq + 3, stores their row-major quads and repacks the same bf16 halves into the
     // transposed (dim, row pair) words
     for (int f = tid; f < 256; f += blockDim.x) {
-      const int kp = f & 15, dq = f >> 4;
+      int kp, dq;
+      tile_slot(f, kp, dq);
       const int j = j0 + 2 * kp;
       const float* vb = base + (row0 + j) * ld + col + 4 * dq;
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
@@ -736,7 +749,8 @@ __device__ __forceinline__ void stage_planes(uint16_t (*P)[32][kKR], uint16_t (*
   }
   if (T) {
     for (int f = tid; f < 256; f += blockDim.x) {
-      const int kp = f & 15, dq = f >> 4;   // rows 2 kp, 2 kp + 1; dims 4 dq .. 4 dq + 3
+      int kp, dq;   // rows 2 kp, 2 kp + 1; dims 4 dq .. 4 dq + 3
+      tile_slot(f, kp, dq);
       const int j = j0 + 2 * kp;
       const float* vb = base + (row0 + j) * ld + col + 4 * dq;
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
@@ -793,7 +807,7 @@ __device__ __forceinline__ void own_rows(Planes<NP> (&out)[4], const float* p, b
 }
 
 // Register-prefetched staging (workgroups of four waves): thread f holds rows 2 kp, 2 kp + 1 and dims
-// 4 dq .. 4 dq + 3 (kp = f & 15, dq = f >> 4) of the NEXT tile of one tensor, loaded while the current
+// 4 dq .. 4 dq + 3 (tile_slot) of the NEXT tile of one tensor, loaded while the current
 // tile's products run, and writes both plane images of it from one split after the barrier.  Without
 // it every tile paid a full load latency between its two barriers (one to three waves per SIMD
 // cannot hide it): XFormer train step 74.3 -> 71.3 ms (profiles/r04_h_xf_*.json, same box).
@@ -801,7 +815,8 @@ template <int NP>
 struct TileFetch {
   float4 a, b;
   __device__ __forceinline__ void fetch(const float* base, int64_t ld, int64_t row0, int j0, int L, int64_t col) {
-    const int f = threadIdx.x, kp = f & 15, dq = f >> 4;
+    int kp, dq;
+    tile_slot(threadIdx.x, kp, dq);
     const int j = j0 + 2 * kp;
     const float* vb = base + (row0 + j) * ld + col + 4 * dq;
     a = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -810,7 +825,8 @@ struct TileFetch {
     if (j + 1 < L) b = ld4(vb + ld);
   }
   __device__ __forceinline__ void store(uint16_t (*P)[32][kKR], uint16_t (*T)[kHD][kVR]) const {
-    const int f = threadIdx.x, kp = f & 15, dq = f >> 4;
+    int kp, dq;
+    tile_slot(threadIdx.x, kp, dq);
     uint2 pa[NP], pb[NP];
     if constexpr (NP == 1) {
       pa[0] = nrfast::hi4(a.x, a.y, a.z, a.w);
