@@ -347,10 +347,10 @@ __global__ __launch_bounds__(64 * NB) void cnn_keypool_fwd_planes_kernel(KPArgs 
 
 // Backward: KP_BW = 8 waves (one workgroup per CU, two waves per SIMD).  Waves 0 .. NB-1 are COLUMN
 // waves (key block, dK block and dC block w); the other 8 - NB are dWq waves, each owning a fixed
-// round-robin share of dWq's NB² 32 x 32 blocks, accumulated across the workgroup's titles in LDS
-// ([block][register][lane]: conflict-free, 100 KB at NB = 5 -- in registers they would cost every
-// wave 144 VGPRs and spill) and computed while the column waves run the dC products; the first dWq
-// wave also forms dp / ds.  With NB = 5 each SIMD carries 18-20
+// share of dWq's NB² 32 x 32 blocks (bf16x6: a kb-major range; otherwise round-robin), accumulated
+// across the workgroup's titles in LDS ([block][register][lane]: conflict-free, 100 KB at NB = 5 -- in registers they would cost every
+// wave 144 VGPRs and spill) and computed while the column waves run the dC products; the column
+// waves also form dp (each over its own 32 columns) and ds.  With NB = 5 each SIMD carries 18-20
 // fragment products per title (five column waves on four SIMDs alone would leave one SIMD with
 // twice the others' work).
 constexpr int KP_BW = 8;
@@ -521,7 +521,41 @@ __global__ __launch_bounds__(64 * KP_BW) void cnn_keypool_bwd_kernel(KPArgs g) {
           dcb_acc += gated;
         }
       }
-    } else {   // dWq blocks of this wave += dKᵀ C over the title's tokens
+    } else if constexpr (NP == 3) {   // dWq blocks of this wave += dKᵀ C over the title's tokens
+      // bf16x6: a contiguous kb-major range of blocks, C column block kb (the B operand) read and
+      // split once per kb and reused across the range's jb (round-robin blocks split both operands
+      // of every block: 18 splits per title on the busiest wave at NB = 5, now 11; backward 94.0 ->
+      // 90.5 us, profiles/r04_m_*).  bf16's split is one rounding: the round-robin form below
+      // measured faster there (53.4 vs 58.0 us).
+      const int b0 = d * NB * NB / ND, b1 = (d + 1) * NB * NB / ND;
+      float bb[16];
+      Planes<NP> bp[2];
+#pragma unroll 1
+      for (int i = 0; i < MAXB; ++i) {
+        const int bq = b0 + i;
+        if (bq < b1) {
+          const int kb = bq / NB, jb = bq - kb * NB;
+          if (i == 0 || jb == 0) {
+#pragma unroll
+            for (int s2 = 0; s2 < 16; ++s2) bb[s2] = sm.ct[16 * h + s2][32 * kb + c];
+            bp[0] = planes8<NP>(bb);
+            bp[1] = planes8<NP>(bb + 8);
+          }
+          float a[16];
+#pragma unroll
+          for (int s2 = 0; s2 < 16; ++s2) a[s2] = sm.dk[16 * h + s2][32 * jb + c];
+          const int b = jb * NB + kb;   // accumulator slot (rows 32 jb.., columns 32 kb..)
+          f32x16 acc;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = wacc[b][r][lane];
+          mfma_x<NP>(acc, planes8<NP>(a), bp[0]);
+          mfma_x<NP>(acc, planes8<NP>(a + 8), bp[1]);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) wacc[b][r][lane] = acc[r];
+        }
+        __builtin_amdgcn_sched_barrier(0);   // keep the next block's fragment reads out of this one
+      }
+    } else {   // f32 / bf16: round-robin blocks, both fragments per block
 #pragma unroll
       for (int i = 0; i < MAXB; ++i) {
         const int b = d + i * ND;
