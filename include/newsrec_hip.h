@@ -214,7 +214,8 @@ int nr_cnn_unpack_grads(const float* dw3t, const float* dwqp, const float* dbqp,
  * projection reaches HBM only through kout.  C [nseq*L][Hp] (ldc % 4 == 0, 16-B aligned, exactly zero past the
  * valid width), wq [Hp][Hp] / bq [Hp] zero-padded (nr_cnn_pack_weights), q [qn]; Hp a multiple of
  * 32 up to 160, L <= 32.  prec: enum nr_gemm_precision of the key products.  news [nseq][Hp]
- * (ldn >= Hp), probs [nseq*L].  kout (optional, [nseq*L][ldk >= Hp], ldk % 4 == 0, 16-B aligned): K
+ * (ldn >= Hp), probs [nseq*L].  kout (optional, [nseq*L][ldk >= Hp], ldk % 4 == 0, 16-B aligned,
+ * L * ldk * 4 < 2^31): K
  * stored for the backward (which then skips the key recompute); NULL keeps the key projection on chip. */
 int nr_cnn_keypool_fwd(const float* C, int64_t ldc, const float* wq, const float* bq, const float* q, int32_t qn,
                        const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L, int32_t Hp, float scale,

@@ -728,7 +728,8 @@ extern "C" int nr_cnn_keypool_fwd(const float* C, int64_t ldc, const float* wq, 
     return NR_EINVAL(0);
   if (!C || !wq || !bq || !q || !mask || !news || !probs) return NR_EINVAL(1);
   if (!al16(C) || !al16(wq)) return NR_EINVAL(2);
-  if (kout && (ldk < Hp || (ldk & 3) || !al16(kout))) return NR_EINVAL(3);
+  // (the buffer-store K output addresses one title's L rows with a 32-bit byte range)
+  if (kout && (ldk < Hp || (ldk & 3) || !al16(kout) || (int64_t)L * ldk * 4 > INT32_MAX)) return NR_EINVAL(3);
   if (nseq == 0) return NR_OK;
   KPArgs g{};
   g.c = C; g.ldc = ldc; g.wq = wq; g.bq = bq; g.q = q; g.qn = qn; g.mask = mask; g.mask_dt = mask_dtype;
