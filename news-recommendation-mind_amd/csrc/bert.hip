@@ -967,6 +967,8 @@ __global__ void __launch_bounds__(256) attn_fwd_mp_kernel(AttnArgs g) {
 
 // dK, dV (attn_bwd_kv_kernel's products): a wave owns 32 keys, split once; per query tile the Q and
 // dctx rows are staged split, row-major (S, dP) and transposed (dV, dK).
+// (Bounded to two waves per SIMD, as attn_bwd_q_mp_kernel is, the bf16x6 form spilled 36 VGPRs and
+// ran slower than that one alone: XFormer step 70.1 vs 69.9 ms, profiles/r04_o_xf_ab.json.)
 template <int NP, bool DROP, bool PF>
 __global__ void __launch_bounds__(256) attn_bwd_kv_mp_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t Qp[NP][32][kKR];
@@ -1090,8 +1092,11 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_mp_kernel(AttnArgs g) {
 
 // dQ (attn_bwd_q_kernel's products): a wave owns 32 queries (Q and dctx split once); per key tile
 // K and V staged split row-major (S, dP) and K transposed (dQ = dS K).
+// Two waves per SIMD: unbounded, the bf16x6 prefetching form took 270 VGPRs -- one wave per SIMD,
+// its softmax / dS arithmetic never overlapping another wave's MFMAs; at <= 256 it fits without
+// spills: XFormer step 71.5 -> 69.9 ms on one box (profiles/r04_o_xf_ab.json).
 template <int NP, bool DROP, bool PF>
-__global__ void __launch_bounds__(256) attn_bwd_q_mp_kernel(AttnArgs g) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) attn_bwd_q_mp_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t Kp[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Vp[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Kt[NP][kHD][kVR];

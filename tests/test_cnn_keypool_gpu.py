@@ -76,7 +76,11 @@ def test_cnn_keypool_matches_float64(prec, tol, nseq, L_, H, with_dz, save_k):
     M = mask.to(dev).reshape(-1)
     news = torch.empty(nseq, Hp, device=dev)
     probs = torch.empty(T, device=dev)
-    kbuf = torch.full((T, Hp + 4), float("nan"), device=dev)[:, :Hp] if save_k else None
+    # K rows live in [T, Hp] of a NaN-filled [T + 32, Hp + 4] block: the forward's stores must stay
+    # inside the title's L rows (a title's slots past L are dropped, not written into the next
+    # title's rows or past the last one) and inside the Hp columns
+    kfull = torch.full((T + 32, Hp + 4), float("nan"), device=dev) if save_k else None
+    kbuf = kfull[:T, :Hp] if save_k else None
     K.cnn_keypool_fwd(Cd, wqp, bqp, qd, M, nseq, L_, news, probs, qn=H, prec=prec, kout=kbuf)
     dc = torch.full((T, Hp), float("nan"), device=dev)
     dwq = torch.full((Hp, Hp), float("nan"), device=dev)
@@ -99,6 +103,7 @@ def test_cnn_keypool_matches_float64(prec, tol, nseq, L_, H, with_dz, save_k):
         close(kbuf[:, :H], k_r, "K")
         if Hp > H:
             assert kbuf[:, H:].abs().max().item() < 1e-6   # tanh(0 + 0) past H
+        assert torch.isnan(kfull[T:]).all() and torch.isnan(kfull[:, Hp:]).all(), "K store outside [T, Hp]"
     close(news[:, :H], news_r, "news")
     assert news[:, H:].abs().sum().item() == 0.0 and news[0].abs().max().item() == 0.0
     close(probs.view(nseq, L_), p_r, "probs")
