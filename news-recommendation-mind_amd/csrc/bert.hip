@@ -855,6 +855,8 @@ __device__ __forceinline__ float key_add(const AttnArgs& g, int64_t row0, int j,
   return j >= L ? -INFINITY : (nr_mask_at(g.mask, g.mdt, row0 + j) ? 0.f : kNegMax);
 }
 
+// (232 VGPRs: two waves per SIMD.  Bounded to three, 13 spilled and the XFormer step did not move,
+// 69.0 vs 69.1 ms, profiles/r04_p_xf_ab.json.)
 template <int NP, bool DROP, bool PF>
 __global__ void __launch_bounds__(256) attn_fwd_mp_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t Kp[NP][32][kKR];
