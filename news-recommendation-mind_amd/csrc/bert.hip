@@ -969,10 +969,11 @@ __global__ void __launch_bounds__(256) attn_fwd_mp_kernel(AttnArgs g) {
 
 // dK, dV (attn_bwd_kv_kernel's products): a wave owns 32 keys, split once; per query tile the Q and
 // dctx rows are staged split, row-major (S, dP) and transposed (dV, dK).
-// (Bounded to two waves per SIMD, as attn_bwd_q_mp_kernel is, the bf16x6 form spilled 36 VGPRs and
-// ran slower than that one alone: XFormer step 70.1 vs 69.9 ms, profiles/r04_o_xf_ab.json.)
+// Two waves per SIMD, as attn_bwd_q_mp_kernel: with the own K / V rows held as split planes (96
+// VGPRs) the bound spilled 36 and ran slower (profiles/r04_o_xf_ab.json); held as fp32 and split per
+// query tile it spills 9 and the XFormer step gains 68.15 -> 67.86 ms (profiles/r04_q_xf_ab.json).
 template <int NP, bool DROP, bool PF>
-__global__ void __launch_bounds__(256) attn_bwd_kv_mp_kernel(AttnArgs g) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) attn_bwd_kv_mp_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t Qp[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Op[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Qt[NP][kHD][kVR];
@@ -993,9 +994,20 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_mp_kernel(AttnArgs g) {
   const bool own = active && key < L;
   const uint32_t dkey = DROP ? attn_key(g, seq, head) : 0u;
 
-  Planes<NP> kp4[4], vp4[4];
-  own_rows<NP>(kp4, g.qkv + (row0 + key) * g.ldq + g.koff + head * kHD + 32 * hh, own, 0.125f);
-  own_rows<NP>(vp4, g.qkv + (row0 + key) * g.ldq + g.voff + head * kHD + 32 * hh, own, 1.f);
+  // the wave's own K / V half-rows kept as fp32 and split per use (planes held for all four steps of
+  // both would take 96 VGPRs)
+  float kf[32], vf[32];
+  {
+    const float* kr = g.qkv + (row0 + key) * g.ldq + g.koff + head * kHD + 32 * hh;
+    const float* vr = g.qkv + (row0 + key) * g.ldq + g.voff + head * kHD + 32 * hh;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 x = own ? ld4(kr + 4 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 y = own ? ld4(vr + 4 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      kf[4 * j] = x.x * 0.125f; kf[4 * j + 1] = x.y * 0.125f; kf[4 * j + 2] = x.z * 0.125f; kf[4 * j + 3] = x.w * 0.125f;
+      vf[4 * j] = y.x; vf[4 * j + 1] = y.y; vf[4 * j + 2] = y.z; vf[4 * j + 3] = y.w;
+    }
+  }
   const float kadd = own ? (nr_mask_at(g.mask, g.mdt, row0 + key) ? 0.f : kNegMax) : -INFINITY;
   f32x16 dk0, dk1, dv0, dv1;
 #pragma unroll
@@ -1047,9 +1059,11 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_mp_kernel(AttnArgs g) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
 #pragma unroll
+    for (int j = 0; j < 32; ++j) asm volatile("" : "+v"(kf[j]), "+v"(vf[j]));   // split per tile, not hoisted
+#pragma unroll
     for (int t = 0; t < 4; ++t) {
-      mfma_x<NP>(s, rowfrag<NP>(Qp, c, hh, t), kp4[t]);
-      mfma_x<NP>(dp, rowfrag<NP>(Op, c, hh, t), vp4[t]);
+      mfma_x<NP>(s, rowfrag<NP>(Qp, c, hh, t), planes8<NP>(kf + 8 * t));
+      mfma_x<NP>(dp, rowfrag<NP>(Op, c, hh, t), planes8<NP>(vf + 8 * t));
     }
     // S rows = queries crow(r, hh) of the tile, column = this lane's key
     float pd[16], ds[16];
