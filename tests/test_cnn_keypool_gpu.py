@@ -53,8 +53,10 @@ def _ref(pre, wq, bq, q, mask, dnews, dz):
 
 
 @pytest.mark.parametrize("prec,tol", [(L.GEMM_F32, 5e-5), (L.GEMM_BF16X6, 5e-5), (L.GEMM_BF16, 3e-2)])
-@pytest.mark.parametrize("nseq,L_,H,with_dz", [(700, 30, 150, False), (37, 32, 150, True), (300, 17, 64, True),
-                                               (5, 30, 20, False)])
+# 1000 titles: more than the forward's resident workgroups (three per CU), so its persistent loop
+# runs several titles per workgroup, as the full-size step does
+@pytest.mark.parametrize("nseq,L_,H,with_dz", [(700, 30, 150, False), (1000, 30, 150, True), (37, 32, 150, True),
+                                               (300, 17, 64, True), (5, 30, 20, False)])
 @pytest.mark.parametrize("save_k", [False, True])
 def test_cnn_keypool_matches_float64(prec, tol, nseq, L_, H, with_dz, save_k):
     """save_k: the forward stores K = tanh(C wqᵀ + bq) (checked here too) and the backward reads it
