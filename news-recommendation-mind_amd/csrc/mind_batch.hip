@@ -30,12 +30,14 @@ __device__ __forceinline__ uint32_t draw_below(uint64_t seed, uint64_t ctr, uint
 // (utils/MIND.py:327), reversed when `reverse` (descend_history, :339-342; the test branch
 // inverts the flag, :433-436), right-padded with news 0; his_mask[:len] = 1, his_mask[0] = 1
 // when the history is empty (:330-337)
+// (threads t0, t0 + nt, ... of the workgroup take part)
 __device__ void history_ids(const int64_t* his_off, const int32_t* his_ids, int64_t imp, int his_size,
-                            bool reverse, int32_t* s_ids, double* his_mask_row) {
+                            bool reverse, int32_t* s_ids, double* his_mask_row, int t0 = 0, int nt = 0) {
+  if (nt == 0) nt = blockDim.x;
   const int64_t h0 = his_off[imp];
   const int64_t full = his_off[imp + 1] - h0;
   const int hl = full < his_size ? (int)full : his_size;
-  for (int j = threadIdx.x; j < his_size; j += blockDim.x) {
+  for (int j = (int)threadIdx.x - t0; j < his_size; j += nt) {
     int32_t id = 0;
     if (j < hl) id = his_ids[h0 + (reverse ? hl - 1 - j : j)];
     s_ids[j] = id;
@@ -99,9 +101,17 @@ __global__ __launch_bounds__(256) void form_train_kernel(TrainArgs a) {
     }
     int64_t idx = a.sample_idx[sb];
     if (idx < 0 || idx >= a.P) { atomicOr(a.status, 1); idx = 0; }
-    const int64_t imp = a.imprs[2 * idx];
-    s_imp = imp;
+    s_imp = a.imprs[2 * idx];
     s_ids[0] = a.imprs[2 * idx + 1];
+  }
+  __syncthreads();
+  // the negative sampling (thread 0's chain of dependent loads and draws) and the history ids (waves
+  // 1..: his_off -> his_ids) run side by side, not one after the other
+  if (threadIdx.x >= 64) {
+    history_ids(a.his_off, a.his_ids, s_imp, NH, (a.flags & NR_BATCH_REVERSE_HISTORY) != 0, s_ids + C,
+                a.his_mask + b * NH, 64, (int)blockDim.x - 64);
+  } else if (threadIdx.x == 0) {
+    const int64_t imp = s_imp;
     const int64_t nb = a.neg_off[imp];
     const int n = (int)(a.neg_off[imp + 1] - nb);
     const int k = a.npratio;
@@ -140,9 +150,6 @@ __global__ __launch_bounds__(256) void form_train_kernel(TrainArgs a) {
     }
     s_label = lab;
   }
-  __syncthreads();
-  history_ids(a.his_off, a.his_ids, s_imp, NH, (a.flags & NR_BATCH_REVERSE_HISTORY) != 0, s_ids + C,
-              a.his_mask + b * NH);
   __syncthreads();
 
   for (int i = threadIdx.x; i < C; i += blockDim.x) {
