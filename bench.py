@@ -262,47 +262,79 @@ def fast_eval_leg(model, dev, world, rank, n_impr):
             "metrics_random_model": res}
 
 
-def xformer_leg(dev, steps=5, warmup=2, b=B):
+def _dp_setup(model, world):
+    """Data parallel (N > 1): rank 0's parameters broadcast (DDP's construction, twotower.py:49-50) and
+    a GradSync for the model (its gradient hooks are process-wide: one live GradSync at a time)."""
+    if world == 1:
+        return None
+    from newsrec_amd.dist import GradSync
+    with torch.no_grad():
+        for p in model.parameters():
+            dist.broadcast(p, 0)
+    return GradSync(model)
+
+
+def _timed(step_fn, steps, world, dev):
+    """Time exactly ``steps`` calls bracketed by a barrier + synchronize on both sides; the max over
+    ranks (seconds per step)."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step_fn(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el / steps
+
+
+def xformer_leg(dev, steps=5, warmup=2, b=B, world=1, rank=0):
     """configs[4] beside the headline: XFormer (bert-base news encoder + 501-token user sequence,
-    12 layers, dropout 0.1, Adam) train steps and eval forwards on synthetic MIND-shaped batches,
-    one GPU; the train step replayed as a HIP graph like the headline (dropout draws advance on the
-    device).  FLOPs are algorithmic (dense layers + attention + pooler, train = 3x fwd)."""
+    12 layers, dropout 0.1, Adam) train steps and eval forwards on synthetic MIND-shaped batches;
+    the train step replayed as HIP graphs like the headline (dropout draws advance on the device).
+    N > 1: every rank trains on its own batch and GradSync forms the DDP gradient mean between the
+    graphs (xformer.py:19-20; the 94 MB word table in place, the other 344 MB of BERT gradients in
+    128 MB buckets); the replicas are checked after the timed steps (dp_check).  FLOPs are
+    algorithmic (dense layers + attention + pooler, train = 3x fwd)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import bench_bert as BB
     from newsrec_amd.manager import get_optim
     model = BB.build("xformer", 12, dev)
+    sync = _dp_setup(model, world)
     opt = get_optim(model, capturable=True)
-    gen = torch.Generator().manual_seed(3)
+    gen = torch.Generator().manual_seed(3 + rank)
     x = {k: v.to(dev) for k, v in BB.synth(gen, b).items()}
     model.train()
-    step = GraphedStep(model, opt, ResidentFeed([x]), None, warmup)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        step(i)
-    torch.cuda.synchronize()
-    el = (time.perf_counter() - t0) / steps
+    step = GraphedStep(model, opt, ResidentFeed([x]), sync, warmup)
+    el = _timed(step, steps, world, dev)
+    chk = dp_check(model, opt, world, dev) if world > 1 else {}
+    if sync is not None:
+        sync.close()
     model.eval()
     with torch.no_grad():
         model(x)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(steps):
-            model(x)
-        torch.cuda.synchronize()
-        ev = (time.perf_counter() - t1) / steps
+        ev = _timed(lambda i: model(x), steps, world, dev)
     f = BB.flops_per_impression("xformer", 12) * b
     del step, model, opt
     torch.cuda.empty_cache()
-    return {"workload": "XFormer train step: bert-base (12 layers, 768, 12 heads) over 5x30-token candidates + "
-                        "501-token user sequence, dropout 0.1, Adam; synthetic batches, random init",
-            "launch": "hipGraph replay of the train step",
-            "per_gpu_batch": b, "impressions_per_s": round(b / el, 1), "ms_per_step": round(el * 1e3, 2),
-            "train_tflops": round(3 * f / el / 1e12, 1), "eval_impressions_per_s": round(b / ev, 1),
-            "eval_tflops": round(f / ev / 1e12, 1),
-            "roofline": {"bound": "mfma", "peak_tflops": round(BF16_MFMA_PEAK_TF / 6, 1),
-                         "peak_basis": "fp32-equivalent bf16x6 (2.5 PF bf16 dense / 6)",
-                         "frac": round(3 * f / el / 1e12 / (BF16_MFMA_PEAK_TF / 6), 4)}}
+    out = {"workload": "XFormer train step: bert-base (12 layers, 768, 12 heads) over 5x30-token candidates + "
+                       "501-token user sequence, dropout 0.1, Adam; synthetic batches, random init",
+           "launch": "hipGraph replay of the train step" + (" (three graphs, RCCL collectives between them)"
+                                                            if world > 1 else ""),
+           "n_gpus": world, "per_gpu_batch": b, "impressions_per_s": round(world * b / el, 1),
+           "ms_per_step": round(el * 1e3, 2), "train_tflops": round(world * 3 * f / el / 1e12, 1),
+           "eval_impressions_per_s": round(world * b / ev, 1), "eval_tflops": round(world * f / ev / 1e12, 1),
+           "roofline": {"bound": "mfma", "peak_tflops": round(BF16_MFMA_PEAK_TF / 6, 1),
+                        "peak_basis": "fp32-equivalent bf16x6 (2.5 PF bf16 dense / 6), per GPU",
+                        "frac": round(3 * f / el / 1e12 / (BF16_MFMA_PEAK_TF / 6), 4)}}
+    out.update(chk)
+    return out
 
 
 # SURVEY.md §8(d): algorithmic train FLOPs per impression (token-wise count, fwd x 3) and the
@@ -332,12 +364,15 @@ def _leg_floor(name, model, ms):
             "gemm_arithmetic": "bf16 (operands rounded to bf16, fp32 accumulate)" if bf16 else "bf16x6 (fp32-class)"}
 
 
-def config_legs(dev, feed, steps=20, warmup=3, only=None):
+def config_legs(dev, feed, steps=20, warmup=3, only=None, world=1):
     """The other two-tower configurations of BASELINE.json beside the headline: configs[1] CNN news +
     additive-attention user (fp32-class and the bf16 configuration), configs[3] LSTUR (CNN news +
     LSTM with user embedding, MIND-large user table) and the GRU variant.  Train steps (batch
-    formation on the device, fwd, NLL, bwd, Adam) of B = 32, H = 150, V = 30522, one GPU, each leg's
-    whole step replayed as a HIP graph like the headline."""
+    formation on the device, fwd, NLL, bwd, Adam) of B = 32 per GPU, H = 150, V = 30522, each leg's
+    whole step replayed as HIP graphs like the headline.  N > 1 (configs[3] is quoted on 8 GPUs):
+    every rank forms its own batches (its DistributedSampler shard), GradSync forms the DDP mean (the
+    LSTUR user table by the exact row-sparse exchange) and the replicas are checked after the timed
+    steps (dp_check)."""
     from newsrec_amd.manager import build_model, get_optim
     out = {}
     for name, encN, encU, prec in (("cnn_attn", "cnn", "attn", None), ("cnn_attn_bf16", "cnn", "attn", "bf16"),
@@ -347,23 +382,23 @@ def config_legs(dev, feed, steps=20, warmup=3, only=None):
         torch.manual_seed(42)
         model = build_model(encN, encU, 150, vocab=V, device=dev, user_num=USERS_LARGE, precision=prec)
         model.train()
+        sync = _dp_setup(model, world)
         opt = get_optim(model, capturable=True)
-        step = GraphedStep(model, opt, feed, None, warmup)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(steps):
-            step(i)
-        torch.cuda.synchronize()
-        el = (time.perf_counter() - t0) / steps
+        step = GraphedStep(model, opt, feed, sync, warmup)
+        el = _timed(step, steps, world, dev)
         ms = el * 1e3
-        out[name] = {"impressions_per_s": round(B / el, 1), "ms_per_step": round(ms, 3),
+        out[name] = {"n_gpus": world, "impressions_per_s": round(world * B / el, 1), "ms_per_step": round(ms, 3),
                      "roofline": _leg_floor(name, model, ms)}
+        if world > 1:
+            out[name].update(dp_check(model, opt, world, dev))
+            sync.close()
         del step, model, opt
         torch.cuda.empty_cache()
-    out["note"] = ("hipGraph replay of the whole train step (device batch formation, fwd, NLL, bwd, Adam), B=32, "
-                   "H=150, V=30522 trainable table, MIND-large user table for LSTUR (876,957 rows); cnn_attn_bf16 = "
+    out["note"] = ("hipGraph replay of the whole train step (device batch formation, fwd, NLL, bwd, Adam), B=32 per "
+                   "GPU, H=150, V=30522 trainable table, MIND-large user table for LSTUR (876,957 rows); cnn_attn_bf16 = "
                    "configs[1]'s bf16 configuration (GEMM operands rounded to bf16, fp32 accumulation, fp32 master "
-                   "weights); lstur = the reference's LSTUR_User_Encoder (LSTM, RNN.py:76-104)")
+                   "weights); lstur = the reference's LSTUR_User_Encoder (LSTM, RNN.py:76-104); impressions_per_s is "
+                   "the whole job's over n_gpus ranks, the roofline per GPU")
     return out
 
 
@@ -463,9 +498,11 @@ def main():
                     help="device: form each batch on the GPU from a resident MIND split; resident: pre-formed")
     ap.add_argument("--eval-impr", type=int, default=DEV_IMPR_LARGE,
                     help="dev impressions of the fast-eval leg (0 skips it)")
-    ap.add_argument("--config-legs", type=int, default=1, help="1: time configs[1]/[3] beside the headline (N=1)")
+    ap.add_argument("--config-legs", type=int, default=1, help="1: time configs[1]/[3] beside the headline")
+    ap.add_argument("--legs", default="", help="comma list of config legs to run (default: all of "
+                                               "cnn_attn, cnn_attn_bf16, cnn_lstur, cnn_gru)")
     ap.add_argument("--xformer-steps", type=int, default=5,
-                    help="timed XFormer (configs[4]) train steps reported beside the headline (0 skips; N=1 only)")
+                    help="timed XFormer (configs[4]) train steps reported beside the headline (0 skips)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the train step as HIP graphs (auto = on; N > 1: forward/backward and "
                          "optimizer graphs with the RCCL collectives between them)")
@@ -583,10 +620,14 @@ def main():
         torch.cuda.synchronize()
         el_eval = time.perf_counter() - t1
     del evb
+    if sync is not None:
+        sync.close()   # the legs below install their own GradSync (the hooks are process-wide)
     # eval (b): the fast-eval pipeline over a MIND-large-shaped dev split
     fast = fast_eval_leg(model, dev, world, rank, a.eval_impr) if a.eval_impr > 0 else None
-    xf = xformer_leg(dev, a.xformer_steps) if (a.xformer_steps > 0 and world == 1) else None
-    legs = config_legs(dev, feed) if (a.config_legs and world == 1 and a.data == "device") else None
+    # configs[4] (XFormer) and configs[1]/[3] at every N: the 8-GPU configurations are measured on N ranks
+    xf = xformer_leg(dev, a.xformer_steps, world=world, rank=rank) if a.xformer_steps > 0 else None
+    only = [n for n in a.legs.split(",") if n] or None
+    legs = config_legs(dev, feed, world=world, only=only) if (a.config_legs and a.data == "device") else None
     gather = gather_probe(dev) if world == 1 else None
 
     if rank == 0:
@@ -674,7 +715,10 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    if in_sync is not None and not in_sync["dp_in_sync"]:
+    diverged = [k for k, v in [("headline", in_sync), ("xformer", xf)] + list((legs or {}).items())
+                if isinstance(v, dict) and v.get("dp_in_sync") is False]
+    if diverged:
+        print("bench.py: replicas diverged in %s" % ", ".join(diverged), file=sys.stderr)
         sys.exit(3)
 
 

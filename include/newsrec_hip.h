@@ -468,6 +468,15 @@ int nr_embedding_fwd(const float* table, int64_t V, int64_t E, const int64_t* id
 int nr_embedding_bwd(const float* dout, int64_t V, int64_t E, const int64_t* idx, int64_t n,
                      int64_t padding_idx, float* dtable, hipStream_t stream);
 
+/* dtable[idx[i]] += dout[i] (rows of E floats, leading dimensions ldo / ldt) for idx[i] != padding_idx,
+ * the rows of each id summed in ascending i by one wave and added once: deterministic with duplicate
+ * ids (no atomics).  For row-sparse gradients of few rows (n <= 2^20; O(n^2) id reads): LSTUR's user
+ * table (embedding_dense_backward of userEmbedding, models/Encoders/RNN.py:100-104) on one process and
+ * in the data-parallel row-sparse exchange (the DDP mean of twotower.py:49-50), so every rank forms
+ * the same bits. */
+int nr_rows_add_ordered(const float* dout, int64_t ldo, int64_t V, int64_t E, const int64_t* idx, int64_t n,
+                        int64_t padding_idx, float* dtable, int64_t ldt, hipStream_t stream);
+
 /* out[c] += Σ_r x[r][c]  (bias gradients; out pre-zeroed or accumulated).  Deterministic two-pass
  * reduction (no atomics) through `work` of nr_colsum_workspace(rows, cols) bytes. */
 int64_t nr_colsum_workspace(int64_t rows, int64_t cols);

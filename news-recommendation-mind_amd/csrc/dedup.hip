@@ -24,10 +24,7 @@
 namespace {
 
 constexpr int SEG_RANGE = 64;   // CSR positions per segment-sum workgroup
-#ifndef NR_SEG_BATCH   // A/B builds only (tools/build_variant.sh)
-#define NR_SEG_BATCH 8
-#endif
-constexpr int SEG_BATCH = NR_SEG_BATCH;   // row loads in flight per thread (16 measured equal: 1.4273 vs 1.4259 ms per NRMS step)
+constexpr int SEG_BATCH = 8;   // row loads in flight per thread (16 measured equal: 1.4273 vs 1.4259 ms per NRMS step)
 constexpr int CNT_THREADS = 1024;
 constexpr int HASH_SLOTS = 2048;
 

@@ -133,10 +133,11 @@ struct BigMN {
     if (ACT < 512 && tid >= ACT) return;
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-      cs[j][0] += f * (v[S][j][0].x + v[S][j][1].x);
-      cs[j][1] += f * (v[S][j][0].y + v[S][j][1].y);
-      cs[j][2] += f * (v[S][j][0].z + v[S][j][1].z);
-      cs[j][3] += f * (v[S][j][0].w + v[S][j][1].w);
+      // a select, not a multiply by f: a weighted-out tile (f = 0) holding an Inf must not add NaN
+      cs[j][0] += f != 0.f ? v[S][j][0].x + v[S][j][1].x : 0.f;
+      cs[j][1] += f != 0.f ? v[S][j][0].y + v[S][j][1].y : 0.f;
+      cs[j][2] += f != 0.f ? v[S][j][0].z + v[S][j][1].z : 0.f;
+      cs[j][3] += f != 0.f ? v[S][j][0].w + v[S][j][1].w : 0.f;
     }
   }
   // the per-thread sums of the KP threads of one column group (adjacent lanes) combined; the
@@ -444,12 +445,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
       // projection fwd 258 -> 248, NRMS weight gradient 292 -> 273, BERT FFN-out 383 -> 376; off for
       // the dgrad pair (K-contiguous A x MN-contiguous B: table dgrad 258 -> 269) and the plain weight
       // gradient (MN x MN: BERT FFN weight gradient 416 -> 447 us, profiles/r04_f_gemm_ab.json)
-#ifdef NR_BIG_NO_ILV
-      constexpr bool ILV = false;
-#else
       constexpr bool ILV = LIVE && NP == 3 && KS == 1 && TJ == 2 && LA::PIECES == 2 && LB::PIECES == 2 &&
                            ((is_kc(AM) && is_kc(BMODE)) || (AM == MN_PLAIN && BMODE == MN_GATHER));
-#endif
       const uint16_t* a_s = As + st * NP * PA;
       const uint16_t* b_s = Bs + st * NP * PB;
       // after MFMA m (of 12) of row block i: A pieces behind row block ia's MFMAs 2 and 5 (j = 0),
@@ -535,36 +532,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
         }
       }
       }
-#ifdef NR_BIG_SGB
-      if constexpr (LIVE && NP == 3 && KS == 1 && TI == 4 && TJ == 2) {
-        // A/B experiment: pin the interleave of the tile's 48 MFMAs with the next row block's fragment
-        // reads, the two operand splits (VALU + LDS writes) and the loads (masks: MFMA 0x8, VALU 0x2,
-        // DS read 0x100, DS write 0x200, VMEM read 0x20)
-        __builtin_amdgcn_sched_group_barrier(0x100, 9, 0);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-#pragma unroll
-          for (int u = 0; u < 3; ++u) {
-            __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x2, 2, 0);
-          }
-#pragma unroll
-          for (int u = 0; u < 9; ++u) {
-            __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x2, 5, 0);
-            if (u % 2 == 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-          }
-          if (q == 1) __builtin_amdgcn_sched_group_barrier(0x20, 4, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x8, 21, 0);
-      }
-#endif
       __syncthreads();   // stage st fully read; stage st^1 fully written
     };
     // unrolled by two: the register sets alternate statically; a wave with no live rows / columns

@@ -40,9 +40,6 @@ double round_eff(int64_t units, int64_t slots) {
 
 int big_bn(int64_t M, int64_t N, int64_t K, int splits, bool resplit, bool m_dyn, int kmin) {
   if (N < 128) return 0;
-#ifdef NR_AB_BIG_BN   // A/B builds only (tools/build_variant.sh): force the big kernel's tile width
-  if (K >= kmin || resplit) return NR_AB_BIG_BN;
-#endif
   // a short contraction (K < kmin) does not amortise the per-unit pipeline fill
   if (!resplit && K < kmin) return 0;
   const int64_t gm = (M + 255) / 256;
@@ -191,11 +188,7 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
     // bf16 split-K (atomic) launches take the big kernel too: its fewer, larger units halve the operand
     // re-reads and keep three k-tiles of loads in flight (CNN conv weight gradient 200 -> 138 us)
     const int bb = big_bn(M, N, K, splits, resplit, m_dev != nullptr, kmin);
-#ifdef NR_AB_BIG_BN
-    const int BN = bb > 0 ? bb : (tailed ? 256 : 0);
-#else
     const int BN = tailed ? 256 : (bb > 0 ? bb : 0);
-#endif
     if (BN) {
       Args gb = g;
       if (tailed) gb.tail = 16;

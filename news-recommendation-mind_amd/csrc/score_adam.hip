@@ -392,6 +392,40 @@ __global__ __launch_bounds__(256) void embedding_bwd_kernel(const float* dout, i
   for (int64_t c = lane; c < E; c += 64) atomicAdd(&dtable[t * E + c], dout[row * E + c]);
 }
 
+// Row-sparse gradient rows added in a FIXED order (nr_rows_add_ordered): the wave of an id's first
+// occurrence sums every row j >= i of that id in ascending j and adds the sum to its table row; the
+// waves of later occurrences do nothing.  No atomics, so duplicate ids (LSTUR's dropped user ids all
+// land on row 0, RNN.py:100-101) give the same bits on every run and every rank.  A wave scans the
+// ids in chunks of 64 (one ballot per chunk): O(n^2 / 64) id reads, for the few rows a row-sparse
+// table receives per step (B per rank, B x world in the data-parallel exchange).
+__global__ __launch_bounds__(256) void rows_add_ordered_kernel(const float* __restrict__ dout, int64_t ldo,
+                                                               int64_t V, int64_t E, const int64_t* __restrict__ idx,
+                                                               int64_t n, int64_t pad, float* __restrict__ dtable,
+                                                               int64_t ldt) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  const int64_t t = idx[i];
+  if (t == pad || t < 0 || t >= V) return;   // out-of-range ids are dropped, never written
+  for (int64_t j0 = 0; j0 < i; j0 += 64) {   // an earlier occurrence owns the row
+    const int64_t j = j0 + lane;
+    if (__ballot(j < i && idx[j] == t) != 0ull) return;
+  }
+  for (int64_t c = lane; c < E; c += 64) {
+    float s = 0.f;
+    for (int64_t j0 = i; j0 < n; j0 += 64) {
+      const int64_t j = j0 + lane;
+      unsigned long long m = __ballot(j < n && idx[j] == t);
+      while (m) {   // ascending j: the fixed summation order
+        const int b = __builtin_ctzll(m);
+        m &= m - 1;
+        s += dout[(j0 + b) * ldo + c];
+      }
+    }
+    dtable[t * ldt + c] += s;
+  }
+}
+
 // Column sums, deterministic two-pass: pass 1 = one block per (64-column chunk, row block), each of
 // its 4 waves strides the block's rows with its 64 lanes on 64 consecutive columns (256-B row
 // segments, 8 loads in flight), the waves combine in LDS and store the block's partial row; pass 2
@@ -588,6 +622,17 @@ extern "C" int nr_embedding_bwd(const float* dout, int64_t V, int64_t E, const i
   if (n == 0) return NR_OK;
   hipLaunchKernelGGL(embedding_bwd_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, stream, dout, E, idx,
                      n, padding_idx, dtable);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_rows_add_ordered(const float* dout, int64_t ldo, int64_t V, int64_t E, const int64_t* idx, int64_t n,
+                                   int64_t padding_idx, float* dtable, int64_t ldt, hipStream_t stream) {
+  if (V < 1 || E < 1 || n < 0 || n > (1 << 20) || ldo < E || ldt < E) return NR_EINVAL(0);
+  if (!dout || !idx || !dtable) return NR_EINVAL(1);
+  if (n == 0) return NR_OK;
+  hipLaunchKernelGGL(rows_add_ordered_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, stream, dout, ldo, V, E,
+                     idx, n, padding_idx, dtable, ldt);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

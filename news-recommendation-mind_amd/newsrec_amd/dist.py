@@ -16,6 +16,7 @@ import torch
 import torch.distributed as dist
 
 from . import functions
+from . import kernels as K
 
 
 def setup(rank, world_size, backend="nccl", master_port="12355"):
@@ -145,8 +146,11 @@ class GradSync:
     """
 
     def __init__(self, model, group=None, overlap_tables=True, sparse_tables=True, bucket_mb=128, inplace_mb=16,
-                 deferred=False, collective_cus=16):
+                 deferred=False, collective_cus=16, rows_add=None):
         self.model = model
+        # the ordered row-sparse sum (nr_rows_add_ordered); host-only tests of this plumbing on CPU
+        # tensors inject their own
+        self.rows_add = rows_add if rows_add is not None else K.rows_add_ordered
         self.group = group
         self.world = dist.get_world_size(group)
         self.pending = []
@@ -258,8 +262,10 @@ class GradSync:
             raise RuntimeError("GradSync: %s.grad is still the row-sparse exchange buffer; call "
                                "optimizer.zero_grad(set_to_none=True) before backward" % type(table).__name__)
         g = self._sparse_buffer(table)
-        for r in range(self.world):      # rank order: every rank forms the same sum
-            g.index_add_(0, ids[r], gs[r])
+        # every rank adds the same [world * n] rows in the same fixed order (rank-major, each id's rows
+        # summed in ascending position by one wave, no atomics): the replicas stay bitwise identical
+        # although LSTUR's dropped ids put about half of every rank's rows on row 0 (RNN.py:100-101)
+        self.rows_add(gs.view(-1, gs.shape[-1]), ids.view(-1), g)
         self._touched[id(table)] = ids.reshape(-1).clone()   # the gather buffer is reused next step
         return g
 

@@ -120,9 +120,15 @@ class _ZeroArena:
 ZERO_ARENA = _ZeroArena()
 
 
+def _backward_possible(ctx):
+    """A backward can follow this forward: autograd is recording (not torch.no_grad(), where
+    needs_input_grad still reports the parameters' requires_grad) and some input wants a gradient."""
+    return torch.is_grad_enabled() and any(ctx.needs_input_grad)
+
+
 def _reserve_zeros(ctx, dev, *shapes):
     """Forward side of ZERO_ARENA: reserve the backward's zero-initialised gradients (when one can run)."""
-    ctx.zero_tok = ZERO_ARENA.reserve(dev, *shapes) if any(ctx.needs_input_grad) else None
+    ctx.zero_tok = ZERO_ARENA.reserve(dev, *shapes) if _backward_possible(ctx) else None
 
 
 def _backward_zeros(ctx, dev, *shapes):
@@ -407,7 +413,8 @@ class _LocalRowGrad:
         if prev is not None:
             buf.index_fill_(0, prev, 0.0)
             flags.index_fill_(0, prev, 0)
-        K.embedding_bwd(grads, rows, buf, padding_idx=None)
+        # fixed summation order for duplicate ids (no atomics): the same bits every run
+        K.rows_add_ordered(grads.reshape(rows.numel(), -1), rows.reshape(-1), buf)
         flags.index_fill_(0, rows.reshape(-1), 1)
         if prev is not None and prev.numel() == rows.numel():
             prev.copy_(rows.reshape(-1))      # in place: a captured step replays the same buffer
@@ -499,7 +506,7 @@ class MHANewsFn(torch.autograd.Function):
         if fused:
             # attention + LN + dropout + pooling in one kernel per title; when a backward will
             # run, the attention output O is saved too (the backward then skips recomputing it)
-            O = _empty(T, H, table) if SPLIT_BWD and any(ctx.needs_input_grad) else None
+            O = _empty(T, H, table) if SPLIT_BWD and _backward_possible(ctx) else None
             # rng (device (seed, offset) snapshot) supersedes the host pair: kernel offset 0
             K.mha_pool_fwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, news, stats, probs,
                            p_drop=p_drop, seed=seed, offset=0 if rng is not None else offset, zout=tok,
@@ -558,7 +565,7 @@ class MHANewsFn(torch.autograd.Function):
                 # distinct rows (M = U, not U_pad: no duplicate pad ids): plain row stores
                 wt = w_cat.t().contiguous() if PROJ_DGRAD_KC else None   # kept alive by the closure
 
-                def dgrad():
+                def dgrad(dtable=dtable):   # bound now: the hook below may take the name's buffer
                     w_b = K.operand(wt, L.KCONTIG) if wt is not None else K.operand(w_cat, L.MNCONTIG)
                     K.gemm_dyn(ur.cap, E, NY, K.operand(dYu, L.KCONTIG), w_b, dtable,
                                m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_ZEROED,
@@ -738,7 +745,7 @@ class CNNNewsRowsFn(torch.autograd.Function):
         if fused:
             # key projection + tanh + pooling per title; with a backward to come K is kept (the backward
             # reads it instead of recomputing the key products, KEYPOOL_SAVE_K)
-            Kq = _empty(T, Hp, table) if KEYPOOL_SAVE_K and any(ctx.needs_input_grad) else None
+            Kq = _empty(T, Hp, table) if KEYPOOL_SAVE_K and _backward_possible(ctx) else None
             K.cnn_keypool_fwd(C, wq, bq, query, mask, n, seq_len, news, probs, qn=H, prec=ctx.prec, kout=Kq)
         else:
             Kq = _empty(T, Hp, table)

@@ -713,6 +713,20 @@ def embedding_bwd(dout, idx, dtable, padding_idx=-1):
            -1 if padding_idx is None else padding_idx, L.ptr(dtable), L.stream_ptr(dtable))
 
 
+def rows_add_ordered(dout, idx, dtable, padding_idx=None):
+    """dtable[idx[i]] += dout[i], each id's rows summed in ascending i by one wave (nr_rows_add_ordered:
+    deterministic with duplicate ids, for row-sparse gradients of few rows).  dout [n, E] and dtable
+    [V, E] row-major (any leading dimension), idx int64 [n]."""
+    _f32(dout, dtable)
+    _check_rows(idx, None, "idx")
+    n = idx.numel()
+    V, E = dtable.shape
+    if dout.dim() != 2 or dout.shape != (n, E) or dout.stride(1) != 1 or dtable.stride(1) != 1:
+        raise L.HipError("rows_add_ordered: dout [n, E] and dtable [V, E] must be row-major")
+    L.call("nr_rows_add_ordered", L.ptr(dout), dout.stride(0), V, E, L.ptr(idx), n,
+           -1 if padding_idx is None else padding_idx, L.ptr(dtable), dtable.stride(0), L.stream_ptr(dtable))
+
+
 def colsum(x, rows, cols, out):
     _f32(x, out)
     _rows_ok(x, rows, cols, "x")

@@ -64,12 +64,18 @@ def get_optim(model, lr=1e-4, bert_lr=6e-6, capturable=False):
     return FusedAdam([{"params": base, "lr": lr}, {"params": bert, "lr": bert_lr}], capturable=capturable)
 
 
-def train_step(model, optimizer, x, grad_sync=None):
+def train_step(model, optimizer, x, grad_sync=None, check_labels=True):
     """Manager._train :636-647 (zero_grad(set_to_none), forward, NLLLoss, backward, step);
-    ``grad_sync`` averages gradients over data-parallel ranks before the step."""
+    ``grad_sync`` averages gradients over data-parallel ranks before the step.  ``check_labels``: raise,
+    as torch's NLLLoss does, when the fused head saw a label outside [0, C) (its sticky status word;
+    reading it synchronises, as the reference's per-step ``float(loss)`` at Manager.py:642 does)."""
     optimizer.zero_grad(set_to_none=True)
     if hasattr(model, "forward_loss") and model.training:
         loss = model.forward_loss(x)[1]   # NLLLoss fused into the head (same numbers)
+        if check_labels:
+            from . import kernels as K
+            if K.score_nll_status(loss.device):
+                raise IndexError("NLLLoss: a label is outside [0, C) and not the ignored -100")
     else:
         logits = model(x)[0]
         loss = torch.nn.functional.nll_loss(logits, x["label"].to(logits.device))

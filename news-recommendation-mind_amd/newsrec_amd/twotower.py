@@ -15,7 +15,7 @@ from torch import nn
 from . import _lib as L
 from . import kernels as K
 from .attention import _joined_view
-from .functions import ScoreFn, ScoreNLLFn, SplitRowsFn
+from .functions import GRAD_DEST, ScoreFn, ScoreNLLFn, SplitRowsFn
 
 
 class TwoTowerBaseModel(nn.Module):
@@ -72,10 +72,13 @@ class TwoTowerBaseModel(nn.Module):
 
     def forward(self, x):
         """TwoTowerBaseModel.py:65-75: (log_softmax logits when training, sigmoid otherwise, kid)."""
-        with self.arithmetic():
-            cdd_repr, user_repr, kid = self._encode_both(x)
-            mode = L.SCORE_LOG_SOFTMAX if self.training else L.SCORE_SIGMOID
-            return self.compute_score(cdd_repr, user_repr, mode), kid
+        try:
+            with self.arithmetic():
+                cdd_repr, user_repr, kid = self._encode_both(x)
+                mode = L.SCORE_LOG_SOFTMAX if self.training else L.SCORE_SIGMOID
+                return self.compute_score(cdd_repr, user_repr, mode), kid
+        finally:
+            GRAD_DEST.clear()   # the split's gradient offers are good for this forward only
 
     def forward_loss(self, x):
         """Training forward with the loss of Manager._train (utils/Manager.py:641, NLLLoss on
@@ -83,16 +86,19 @@ class TwoTowerBaseModel(nn.Module):
         as ``nll_loss(self(x)[0], x["label"])``, one kernel each way instead of three and two."""
         if not self.training:
             raise RuntimeError("forward_loss is the training head (log-softmax logits)")
-        with self.arithmetic():
-            cdd_repr, user_repr, _ = self._encode_both(x)
-            B, C, H = cdd_repr.shape
-            cdd = cdd_repr.reshape(B * C, H)
-            user = user_repr.reshape(B, H)
-            if cdd.stride(-1) != 1:
-                cdd = cdd.contiguous()
-            if user.stride(-1) != 1:
-                user = user.contiguous()
-            return ScoreNLLFn.apply(cdd, user, B, C, x["label"])
+        try:
+            with self.arithmetic():
+                cdd_repr, user_repr, _ = self._encode_both(x)
+                B, C, H = cdd_repr.shape
+                cdd = cdd_repr.reshape(B * C, H)
+                user = user_repr.reshape(B, H)
+                if cdd.stride(-1) != 1:
+                    cdd = cdd.contiguous()
+                if user.stride(-1) != 1:
+                    user = user.contiguous()
+                return ScoreNLLFn.apply(cdd, user, B, C, x["label"])
+        finally:
+            GRAD_DEST.clear()   # an offer no consumer took must not outlive this forward
 
     def _encode_both(self, x):
         cdd_repr = self.encode_news(x)

@@ -66,13 +66,28 @@ def _grads(model, x, use_hook):
     (out ** 2).sum().backward()
 
 
+def _rows_add_cpu(dout, idx, dtable):
+    """nr_rows_add_ordered restated for CPU tensors (this host-only test cannot launch it): each id's
+    rows summed in ascending position, the sum added once."""
+    seen = set()
+    for i, t in enumerate(idx.tolist()):
+        if t in seen:
+            continue
+        seen.add(t)
+        rows = [j for j in range(i, idx.numel()) if int(idx[j]) == t]
+        s = dout[rows[0]].clone()
+        for j in rows[1:]:
+            s += dout[j]
+        dtable[t] += s
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     D.setup(rank, world, backend="gloo", master_port=str(port))
     model = Tiny()
     x = torch.tensor([rank, rank + 3, 7])
-    sync = D.GradSync(model, bucket_mb=1e-4)   # tiny buckets: several collectives
+    sync = D.GradSync(model, bucket_mb=1e-4, rows_add=_rows_add_cpu)   # tiny buckets: several collectives
     _grads(model, x, use_hook=True)
     scale = sync()
     sync.close()

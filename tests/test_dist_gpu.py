@@ -20,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
-CASES = {"nrms": ("mha", "mha", 384), "lstur": ("cnn", "lstur", 150)}
+CASES = {"nrms": ("mha", "mha", 384), "lstur": ("cnn", "lstur", 150), "xformer": ("bert", "xformer", 768)}
 V, USERS, BT, C, NH, L = 2000, 40, 8, 5, 10, 30
 
 
@@ -36,6 +36,18 @@ def _model(case, dev):
     from newsrec_amd.manager import build_model
     encN, encU, H = CASES[case]
     torch.manual_seed(11)
+    if case == "xformer":
+        # configs[4] (xformer.py:17-20): BERT-base width, 2 layers, the word table trained at bert_lr
+        from newsrec_amd.bert import BertConfig
+        from newsrec_amd.manager import ManagerConfig
+        from newsrec_amd.xformer import XFormer
+        bc = BertConfig(vocab_size=V, num_hidden_layers=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+        m = XFormer(ManagerConfig("bert", "xformer", H, bert_dim=H), bert_config=bc).to(dev)
+        with torch.no_grad():   # spread the scores (BERT's 0.02 init gives near-equal logits)
+            for n, p in m.named_parameters():
+                if p.dim() == 2 and "embeddings" not in n:
+                    p.normal_(0, 1.5 / p.shape[1] ** 0.5)
+        return m
     m = build_model(encN, encU, H, vocab=V, device=dev, user_num=USERS, dropout_p=0.0)
     with torch.no_grad():
         m.embedding.bert_word_embedding.weight.normal_(0, 0.5)
@@ -145,17 +157,20 @@ def test_data_parallel_real_model_world2(case, mode):
             assert n_off <= max(4, 1e-3 * n_all), (rank, n, n_off, n_all)
 
 
-@pytest.mark.timeout(400)
+@pytest.mark.timeout(600)
 def test_bench_gpus2_spawns_two_ranks():
     """`bench.py --gpus 2` (no WORLD_SIZE) must launch two ranks itself (twotower.py:62-73) and
-    report the live world size; gloo on the one leased GPU stands in for RCCL here."""
+    report the live world size, with the 8-GPU configurations of BASELINE.json measured on those
+    ranks too: configs[3] LSTUR (the row-sparse user-table exchange) and configs[4] XFormer, each
+    with its replicas bitwise identical after the timed steps; gloo on the one leased GPU stands in
+    for RCCL here."""
     import json
     import subprocess
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     env["NR_DIST_BACKEND"] = "gloo"
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
-           "--eval-impr", "0", "--config-legs", "0", "--xformer-steps", "0", "--no-cpu-baseline"]
-    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=380)
+           "--eval-impr", "0", "--legs", "cnn_lstur", "--xformer-steps", "2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=580)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-4000:]
@@ -164,3 +179,8 @@ def test_bench_gpus2_spawns_two_ranks():
     assert out["config"]["parallelism"] == "dp2"
     assert out["config"]["global_batch"] == 64
     assert out["value"] > 0
+    assert out["dp_bitwise_equal"] is True and out["dp_world_size"] == 2
+    for leg in (out["other_configs"]["cnn_lstur"], out["xformer"]):
+        assert leg["n_gpus"] == 2 and leg["impressions_per_s"] > 0, leg
+        assert leg["dp_world_size"] == 2 and leg["dp_in_sync"] is True, leg
+        assert leg["dp_bitwise_equal"] is True, leg

@@ -142,3 +142,38 @@ def test_score_nll_label_semantics():
     assert K.score_nll_status("cuda")            # seen, and cleared by the read
     assert not K.score_nll_status("cuda")
     assert K.self_cleaning_check("cuda") == []
+
+
+def test_rows_add_ordered_duplicates_fixed_order():
+    """nr_rows_add_ordered (the row-sparse sums of LSTUR's user table, on one process and in GradSync's
+    data-parallel exchange): every id's rows summed in ascending position and added once -- equal to the
+    float64 sum to fp32 rounding, BITWISE equal to a sequential fp32 sum in that order, and the same
+    bits on every run (torch's index_add_ resolves duplicates with atomics).  Half the ids are row 0
+    (LSTUR's dropped user ids, RNN.py:100-101), one id repeats across the 'ranks', the padding id is
+    skipped, and a leading dimension wider than E is honoured."""
+    from newsrec_amd import kernels as K
+    torch.manual_seed(3)
+    V, E, n = 4000, 150, 256            # 8 ranks x 32 rows
+    idx = torch.randint(1, V, (n,), device="cuda")
+    idx[::2] = 0
+    idx[5] = idx[200] = idx[77] = 1234
+    idx[9] = 17                         # the padding id below
+    src = torch.randn(n, E + 6, device="cuda")[:, :E]
+    base = torch.randn(V, E + 2, device="cuda")[:, :E]
+    outs = []
+    for _ in range(3):
+        dt = base.clone()
+        K.rows_add_ordered(src, idx, dt, padding_idx=17)
+        outs.append(dt)
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+    keep = idx != 17
+    want = base.double().index_add(0, idx[keep], src[keep].double())
+    torch.testing.assert_close(outs[0].double(), want, rtol=0, atol=1e-5)
+    # bitwise: row 0 and row 1234 as fp32 sums in ascending position, added to the base row once
+    for t in (0, 1234):
+        pos = [j for j in range(n) if int(idx[j]) == t]
+        s = src[pos[0]].clone()
+        for j in pos[1:]:
+            s = s + src[j]
+        assert torch.equal(outs[0][t], base[t] + s), t
+    assert torch.equal(outs[0][17], base[17])

@@ -1,13 +1,12 @@
-# Round 4, pass g: the -m gpu suite, the default bench line, kernel traces (NRMS graphed steps, CNN
-# legs) and the NRMS PMC passes on HEAD (branch-free MN loaders, bf16-MFMA BERT attention).
+# Full validation of HEAD: the whole -m gpu suite, the default bench line, the
+# NRMS graphed-step trace, the XFormer and CNN-leg traces.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/${1:-r4g}
+O=gpurun_out/${1:-val}
 mkdir -p $O
 echo tests; timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 500 --timeout-method thread > $O/tests.log 2>&1; rc=$?; echo "tests rc=$rc"; [ $rc -le 1 ] || exit 1
 echo bench; timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 3
 B="python bench.py --steps 20 --warmup 3 --eval-impr 0 --config-legs 0 --xformer-steps 0 --no-cpu-baseline"
 echo trace; timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- $B > $O/kt.log 2>&1 || exit 4
+echo xf; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_xf -o run -- python tools/legs_only.py xformer --steps 3 > $O/kt_xf.log 2>&1 || exit 6
 echo legs; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_legs -o run -- python tools/legs_only.py cnn_attn cnn_attn_bf16 cnn_lstur cnn_gru --steps 5 > $O/kt_legs.log 2>&1 || exit 5
-B3="python bench.py --steps 3 --warmup 2 --eval-impr 0 --config-legs 0 --xformer-steps 0 --no-cpu-baseline"
-echo pmc; bash tools/pmc_passes.sh $O/pmc $B3 || exit 7
 echo done
