@@ -411,7 +411,8 @@ __global__ __launch_bounds__(256) void rows_add_ordered_kernel(const float* __re
     const int64_t j = j0 + lane;
     if (__ballot(j < i && idx[j] == t) != 0ull) return;
   }
-  for (int64_t c = lane; c < E; c += 64) {
+  for (int64_t c0 = 0; c0 < E; c0 += 64) {   // wave-uniform trip counts: every lane takes part in each ballot
+    const int64_t c = c0 + lane;
     float s = 0.f;
     for (int64_t j0 = i; j0 < n; j0 += 64) {
       const int64_t j = j0 + lane;
@@ -419,10 +420,10 @@ __global__ __launch_bounds__(256) void rows_add_ordered_kernel(const float* __re
       while (m) {   // ascending j: the fixed summation order
         const int b = __builtin_ctzll(m);
         m &= m - 1;
-        s += dout[(j0 + b) * ldo + c];
+        if (c < E) s += dout[(j0 + b) * ldo + c];
       }
     }
-    dtable[t * ldt + c] += s;
+    if (c < E) dtable[t * ldt + c] += s;
   }
 }
 

@@ -149,6 +149,12 @@ def test_data_parallel_real_model_world2(case, mode):
     for rank, err, diffs in res:
         assert err is None, err
         for n, (dmax, n_off, n_all) in diffs.items():
+            if n.endswith("attention.self.key.bias"):
+                # BERT's key bias adds q . b_k to every score of a query: softmax cancels it, so its
+                # gradient is zero in exact arithmetic and rounding noise here -- Adam's lr * g / |g|
+                # turns that noise into +-lr moves on both sides; only the common bound applies
+                assert dmax <= 4 * 2 * 6e-6 + 1e-7, (rank, n, dmax)
+                continue
             # 4 Adam steps from identical state.  Adam moves each element by ~lr * g / |g|, so an
             # element whose gradient sits at the rounding level (the two ranks' half-batch means vs
             # one whole-batch mean) may differ by up to 2 lr per step; every other element agrees to

@@ -17,8 +17,10 @@ goldens by tests/test_oracle_golden.py):
 * configs[1] in its bf16 configuration (the bench's ``cnn_attn_bf16`` leg: every GEMM on bf16
   operands with fp32 accumulation — the bf16 big-kernel conv weight gradient through the split-K
   workspace, the bf16 table dgrad over k-contiguous conv weights, the bf16 key-pool kernels) against
-  the same fp32 oracle at DESIGN.md §7's bf16 bar: logits within 2e-2, every gradient within 5e-2 in
-  relative Frobenius norm and 2e-1 of its max magnitude elementwise (see BF16_GRAD_RTOL).
+  a bf16-EMULATING oracle (R.train_step(gemm="bf16"): the same operands rounded to bf16 at the same
+  points) at bars 20x tighter than the fp32 ones, and against the fp32 oracle at DESIGN.md §7's bf16
+  bar (logits within 2e-2, every gradient within 5e-2 in relative Frobenius norm and 1e-1 of its max
+  magnitude elementwise but for a 1e-4 fraction of ReLU-gate-flip outliers; see BF16_GRAD_RTOL).
 
 Bars as for NRMS (tests/test_fullsize_gpu.py): logits within the north star's 1e-3, every
 gradient within 1e-3 of its max magnitude, every parameter after one Adam step within 2 lr (all
@@ -42,13 +44,19 @@ B, C, NH, L, V, H, USERS = 32, 5, 50, 30, 30522, 150, 876956
 LEGS = {"cnn_attn": "attn", "cnn_lstur": "lstur", "cnn_gru": "gru"}
 
 
-# bf16 bar (tests/test_cnn_rows_gpu.py): logits 2e-2 absolute, every gradient 5e-2 of its
-# norm (relative Frobenius).  Elementwise, against the fp32 oracle at full size: 2e-1 of each gradient's
-# max magnitude (the golden's 1e-1 elsewhere) -- measured 0.131 for the conv weight on the ragged
-# host-fed batch (0.043 in relative norm): a bf16-rounded conv sum that lands on the other side of
-# zero flips the token's ReLU gate and moves its whole dC row, so single elements of the weight
-# gradient move by a few per cent of its max while the norm of the error stays small
-BF16_LOGIT_ATOL, BF16_GRAD_RTOL, BF16_GRAD_FRO = 2e-2, 2e-1, 5e-2
+# bf16 bars against the fp32 oracle (tests/test_cnn_rows_gpu.py): logits 2e-2 absolute,
+# every gradient 5e-2 of its norm (relative Frobenius) and 1e-1 of its max magnitude elementwise for
+# all but BF16_OUTLIER_FRAC of its elements, none past 2e-1: a bf16-rounded conv sum that lands on the
+# other side of zero flips that token's ReLU gate and moves its whole dC row, so single elements of
+# the conv weight gradient move by a few per cent of its max (measured 0.131 on the ragged host batch,
+# 0.043 in relative norm) while the error's norm stays small.  The test prints the distribution.
+BF16_LOGIT_ATOL, BF16_GRAD_RTOL, BF16_GRAD_CAP, BF16_GRAD_FRO, BF16_OUTLIER_FRAC = 2e-2, 1e-1, 2e-1, 5e-2, 1e-4
+# ... and against the bf16-EMULATING oracle (R.train_step(gemm="bf16"): the same operands rounded to
+# bf16 at the same points, fp32 accumulation), 20x tighter than the fp32-oracle bars: what is left is
+# fp32 summation order (and the rare bf16 rounding-boundary or ReLU-gate flip it causes).  Measured
+# (round 5, both batches): logits 1.1e-4 / 1.3e-4, gradients 3.6e-4 / 1.2e-3 of max, 1.7e-4 / 2.7e-4
+# in relative norm
+EMU_LOGIT_ATOL, EMU_GRAD_RTOL, EMU_GRAD_FRO = 1e-3, 1e-2, 2e-3
 
 
 def _model(encU, dev, precision=None):
@@ -173,27 +181,49 @@ def test_bf16_cnn_attn_fullsize_step_vs_oracle(feed):
     else:
         xg, x = _device_batch(dev)
     P = {n: p.detach().cpu().clone().requires_grad_(True) for n, p in model.named_parameters()}
+    Pe = {n: p.detach().clone().requires_grad_(True) for n, p in P.items()}
     logits, loss = _train_step(model, xg)
+    ps = dict(model.named_parameters())
+    # (1) against the bf16-emulating oracle: the same arithmetic, tight bars
+    emu_loss, emu_logits, _ = R.train_step(Pe, x, "cnn", "attn", gemm="bf16")
+    err = (logits.detach().cpu() - emu_logits).abs().max().item()
+    print("cnn_attn bf16 full size (%s feed) vs bf16-emulating oracle: max |logit err| %.3e, loss %.6f vs %.6f"
+          % (feed, err, loss.item(), emu_loss.item()))
+    assert emu_logits.std().item() > 0.05
+    assert err <= EMU_LOGIT_ATOL
+    assert abs(loss.item() - emu_loss.item()) <= EMU_LOGIT_ATOL
+    worst = (0.0, 0.0)
+    for n in Pe:
+        rel, fro = _grad_err(ps[n].grad.detach().cpu(), Pe[n].grad)
+        worst = (max(worst[0], rel), max(worst[1], fro))
+        assert rel <= EMU_GRAD_RTOL and fro <= EMU_GRAD_FRO, (n, rel, fro)
+    print("  vs bf16-emulating oracle: worst gradient error / max %.3e, relative norm %.3e" % worst)
+    # (2) against the fp32 oracle (the reference's arithmetic): the bf16 error band
     want_loss, want_logits, _ = R.train_step(P, x, "cnn", "attn")
     err = (logits.detach().cpu() - want_logits).abs().max().item()
-    print("cnn_attn bf16 full size (%s feed): logit std %.3f, max |logit err| %.3e, loss %.6f vs %.6f"
-          % (feed, want_logits.std().item(), err, loss.item(), want_loss.item()))
+    print("  vs fp32 oracle: logit std %.3f, max |logit err| %.3e, loss %.6f vs %.6f"
+          % (want_logits.std().item(), err, loss.item(), want_loss.item()))
     assert want_logits.std().item() > 0.05
     assert err <= BF16_LOGIT_ATOL
     assert abs(loss.item() - want_loss.item()) <= BF16_LOGIT_ATOL
-    ps = dict(model.named_parameters())
     worst = (0.0, 0.0)
     for n in P:
         want, got = P[n].grad, ps[n].grad
         assert want is not None and got is not None, n
-        rel, fro = _grad_err(got.detach().cpu(), want)
+        g = got.detach().cpu().double()
+        rel, fro = _grad_err(g, want)
         worst = (max(worst[0], rel), max(worst[1], fro))
-        assert rel <= BF16_GRAD_RTOL and fro <= BF16_GRAD_FRO, (n, rel, fro)
+        e = (g - want.double()).abs() / want.double().abs().max().clamp_min(1e-12)
+        q = torch.quantile(e.flatten()[:1 << 24].float(), torch.tensor([0.5, 0.99, 0.9999])).tolist()
+        out = float((e > BF16_GRAD_RTOL).double().mean())
+        print("  %s: |err| / max quantiles 50%% %.2e 99%% %.2e 99.99%% %.2e max %.2e; beyond %.0e: %.2e of %d"
+              % (n, q[0], q[1], q[2], rel, BF16_GRAD_RTOL, out, e.numel()))
+        assert rel <= BF16_GRAD_CAP and fro <= BF16_GRAD_FRO and out <= BF16_OUTLIER_FRAC, (n, rel, fro, out)
     # Adam's first step moves each element by at most lr (either sign)
     for n, p in model.named_parameters():
         lr = 6e-6 if "bert" in n else 1e-4
         assert (p.detach().cpu() - P[n].detach()).abs().max().item() <= 2 * lr + 1e-7, n
-    print("cnn_attn bf16 full size: worst gradient error / max %.3e, relative norm %.3e" % worst)
+    print("  vs fp32 oracle: worst gradient error / max %.3e, relative norm %.3e" % worst)
 
 
 def test_lstur_fullsize_graph_replay_matches_eager():

@@ -13,8 +13,8 @@ distinct-row projection, the fused attention kernels, the split backward, Adam) 
 * the same step replayed as a HIP graph (bench.GraphedStep) against eager steps;
 * XFormer at BERT-base width with enough rows (B = 16, 2 layers: 10,416 token rows, QKV = 1,476
   tiles of 128x128) that its GEMMs run the bf16x6 kernel, against the oracle.
-Dropout is 0 (the oracle cannot replay the device RNG's masks; dropout itself is covered by the
-kernel tests with recovered keep masks)."""
+The NRMS step runs at dropout 0 and at the bench's 0.2: the oracle restates the device RNG's keep
+masks (R.dropout_keep) and applies them where nn.Dropout would."""
 import copy
 import math
 import os
@@ -35,10 +35,10 @@ from oracle import restatement as R
 B, C, NH, L, V, H = 32, 5, 50, 30, 30522, 384
 
 
-def _nrms(dev):
+def _nrms(dev, p_drop=0.0):
     from newsrec_amd.manager import build_model
     torch.manual_seed(42)
-    m = build_model("mha", "mha", H, vocab=V, device=dev, user_num=876956, dropout_p=0.0)
+    m = build_model("mha", "mha", H, vocab=V, device=dev, user_num=876956, dropout_p=p_drop)
     with torch.no_grad():   # spread the candidate scores (reference init gives near-equal logits)
         m.embedding.bert_word_embedding.weight.normal_(0, 0.5)
         m.encoderN.query_words.normal_(0, 1.0)
@@ -87,13 +87,30 @@ def _close_grads(model, P, names=None, rel=1e-3):
         assert err <= rel * scale, (n, err, scale)
 
 
+def _news_dropout_kw(model, p, B_, C_, N_, L_):
+    """The keep masks of the step's news-encoder dropout (MHA.py:37) restated by the oracle
+    (R.dropout_keep) from the encoder's device RNG pair as the forward is about to take it: one joint
+    token batch, the candidates' B*C*L rows first, then the history's."""
+    if p <= 0:
+        return None, None
+    rng = model.encoderN._rng
+    seed, off = rng.seed, rng.offset
+    T = B_ * (C_ + N_) * L_
+    keep = R.dropout_keep(seed, off, T, H, p)
+    nc = B_ * C_ * L_
+    return {"dropout_keep": keep[:nc], "p_drop": p}, {"dropout_keep": keep[nc:], "p_drop": p}
+
+
+@pytest.mark.parametrize("p_drop", [0.0, 0.2])
 @pytest.mark.parametrize("feed", ["host", "device"])
-def test_nrms_fullsize_step_vs_oracle(feed):
-    """bench.forward_backward's path: forward_loss (fused scorer + log-softmax + NLL) and backward."""
+def test_nrms_fullsize_step_vs_oracle(feed, p_drop):
+    """bench.forward_backward's path: forward_loss (fused scorer + log-softmax + NLL) and backward;
+    p_drop = 0.2 is the bench's own step (MHA.py:19,37's Dropout(0.2) on the device RNG), the oracle
+    applying the same keep masks (R.dropout_keep)."""
     import bench
     from newsrec_amd.manager import get_optim
     dev = torch.device("cuda", 0)
-    model = _nrms(dev)
+    model = _nrms(dev, p_drop)
     model.train()
     if feed == "host":
         x = _batch(1)
@@ -102,13 +119,14 @@ def test_nrms_fullsize_step_vs_oracle(feed):
         xg, x = _device_batch(dev)
     P = _oracle_params(model)
     opt = get_optim(model)
+    cdd_kw, his_kw = _news_dropout_kw(model, p_drop, B, C, NH, L)
     # bench.forward_backward, keeping the logits
     opt.zero_grad(set_to_none=True)
     logits, loss = model.forward_loss(xg)
     loss.backward(bench._one(loss))
     opt.step()
     torch.cuda.synchronize()
-    want_loss, want_logits, _ = R.train_step(P, x, "mha", "mha")
+    want_loss, want_logits, _ = R.train_step(P, x, "mha", "mha", cdd_kw=cdd_kw, his_kw=his_kw)
     assert want_logits.std().item() > 0.05   # the comparison is not between constants
     err = (logits.detach().cpu() - want_logits).abs().max().item()
     print("NRMS full size: max |logit err| %.3e, loss %.6f vs %.6f" % (err, loss.item(), want_loss.item()))
@@ -202,3 +220,97 @@ def test_xformer_bf16x6_gemms_vs_oracle():
                             "bert.encoder.layer.1.intermediate.dense.weight",
                             "bert.encoder.layer.1.output.dense.weight", "bert.pooler.dense.weight", "userBias"],
                  rel=5e-3)
+
+
+def test_xformer_12_layers_step_vs_oracle():
+    """configs[4] at full BERT-base depth: XFormer (12 layers, 768 wide, 12 heads, 3072 FFN, V = 30522)
+    over B = 2 impressions -- 5 candidate titles each and the 501-token user sequence (CLS + 10
+    word-pieces of each of 50 history titles, XFormer.py:80-89) -- one train step through the bench's
+    path (forward_loss, backward, FusedAdam with the two parameter groups) against the fp32 oracle:
+    logits within 1e-3, EVERY gradient within 1e-3 of its max magnitude, every parameter after Adam
+    within 2 lr (all but a rounding-level handful within 1e-3 lr).  Gradients are checked against the
+    oracle run in float64 (see below).  Dropout 0 (BertFn's dropout sites are checked against their
+    kernels in tests/test_bert_gpu.py).  The key biases' gradient is zero in exact arithmetic (softmax
+    cancels q . b_k), so it is held to its layer's query-bias scale."""
+    import bench
+    from newsrec_amd import _lib as Lb, kernels as Kn
+    from newsrec_amd.bert import BertConfig
+    from newsrec_amd.manager import ManagerConfig, get_optim
+    from newsrec_amd.xformer import XFormer
+    assert Kn.get_gemm_precision() == Lb.GEMM_BF16X6
+    torch.manual_seed(5)
+    Bx, Cx, N, Lt = 2, 5, 50, 30
+    bc = BertConfig(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    model = XFormer(ManagerConfig("bert", "xformer", 768, bert_dim=768), bert_config=bc).cuda()
+    with torch.no_grad():
+        for n, p in model.named_parameters():
+            if p.dim() == 2 and "embeddings" not in n:
+                p.normal_(0, 1.5 / math.sqrt(p.shape[1]))
+    gen = torch.Generator().manual_seed(1)
+
+    def titles(n):
+        t = torch.randint(1000, V, (n, Lt), generator=gen)
+        lens = torch.randint(12, Lt + 1, (n,), generator=gen)
+        msk = (torch.arange(Lt)[None] < lens[:, None]).long()
+        t = t * msk
+        t[:, 0] = 101
+        return t, msk
+    ct, cm = titles(Bx * Cx)
+    ht, hm = titles(Bx * N)
+    x = {"cdd_encoded_index": ct.view(Bx, Cx, Lt), "cdd_attn_mask": cm.view(Bx, Cx, Lt),
+         "his_encoded_index": ht.view(Bx, N, Lt), "his_attn_mask": hm.view(Bx, N, Lt),
+         "label": torch.tensor([0, 3])}
+    xg = {k: v.cuda() for k, v in x.items()}
+    P = _oracle_params(model)
+    model.train()
+    opt = get_optim(model)
+    opt.zero_grad(set_to_none=True)
+    logits, loss = model.forward_loss(xg)
+    loss.backward(bench._one(loss))
+    opt.step()
+    torch.cuda.synchronize()
+    base, bert = R.adam_groups(P)
+    ropt = torch.optim.Adam([{"params": [P[k] for k in base], "lr": 1e-4},
+                             {"params": [P[k] for k in bert], "lr": 6e-6}])
+    want = R.xformer_forward(P, x, True, 12)
+    want_loss = R.nll_loss(want, x["label"])
+    want_loss.backward()
+    ropt.step()
+    err = (logits.detach().cpu() - want.detach()).abs().max().item()
+    print("XFormer 12 layers B=2: logit std %.3f, max |logit err| %.3e, loss %.6f vs %.6f"
+          % (want.detach().std().item(), err, loss.item(), want_loss.item()))
+    assert want.detach().std().item() > 0.05
+    assert err <= 1e-3
+    assert abs(loss.item() - want_loss.item()) <= 1e-3
+    # gradients against the oracle in float64 (the exact values to ~1e-15): within 1e-3 of each one's max
+    # magnitude, or -- where cancellation makes a tensor ill-conditioned (the attention-softmax gradients
+    # of the deep layers are small differences of large terms) -- no further from the exact value than
+    # twice the fp32 oracle's own error: fp32-class arithmetic, which the bf16x6 GEMMs are held to
+    P64 = {n: p.detach().double().requires_grad_(True) for n, p in P.items()}
+    R.nll_loss(R.xformer_forward(P64, x, True, 12), x["label"]).backward()
+    ps = dict(model.named_parameters())
+    worst, n_fp32 = 0.0, 0
+    for n in P:
+        want_g, got, g32 = P64[n].grad, ps[n].grad, P[n].grad
+        assert got is not None and g32 is not None, n
+        scale = max(want_g.abs().max().item(), 1e-12)
+        if n.endswith("attention.self.key.bias"):
+            scale = P64[n.replace(".key.bias", ".query.bias")].grad.abs().max().item()
+        gerr = (got.detach().cpu().double() - want_g).abs().max().item()
+        e32 = (g32.double() - want_g).abs().max().item()
+        worst = max(worst, gerr / scale)
+        if gerr > 1e-3 * scale:
+            n_fp32 += 1
+            print("  %s: |err| / max %.2e (fp32 oracle %.2e)" % (n, gerr / scale, e32 / scale))
+        assert gerr <= max(1e-3 * scale, 2 * e32), (n, gerr, e32, scale)
+    print("XFormer 12 layers: worst gradient error / max %.3e over %d tensors (%d held to the fp32-oracle bar)"
+          % (worst, len(P), n_fp32))
+    for n, p in model.named_parameters():
+        d = (p.detach().cpu() - P[n].detach()).abs()
+        lr = 6e-6 if "bert" in n else 1e-4
+        assert d.max().item() <= 2 * lr + 1e-7, n
+        if n.endswith("attention.self.key.bias"):
+            continue
+        moved = P[n].grad != 0
+        off = int((d[moved] > 1e-3 * lr).sum().item())
+        assert off <= max(2, 1e-3 * int(moved.sum().item())), (n, off)

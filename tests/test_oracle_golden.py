@@ -70,3 +70,37 @@ def test_oracle_cal_metric_known_answers():
         got = R.cal_metric(r["labels"], r["preds"], ["auc", "mean_mrr", "ndcg@5;10"])
         for k, v in got.items():
             assert abs(v - r["res"][k]) < 1e-4, (k, v, r["res"][k])
+
+
+def test_bf16_restatement_structure_matches_reference(monkeypatch):
+    """R.forward_cnn_bf16 (configs[1]'s bf16 GEMM arithmetic) with its rounding switched off is the
+    reference's CNN + attention step: logits, loss and every gradient against the reference golden
+    (the per-tap products, the per-distinct-id gradient sums and the joint candidate | history pass
+    are a refactoring of CNN.py:30-50, not another algorithm).  With the rounding on, the step moves
+    by the bf16 error only (logits ~1e-2, gradients a few 1e-2 of their norm)."""
+    g = Golden("cnn_attn")
+    x = g.inputs()
+
+    def step(P):
+        logits = R.forward_cnn_bf16(P, x, g.encU, True)
+        loss = R.nll_loss(logits, x["label"])
+        loss.backward()
+        return logits.detach(), loss.item()
+
+    monkeypatch.setattr(R, "bf16_round", lambda t: t)
+    P = g.torch_params(requires_grad=True)
+    logits, loss = step(P)
+    np.testing.assert_allclose(logits.numpy(), g["out.train_logits"], rtol=0, atol=1e-5)
+    assert abs(loss - float(g["out.loss"])) < 1e-5
+    for n in g.names:
+        want = g["grad." + n]
+        scale = max(np.abs(want).max(), 1e-6)
+        np.testing.assert_allclose(P[n].grad.numpy(), want, rtol=0, atol=2e-4 * scale, err_msg=n)
+    monkeypatch.undo()
+    P = g.torch_params(requires_grad=True)
+    logits, loss = step(P)
+    assert 1e-5 < np.abs(logits.numpy() - g["out.train_logits"]).max() < 2e-2
+    for n in g.names:
+        want = g["grad." + n]
+        rel = np.linalg.norm(P[n].grad.numpy() - want) / max(np.linalg.norm(want), 1e-12)
+        assert rel < 5e-2, (n, rel)
