@@ -616,7 +616,14 @@ int nr_bert_add_ln_bwd(const float* x, int64_t ldx, const float* res, int64_t ld
 int nr_bert_attn_fwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
                      int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, float p_drop,
                      uint64_t seed, uint64_t offset, const uint64_t* rng, float* ctx, int64_t ldc,
-                     float* ml, int32_t prec, hipStream_t stream);
+                     float* ml, uint32_t* keep, int32_t prec, hipStream_t stream);
+
+/* Words of the optional `keep` buffer of nr_bert_attn_fwd / _bwd: one 32-bit word per (sequence, head,
+ * query, 32-key tile) holding the dropout keep bits of that query's probabilities (ceil(L / 32) words
+ * per query).  The bf16-MFMA forward (prec != NR_GEMM_F32) with p_drop > 0 stores them; the backward
+ * reads them instead of re-deriving each element's counter hash (the attention-probability dropout of
+ * BertSelfAttention, models/XFormer.py:68,94).  NULL: the backward re-hashes (same masks). */
+int64_t nr_bert_attn_keep_words(int64_t nseq, int32_t L, int32_t heads);
 
 /* Bytes of `work` nr_bert_attn_bwd needs. */
 int64_t nr_bert_attn_bwd_workspace(int64_t nseq, int32_t L, int32_t heads);
@@ -627,8 +634,8 @@ int64_t nr_bert_attn_bwd_workspace(int64_t nseq, int32_t L, int32_t heads);
 int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
                      int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, float p_drop,
                      uint64_t seed, uint64_t offset, const uint64_t* rng, const float* ctx, int64_t ldc,
-                     const float* ml, const float* dctx, int64_t ldd, float* work, float* dqkv,
-                     int64_t lddq, int32_t prec, hipStream_t stream);
+                     const float* ml, const uint32_t* keep, const float* dctx, int64_t ldd, float* work,
+                     float* dqkv, int64_t lddq, int32_t prec, hipStream_t stream);
 
 /* dx = dy * (1 - y^2): the pooler's tanh backward (BertPooler). */
 int nr_tanh_bwd(const float* y, int64_t ldy, const float* dy, int64_t lddy, int64_t rows, int32_t cols,

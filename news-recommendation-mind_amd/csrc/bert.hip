@@ -275,7 +275,15 @@ struct AttnArgs {
   const float* dctx; int64_t ldd;   // bwd: upstream grad of ctx
   const float* Dq;                  // bwd: [T][heads] rowsum(dctx * ctx)
   float* dqkv; int64_t lddq;        // bwd output (same column layout as qkv)
+  // dropout keep bits (optional): word ((seq * heads + head) * L + q) * nkb + kb holds query q's 32 keys
+  // of key tile kb, bit r + 16 h = key kb * 32 + crow(r, h) (the forward lane's own 16 bits per half);
+  // the bf16-MFMA forward stores them, both backward kernels read them instead of re-hashing
+  uint32_t* keep; int nkb;
 };
+
+__device__ __forceinline__ int64_t keep_word(const AttnArgs& g, int64_t seq, int head, int q, int kb) {
+  return ((seq * g.heads + head) * (int64_t)g.L + q) * g.nkb + kb;
+}
 
 __device__ __forceinline__ uint32_t attn_key(const AttnArgs& g, int64_t seq, int head) {
   const uint32_t k = g.rng ? nr_dropout_key(g.rng[0], g.rng[1] + g.offset) : g.key;
@@ -433,6 +441,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(AttnArgs g) {
   __shared__ float Qs[32][kLS];
   __shared__ float Os[32][kLS];   // dctx tile
   __shared__ float qm[32], qi[32], qd[32];
+  __shared__ __attribute__((aligned(16))) uint32_t kwd[4][32];   // per wave: the tile's 32 queries' words of its key tile
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, hh = lane >> 5;
   const int nw = blockDim.x >> 6;
   int64_t bid = blockIdx.x;
@@ -938,11 +947,16 @@ __global__ void __launch_bounds__(256) attn_fwd_mp_kernel(AttnArgs g) {
       o1[r] *= alpha;
     }
     if (DROP) {
+      uint32_t bits = 0u;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const uint32_t e = (uint32_t)q * (uint32_t)L + (uint32_t)(kb * 32 + crow(r, hh));
-        pe[r] = nr_dropout_keep(dkey, e, g.thresh) ? pe[r] * g.pscale : 0.f;
+        const bool kp = nr_dropout_keep(dkey, e, g.thresh);
+        bits |= (kp ? 1u : 0u) << r;
+        pe[r] = kp ? pe[r] * g.pscale : 0.f;
       }
+      if (g.keep && q < L)   // this lane's half of the (query, key tile) word
+        reinterpret_cast<uint16_t*>(g.keep)[2 * keep_word(g, seq, head, q, kb) + hh] = (uint16_t)bits;
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -972,13 +986,14 @@ __global__ void __launch_bounds__(256) attn_fwd_mp_kernel(AttnArgs g) {
 // Two waves per SIMD, as attn_bwd_q_mp_kernel: with the own K / V rows held as split planes (96
 // VGPRs) the bound spilled 36 and ran slower (profiles/r04_o_xf_ab.json); held as fp32 and split per
 // query tile it spills 9 and the XFormer step gains 68.15 -> 67.86 ms (profiles/r04_q_xf_ab.json).
-template <int NP, bool DROP, bool PF>
+template <int NP, bool DROP, bool PF, bool KB = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) attn_bwd_kv_mp_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t Qp[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Op[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Qt[NP][kHD][kVR];
   __shared__ __attribute__((aligned(16))) uint16_t Ot[NP][kHD][kVR];
   __shared__ float qm[32], qi[32], qd[32];
+  __shared__ __attribute__((aligned(16))) uint32_t kwd[4][32];   // per wave: the tile's 32 queries' words of its key tile
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, hh = lane >> 5;
   const int nw = blockDim.x >> 6;
   int64_t bid = blockIdx.x;
@@ -1009,6 +1024,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) a
     }
   }
   const float kadd = own ? (nr_mask_at(g.mask, g.mdt, row0 + key) ? 0.f : kNegMax) : -INFINITY;
+  // stored keep bits: lane c's key is bit ((c >> 3) << 2 | (c & 3)) + 16 ((c >> 2) & 1) of a query's word
+  constexpr bool kbits = DROP && KB;   // KB: g.keep holds the forward's bits (the launcher checks)
+  const int kbit = (((c >> 3) << 2) | (c & 3)) + 16 * ((c >> 2) & 1);
+  const int kbt = k0 >> 5;   // this wave's key tile
+  auto kword = [&](int j) -> uint32_t {   // query j's word of this wave's key tile (0 past L)
+    return j < L && active ? g.keep[keep_word(g, seq, head, j, kbt)] : 0u;
+  };
+  uint32_t kw_n = 0u;
+  if (kbits && PF && lane < 32) kw_n = kword(lane);
   f32x16 dk0, dk1, dv0, dv1;
 #pragma unroll
   for (int r = 0; r < 16; ++r) dk0[r] = dk1[r] = dv0[r] = dv1[r] = 0.f;
@@ -1043,18 +1067,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) a
         qi[threadIdx.x] = qi_n;
         qd[threadIdx.x] = qd_n;
       }
+      if (kbits && lane < 32) kwd[wave][lane] = kw_n;
       if (qb + 1 < nqb) {
         fq.fetch(g.qkv, g.ldq, row0, (qb + 1) * 32, L, head * kHD);
         fo.fetch(g.dctx, g.ldd, row0, (qb + 1) * 32, L, head * kHD);
         if (threadIdx.x < 32) qstats((qb + 1) * 32 + threadIdx.x, qm_n, qi_n, qd_n);
+        if (kbits && lane < 32) kw_n = kword((qb + 1) * 32 + lane);
       }
     } else {
       stage_planes<NP>(Qp, Qt, g.qkv, g.ldq, row0, qb * 32, L, head * kHD);
       stage_planes<NP>(Op, Ot, g.dctx, g.ldd, row0, qb * 32, L, head * kHD);
       if (threadIdx.x < 32) qstats(qb * 32 + threadIdx.x, qm[threadIdx.x], qi[threadIdx.x], qd[threadIdx.x]);
+      if (kbits && lane < 32) kwd[wave][lane] = kword(qb * 32 + lane);
     }
     __syncthreads();
     if (!active) continue;
+    // this lane's keep bits of the 16 queries crow(r, hh) (four runs of four consecutive words): bit r
+    uint32_t kmask = 0u;
+    if constexpr (kbits) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const uint4 w4 = *reinterpret_cast<const uint4*>(&kwd[wave][8 * g4 + 4 * hh]);
+        kmask |= (((w4.x >> kbit) & 1u) | (((w4.y >> kbit) & 1u) << 1) | (((w4.z >> kbit) & 1u) << 2) |
+                  (((w4.w >> kbit) & 1u) << 3)) << (4 * g4);
+        asm volatile("" : "+v"(kmask));   // one run's four words live at a time
+      }
+    }
     f32x16 s, dp;
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = dp[r] = 0.f;
@@ -1074,8 +1112,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) a
       float d = dp[r];
       float pdr = pr;
       if (DROP) {
-        const uint32_t e = (uint32_t)(qb * 32 + qr) * (uint32_t)L + (uint32_t)key;
-        const bool kp = nr_dropout_keep(dkey, e, g.thresh);
+        bool kp;
+        if constexpr (kbits) {
+          kp = (kmask >> r) & 1u;
+        } else {
+          const uint32_t e = (uint32_t)(qb * 32 + qr) * (uint32_t)L + (uint32_t)key;
+          kp = nr_dropout_keep(dkey, e, g.thresh);
+        }
         d = kp ? d * g.pscale : 0.f;
         pdr = kp ? pr * g.pscale : 0.f;
       }
@@ -1111,7 +1154,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) a
 // Two waves per SIMD: unbounded, the bf16x6 prefetching form took 270 VGPRs -- one wave per SIMD,
 // its softmax / dS arithmetic never overlapping another wave's MFMAs; at <= 256 it fits without
 // spills: XFormer step 71.5 -> 69.9 ms on one box (profiles/r04_o_xf_ab.json).
-template <int NP, bool DROP, bool PF>
+template <int NP, bool DROP, bool PF, bool KB = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) attn_bwd_q_mp_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t Kp[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Vp[NP][32][kKR];
@@ -1146,6 +1189,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) a
 #pragma unroll
   for (int r = 0; r < 16; ++r) a0[r] = a1[r] = 0.f;
   const int nkb = (L + 31) / 32;
+  // stored keep bits: this lane's half of its query's word of each key tile, loaded a tile ahead
+  constexpr bool kbits = DROP && KB;   // KB: g.keep holds the forward's bits (the launcher checks)
+  auto kword = [&](int kb) -> uint32_t { return own ? g.keep[keep_word(g, seq, head, q, kb)] >> (16 * hh) : 0u; };
+  uint32_t kw_c = kbits ? kword(0) : 0u;
   TileFetch<NP> fk, fv;
   float kadd_n = 0.f;
   if constexpr (PF) {
@@ -1154,6 +1201,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) a
     if (threadIdx.x < 32) kadd_n = key_add(g, row0, threadIdx.x, L);
   }
   for (int kb = 0; kb < nkb; ++kb) {
+    const uint32_t kw = kw_c;
+    if (kbits && kb + 1 < nkb) kw_c = kword(kb + 1);
     __syncthreads();
     if constexpr (PF) {
       fk.store(Kp, Kt);
@@ -1186,8 +1235,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) a
       const float pr = __expf(s[r] + kadd[kr] - mq) * iq;
       float d = dp[r];
       if (DROP) {
-        const uint32_t e = (uint32_t)q * (uint32_t)L + (uint32_t)(kb * 32 + kr);
-        d = nr_dropout_keep(dkey, e, g.thresh) ? d * g.pscale : 0.f;
+        bool kp;
+        if constexpr (kbits) {
+          kp = (kw >> r) & 1u;
+        } else {
+          const uint32_t e = (uint32_t)q * (uint32_t)L + (uint32_t)(kb * 32 + kr);
+          kp = nr_dropout_keep(dkey, e, g.thresh);
+        }
+        d = kp ? d * g.pscale : 0.f;
       }
       ds[r] = pr * (d - dq);
     }
@@ -1312,17 +1367,24 @@ extern "C" int nr_bert_add_ln_bwd(const float* x, int64_t ldx, const float* res,
   return launch_ln<false, true>(g, stream);
 }
 
+extern "C" int64_t nr_bert_attn_keep_words(int64_t nseq, int32_t L, int32_t heads) {
+  if (nseq < 0 || L <= 0 || heads <= 0) return 0;
+  return nseq * heads * (int64_t)L * ((L + 31) / 32);
+}
+
 extern "C" int nr_bert_attn_fwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
                                 int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, float p_drop,
                                 uint64_t seed, uint64_t offset, const uint64_t* rng, float* ctx, int64_t ldc,
-                                float* ml, int32_t prec, hipStream_t stream) {
+                                float* ml, uint32_t* keep, int32_t prec, hipStream_t stream) {
   AttnArgs g{};
   int rc = attn_setup(g, qkv, ldq, koff, voff, mask, mask_dtype, nseq, L, heads, p_drop, seed, offset, rng, ml);
   if (rc) return rc;
   if (!ctx || !al16(ctx) || (ldc & 3)) return NR_EINVAL(4);
   if (!prec_ok(prec)) return NR_EINVAL(6);
+  if (keep && prec == NR_GEMM_F32) return NR_EINVAL(7);   // the f32 forward does not store keep bits
   if (nseq == 0) return NR_OK;
   g.ctx = ctx; g.ldc = ldc;
+  g.keep = p_drop > 0.f ? keep : nullptr; g.nkb = (L + 31) / 32;
   const int nw = attn_waves(L);
   g.chunks = (L + 32 * nw - 1) / (32 * nw);
   const dim3 grid((unsigned)(nseq * heads * g.chunks)), block(64 * nw);
@@ -1358,8 +1420,8 @@ extern "C" int64_t nr_bert_attn_bwd_workspace(int64_t nseq, int32_t L, int32_t h
 extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
                                 int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, float p_drop,
                                 uint64_t seed, uint64_t offset, const uint64_t* rng, const float* ctx, int64_t ldc,
-                                const float* ml, const float* dctx, int64_t ldd, float* work, float* dqkv,
-                                int64_t lddq, int32_t prec, hipStream_t stream) {
+                                const float* ml, const uint32_t* keep, const float* dctx, int64_t ldd, float* work,
+                                float* dqkv, int64_t lddq, int32_t prec, hipStream_t stream) {
   AttnArgs g{};
   int rc = attn_setup(g, qkv, ldq, koff, voff, mask, mask_dtype, nseq, L, heads, p_drop, seed, offset, rng,
                       const_cast<float*>(ml));
@@ -1373,6 +1435,9 @@ extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int
                      ldc, T, heads, work);
   NR_LAUNCH_CHECK();
   g.dctx = dctx; g.ldd = ldd; g.Dq = work; g.dqkv = dqkv; g.lddq = lddq;
+  // the f32 kernels re-hash (their forward stored no bits: the same masks either way)
+  g.keep = p_drop > 0.f && prec != NR_GEMM_F32 ? const_cast<uint32_t*>(keep) : nullptr;
+  g.nkb = (L + 31) / 32;
   const int nw = attn_waves(L);
   g.chunks = (L + 32 * nw - 1) / (32 * nw);
   const dim3 grid((unsigned)(nseq * heads * g.chunks)), block(64 * nw);
@@ -1382,9 +1447,16 @@ extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int
     hipLaunchKernelGGL(KV, grid, block, 0, stream, g);         \
     hipLaunchKernelGGL(Q, grid, block, 0, stream, g);          \
   } while (0)
+  const bool kb = drop && g.keep != nullptr;
   if (prec == NR_GEMM_F32) {
     if (drop) NR_BWD(attn_bwd_kv_kernel<true>, attn_bwd_q_kernel<true>);
     else NR_BWD(attn_bwd_kv_kernel<false>, attn_bwd_q_kernel<false>);
+  } else if (kb && nw == 4) {   // the forward's keep bits instead of the per-element hash
+    if (prec == NR_GEMM_BF16) NR_BWD((attn_bwd_kv_mp_kernel<1, true, true, true>), (attn_bwd_q_mp_kernel<1, true, true, true>));
+    else NR_BWD((attn_bwd_kv_mp_kernel<3, true, true, true>), (attn_bwd_q_mp_kernel<3, true, true, true>));
+  } else if (kb) {
+    if (prec == NR_GEMM_BF16) NR_BWD((attn_bwd_kv_mp_kernel<1, true, false, true>), (attn_bwd_q_mp_kernel<1, true, false, true>));
+    else NR_BWD((attn_bwd_kv_mp_kernel<3, true, false, true>), (attn_bwd_q_mp_kernel<3, true, false, true>));
   } else if (nw == 4) {
     if (prec == NR_GEMM_BF16) {
       if (drop) NR_BWD((attn_bwd_kv_mp_kernel<1, true, true>), (attn_bwd_q_mp_kernel<1, true, true>));

@@ -131,10 +131,11 @@ _SIGS = {
     "nr_bert_add_ln_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_f32, c_u64, c_u64, c_ptr, c_ptr,
                            c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr],
     "nr_bert_attn_fwd": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_u64, c_u64,
-                         c_ptr, c_ptr, c_i64, c_ptr, c_i32, c_ptr],
+                         c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_ptr],
+    "nr_bert_attn_keep_words": [c_i64, c_i32, c_i32],
     "nr_bert_attn_bwd_workspace": [c_i64, c_i32, c_i32],
     "nr_bert_attn_bwd": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, c_i64, c_i32, c_i32, c_f32, c_u64, c_u64,
-                         c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i32, c_ptr],
+                         c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64, c_i32, c_ptr],
     "nr_tanh_bwd": [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i32, c_ptr, c_i64, c_ptr],
     "nr_adam_multi": [ctypes.POINTER(nr_adam_tensor), c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_ptr],
     "nr_adam_multi_step": [ctypes.POINTER(nr_adam_tensor), c_i32, c_f32, c_f32, c_f32, c_f32, c_f32, c_ptr,
@@ -142,7 +143,7 @@ _SIGS = {
     "nr_build_hash": [],
 }
 
-_RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_unique_rows_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64,
+_RESTYPES = {"nr_segment_rows_sum_workspace": c_i64, "nr_bert_attn_keep_words": c_i64, "nr_unique_rows_workspace": c_i64, "nr_bert_attn_bwd_workspace": c_i64,
              "nr_colsum_workspace": c_i64, "nr_score_nll_workspace": c_i64,
              "nr_gemm_splitk_workspace": c_i64, "nr_cnn_keypool_workspace": c_i64,
              "nr_build_hash": ctypes.c_char_p}

@@ -30,6 +30,11 @@ from . import kernels as K
 from .functions import _empty, _gemm_backward, _proj_wgrad, _zeros_views
 
 
+# the bf16-MFMA attention forward stores its dropout keep bits for the backward (False: the backward
+# re-hashes every probability's counter, the same masks)
+ATTN_KEEP_BITS = True
+
+
 class BertConfig:
     """transformers.BertConfig defaults (bert-base-uncased)."""
 
@@ -177,7 +182,7 @@ class BertFn(torch.autograd.Function):
             K.bert_embed_fwd(word, pos, typ[0], s.ids, s.nseq, s.L, elw, elb, c.layer_norm_eps,
                              x[r0:r0 + s.nseq * s.L], st_e[r0:r0 + s.nseq * s.L],
                              **dsite_seg(0, p_h, r0 * H))
-        saved = []
+        saved, keeps_all = [], []
         for li, w in enumerate(lp):
             wq, bq, wk, bk, wv, bv, wo, bo, l1w, l1b, wi, bi, wo2, bo2, l2w, l2b = w
             wqkv = torch.cat([wq, wk, wv], 0)
@@ -186,10 +191,14 @@ class BertFn(torch.autograd.Function):
             K.gemm(T, 3 * H, H, K.operand(x, L.KCONTIG), K.operand(wqkv, L.KCONTIG), qkv, bias=bqkv)
             cx = _empty(T, H, word)
             ml = torch.empty(T * heads * 2, device=dev)
-            for s, r0 in zip(segs, r0s):
+            # the bf16-MFMA attention keeps its dropout bits for the backward (instead of re-hashing
+            # every probability's counter twice there): ~12 MB per layer for B = 32's user sequences
+            keeps = [K.bert_attn_keep_buffer(s.nseq, s.L, heads, dev)
+                     if p_a > 0 and ctx.prec != L.GEMM_F32 and ATTN_KEEP_BITS else None for s in segs]
+            for s, r0, kp in zip(segs, r0s, keeps):
                 n = s.nseq * s.L
                 K.bert_attn_fwd(qkv[r0:r0 + n], heads, s.mask, s.nseq, s.L, cx[r0:r0 + n],
-                                ml[r0 * heads * 2:(r0 + n) * heads * 2], **dsite_seg(1 + 3 * li, p_a, r0))
+                                ml[r0 * heads * 2:(r0 + n) * heads * 2], keep=kp, **dsite_seg(1 + 3 * li, p_a, r0))
             a = _empty(T, H, word)
             K.gemm(T, H, H, K.operand(cx, L.KCONTIG), K.operand(wo, L.KCONTIG), a, bias=bo)
             h1 = _empty(T, H, word)
@@ -205,12 +214,14 @@ class BertFn(torch.autograd.Function):
             st2 = torch.empty(T, 2, device=dev)
             K.bert_add_ln_fwd(o, h1, l2w, l2b, c.layer_norm_eps, h2, st2, **dsite_seg(3 + 3 * li, p_h, 0))
             saved += [x, wqkv, qkv, cx, ml, a, st1, h1, U, G, o, st2]
+            keeps_all.append(keeps)
             x = h2
         pooled = _empty(S, H, word)
         K.gemm(S, H, H, K.operand(x, L.KCONTIG, rows=cls_idx, mapping=L.ROWS_GATHER), K.operand(pw, L.KCONTIG),
                pooled, bias=pb, epilogue=L.EPI_STORE_TANH)
         ctx.save_for_backward(*params, st_e, cls_idx, x, pooled, *saved)
         ctx.cfg, ctx.segs, ctx.r0s, ctx.drop = cfg, segs, r0s, drop
+        ctx.keeps = keeps_all
         ctx.dsite_seg, ctx.p = dsite_seg, (p_h, p_a)
         ctx.n_params = len(params)
         return x, pooled
@@ -274,11 +285,11 @@ class BertFn(torch.autograd.Function):
             K.gemm(T, H, H, K.operand(da, L.KCONTIG), K.operand(wo, L.MNCONTIG), dcx)
             _proj_wgrad(da, K.operand(cx, L.MNCONTIG), g[6], g[7], T)
             dqkv = _empty(T, 3 * H, word)
-            for s, r0 in zip(segs, r0s):
+            for s, r0, kp in zip(segs, r0s, ctx.keeps[li]):
                 n = s.nseq * s.L
                 K.bert_attn_bwd(qkv[r0:r0 + n], heads, s.mask, s.nseq, s.L, cx[r0:r0 + n],
                                 ml[r0 * heads * 2:(r0 + n) * heads * 2], dcx[r0:r0 + n], dqkv[r0:r0 + n],
-                                **dsite_seg(1 + 3 * li, p_a, r0))
+                                keep=kp, **dsite_seg(1 + 3 * li, p_a, r0))
             K.gemm(T, H, 3 * H, K.operand(dqkv, L.KCONTIG), K.operand(wqkv, L.MNCONTIG), dx, epilogue=L.EPI_ACCUM)
             _proj_wgrad(dqkv, K.operand(x, L.MNCONTIG), dwqkv, dbqkv, T)
             for k in range(16):

@@ -892,10 +892,26 @@ def _attn_check(qkv, heads, koff, voff, mask, nseq, seq_len):
     return mask_arg(mask, T)
 
 
+def bert_attn_keep_buffer(nseq, seq_len, heads, device):
+    """The dropout keep-bit words of one nr_bert_attn_fwd call (nr_bert_attn_keep_words int32)."""
+    n = int(L.load().nr_bert_attn_keep_words(nseq, seq_len, heads))
+    return torch.empty(max(n, 1), device=device, dtype=torch.int32)
+
+
+def _keep_ok(keep, nseq, seq_len, heads, name):
+    if keep is None:
+        return
+    if keep.dtype != torch.int32 or not keep.is_cuda or not keep.is_contiguous() or \
+            keep.numel() < int(L.load().nr_bert_attn_keep_words(nseq, seq_len, heads)):
+        raise L.HipError("%s: keep must be a contiguous int32 CUDA buffer of nr_bert_attn_keep_words words" % name)
+
+
 def bert_attn_fwd(qkv, heads, mask, nseq, seq_len, ctx, ml, koff=None, voff=None, p_drop=0.0, seed=0, offset=0,
-                  rng=None, prec=None):
+                  rng=None, prec=None, keep=None):
     """BertSelfAttention core on a fused [T, 3*heads*64] (Q | K | V) projection.  ``prec``: the
-    attention products' arithmetic (default: this thread's GEMM precision)."""
+    attention products' arithmetic (default: this thread's GEMM precision).  ``keep``
+    (bert_attn_keep_buffer; bf16-MFMA arithmetic with dropout): the dropout keep bits are stored
+    there for the backward."""
     koff = heads * 64 if koff is None else koff
     voff = 2 * heads * 64 if voff is None else voff
     mp, mdt = _attn_check(qkv, heads, koff, voff, mask, nseq, seq_len)
@@ -905,13 +921,14 @@ def bert_attn_fwd(qkv, heads, mask, nseq, seq_len, ctx, ml, koff=None, voff=None
     _rows_ok(ctx, T, heads * 64, "ctx")
     if ml.numel() < 2 * T * heads:
         raise L.HipError("bert_attn_fwd: ml too small")
+    _keep_ok(keep, nseq, seq_len, heads, "bert_attn_fwd")
     p, s, o, r = _drop(p_drop, seed, offset, rng)
     L.call("nr_bert_attn_fwd", L.ptr(qkv), qkv.stride(0), koff, voff, mp, mdt, nseq, seq_len, heads, p, s, o, r,
-           L.ptr(ctx), ctx.stride(0), L.ptr(ml), _prec(prec), L.stream_ptr(qkv))
+           L.ptr(ctx), ctx.stride(0), L.ptr(ml), L.ptr(keep), _prec(prec), L.stream_ptr(qkv))
 
 
 def bert_attn_bwd(qkv, heads, mask, nseq, seq_len, ctx, ml, dctx, dqkv, koff=None, voff=None, p_drop=0.0, seed=0,
-                  offset=0, rng=None, prec=None):
+                  offset=0, rng=None, prec=None, keep=None):
     koff = heads * 64 if koff is None else koff
     voff = 2 * heads * 64 if voff is None else voff
     mp, mdt = _attn_check(qkv, heads, koff, voff, mask, nseq, seq_len)
@@ -922,9 +939,10 @@ def bert_attn_bwd(qkv, heads, mask, nseq, seq_len, ctx, ml, dctx, dqkv, koff=Non
         _rows_ok(t, T, w, n)
     nbytes = L.load().nr_bert_attn_bwd_workspace(nseq, seq_len, heads)
     work = torch.empty(max(1, nbytes // 4), device=qkv.device, dtype=torch.float32)
+    _keep_ok(keep, nseq, seq_len, heads, "bert_attn_bwd")
     p, s, o, r = _drop(p_drop, seed, offset, rng)
     L.call("nr_bert_attn_bwd", L.ptr(qkv), qkv.stride(0), koff, voff, mp, mdt, nseq, seq_len, heads, p, s, o, r,
-           L.ptr(ctx), ctx.stride(0), L.ptr(ml), L.ptr(dctx), dctx.stride(0), L.ptr(work), L.ptr(dqkv),
+           L.ptr(ctx), ctx.stride(0), L.ptr(ml), L.ptr(keep), L.ptr(dctx), dctx.stride(0), L.ptr(work), L.ptr(dqkv),
            dqkv.stride(0), _prec(prec), L.stream_ptr(qkv))
 
 

@@ -98,6 +98,49 @@ def test_attention_dropout_consistent(prec, request):
     assert 0.05 < rel < 2.0
 
 
+@pytest.mark.parametrize("prec", ["bf16x6", "bf16"])
+@pytest.mark.parametrize("nseq,L,heads", [(3, 45, 2), (2, 501, 12), (4, 30, 12), (2, 33, 1)])
+def test_attention_dropout_keep_bits(nseq, L, heads, prec):
+    """The bf16-MFMA forward's stored keep bits (nr_bert_attn_keep_words): the backward reading them
+    is BITWISE the backward that re-hashes every probability's counter (the same masks, the same
+    arithmetic), for the title shape, the 501-token user sequence, ragged key tiles and graph RNG
+    pairs; about p of the bits are clear; a keep buffer with the f32 forward is refused."""
+    from newsrec_amd import _lib as Lb, kernels as K
+    mode = Lb.GEMM_BF16X6 if prec == "bf16x6" else Lb.GEMM_BF16
+    torch.manual_seed(L + heads)
+    p = 0.1
+    H, T = heads * 64, nseq * L
+    qkv = torch.randn(T, 3 * H, device="cuda")
+    lens = torch.randint(1, L + 1, (nseq,))
+    mask = (torch.arange(L)[None] < lens[:, None]).long().reshape(-1).cuda()
+    rng = torch.tensor([123456789, 4242], dtype=torch.int64, device="cuda")
+    ml = torch.empty(T * heads * 2, device="cuda")
+    ctx0, ctx1 = torch.empty(T, H, device="cuda"), torch.empty(T, H, device="cuda")
+    keep = K.bert_attn_keep_buffer(nseq, L, heads, "cuda")
+    keep.fill_(-1)
+    K.bert_attn_fwd(qkv, heads, mask, nseq, L, ctx0, ml, p_drop=p, rng=rng, prec=mode)
+    K.bert_attn_fwd(qkv, heads, mask, nseq, L, ctx1, ml, p_drop=p, rng=rng, prec=mode, keep=keep)
+    assert torch.equal(ctx0, ctx1)
+    nkb = (L + 31) // 32
+    words = keep[:nseq * heads * L * nkb].view(nseq * heads, L, nkb).cpu().numpy().view(np.uint32)
+    valid = np.zeros((L, nkb, 32), bool)          # bit b of (q, kb) is a key < L
+    for kb in range(nkb):
+        for b in range(32):
+            r, h = b % 16, b // 16
+            valid[:, kb, b] = kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h < L
+    bits = (words[..., None] >> np.arange(32, dtype=np.uint32)) & 1
+    frac = bits[:, valid].mean()
+    assert abs((1 - frac) - p) < 0.02, frac
+    d = torch.randn(T, H, device="cuda")
+    g0 = torch.empty(T, 3 * H, device="cuda")
+    g1 = torch.empty(T, 3 * H, device="cuda")
+    K.bert_attn_bwd(qkv, heads, mask, nseq, L, ctx0, ml, d, g0, p_drop=p, rng=rng, prec=mode)
+    K.bert_attn_bwd(qkv, heads, mask, nseq, L, ctx0, ml, d, g1, p_drop=p, rng=rng, prec=mode, keep=keep)
+    assert torch.equal(g0, g1)
+    with pytest.raises(Lb.HipError):
+        K.bert_attn_fwd(qkv, heads, mask, nseq, L, ctx1, ml, p_drop=p, rng=rng, prec=Lb.GEMM_F32, keep=keep)
+
+
 def test_add_ln_and_embed():
     from newsrec_amd import kernels as K
     torch.manual_seed(0)

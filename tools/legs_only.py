@@ -16,7 +16,12 @@ a = ap.parse_args()
 from newsrec_amd import functions as F  # noqa: E402
 for kv in a.set:
     k, v = kv.split("=")
-    setattr(F, k, bool(int(v)) if isinstance(getattr(F, k), bool) else int(v))
+    mod = F
+    if "." in k:   # module.NAME (e.g. bert.ATTN_KEEP_BITS)
+        import importlib
+        m, k = k.rsplit(".", 1)
+        mod = importlib.import_module("newsrec_amd." + m)
+    setattr(mod, k, bool(int(v)) if isinstance(getattr(mod, k), bool) else int(v))
 dev = torch.device("cuda", 0)
 if a.legs == ["xformer"]:
     print(json.dumps(bench.xformer_leg(dev, steps=a.steps)))
