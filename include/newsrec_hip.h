@@ -477,6 +477,12 @@ int nr_embedding_bwd(const float* dout, int64_t V, int64_t E, const int64_t* idx
 int nr_rows_add_ordered(const float* dout, int64_t ldo, int64_t V, int64_t E, const int64_t* idx, int64_t n,
                         int64_t padding_idx, float* dtable, int64_t ldt, hipStream_t stream);
 
+/* dst[c][r] = src[r][c] for a [rows, cols] fp32 matrix (leading dimensions lds >= cols, ldd >= rows):
+ * the NRMS table-gradient GEMM's k-contiguous copy of the joint [keyProject; valueProject] weight
+ * (models/Modules/Attention.py:107-108), so both of its operands take the K-contiguous loaders. */
+int nr_transpose_f32(const float* src, int64_t lds, int64_t rows, int64_t cols, float* dst, int64_t ldd,
+                     hipStream_t stream);
+
 /* out[c] += Σ_r x[r][c]  (bias gradients; out pre-zeroed or accumulated).  Deterministic two-pass
  * reduction (no atomics) through `work` of nr_colsum_workspace(rows, cols) bytes. */
 int64_t nr_colsum_workspace(int64_t rows, int64_t cols);

@@ -427,6 +427,24 @@ __global__ __launch_bounds__(256) void rows_add_ordered_kernel(const float* __re
   }
 }
 
+// dst[c][r] = src[r][c]: 64 x 64 tiles through LDS (row pad of one float: the column reads are
+// conflict-free), coalesced float reads and writes.  The NRMS table dgrad's k-contiguous weight.
+__global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ src, int64_t lds, int64_t rows,
+                                                        int64_t cols, float* __restrict__ dst, int64_t ldd) {
+  __shared__ float t[64][65];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t r = r0 + i, c = c0 + tx;
+    t[i][tx] = r < rows && c < cols ? src[r * lds + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, r = r0 + tx;
+    if (c < cols && r < rows) dst[c * ldd + r] = t[tx][i];
+  }
+}
+
 // Column sums, deterministic two-pass: pass 1 = one block per (64-column chunk, row block), each of
 // its 4 waves strides the block's rows with its 64 lanes on 64 consecutive columns (256-B row
 // segments, 8 loads in flight), the waves combine in LDS and store the block's partial row; pass 2
@@ -634,6 +652,18 @@ extern "C" int nr_rows_add_ordered(const float* dout, int64_t ldo, int64_t V, in
   if (n == 0) return NR_OK;
   hipLaunchKernelGGL(rows_add_ordered_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, stream, dout, ldo, V, E,
                      idx, n, padding_idx, dtable, ldt);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_transpose_f32(const float* src, int64_t lds, int64_t rows, int64_t cols, float* dst, int64_t ldd,
+                                hipStream_t stream) {
+  if (rows < 0 || cols < 0 || lds < cols || ldd < rows || rows > (int64_t)65535 * 64 || cols > ((int64_t)1 << 31))
+    return NR_EINVAL(0);
+  if (!src || !dst) return NR_EINVAL(1);
+  if (rows == 0 || cols == 0) return NR_OK;
+  hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64)), dim3(256), 0,
+                     stream, src, lds, rows, cols, dst, ldd);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

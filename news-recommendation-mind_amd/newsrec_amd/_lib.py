@@ -103,6 +103,7 @@ _SIGS = {
     "nr_embedding_fwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr],
     "nr_embedding_bwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_ptr],
     "nr_rows_add_ordered": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],
+    "nr_transpose_f32": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_ptr],
     "nr_colsum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr],
     "nr_colsum_ws": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr],
     "nr_colsum_workspace": [c_i64, c_i64],

@@ -563,7 +563,7 @@ class MHANewsFn(torch.autograd.Function):
             if ctx.needs_input_grad[0]:
                 dtable = torch.zeros(V, E, device=table.device)
                 # distinct rows (M = U, not U_pad: no duplicate pad ids): plain row stores
-                wt = w_cat.t().contiguous() if PROJ_DGRAD_KC else None   # kept alive by the closure
+                wt = K.transpose(w_cat) if PROJ_DGRAD_KC else None   # kept alive by the closure
 
                 def dgrad(dtable=dtable):   # bound now: the hook below may take the name's buffer
                     w_b = K.operand(wt, L.KCONTIG) if wt is not None else K.operand(w_cat, L.MNCONTIG)

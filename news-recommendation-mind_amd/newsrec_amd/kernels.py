@@ -713,6 +713,21 @@ def embedding_bwd(dout, idx, dtable, padding_idx=-1):
            -1 if padding_idx is None else padding_idx, L.ptr(dtable), L.stream_ptr(dtable))
 
 
+def transpose(src, out=None):
+    """src [rows, cols] (row-major, any leading dimension) -> out [cols, rows] contiguous
+    (nr_transpose_f32)."""
+    _f32(src, out)
+    if src.dim() != 2 or src.stride(1) != 1:
+        raise L.HipError("transpose: a row-major 2-D source required")
+    rows, cols = src.shape
+    if out is None:
+        out = torch.empty(cols, rows, device=src.device)
+    elif out.shape != (cols, rows) or out.stride(1) != 1:
+        raise L.HipError("transpose: out must be a row-major [cols, rows] matrix")
+    L.call("nr_transpose_f32", L.ptr(src), src.stride(0), rows, cols, L.ptr(out), out.stride(0), L.stream_ptr(src))
+    return out
+
+
 def rows_add_ordered(dout, idx, dtable, padding_idx=None):
     """dtable[idx[i]] += dout[i], each id's rows summed in ascending i by one wave (nr_rows_add_ordered:
     deterministic with duplicate ids, for row-sparse gradients of few rows).  dout [n, E] and dtable

@@ -177,3 +177,12 @@ def test_rows_add_ordered_duplicates_fixed_order():
             s = s + src[j]
         assert torch.equal(outs[0][t], base[t] + s), t
     assert torch.equal(outs[0][17], base[17])
+
+
+@pytest.mark.parametrize("rows,cols", [(1152, 768), (1, 5), (130, 67)])
+def test_transpose(rows, cols):
+    """nr_transpose_f32 (the NRMS table dgrad's k-contiguous weight): exact, ragged tiles, a source
+    leading dimension wider than its columns."""
+    from newsrec_amd import kernels as K
+    src = torch.randn(rows, cols + 3, device="cuda")[:, :cols]
+    assert torch.equal(K.transpose(src), src.t().contiguous())
