@@ -477,6 +477,20 @@ int nr_embedding_bwd(const float* dout, int64_t V, int64_t E, const int64_t* idx
 int nr_rows_add_ordered(const float* dout, int64_t ldo, int64_t V, int64_t E, const int64_t* idx, int64_t n,
                         int64_t padding_idx, float* dtable, int64_t ldt, hipStream_t stream);
 
+/* XSoftmax (models/Modules/Attention.py:56-80) over the last dimension: out = softmax of x's rows
+ * with the entries whose mask (same [rows, cols] shape, enum nr_mask_dtype) is zero excluded, those
+ * entries exactly 0, a fully masked row all 0.  Backward (_softmax_backward_data, Attention.py:77-80):
+ * dx = y (dy - Σ_row dy y).  Contiguous [rows, cols] tensors, one wave per row. */
+int nr_xsoftmax_fwd(const float* x, const void* mask, int32_t mask_dtype, int64_t rows, int64_t cols,
+                    float* out, hipStream_t stream);
+int nr_xsoftmax_bwd(const float* y, const float* dy, int64_t rows, int64_t cols, float* dx, hipStream_t stream);
+
+/* dst[i][:] = src[idx[i]][:] for rows of `cols` floats (any width; leading dimensions lds / ldd): the
+ * news-table rows of the fast-eval history slots (predict_fast's encode_user over the cached table,
+ * TwoTowerBaseModel.py:78-83 / Manager.py:516). */
+int nr_gather_rows_f32(const float* src, int64_t lds, int64_t V, const int64_t* idx, int64_t n, int64_t cols,
+                       float* dst, int64_t ldd, hipStream_t stream);
+
 /* dst[c][r] = src[r][c] for a [rows, cols] fp32 matrix (leading dimensions lds >= cols, ldd >= rows):
  * the NRMS table-gradient GEMM's k-contiguous copy of the joint [keyProject; valueProject] weight
  * (models/Modules/Attention.py:107-108), so both of its operands take the K-contiguous loaders. */

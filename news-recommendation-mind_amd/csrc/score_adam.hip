@@ -427,6 +427,58 @@ __global__ __launch_bounds__(256) void rows_add_ordered_kernel(const float* __re
   }
 }
 
+// XSoftmax (models/Modules/Attention.py:56-80) along rows of `cols` values, one wave per row:
+// masked entries -> -inf, softmax, masked entries set to exactly 0 (a fully masked row is all zero);
+// the backward is _softmax_backward_data: dx = y (dy - Σ dy y).
+__global__ __launch_bounds__(256) void xsoftmax_fwd_kernel(const float* __restrict__ x, const void* __restrict__ mask,
+                                                           int mdt, int64_t rows, int64_t cols,
+                                                           float* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float* xr = x + r * cols;
+  float mx = -INFINITY;
+  for (int64_t c = lane; c < cols; c += 64)
+    if (nr_mask_at(mask, mdt, r * cols + c)) mx = fmaxf(mx, xr[c]);
+  mx = nr_wave_max(mx);
+  float s = 0.f;
+  for (int64_t c = lane; c < cols; c += 64)
+    if (nr_mask_at(mask, mdt, r * cols + c)) s += __expf(xr[c] - mx);
+  s = nr_wave_sum(s);
+  const float inv = s > 0.f ? 1.f / s : 0.f;   // no unmasked entry: the row is all zero
+  for (int64_t c = lane; c < cols; c += 64)
+    out[r * cols + c] = nr_mask_at(mask, mdt, r * cols + c) ? __expf(xr[c] - mx) * inv : 0.f;
+}
+
+__global__ __launch_bounds__(256) void xsoftmax_bwd_kernel(const float* __restrict__ y, const float* __restrict__ dy,
+                                                           int64_t rows, int64_t cols, float* __restrict__ dx) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  float s = 0.f;
+  for (int64_t c = lane; c < cols; c += 64) s += dy[r * cols + c] * y[r * cols + c];
+  s = nr_wave_sum(s);
+  for (int64_t c = lane; c < cols; c += 64) dx[r * cols + c] = y[r * cols + c] * (dy[r * cols + c] - s);
+}
+
+// dst[i] = src[idx[i]] rows of `cols` floats (any width; float4 when the rows allow), one wave per row:
+// the fast-eval history gather (the news table rows of each history slot, Manager.py:516).
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restrict__ src, int64_t lds,
+                                                          const int64_t* __restrict__ idx, int64_t n, int64_t cols,
+                                                          float* __restrict__ dst, int64_t ldd, int vec4) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  const float* s = src + idx[i] * lds;
+  float* d = dst + i * ldd;
+  if (vec4) {
+    for (int64_t c = lane; c < cols / 4; c += 64)
+      reinterpret_cast<float4*>(d)[c] = reinterpret_cast<const float4*>(s)[c];
+  } else {
+    for (int64_t c = lane; c < cols; c += 64) d[c] = s[c];
+  }
+}
+
 // dst[c][r] = src[r][c]: 64 x 64 tiles through LDS (row pad of one float: the column reads are
 // conflict-free), coalesced float reads and writes.  The NRMS table dgrad's k-contiguous weight.
 __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ src, int64_t lds, int64_t rows,
@@ -652,6 +704,40 @@ extern "C" int nr_rows_add_ordered(const float* dout, int64_t ldo, int64_t V, in
   if (n == 0) return NR_OK;
   hipLaunchKernelGGL(rows_add_ordered_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, stream, dout, ldo, V, E,
                      idx, n, padding_idx, dtable, ldt);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_xsoftmax_fwd(const float* x, const void* mask, int32_t mask_dtype, int64_t rows, int64_t cols,
+                               float* out, hipStream_t stream) {
+  if (rows < 0 || cols < 0 || mask_dtype < NR_MASK_U8 || mask_dtype > NR_MASK_F32) return NR_EINVAL(0);
+  if (!x || !mask || !out) return NR_EINVAL(1);
+  if (rows == 0 || cols == 0) return NR_OK;
+  hipLaunchKernelGGL(xsoftmax_fwd_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, x, mask, mask_dtype,
+                     rows, cols, out);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_xsoftmax_bwd(const float* y, const float* dy, int64_t rows, int64_t cols, float* dx,
+                               hipStream_t stream) {
+  if (rows < 0 || cols < 0) return NR_EINVAL(0);
+  if (!y || !dy || !dx) return NR_EINVAL(1);
+  if (rows == 0 || cols == 0) return NR_OK;
+  hipLaunchKernelGGL(xsoftmax_bwd_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, y, dy, rows, cols,
+                     dx);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
+extern "C" int nr_gather_rows_f32(const float* src, int64_t lds, int64_t V, const int64_t* idx, int64_t n,
+                                  int64_t cols, float* dst, int64_t ldd, hipStream_t stream) {
+  if (n < 0 || cols < 0 || V < 1 || lds < cols || ldd < cols) return NR_EINVAL(0);
+  if (!src || !idx || !dst) return NR_EINVAL(1);
+  if (n == 0 || cols == 0) return NR_OK;
+  const int vec4 = ((cols | lds | ldd) & 3) == 0 && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, stream, src, lds, idx, n, cols, dst,
+                     ldd, vec4);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

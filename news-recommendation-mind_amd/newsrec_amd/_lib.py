@@ -104,6 +104,9 @@ _SIGS = {
     "nr_embedding_bwd": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_ptr],
     "nr_rows_add_ordered": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],
     "nr_transpose_f32": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_ptr],
+    "nr_xsoftmax_fwd": [c_ptr, c_ptr, c_i32, c_i64, c_i64, c_ptr, c_ptr],
+    "nr_xsoftmax_bwd": [c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_ptr],
+    "nr_gather_rows_f32": [c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],
     "nr_colsum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr],
     "nr_colsum_ws": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr],
     "nr_colsum_workspace": [c_i64, c_i64],

@@ -7,12 +7,12 @@
 fp32 MFMA GEMM and the attention core in ``nr_mha_attn_fwd``.  The towers do not call it:
 they run the whole encoder as one fused autograd Function (functions.py).
 """
-import math
 
 import torch
 from torch import nn
 
 from . import _lib as L
+from . import kernels as K
 from .functions import MHAFn, AttnPoolFn
 
 
@@ -26,28 +26,84 @@ def get_attn_mask(attn_mask):
 
 class XSoftmax(torch.autograd.Function):
     """Attention.py:56-80 — masked softmax whose masked (and fully masked) entries are exactly
-    zero.  Interface kept for callers that use it directly; the fused kernels inline it."""
+    zero, on nr_xsoftmax_fwd/bwd (one wave per row of the softmax dimension).  The mask broadcasts
+    to the input's shape as in the reference; ``dim`` is the last dimension (every reference call,
+    Attention.py:22,139)."""
 
     @staticmethod
     def forward(ctx, input, mask, dim):
-        keep = mask.bool()
-        out = torch.softmax(input.masked_fill(~keep, float("-inf")), dim).masked_fill(~keep, 0.0)
-        ctx.dim = dim
+        L.require_gpu(input)
+        if dim not in (-1, input.dim() - 1):
+            raise L.HipError("XSoftmax: the HIP kernel normalises over the last dimension (dim=-1)")
+        x = input.contiguous()
+        m = mask.to(x.device)
+        m = m if m.shape == x.shape else m.expand(x.shape)
+        m = m.contiguous() if m.dtype in (torch.uint8, torch.bool, torch.int64, torch.float64, torch.float32) \
+            else m.to(torch.uint8).contiguous()
+        out = torch.empty_like(x)
+        K.xsoftmax_fwd(x, m, out)
         ctx.save_for_backward(out)
         return out
 
     @staticmethod
     def backward(ctx, grad):
         (out,) = ctx.saved_tensors
-        return torch._softmax_backward_data(grad, out, ctx.dim, out.dtype), None, None
+        dx = torch.empty_like(out)
+        K.xsoftmax_bwd(out, grad.contiguous(), dx)
+        return dx, None, None
+
+
+class _QueryPoolFn(torch.autograd.Function):
+    """scaled_dp_attention with one learned query (every reference call: CNN.py:46, Pooling.py:22-24,
+    MHA.py:38,72): out[s] = Σ_l XSoftmax(q · key[s, l] / sqrt(D), mask[s, l]) value[s, l] on
+    nr_attn_pool_fwd/bwd.  rows [S * L, D]; key None = the value rows."""
+
+    @staticmethod
+    def forward(ctx, q, key, value, mask, S, Lq):
+        D = q.numel()
+        probs = torch.empty(S * Lq, device=value.device)
+        out = torch.empty(S, D, device=value.device)
+        K.attn_pool_fwd(value, q, mask, S, Lq, out, probs, key=key)
+        ctx.save_for_backward(q, key, value, mask, probs)
+        ctx.cfg = (S, Lq)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, key, value, mask, probs = ctx.saved_tensors
+        S, Lq = ctx.cfg
+        dv = torch.empty_like(value)
+        dk = torch.empty_like(key) if key is not None else None
+        dq = torch.zeros(q.numel(), device=q.device)
+        K.attn_pool_bwd(value, q, mask, S, Lq, probs, dout.contiguous(), dv, dq, key=key, dk=dk)
+        return dq.view_as(q), dk, dv, None, None, None
 
 
 def scaled_dp_attention(query, key, value, attn_mask=None):
-    """Attention.py:5-30: softmax(q kᵀ / sqrt(d)) v with an optional XSoftmax mask."""
+    """Attention.py:5-30: softmax(q kᵀ / sqrt(d)) v with an optional XSoftmax mask, for a learned
+    query of one row ([1, D] or [..., 1, D] broadcast over the batch) -- the form every reference
+    call site uses (learned-query pooling) -- on the pooling kernels.  Other query shapes raise (the
+    encoders run multi-query attention inside their fused kernels)."""
+    L.require_gpu(key, value)
     assert query.shape[-1] == key.shape[-1]
-    s = torch.matmul(query, key.transpose(-2, -1)) / math.sqrt(query.shape[-1])
-    p = torch.softmax(s, -1) if attn_mask is None else XSoftmax.apply(s, attn_mask, -1)
-    return torch.matmul(p, value)
+    D = query.shape[-1]
+    if query.numel() != D or key.shape != value.shape or key.shape[-2] > 64:
+        raise L.HipError("scaled_dp_attention: the HIP path takes one query row over <= 64 keys with value "
+                         "rows of the key's shape (got q %s, k %s, v %s)" % (tuple(query.shape), tuple(key.shape),
+                                                                          tuple(value.shape)))
+    lead = key.shape[:-2]
+    Lq = key.shape[-2]
+    S = int(torch.Size(lead).numel())
+    v = value.reshape(S * Lq, D).contiguous()
+    k = None if key is value else key.reshape(S * Lq, D).contiguous()
+    if attn_mask is None:
+        m = torch.ones(S * Lq, dtype=torch.uint8, device=v.device)
+    else:
+        m = attn_mask.to(v.device).expand(*lead, 1, Lq).reshape(S * Lq)
+        m = m.contiguous() if m.dtype in (torch.uint8, torch.bool, torch.int64, torch.float64, torch.float32) \
+            else m.to(torch.uint8).contiguous()
+    out = _QueryPoolFn.apply(query.reshape(D), k, v, m, S, Lq)
+    return out.view(*lead, 1, D)
 
 
 def _joined_view(a, b):

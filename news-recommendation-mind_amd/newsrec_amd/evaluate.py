@@ -27,6 +27,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib as L
+from . import kernels as K
 
 
 def _chunk_range(n_chunks, world, rank):
@@ -115,7 +116,7 @@ def user_reprs(model, table, batch, history_from_table=True, cache=None):
                 cache["Y"] = enc.project_rows(table)
             user = enc.forward_rows(cache["Y"], batch["his_id"], batch["his_mask"], B, NH)
         else:
-            his = table.index_select(0, batch["his_id"].reshape(-1)).view(B, NH, -1)
+            his = K.gather_rows(table, batch["his_id"].reshape(-1).contiguous()).view(B, NH, -1)
             user = model._user_from_his(his, batch)
     user = user.reshape(user.shape[0], -1)
     if user.stride(-1) != 1 or user.stride(0) != user.shape[1]:

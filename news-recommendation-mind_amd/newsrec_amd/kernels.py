@@ -713,6 +713,41 @@ def embedding_bwd(dout, idx, dtable, padding_idx=-1):
            -1 if padding_idx is None else padding_idx, L.ptr(dtable), L.stream_ptr(dtable))
 
 
+def xsoftmax_fwd(x, mask, out):
+    """nr_xsoftmax_fwd over the last dimension of contiguous x / mask (mask: same shape, any mask dtype)."""
+    _f32(x, out)
+    if not x.is_contiguous() or not out.is_contiguous() or out.shape != x.shape:
+        raise L.HipError("xsoftmax: contiguous x / out of one shape required")
+    cols = x.shape[-1] if x.dim() else 1
+    mp, mdt = mask_arg(mask, x.numel())
+    L.call("nr_xsoftmax_fwd", L.ptr(x), mp, mdt, x.numel() // max(cols, 1), cols, L.ptr(out), L.stream_ptr(x))
+
+
+def xsoftmax_bwd(y, dy, dx):
+    _f32(y, dy, dx)
+    for t in (y, dy, dx):
+        if not t.is_contiguous() or t.shape != y.shape:
+            raise L.HipError("xsoftmax_bwd: contiguous tensors of one shape required")
+    cols = y.shape[-1] if y.dim() else 1
+    L.call("nr_xsoftmax_bwd", L.ptr(y), L.ptr(dy), y.numel() // max(cols, 1), cols, L.ptr(dx), L.stream_ptr(y))
+
+
+def gather_rows(src, idx, out=None):
+    """out[i] = src[idx[i]] (nr_gather_rows_f32): src [V, cols] row-major, idx int64 [n]."""
+    _f32(src, out)
+    _check_rows(idx, None, "gather_rows")
+    if src.dim() != 2 or src.stride(1) != 1:
+        raise L.HipError("gather_rows: a row-major 2-D source required")
+    n = idx.numel()
+    if out is None:
+        out = torch.empty(n, src.shape[1], device=src.device)
+    elif out.dim() != 2 or out.shape != (n, src.shape[1]) or out.stride(1) != 1:
+        raise L.HipError("gather_rows: out must be a row-major [n, cols] matrix")
+    L.call("nr_gather_rows_f32", L.ptr(src), src.stride(0), src.shape[0], L.ptr(idx), n, src.shape[1], L.ptr(out),
+           out.stride(0), L.stream_ptr(src))
+    return out
+
+
 def transpose(src, out=None):
     """src [rows, cols] (row-major, any leading dimension) -> out [cols, rows] contiguous
     (nr_transpose_f32)."""

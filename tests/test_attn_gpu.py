@@ -55,3 +55,60 @@ def test_mha_attn(L, heads, dk, dv, mdt):
                    dout.reshape(n * L, -1).float().cuda(), dqk, dvv)
     torch.testing.assert_close(dqk.cpu().double().view(n, L, -1), qk.grad, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dvv.cpu().double().view(n, L, -1), v.grad, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape,mshape", [((4, 3, 30), (4, 1, 30)), ((2, 12, 30, 30), (2, 1, 30, 30)), ((5, 50), (5, 50))])
+def test_xsoftmax_public(shape, mshape):
+    """attention.XSoftmax (Attention.py:56-80) on nr_xsoftmax_fwd/bwd against the float64 restatement:
+    masked entries exactly zero, a fully masked row all zero, the backward _softmax_backward_data."""
+    from newsrec_amd.attention import XSoftmax
+    from oracle import restatement as R
+    torch.manual_seed(len(shape))
+    x = torch.randn(*shape, device="cuda", requires_grad=True)
+    mask = (torch.rand(*mshape, device="cuda") > 0.3).long()
+    mask.view(-1, mshape[-1])[0] = 0                       # a fully masked row
+    y = XSoftmax.apply(x, mask, -1)
+    x64 = x.detach().cpu().double().requires_grad_()
+    want = R.xsoftmax(x64, mask.cpu().expand(shape), -1)
+    torch.testing.assert_close(y.detach().cpu().double(), want, rtol=0, atol=1e-6)
+    assert bool((y.detach()[mask.expand(shape) == 0] == 0).all())
+    g = torch.randn(*shape, device="cuda")
+    y.backward(g)
+    want.backward(g.cpu().double())
+    torch.testing.assert_close(x.grad.cpu().double(), x64.grad, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("sep_key", [False, True])
+def test_scaled_dp_attention_public(sep_key):
+    """attention.scaled_dp_attention (Attention.py:5-30) in its reference form -- one learned query over
+    [..., L, D] keys / values with a [..., 1, L] mask (CNN.py:46, Pooling.py:22-24) -- on the pooling
+    kernels: values and every gradient against the float64 restatement."""
+    from newsrec_amd.attention import scaled_dp_attention
+    from oracle import restatement as R
+    torch.manual_seed(7)
+    B, n, Lk, D = 3, 4, 30, 150
+    q = torch.randn(1, D, device="cuda", requires_grad=True)
+    v = torch.randn(B, n, Lk, D, device="cuda", requires_grad=True)
+    k = torch.randn(B, n, Lk, D, device="cuda", requires_grad=True) if sep_key else v
+    m = (torch.rand(B, n, 1, Lk, device="cuda") > 0.2).long()
+    m[0, 0] = 0
+    out = scaled_dp_attention(q, k, v, m)
+    ts = [t.detach().cpu().double().requires_grad_() for t in (q, k, v)] if sep_key else \
+        [t.detach().cpu().double().requires_grad_() for t in (q, v)]
+    q64, k64, v64 = (ts[0], ts[1], ts[2]) if sep_key else (ts[0], ts[1], ts[1])
+    want = R.scaled_dp_attention(q64, k64, v64, m.cpu())
+    torch.testing.assert_close(out.detach().cpu().double(), want, rtol=0, atol=1e-5)
+    g = torch.randn_like(out)
+    out.backward(g)
+    want.backward(g.cpu().double())
+    for a, b in zip([q, k, v] if sep_key else [q, v], ts):
+        torch.testing.assert_close(a.grad.cpu().double(), b.grad, rtol=0, atol=1e-4)
+
+
+def test_gather_rows():
+    """nr_gather_rows_f32 (the fast-eval history gather): widths with and without float4 rows."""
+    from newsrec_amd import kernels as K
+    for cols in (150, 384, 3):
+        t = torch.randn(500, cols, device="cuda")
+        idx = torch.randint(0, 500, (777,), device="cuda")
+        assert torch.equal(K.gather_rows(t, idx), t[idx])
