@@ -537,9 +537,21 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
     // unrolled by two: the register sets alternate statically; a wave with no live rows / columns
     // runs the same loads, splits, stores and barriers without fragment reads or MFMAs
     auto kloop = [&](auto live_t) {
-      for (int kt = 0; kt < nt; kt += 2) {
-        ktile(live_t, S1{}, kt, 0);
-        if (kt + 1 < nt) ktile(live_t, S0{}, kt + 1, 1);
+      if constexpr (NP == 3) {
+        // bf16x6 units always hold an even number of 16-deep k-tiles (the launcher takes K % 32 == 0
+        // only; k chunks are multiples of 32): the two-tile body has no branch, so the loop head has
+        // one incoming state and hipcc's wait counts at the first split wait for that set's loads
+        // only (vmcnt(7..4)), not for the loads issued one tile earlier as well (the merged
+        // conditional form waited vmcnt(3..0): one tile of latency cover instead of two)
+        for (int kt = 0; kt < nt; kt += 2) {
+          ktile(live_t, S1{}, kt, 0);
+          ktile(live_t, S0{}, kt + 1, 1);
+        }
+      } else {
+        for (int kt = 0; kt < nt; kt += 2) {
+          ktile(live_t, S1{}, kt, 0);
+          if (kt + 1 < nt) ktile(live_t, S0{}, kt + 1, 1);
+        }
       }
     };
     if (live)

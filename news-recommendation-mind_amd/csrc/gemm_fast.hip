@@ -188,7 +188,9 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
     // bf16 split-K (atomic) launches take the big kernel too: its fewer, larger units halve the operand
     // re-reads and keep three k-tiles of loads in flight (CNN conv weight gradient 200 -> 138 us)
     const int bb = big_bn(M, N, K, splits, resplit, m_dev != nullptr, kmin);
-    const int BN = tailed ? 256 : (bb > 0 ? bb : 0);
+    // the bf16x6 big kernel runs its k-loop two 16-deep k-tiles per iteration with no branch: every
+    // unit's k range must be a multiple of 32 (k chunks are; K must be)
+    const int BN = prec == NR_GEMM_BF16X6 && K % 32 != 0 ? 0 : (tailed ? 256 : (bb > 0 ? bb : 0));
     if (BN) {
       Args gb = g;
       if (tailed) gb.tail = 16;

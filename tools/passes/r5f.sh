@@ -2,7 +2,7 @@
 # processes, alternating), the NRMS dgrad k-contiguous A/B with its kernel trace.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-r5f}; mkdir -p $O
-timeout -k 10 700 python -u -m pytest tests/test_bert_gpu.py tests/test_row_grad_gpu.py tests/test_fullsize_gpu.py::test_xformer_12_layers_step_vs_oracle tests/test_fullsize_cnn_gpu.py::test_bf16_cnn_attn_fullsize_step_vs_oracle -v -s --timeout 600 --timeout-method thread > $O/tests.log 2>&1; echo "tests rc=$?"
+timeout -k 10 700 python -u -m pytest tests/test_bert_gpu.py tests/test_row_grad_gpu.py tests/test_attn_gpu.py tests/test_fullsize_gpu.py::test_xformer_12_layers_step_vs_oracle tests/test_fullsize_cnn_gpu.py::test_bf16_cnn_attn_fullsize_step_vs_oracle -v -s --timeout 600 --timeout-method thread > $O/tests.log 2>&1; echo "tests rc=$?"
 for i in 1 2; do
   for kb in 1 0; do
     timeout -k 10 200 python tools/legs_only.py xformer --steps 5 --set bert.ATTN_KEEP_BITS=$kb > $O/xf_kb${kb}_$i.json 2>> $O/xf.err || exit 2
