@@ -231,7 +231,7 @@ def test_xformer_12_layers_step_vs_oracle():
     within 2 lr (all but a rounding-level handful within 1e-3 lr).  Gradients are checked against the
     oracle run in float64 (see below).  Dropout 0 (BertFn's dropout sites are checked against their
     kernels in tests/test_bert_gpu.py).  The key biases' gradient is zero in exact arithmetic (softmax
-    cancels q . b_k), so it is held to its layer's query-bias scale."""
+    cancels q . b_k), so it is held to its layer's key-weight gradient scale."""
     import bench
     from newsrec_amd import _lib as Lb, kernels as Kn
     from newsrec_amd.bert import BertConfig
@@ -295,7 +295,9 @@ def test_xformer_12_layers_step_vs_oracle():
         assert got is not None and g32 is not None, n
         scale = max(want_g.abs().max().item(), 1e-12)
         if n.endswith("attention.self.key.bias"):
-            scale = P64[n.replace(".key.bias", ".query.bias")].grad.abs().max().item()
+            # exact value 0: the column sums of dK, whose terms the key weight's gradient X^T dK
+            # carries over the unit-scale LayerNorm output X -- that gradient's max is the terms' scale
+            scale = P64[n.replace(".key.bias", ".key.weight")].grad.abs().max().item()
         gerr = (got.detach().cpu().double() - want_g).abs().max().item()
         e32 = (g32.double() - want_g).abs().max().item()
         worst = max(worst, gerr / scale)
