@@ -11,6 +11,7 @@ call uses the same functions with the embeddings as the "table" and identity row
 """
 import functools
 import os
+import threading
 
 import torch
 
@@ -120,10 +121,32 @@ class _ZeroArena:
 ZERO_ARENA = _ZeroArena()
 
 
+_CALLER_GRAD = threading.local()
+
+
+class _GradAwareFn(torch.autograd.Function):
+    """A Function whose forward may ask ``_backward_possible``: torch runs forward() with grad mode
+    OFF whatever the caller's mode, so apply() records the caller's mode for it (per thread, restored
+    on exit, so nested applies see their own caller's)."""
+
+    @classmethod
+    def apply(cls, *args, **kwargs):
+        prev = getattr(_CALLER_GRAD, "on", None)
+        _CALLER_GRAD.on = torch.is_grad_enabled()
+        try:
+            return super().apply(*args, **kwargs)
+        finally:
+            _CALLER_GRAD.on = prev
+
+
 def _backward_possible(ctx):
-    """A backward can follow this forward: autograd is recording (not torch.no_grad(), where
-    needs_input_grad still reports the parameters' requires_grad) and some input wants a gradient."""
-    return torch.is_grad_enabled() and any(ctx.needs_input_grad)
+    """A backward can follow this forward (of a _GradAwareFn): its caller had autograd recording (not
+    torch.no_grad(), where needs_input_grad still reports the parameters' requires_grad) and some input
+    wants a gradient."""
+    on = getattr(_CALLER_GRAD, "on", None)
+    if on is None:
+        raise RuntimeError("_backward_possible needs a _GradAwareFn forward")
+    return on and any(ctx.needs_input_grad)
 
 
 def _reserve_zeros(ctx, dev, *shapes):
@@ -468,7 +491,7 @@ WGRAD_DEFER_HOOK = _WgradDeferHook()
 
 # ---------------------------------------------------------------------- MHA news encoder
 
-class MHANewsFn(torch.autograd.Function):
+class MHANewsFn(_GradAwareFn):
     """MHA_Encoder.forward (models/Encoders/MHA.py:21-39) on gathered token rows:
     Y = X [Wk; Wv]ᵀ + b  (one GEMM, gather fused)  ->  tied-QK 12-head attention
     -> LayerNorm -> Dropout -> learned-query pooling.   Returns (news [n, H], tok [T, H] or None)."""
@@ -706,7 +729,7 @@ class CNNWeightsFn(torch.autograd.Function):
         return dcw, dwq, dbq, None
 
 
-class CNNNewsRowsFn(torch.autograd.Function):
+class CNNNewsRowsFn(_GradAwareFn):
     """CNN_Encoder.forward (models/Encoders/CNN.py:30-50) over DISTINCT word rows.
 
     The k = 3 Conv1d is linear per tap and the embedding lookup (BERT.py:39) is a row gather, so
@@ -823,7 +846,7 @@ class CNNNewsRowsFn(torch.autograd.Function):
 
 # ---------------------------------------------------------------------- pooling user encoder
 
-class AttnPoolFn(torch.autograd.Function):
+class AttnPoolFn(_GradAwareFn):
     """Attention_Pooling.forward (models/Encoders/Pooling.py:12-25): learned-query pooling of
     the history with the history mask.  x: [B*N, H] rows view; returns [B, H]."""
 
@@ -859,7 +882,7 @@ class AttnPoolFn(torch.autograd.Function):
 
 # ---------------------------------------------------------------------- MHA over rows
 
-class MHAFn(torch.autograd.Function):
+class MHAFn(_GradAwareFn):
     """MultiheadAttention.forward (models/Modules/Attention.py:115-147) on plain rows:
     Y = x [Wk; Wv]ᵀ + b (GEMM) -> tied-QK attention core (pairwise token mask).
     x: [nseq*L, D] -> [nseq*L, heads*dv].  Used by MHA_User_Encoder (MHA.py:58-75) and the
@@ -913,7 +936,7 @@ class MHAFn(torch.autograd.Function):
 
 # ---------------------------------------------------------------------- recurrent user encoders
 
-class RNNUserFn(torch.autograd.Function):
+class RNNUserFn(_GradAwareFn):
     """RNN_User_Encoder (RNN.py:50-73) and LSTUR_User_Encoder (RNN.py:88-104):
     gx = x W_ihᵀ + b_ih for all steps (GEMM) -> sequential cell kernel -> h at step len-1.
     LSTUR: reverse=True, mask=None (all N steps), h0 = user_table[h0_idx]."""

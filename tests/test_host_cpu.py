@@ -37,7 +37,11 @@ def test_zero_arena_fallbacks():
     from newsrec_amd import functions as F
     dev = torch.device("cpu")
     ctx = _Ctx(needs=False)
-    F._reserve_zeros(ctx, dev, (8,))
+    F._CALLER_GRAD.on = True   # what _GradAwareFn.apply records
+    try:
+        F._reserve_zeros(ctx, dev, (8,))
+    finally:
+        F._CALLER_GRAD.on = None
     assert ctx.zero_tok is None
     (z,) = F._backward_zeros(ctx, dev, (8,))
     assert z.shape == (8,) and z.abs().sum().item() == 0.0
@@ -87,3 +91,41 @@ def test_split_rows_offers_and_join():
     a, b = SplitRowsFn.apply(x, 3)
     (2.0 * a.sum()).backward()
     assert torch.equal(x.grad[3:], torch.zeros(4, 5)) and torch.equal(x.grad[:3], torch.full((3, 5), 2.0))
+
+
+def test_backward_possible_sees_the_callers_grad_mode():
+    """torch runs Function.forward with grad mode off; _GradAwareFn.apply records the caller's mode, so
+    a forward saves backward-only state (the split MHA backward's O rows, the arena's reservations)
+    exactly when autograd is recording and an input wants a gradient."""
+    from newsrec_amd import functions as F
+    seen = []
+
+    class Probe(F._GradAwareFn):
+        @staticmethod
+        def forward(ctx, t):
+            assert not torch.is_grad_enabled()
+            seen.append(F._backward_possible(ctx))
+            return t * 2
+
+        @staticmethod
+        def backward(ctx, g):
+            return g * 2
+
+    x = torch.randn(3, requires_grad=True)
+    Probe.apply(x).sum().backward()
+    with torch.no_grad():
+        Probe.apply(x)
+    Probe.apply(x.detach())
+    with torch.enable_grad():
+        with torch.no_grad():
+            with torch.enable_grad():
+                Probe.apply(x)
+    assert seen == [True, False, False, True]
+    assert torch.equal(x.grad, torch.full((3,), 2.0))
+    assert getattr(F._CALLER_GRAD, "on", None) is None   # restored after each apply
+    ctx = _Ctx()
+    try:
+        F._backward_possible(ctx)
+        raise AssertionError("outside a _GradAwareFn forward it must raise")
+    except RuntimeError:
+        pass

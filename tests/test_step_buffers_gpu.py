@@ -61,3 +61,33 @@ def test_retained_graph_second_backward(cfg):
     loss.backward(retain_graph=True)
     loss.backward()
     _check(g, model, mult=2.0)
+
+
+def test_nrms_training_forward_saves_for_the_split_backward(monkeypatch):
+    """A training forward (autograd recording) saves the attention output O and the arena reservations,
+    so the backward runs the split MHA backward (nr_mha_pool_bwd with o and dob) and one zero fill; under
+    torch.no_grad() nothing backward-only is saved.  (torch runs Function.forward with grad mode off:
+    the gate must look at the CALLER's mode, functions._GradAwareFn.)"""
+    from newsrec_amd import functions as F, kernels as Kn
+    calls = []
+    fwd, bwd = Kn.mha_pool_fwd, Kn.mha_pool_bwd
+
+    def rec_fwd(*a, **kw):
+        calls.append(("fwd", kw.get("oout") is not None))
+        return fwd(*a, **kw)
+
+    def rec_bwd(*a, **kw):
+        calls.append(("bwd", kw.get("o") is not None and kw.get("dob") is not None))
+        return bwd(*a, **kw)
+    monkeypatch.setattr(Kn, "mha_pool_fwd", rec_fwd)
+    monkeypatch.setattr(Kn, "mha_pool_bwd", rec_bwd)
+    g, model, x = _setup("nrms")
+    model.train()
+    _, loss = model.forward_loss(x)
+    loss.backward()
+    assert calls and all(ok for _, ok in calls) and ("bwd", True) in calls, calls
+    calls.clear()
+    with torch.no_grad():
+        model.forward_loss(x)
+    assert calls and not any(ok for _, ok in calls), calls
+    _check(g, model)
