@@ -124,7 +124,11 @@ int nr_gemm_f32_dyn_cus(int64_t M, int64_t N, int64_t K, const nr_operand* A, co
  * the static form).  When a split-K NR_EPI_ATOMIC contraction runs on the 256 x 256 kernel and
  * `work` (16-B aligned, work_elems floats) holds its partial tiles, every split stores its partial
  * tile with plain stores and one reduction launch adds the splits into C in split order
- * (deterministic) -- instead of fp32 atomics.  Any other call ignores `work`.
+ * (deterministic) -- instead of fp32 atomics.  Likewise an NR_EPI_SCATTER_ZEROED bf16x6 contraction
+ * on that kernel (the distinct-row table dgrad, nn.Embedding's backward through BERT.py:39): the K
+ * pieces of its last partial round of tiles (the stream-K tail) store plain partial tiles there and
+ * one reduction adds each tile's pieces in piece order into its destination rows, instead of fp32
+ * atomics into the zeroed rows.  Any other call ignores `work`.
  * nr_gemm_splitk_workspace() elements always suffice.  Measured: without colsum this path is
  * slower than the atomic epilogue on the NRMS weight gradient (292-301 vs 277 µs) and equal on
  * BERT's; it pays when it also carries the bias gradient (below).

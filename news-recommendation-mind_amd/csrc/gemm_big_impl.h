@@ -251,6 +251,25 @@ struct BigMN {
 template <int R, int MODE, int BK>
 using BigLoader = typename std::conditional<is_kc(MODE), BigKC<R, MODE, BK>, BigMN<R, MODE, BK>>::type;
 
+// Tail pieces through a workspace (NR_EPI_SCATTER_ZEROED with Args::slab): header ints {full, rem,
+// pieces, gn} at slab[0..4) (block 0 writes them every launch), then one 256 x 256 partial tile per
+// tail unit j = id - full at slab + TAIL_WS_HDR + j * 65536, row-major in the tile's local (row,
+// column) -- stored with plain float4 stores in the transposed accumulator layout (lane (h, c) holds
+// row c, columns 8q + 4h .. + 3).  tail_reduce_kernel adds a tile's pieces in piece order and stores
+// the sums to their destination rows: deterministic, and no fp32 atomics (a round of 234 partial
+// tiles added atomically cost ~47 us at the chip's ~1.3 TB/s atomic rate).
+template <int TI, int TJ>
+__device__ __forceinline__ void tail_slab_tr(f32x16 (&acc)[TI][TJ], int wm, int wn, int h, int c, float* dst) {
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<float4*>(dst + (wm + 32 * i + c) * 256 + wn + 32 * j + 8 * q + 4 * h) =
+            make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+}
+
 // Atomic scatter-add of a tail piece in the transposed accumulator layout (lane (h, c) holds row c,
 // columns 8q + 4h + 0..3 of each 32 x 32 block): one block at a time goes through LDS (waves 0-3 in
 // the A image, 4-7 in the B image, 32 x 36 floats each) and is read back two rows x 32 consecutive
@@ -331,6 +350,10 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
       full = f;
       rem = r;
       units = f + r * pieces;
+    }
+    if (TR && g.slab && blockIdx.x == 0 && tid == 0) {   // the tail reduction's plan (see tail_slab_tr)
+      int* hd = reinterpret_cast<int*>(g.slab);
+      hd[0] = full; hd[1] = rem; hd[2] = pieces; hd[3] = gn;
     }
   }
 
@@ -569,6 +592,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
         epilogue_slab<TI, TJ>(g, acc, u.m0, u.n0, wm, wn, h, c, g.slab + (u.kbeg / g.kchunk) * g.slab_stride);
       else
         epilogue_any<TR, TI, TJ>(g, acc, u.m0, u.n0, wm, wn, h, c);
+    } else if (TR && g.slab) {   // pieces of one tile meet in the workspace, summed by tail_reduce_kernel
+      tail_slab_tr<TI, TJ>(acc, wm, wn, h, c, g.slab + TAIL_WS_HDR + (int64_t)(id - full) * 65536);
     } else if (TR) {   // pieces of one tile meet in C: atomic adds into the zeroed destination rows
       static_assert(4 * 32 * 36 * 4 <= 2 * NP * PA * 2 || BN != 256, "tail chunks fit the A image");
       if constexpr (BN == 256 && 4 * 32 * 36 * 4 <= 2 * NP * PB * 2) {

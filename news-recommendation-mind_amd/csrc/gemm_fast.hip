@@ -112,6 +112,46 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ 
   }
 }
 
+// The big kernel's stream-K tail through its workspace (tail_slab_tr): every tail tile's pieces added
+// in piece order (deterministic) and stored to the tile's distinct destination rows (rows[m]; pad_row
+// and rows past the device-resident M skipped), the plan read from the header the GEMM wrote.
+__global__ __launch_bounds__(256) void tail_reduce_kernel(float* __restrict__ C, int64_t ldc,
+                                                          const float* __restrict__ ws, const int64_t* __restrict__ rows,
+                                                          int64_t pad_row, int64_t M, const int32_t* mdyn, int64_t N,
+                                                          int vec) {
+  const int* hd = reinterpret_cast<const int*>(ws);
+  const int full = hd[0], rem = hd[1], pieces = hd[2], gn = hd[3];
+  if (pieces <= 1 || rem <= 0 || gn <= 0) return;
+  int64_t m_eff = M;
+  if (mdyn) {
+    const int64_t m = *mdyn;
+    m_eff = m < M ? (m > 0 ? m : 0) : M;
+  }
+  const float* part = ws + TAIL_WS_HDR;
+  const int64_t total = (int64_t)rem * 256 * 64;   // float4 of the rem tail tiles
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int t = (int)(e >> 14), w = (int)(e & 16383), r = w >> 6, c4 = w & 63;
+    const int tile = full + t;
+    const int64_t m = (int64_t)(tile / gn) * 256 + r, n = (int64_t)(tile % gn) * 256 + 4 * c4;
+    if (m >= m_eff || n >= N) continue;
+    const int64_t tok = rows[m];
+    if (tok == pad_row) continue;
+    const float* s = part + (int64_t)t * 65536 + r * 256 + 4 * c4;
+    float4 a = *reinterpret_cast<const float4*>(s);
+    for (int q = 1; q < pieces; ++q) {
+      const float4 x = *reinterpret_cast<const float4*>(s + (int64_t)q * rem * 65536);
+      a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+    }
+    float* c = C + tok * ldc + n;
+    if (vec && n + 3 < N) {
+      *reinterpret_cast<float4*>(c) = a;
+    } else {
+      const float v[4] = {a.x, a.y, a.z, a.w};
+      for (int u = 0; u < 4 && n + u < N; ++u) c[u] = v[u];
+    }
+  }
+}
+
 }  // namespace nrfast
 
 // Elements of nr_gemm_f32_ws' split-K workspace that serve any shape: one round of 256 x 256
@@ -213,6 +253,14 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
                         work_elems >= (int64_t)sp * M * sld + (colsum ? (int64_t)sp * M : 0) &&
                         (reinterpret_cast<uintptr_t>(work) & 15) == 0;
       const bool fold = slab && colsum && am == MN_PLAIN;
+      // the stream-K tail's pieces through the workspace too (tail_slab_tr / tail_reduce_kernel): one
+      // 256 x 256 partial tile per tail unit, at most one unit per CU (bf16x6: one 147 KB workgroup per
+      // CU; the bf16 kernel's smaller LDS image admits two, so it keeps the atomic tail)
+      const int cus = device_cus();
+      const bool tail_ws = tailed && prec == NR_GEMM_BF16X6 && work && cus > 0 &&
+                           work_elems >= (int64_t)TAIL_WS_HDR + (int64_t)cus * 65536 &&
+                           (reinterpret_cast<uintptr_t>(work) & 15) == 0;
+      if (tail_ws) gb.slab = work;
       if (slab) {
         gb.slab = work;
         gb.slab_ld = sld;
@@ -222,6 +270,11 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
       const int np = prec == NR_GEMM_BF16 ? 1 : 3;
       const int rc = BN == 256 ? (np == 1 ? launch_big_1_256(gb, am, bmode, sp, stream) : launch_big_3_256(gb, am, bmode, sp, stream))
                                : (np == 1 ? launch_big_1_128(gb, am, bmode, sp, stream) : launch_big_3_128(gb, am, bmode, sp, stream));
+      if (rc == NR_OK && tail_ws) {
+        hipLaunchKernelGGL(tail_reduce_kernel, dim3(1024), dim3(256), 0, stream, C, ldc, work, g.Cm.idx, g.pad_row,
+                           M, m_dev, N, g.vec);
+        NR_LAUNCH_CHECK();
+      }
       if (rc == NR_OK && slab) {
         int64_t blocks = (M * ((N + 3) / 4) + 255) / 256;
         blocks = blocks > 2048 ? 2048 : (blocks < 1 ? 1 : blocks);

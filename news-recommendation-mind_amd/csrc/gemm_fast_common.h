@@ -572,6 +572,10 @@ __device__ __forceinline__ void epilogue_any(const Args& g, f32x16 (&acc)[TI][TJ
   }
 }
 
+// Floats before the big kernel's tail partial tiles in its NR_EPI_SCATTER_ZEROED workspace (ints
+// {full, rem, pieces, gn} of the launch's stream-K tail, padded to 256 B; gemm_big_impl.h tail_slab_tr)
+constexpr int TAIL_WS_HDR = 64;
+
 // A work unit = one BM x BN output tile x one K split.
 struct Unit {
   int64_t m0, n0, kbeg;

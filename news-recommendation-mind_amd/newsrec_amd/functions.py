@@ -337,6 +337,8 @@ PROJ_DGRAD_KC = False
 # the NRMS projection weight gradient on the same workspace path: one process, interleaved rounds,
 # 1.459 -> 1.446 ms per NRMS step (round 2 measured it slower, before the bf16x6 units lost SLP)
 PROJ_WGRAD_WS = True
+# the table dgrad's stream-K tail through the GEMM workspace + an ordered reduction (no fp32 atomics)
+PROJ_DGRAD_TAIL_WS = True
 # CNN word attention (tanh key projection + learned-query pooling) fused per title, forward and
 # backward (nr_cnn_keypool_*; False: the key GEMM + pooling kernels the parity tests compare with).
 FUSED_KEYPOOL = True
@@ -592,7 +594,8 @@ class MHANewsFn(_GradAwareFn):
                     w_b = K.operand(wt, L.KCONTIG) if wt is not None else K.operand(w_cat, L.MNCONTIG)
                     K.gemm_dyn(ur.cap, E, NY, K.operand(dYu, L.KCONTIG), w_b, dtable,
                                m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_ZEROED,
-                               c_rows=K.rows_map(ur.uids, L.ROWS_GATHER), pad_row=pad_row)
+                               c_rows=K.rows_map(ur.uids, L.ROWS_GATHER), pad_row=pad_row,
+                               workspace=PROJ_DGRAD_TAIL_WS)
                 PROBE.run("proj_dgrad", dgrad, dtable, ur)
                 if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
                     dtable = None

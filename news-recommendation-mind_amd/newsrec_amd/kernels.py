@@ -108,8 +108,9 @@ def gemm_dyn(M, N, K, A, B, C, m_dev=None, k_dev=None, ldc=None, bias=None, epil
     """``gemm`` with device-resident extents: M, K are upper bounds, the kernel reads the actual
     M / K from the int32 CUDA scalars ``m_dev`` / ``k_dev`` (e.g. ``UniqueRows.counts[1:2]``).
     ``max_cus`` > 0 limits the persistent grid to that many CUs (nr_gemm_f32_dyn_cus).
-    ``workspace`` (split-K NR_EPI_ATOMIC): partial tiles through plain stores into a workspace and
-    one ordered reduction instead of fp32 atomics (nr_gemm_f32_ws)."""
+    ``workspace`` (split-K NR_EPI_ATOMIC, or the NR_EPI_SCATTER_ZEROED table dgrad's stream-K tail):
+    partial tiles through plain stores into a workspace and one ordered reduction instead of fp32
+    atomics (nr_gemm_f32_ws)."""
     _f32(C, bias)
     for t in (m_dev, k_dev):
         if t is not None and (t.dtype != torch.int32 or not t.is_cuda):
@@ -118,7 +119,7 @@ def gemm_dyn(M, N, K, A, B, C, m_dev=None, k_dev=None, ldc=None, bias=None, epil
         raise L.HipError("gemm_dyn: bias has %d < N=%d entries" % (bias.numel(), N))
     if K % 32:
         raise L.HipError("gemm_dyn: K must be a multiple of 32")
-    if workspace and epilogue == L.EPI_ATOMIC and split_k > 1:
+    if workspace and ((epilogue == L.EPI_ATOMIC and split_k > 1) or epilogue == L.EPI_SCATTER_ZEROED):
         work = _splitk_work(C)
         L.call("nr_gemm_f32_ws", M, N, K, A, B, L.ptr(C), ldc if ldc is not None else C.stride(0),
                L.ptr(bias), epilogue, c_rows, pad_row, split_k, L.ptr(m_dev), L.ptr(k_dev), _prec(prec),

@@ -231,7 +231,7 @@ def test_xformer_12_layers_step_vs_oracle():
     within 2 lr (all but a rounding-level handful within 1e-3 lr).  Gradients are checked against the
     oracle run in float64 (see below).  Dropout 0 (BertFn's dropout sites are checked against their
     kernels in tests/test_bert_gpu.py).  The key biases' gradient is zero in exact arithmetic (softmax
-    cancels q . b_k), so it is held to its layer's key-weight gradient scale."""
+    cancels q . b_k), so it is held to its attention block's gradient scale."""
     import bench
     from newsrec_amd import _lib as Lb, kernels as Kn
     from newsrec_amd.bert import BertConfig
@@ -241,11 +241,17 @@ def test_xformer_12_layers_step_vs_oracle():
     torch.manual_seed(5)
     Bx, Cx, N, Lt = 2, 5, 50, 30
     bc = BertConfig(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
-    model = XFormer(ManagerConfig("bert", "xformer", 768, bert_dim=768), bert_config=bc).cuda()
+    # built and initialised on the host (CPU generator: the draw -- and so the conditioning of every
+    # gradient against the float64 oracle, fp32 error <= 2e-5 of max -- is the same on every box)
+    model = XFormer(ManagerConfig("bert", "xformer", 768, bert_dim=768), bert_config=bc)
     with torch.no_grad():
         for n, p in model.named_parameters():
             if p.dim() == 2 and "embeddings" not in n:
-                p.normal_(0, 1.5 / math.sqrt(p.shape[1]))
+                # 0.8 / sqrt(fan_in) (~0.029, BERT's own init is 0.02): at 1.5 / sqrt(fan_in) the deep
+                # layers' attention saturates and their query / key gradients fall to 1e-8..1e-10 of
+                # the value path's -- rounding noise in every arithmetic, fp32 included
+                p.normal_(0, 0.8 / math.sqrt(p.shape[1]))
+    model = model.cuda()
     gen = torch.Generator().manual_seed(1)
 
     def titles(n):
@@ -262,6 +268,8 @@ def test_xformer_12_layers_step_vs_oracle():
          "label": torch.tensor([0, 3])}
     xg = {k: v.cuda() for k, v in x.items()}
     P = _oracle_params(model)
+    # float64 copies of the SAME starting point (ropt.step() below moves P in place)
+    P64 = {n: p.detach().double().requires_grad_(True) for n, p in P.items()}
     model.train()
     opt = get_optim(model)
     opt.zero_grad(set_to_none=True)
@@ -282,31 +290,26 @@ def test_xformer_12_layers_step_vs_oracle():
     assert want.detach().std().item() > 0.05
     assert err <= 1e-3
     assert abs(loss.item() - want_loss.item()) <= 1e-3
-    # gradients against the oracle in float64 (the exact values to ~1e-15): within 1e-3 of each one's max
-    # magnitude, or -- where cancellation makes a tensor ill-conditioned (the attention-softmax gradients
-    # of the deep layers are small differences of large terms) -- no further from the exact value than
-    # twice the fp32 oracle's own error: fp32-class arithmetic, which the bf16x6 GEMMs are held to
-    P64 = {n: p.detach().double().requires_grad_(True) for n, p in P.items()}
+    # gradients against the oracle in float64 (the exact values to ~1e-15): every one within 1e-3 of its
+    # max magnitude (the fp32 oracle's own error is <= 2e-5 of it at this init)
     R.nll_loss(R.xformer_forward(P64, x, True, 12), x["label"]).backward()
     ps = dict(model.named_parameters())
-    worst, n_fp32 = 0.0, 0
+    worst, worst32 = 0.0, 0.0
     for n in P:
         want_g, got, g32 = P64[n].grad, ps[n].grad, P[n].grad
         assert got is not None and g32 is not None, n
         scale = max(want_g.abs().max().item(), 1e-12)
         if n.endswith("attention.self.key.bias"):
-            # exact value 0: the column sums of dK, whose terms the key weight's gradient X^T dK
-            # carries over the unit-scale LayerNorm output X -- that gradient's max is the terms' scale
-            scale = P64[n.replace(".key.bias", ".key.weight")].grad.abs().max().item()
+            # exact value 0 (softmax cancels q . b_k): rounding noise of the dK column sums, held to
+            # 1e-3 of the attention block's gradient scale (its query / key / value weight gradients)
+            blk = n.rsplit(".", 2)[0]
+            scale = max(P64[blk + "." + w + ".weight"].grad.abs().max().item() for w in ("query", "key", "value"))
         gerr = (got.detach().cpu().double() - want_g).abs().max().item()
         e32 = (g32.double() - want_g).abs().max().item()
-        worst = max(worst, gerr / scale)
-        if gerr > 1e-3 * scale:
-            n_fp32 += 1
-            print("  %s: |err| / max %.2e (fp32 oracle %.2e)" % (n, gerr / scale, e32 / scale))
-        assert gerr <= max(1e-3 * scale, 2 * e32), (n, gerr, e32, scale)
-    print("XFormer 12 layers: worst gradient error / max %.3e over %d tensors (%d held to the fp32-oracle bar)"
-          % (worst, len(P), n_fp32))
+        worst, worst32 = max(worst, gerr / scale), max(worst32, e32 / scale)
+        assert gerr <= 1e-3 * scale, (n, gerr, e32, scale)
+    print("XFormer 12 layers: worst gradient error / max %.3e over %d tensors (fp32 oracle %.3e)"
+          % (worst, len(P), worst32))
     for n, p in model.named_parameters():
         d = (p.detach().cpu() - P[n].detach()).abs()
         lr = 6e-6 if "bert" in n else 1e-4

@@ -52,6 +52,23 @@ def test_big_gather_projection(prec, N):
     assert torch.isnan(Y[2900:]).all()   # rows past the device M untouched
 
 
+@pytest.mark.parametrize("Kd", [544, 800, 1312, 768])
+def test_big_bf16_odd_k_tile_counts(Kd):
+    """bf16 K-contiguous pairs run 32-deep k-tiles: 17 / 25 / 41 tiles take the peeled odd form of the
+    two-tile k-loop (tile 0 alone, then pairs), 24 the even form; the bf16x6 run of the same shape
+    (16-deep tiles, always an even count) alongside."""
+    g = torch.Generator().manual_seed(Kd)
+    V, M, N = 4000, 3000, 1152
+    table = torch.randn(V, Kd, generator=g)
+    ids = torch.randint(0, V, (M,), generator=g)
+    W = torch.randn(N, Kd, generator=g) / 16
+    for prec in PRECS:
+        Y = torch.full((M, N), float("nan"), device="cuda")
+        K.gemm(M, N, Kd, K.operand(table.cuda(), L.KCONTIG, rows=ids.cuda(), mapping=L.ROWS_GATHER),
+               K.operand(W.cuda(), L.KCONTIG), Y, prec=prec)
+        assert _err(Y, _ref(table[ids], W.t(), prec)) <= _tol(table, W, Kd, prec), prec
+
+
 @pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("epi", [L.EPI_STORE_TANH, L.EPI_STORE_GELU])
 def test_big_plain_epilogues(prec, epi):
@@ -161,13 +178,15 @@ def test_big_wgrad_split_k_static(prec):
     assert _err(dW, _ref(G.t(), X, prec)) <= _tol(G, X, R, prec)
 
 
+@pytest.mark.parametrize("ws", [False, True])
 @pytest.mark.parametrize("prec", PRECS)
-@pytest.mark.parametrize("U,u_dev", [(2800, None), (30000, 24600), (24576, None)])
-def test_big_dgrad_scatter_zeroed_tail(prec, U, u_dev):
+@pytest.mark.parametrize("U,u_dev", [(2800, None), (30000, 24600), (24576, None), (256, None)])
+def test_big_dgrad_scatter_zeroed_tail(prec, U, u_dev, ws):
     """NR_EPI_SCATTER_ZEROED (the table dgrad into a zero-filled gradient): the tiles of the persistent
-    grid's last partial round are split along K and their pieces added atomically (a stream-K tail).
-    U = 2800: every tile split (33 tiles); device M 24,600: 291 tiles = one full round + 35 split
-    tiles; 24,576: 288 tiles."""
+    grid's last partial round are split along K and their pieces added atomically (a stream-K tail),
+    or -- with the workspace (bf16x6) -- stored as partial tiles and summed in piece order by one
+    reduction launch, bitwise reproducible.  U = 2800: every tile split (33 tiles); device M 24,600:
+    291 tiles = one full round + 35 split tiles; 24,576: 288 tiles; 256: three tiles."""
     g = torch.Generator().manual_seed(U)
     N, E, V = 1152, 768, 60000
     dY = torch.randn(U, N, generator=g)
@@ -177,13 +196,19 @@ def test_big_dgrad_scatter_zeroed_tail(prec, U, u_dev):
     m = u_dev or U
     dt = torch.zeros(V, E, device="cuda")
     m_dev = torch.tensor([m], dtype=torch.int32, device="cuda")
-    K.gemm_dyn(U, E, N, K.operand(dY.cuda(), L.KCONTIG), K.operand(W.cuda(), L.MNCONTIG), dt, m_dev=m_dev,
-               epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(rows.cuda(), L.ROWS_GATHER), pad_row=0, prec=prec)
+    args = (U, E, N, K.operand(dY.cuda(), L.KCONTIG), K.operand(W.cuda(), L.MNCONTIG))
+    kw = dict(m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(rows.cuda(), L.ROWS_GATHER), pad_row=0,
+              prec=prec, workspace=ws)
+    K.gemm_dyn(*args, dt, **kw)
     want = _ref(dY[:m], W, prec)
     full = torch.zeros(V, E, dtype=torch.float64)
     full[rows[:m]] = want
     full[0] = 0
     assert _err(dt, full) <= _tol(dY, W, N, prec)
+    if ws and prec == L.GEMM_BF16X6:   # no atomics left: a second run is bitwise equal
+        dt2 = torch.zeros(V, E, device="cuda")
+        K.gemm_dyn(*args, dt2, **kw)
+        assert torch.equal(dt, dt2)
 
 
 @pytest.mark.parametrize("kd", [None, 20000])

@@ -50,6 +50,7 @@ cases = {
  "nrms_proj_dgrad": (2*U*E*1152, lambda p: K.gemm_dyn(U, E, 1152, K.operand(dY, L.KCONTIG), K.operand(W, L.MNCONTIG), dX, prec=p)),
  "nrms_dgrad_table": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), K.operand(W, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
  "nrms_dgrad_table_kc": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), K.operand(WT, L.KCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
+ "nrms_dgrad_table_ws": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), K.operand(W, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p, workspace=True)),
  "nrms_dgrad_table_store": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), K.operand(W, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_STORE, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
  "user_fwd": (2*1600*768*384, lambda p: K.gemm(1600, 768, 384, K.operand(ux, L.KCONTIG), K.operand(uw, L.KCONTIG), uy, bias=ub, prec=p)),
  "user_dgrad": (2*1600*768*384, lambda p: K.gemm(1600, 384, 768, K.operand(udy, L.KCONTIG), K.operand(uw, L.MNCONTIG), udx, prec=p)),
