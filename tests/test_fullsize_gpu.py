@@ -310,12 +310,23 @@ def test_xformer_12_layers_step_vs_oracle():
         assert gerr <= 1e-3 * scale, (n, gerr, e32, scale)
     print("XFormer 12 layers: worst gradient error / max %.3e over %d tensors (fp32 oracle %.3e)"
           % (worst, len(P), worst32))
+    # parameters after Adam: within 2 lr of the oracle's step (Adam's first update is lr * g / (|g| + eps),
+    # about lr * sign(g): an element whose exact gradient is within the rounding error of zero may step
+    # either way, so elementwise agreement with the oracle's step is not the test), and the GPU step
+    # equal to torch.optim.Adam's first step applied to the GPU's own gradients from the same start
+    ps = dict(model.named_parameters())
+    names = list(P)
+    base_n = [n for n in names if n in base]
+    bert_n = [n for n in names if n in bert]
+    Q = {n: P64[n].detach().float().clone().requires_grad_(True) for n in names}
+    for n in names:
+        Q[n].grad = ps[n].grad.detach().cpu().clone()
+    qopt = torch.optim.Adam([{"params": [Q[k] for k in base_n], "lr": 1e-4},
+                             {"params": [Q[k] for k in bert_n], "lr": 6e-6}])
+    qopt.step()
     for n, p in model.named_parameters():
-        d = (p.detach().cpu() - P[n].detach()).abs()
+        got = p.detach().cpu()
         lr = 6e-6 if "bert" in n else 1e-4
-        assert d.max().item() <= 2 * lr + 1e-7, n
-        if n.endswith("attention.self.key.bias"):
-            continue
-        moved = P[n].grad != 0
-        off = int((d[moved] > 1e-3 * lr).sum().item())
-        assert off <= max(2, 1e-3 * int(moved.sum().item())), (n, off)
+        assert (got - P[n].detach()).abs().max().item() <= 2 * lr + 1e-7, n
+        dq = (got - Q[n].detach()).abs().max().item()
+        assert dq <= 1e-3 * lr + 2 * torch.finfo(torch.float32).eps * got.abs().max().item(), (n, dq)
