@@ -254,6 +254,19 @@ int nr_mha_attn_fwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v
                     int32_t heads, int32_t dk, int32_t dv, float scale, float* out,
                     int64_t ld_out, hipStream_t stream);
 
+/* Eval-time MHA user encoder + its pooling in one launch (MHA_User_Encoder.forward, models/Encoders/
+ * MHA.py:58-75, with Attention_Pooling, Pooling.py:12-25), for the fast eval's history read through
+ * per-news projections (TwoTowerBaseModel.predict_fast :78-83 over Manager._eval_fast's news table):
+ *   O_s = MultiheadAttention core of sequence s (as nr_mha_attn_fwd: tied key, pairwise mask,
+ *         heads concatenated) over rows y[yrows[s*L + j]] = [key proj (heads*dk) | value proj (heads*dv)],
+ *   out[s] = Σ_l XSoftmax(q · O_{s,l} / sqrt(heads*dv), m)_l O_{s,l}.
+ * One workgroup per sequence, the attention products on the matrix cores in `prec` (nr_gemm_precision
+ * values; bf16x6 = fp32-class).  L <= 64; (dk, dv, heads*dv) in {(32,32,384), (64,32,384), (64,64,768)};
+ * y_rows = rows of y (y_rows * ldy * 4 < 2^32); yrows NULL = identity.  No autograd (eval only). */
+int nr_mha_user_pool_fwd(const float* y, int64_t ldy, int64_t y_rows, const int64_t* yrows, const void* mask,
+                         int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, int32_t dk, int32_t dv,
+                         const float* q, float* out, int64_t ldo, int32_t prec, hipStream_t stream);
+
 /* Backward of nr_mha_attn_fwd (XSoftmax.backward, Attention.py:77-80, and the two matmuls);
  * recomputes P.  dqk receives the gradient of the shared key projection (both roles). */
 int nr_mha_attn_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v,

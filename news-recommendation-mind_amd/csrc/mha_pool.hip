@@ -849,6 +849,197 @@ void allow_smem(K kern, size_t sz) {
   if (sz > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sz);
 }
 
+// ---- Eval-time MHA user encoder + its pooling (MHA_User_Encoder.forward, MHA.py:58-75, over the
+// per-news key / value projections the fast eval computes once per news table): per impression of
+// L <= 64 history slots, per head  O_h = XSoftmax(K_h K_hᵀ / sqrt(dk), m_i m_j) V_h  (tied Q = K,
+// Attention.py:125-147), then  s_l = q·O_l / sqrt(H),  p = XSoftmax(s, m),  user = Σ p_l O_l
+// (Attention_Pooling, Pooling.py:12-25).  One workgroup per impression, one wave per head; the
+// slots sit on 64 = 2 x 32 MFMA rows: lane (c, h) holds key rows c and c + 32 and computes the four
+// 32 x 32 blocks of S from its own registers (S_{ib,jb} = K_ib K_jbᵀ: A and B are both the lane's
+// rows), so it ends up holding 32 of the 64 scores of rows c and c + 32 (S is symmetric) -- the row
+// softmax is in-register plus one cross-half exchange, and P feeds O = P V as the A operand
+// directly (head_out's k order).  O goes to LDS [64][H + 1]; the pooling runs on it as in the
+// title kernel.  Replaces mha_attn_fwd_split (scalar FMAs, 64 ms of a 14.5 M-candidate fast eval)
+// + the pooling launch, and the [B N, H] attention output's HBM round trip.
+template <int DK, int NP>
+__device__ __forceinline__ void load_krow64(const MPArgs& g, int head, int rb, float (&a)[DK / 2]) {
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  const int row = c + 32 * rb;
+  const bool ok = row < g.L;
+  if constexpr (NP > 0) {   // a[8t + u] = K[row][16t + 8h + u]
+    const float* kr = yrow(g, ok ? row : 0) + head * DK + 8 * h;
+#pragma unroll
+    for (int t = 0; t < DK / 16; ++t)
+#pragma unroll
+      for (int q4 = 0; q4 < 2; ++q4) {
+        const float4 v = *reinterpret_cast<const float4*>(kr + 16 * t + 4 * q4);
+        float* d = a + 8 * t + 4 * q4;
+        d[0] = ok ? v.x : 0.f; d[1] = ok ? v.y : 0.f; d[2] = ok ? v.z : 0.f; d[3] = ok ? v.w : 0.f;
+      }
+  } else {                  // a[s + q] = K[row][4h + 2s + q]
+    const float* kr = yrow(g, ok ? row : 0) + head * DK + 4 * h;
+#pragma unroll
+    for (int s = 0; s < DK / 2; s += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(kr + 2 * s);
+      a[s] = ok ? v.x : 0.f; a[s + 1] = ok ? v.y : 0.f; a[s + 2] = ok ? v.z : 0.f; a[s + 3] = ok ? v.w : 0.f;
+    }
+  }
+}
+
+// S_{ib,jb} = K_ib K_jbᵀ over the lanes' half-rows a_i (rows of block ib) and a_j (block jb)
+template <int DK, int NP>
+__device__ __forceinline__ void s_block(const float (&ai)[DK / 2], const float (&aj)[DK / 2], f32x16& S) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) S[r] = 0.f;
+  if constexpr (NP == 0) {
+#pragma unroll
+    for (int s = 0; s < DK / 2; ++s) S = __builtin_amdgcn_mfma_f32_32x32x2f32(ai[s], aj[s], S, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int t = 0; t < DK / 16; ++t) mfma_x<NP>(S, planes8<NP>(ai + 8 * t), planes8<NP>(aj + 8 * t));
+  }
+}
+
+// Rows c + 32 jb of one head (this lane's row of block jb): S over both key blocks, the row softmax,
+// O = P V for those rows into os.  ka_j is the lane's row of block jb (ka0 or ka1).
+template <int DK, int DV, int NP>
+__device__ __forceinline__ void user_rows(const MPArgs& g, uint64_t bits, int head, const float (&ka0)[DK / 2],
+                                          const float (&ka1)[DK / 2], const float (&ka_j)[DK / 2], int jb,
+                                          const uint32_t* rw, float* os, int so) {
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  // p[ib][r] = P[c + 32 jb][crow(r, h) + 32 ib]
+  float p[2][16];
+  {
+    f32x16 S0, S1;
+    s_block<DK, NP>(ka0, ka_j, S0);
+    s_block<DK, NP>(ka1, ka_j, S1);
+    const int R = c + 32 * jb;
+    const bool mr = R < g.L && ((bits >> R) & 1ull);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int C0 = crow(r, h), C1 = C0 + 32;
+      p[0][r] = mr && ((bits >> C0) & 1ull) ? S0[r] * g.scale_attn : -INFINITY;
+      p[1][r] = mr && C1 < g.L && ((bits >> C1) & 1ull) ? S1[r] * g.scale_attn : -INFINITY;
+      mx = fmaxf(mx, fmaxf(p[0][r], p[1][r]));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = p[ib][r] == -INFINITY ? 0.f : __expf(p[ib][r] - mx);
+        p[ib][r] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = sum > 0.f ? 1.f / sum : 0.f;   // a fully masked row: zeros (XSoftmax)
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p[ib][r] *= inv;
+  }
+  const int nq = g.heads * DK;
+#pragma unroll
+  for (int vb = 0; vb < DV / 32; ++vb) {
+    f32x16 O;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[r] = 0.f;
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      // V operand: bv[s] = V[crow(s, h) + 32 ib][vb * 32 + c] (slots past L: 0)
+      float bv[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int k = crow(s, h) + 32 * ib;
+        const float v = ld_off(g.y, rw[k < g.L ? k : 0] + 4u * (uint32_t)(nq + head * DV + vb * 32 + c));
+        bv[s] = k < g.L ? v : 0.f;
+      }
+      mfma16<NP>(O, p[ib], bv);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = crow(r, h) + 32 * jb;
+      if (row < g.L) os[row * so + head * DV + vb * 32 + c] = O[r];   // LDS holds the L real slots
+    }
+  }
+}
+
+template <int DK, int DV, int NH64, int NP>
+__global__ __launch_bounds__(768) void mha_user_pool_fwd_kernel(MPArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int H = NH64 * 64;
+  constexpr int SO = H + 1;
+  uint32_t* rw = reinterpret_cast<uint32_t*>(sm);   // [64] staged row byte offsets (yrow)
+  float* os = sm + 64;                              // [L][SO]  O
+  float* sc = os + g.L * SO;                        // [64] scores -> probabilities
+  const int64_t seq = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
+  const int c = lane & 31, h = lane >> 5;
+  const uint64_t bits = token_bits(g, seq);
+  if (tid < 64) rw[tid] = row_byte_off(g, seq * g.L + (tid < g.L ? tid : 0));
+  __syncthreads();
+  for (int head = w; head < g.heads; head += nw) {
+    float ka0[DK / 2], ka1[DK / 2];
+    load_krow64<DK, NP>(g, head, 0, ka0);
+    load_krow64<DK, NP>(g, head, 1, ka1);
+    user_rows<DK, DV, NP>(g, bits, head, ka0, ka1, ka0, 0, rw, os, SO);
+    __builtin_amdgcn_sched_barrier(0);
+    user_rows<DK, DV, NP>(g, bits, head, ka0, ka1, ka1, 1, rw, os, SO);
+  }
+  __syncthreads();
+  // pooling: s_l = q · O_l / sqrt(H), one wave per slot
+  float qv[NH64];
+#pragma unroll
+  for (int k = 0; k < NH64; ++k) qv[k] = g.q[lane + 64 * k];
+  for (int l = w; l < g.L; l += nw) {
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NH64; ++k) dot = fmaf(qv[k], os[l * SO + lane + 64 * k], dot);
+    dot = nr_wave_sum(dot);
+    if (lane == 0) sc[l] = dot * g.scale_pool;
+  }
+  __syncthreads();
+  if (w == 0) {
+    const bool keep = lane < g.L && ((bits >> lane) & 1ull);
+    const float v = keep ? sc[lane] : -INFINITY;
+    const float mx = nr_wave_max(v);
+    const float e = keep ? __expf(v - mx) : 0.f;
+    const float sum = nr_wave_sum(e);
+    sc[lane] = sum > 0.f ? e / sum : 0.f;
+  }
+  __syncthreads();
+  for (int d = tid; d < H; d += nt) {
+    float acc = 0.f;
+    for (int l = 0; l < g.L; ++l) acc = fmaf(sc[l], os[l * SO + d], acc);
+    g.news[seq * g.ldn + d] = acc;
+  }
+}
+
+size_t user_pool_smem(int H, int L) { return (size_t)(64 + L * (H + 1) + 64) * sizeof(float); }
+
+// One wave per head (twelve per impression, three per SIMD at 167 VGPRs: one workgroup per CU).  Six
+// waves of two heads each, two workgroups per CU (O held for the L real slots, 77.5 KB at L = 50),
+// measured 1.7x slower: predict 61 vs 35 ms (profiles/r05_q_eval_waves_ab.jsonl)
+template <int DK, int DV, int NH64>
+int launch_user_pool(const MPArgs& g, hipStream_t s) {
+  const size_t sz = user_pool_smem(NH64 * 64, g.L);
+  const int nw = g.heads < 4 ? 4 : g.heads;
+  if (g.np == 3) {
+    allow_smem(mha_user_pool_fwd_kernel<DK, DV, NH64, 3>, sz);
+    hipLaunchKernelGGL((mha_user_pool_fwd_kernel<DK, DV, NH64, 3>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
+  } else if (g.np == 1) {
+    allow_smem(mha_user_pool_fwd_kernel<DK, DV, NH64, 1>, sz);
+    hipLaunchKernelGGL((mha_user_pool_fwd_kernel<DK, DV, NH64, 1>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
+  } else {
+    allow_smem(mha_user_pool_fwd_kernel<DK, DV, NH64, 0>, sz);
+    hipLaunchKernelGGL((mha_user_pool_fwd_kernel<DK, DV, NH64, 0>), dim3((unsigned)g.nseq), dim3(64 * nw), sz, s, g);
+  }
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
 template <int DK, int DV, int NH64, int NP>
 int launch_np(const MPArgs& g, Pass pass, hipStream_t s) {
   const int H = NH64 * 64;
@@ -940,6 +1131,30 @@ extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows
   if (oout && ((ldo & 3) || ldo < (int64_t)heads * dv)) return NR_EINVAL(3);
   g.np = prec == NR_GEMM_BF16X6 ? 3 : prec == NR_GEMM_BF16 ? 1 : 0;
   return dispatch(g, dk, dv, FWD, stream);
+}
+
+extern "C" int nr_mha_user_pool_fwd(const float* y, int64_t ldy, int64_t y_rows, const int64_t* yrows,
+                                    const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads,
+                                    int32_t dk, int32_t dv, const float* q, float* out, int64_t ldo, int32_t prec,
+                                    hipStream_t stream) {
+  if (L < 1 || L > 64 || heads < 1 || heads > 12) return NR_EINVAL(0);
+  if (y_rows < 1 || y_rows * ldy * 4 >= ((int64_t)1 << 32)) return NR_EINVAL(5);   // 32-bit row byte offsets
+  if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(4);
+  if (!y || !mask || !q || !out) return NR_EINVAL(1);
+  if ((ldy & 3) || !al16(y) || ldy < (int64_t)heads * (dk + dv)) return NR_EINVAL(2);
+  if (ldo < (int64_t)heads * dv) return NR_EINVAL(3);
+  if (nseq == 0) return NR_OK;
+  MPArgs g{};
+  g.y = y; g.ldy = ldy; g.yrows = yrows; g.mask = mask; g.mask_dt = mask_dtype; g.nseq = nseq; g.L = L;
+  g.heads = heads; g.scale_attn = 1.0f / sqrtf((float)dk); g.scale_pool = 1.0f / sqrtf((float)(heads * dv));
+  g.q = q; g.news = out; g.ldn = ldo;
+  g.np = prec == NR_GEMM_BF16X6 ? 3 : prec == NR_GEMM_BF16 ? 1 : 0;
+  const int nh64 = heads * dv / 64;
+  if ((heads * dv) % 64) return NR_EINVAL(9);
+  if (dk == 32 && dv == 32 && nh64 == 6) return launch_user_pool<32, 32, 6>(g, stream);
+  if (dk == 64 && dv == 32 && nh64 == 6) return launch_user_pool<64, 32, 6>(g, stream);
+  if (dk == 64 && dv == 64 && nh64 == 12) return launch_user_pool<64, 64, 12>(g, stream);
+  return NR_EINVAL(8);
 }
 
 extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,

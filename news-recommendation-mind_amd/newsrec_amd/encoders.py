@@ -17,6 +17,10 @@ from .attention import MultiheadAttention
 from . import functions as F
 from .functions import AttnPoolFn, CNNNewsFn, CNNNewsRowsFn, MHAFn, MHANewsFn, RNNUserFn
 
+# fast eval: the MHA user encoder and its pooling in one launch (nr_mha_user_pool_fwd); False runs the
+# attention core and the pooling as two launches (the form the parity tests compare it with)
+USER_POOL_FUSED = True
+
 
 def _identity_rows(n, device):
     return torch.arange(n, device=device, dtype=torch.int64)
@@ -240,6 +244,12 @@ class MHA_User_Encoder(nn.Module):
         mha = self.mha
         mask = _his_mask_rows(his_mask, B, N, Y.device)
         NQ = mha.head_num * mha.key_dim
+        if USER_POOL_FUSED and K.mha_user_pool_supported(N, mha.head_num, mha.key_dim, mha.value_dim):
+            # attention + pooling in one launch per impression (the attention output never leaves the CU)
+            out = torch.empty(B, mha.head_num * mha.value_dim, device=Y.device)
+            K.mha_user_pool_fwd(Y, rows.reshape(-1).contiguous(), mask, B, N, mha.head_num, mha.key_dim,
+                                mha.value_dim, self.query_news.reshape(-1).contiguous(), out)
+            return out.unsqueeze(1)
         O = torch.empty(B * N, mha.head_num * mha.value_dim, device=Y.device)
         K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:], mask, B, N, mha.head_num, mha.key_dim, mha.value_dim, O,
                        rows=rows.reshape(-1).contiguous())

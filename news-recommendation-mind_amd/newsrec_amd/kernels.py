@@ -415,6 +415,31 @@ def mha_attn_fwd(qk, v, mask, nseq, seq_len, heads, dk, dv, out, rows=None):
            seq_len, heads, dk, dv, 1.0 / float(dk) ** 0.5, L.ptr(out), out.stride(0), L.stream_ptr(out))
 
 
+MHA_USER_POOL_SHAPES = {(32, 32, 384), (64, 32, 384), (64, 64, 768)}
+
+
+def mha_user_pool_supported(seq_len, heads, dk, dv):
+    return seq_len <= 64 and heads <= 12 and (dk, dv, heads * dv) in MHA_USER_POOL_SHAPES
+
+
+def mha_user_pool_fwd(y, rows, mask, nseq, seq_len, heads, dk, dv, q, out, prec=None):
+    """Eval MHA user encoder + pooling (MHA.py:58-75 with Pooling.py:12-25) in one launch
+    (nr_mha_user_pool_fwd): y [R, >= heads*(dk+dv)] per-news [key | value] projections, rows int64
+    [nseq*L] (history slot -> y row), mask [nseq, L], q [heads*dv] -> out [nseq, heads*dv]."""
+    _f32(y, q, out)
+    H = heads * dv
+    _cols(y, heads * (dk + dv), "y")
+    _cols(out, H, "out")
+    if out.shape[0] != nseq or q.numel() != H or not q.is_contiguous():
+        raise L.HipError("mha_user_pool_fwd: out [nseq, H] and a contiguous q [H] expected")
+    _check_rows(rows, None, "rows")
+    if rows.numel() != nseq * seq_len:
+        raise L.HipError("mha_user_pool_fwd: rows must hold nseq*L entries")
+    mp, mdt = mask_arg(mask, nseq * seq_len)
+    L.call("nr_mha_user_pool_fwd", L.ptr(y), y.stride(0), y.shape[0], L.ptr(rows), mp, mdt, nseq, seq_len, heads,
+           dk, dv, L.ptr(q), L.ptr(out), out.stride(0), _prec(prec), L.stream_ptr(out))
+
+
 def mha_attn_bwd(qk, v, mask, nseq, seq_len, heads, dk, dv, dout, dqk, dvv):
     _f32(qk, v, dout, dqk, dvv)
     for t, need, n in ((qk, heads * dk, "qk"), (v, heads * dv, "v"), (dout, heads * dv, "dout"),

@@ -112,3 +112,35 @@ def test_gather_rows():
         t = torch.randn(500, cols, device="cuda")
         idx = torch.randint(0, 500, (777,), device="cuda")
         assert torch.equal(K.gather_rows(t, idx), t[idx])
+
+
+@pytest.mark.parametrize("prec", ["bf16x6", "f32", "bf16"])
+@pytest.mark.parametrize("L,heads,dk,dv", [(50, 12, 32, 32), (64, 12, 64, 32), (33, 12, 64, 64), (20, 12, 32, 32)])
+def test_mha_user_pool(L, heads, dk, dv, prec):
+    """nr_mha_user_pool_fwd (the fast eval's MHA user encoder + Attention_Pooling in one launch) against
+    the fp64 restatement (tied-QK attention core with the pairwise mask, then query pooling with the
+    history mask, MHA.py:58-75 / Pooling.py:12-25), history slots read through a row table; ragged
+    histories, an empty one and a full one; the attention products in each GEMM arithmetic."""
+    from newsrec_amd import _lib as L_
+    g = torch.Generator().manual_seed(L * heads + dk)
+    n, nrow = 41, 700
+    H = heads * dv
+    y = torch.randn(nrow, heads * (dk + dv) + 4, generator=g, dtype=torch.float64)   # padded rows
+    rows = torch.randint(0, nrow, (n * L,), generator=g)
+    q = torch.randn(H, generator=g, dtype=torch.float64)
+    lens = torch.randint(0, L + 1, (n,), generator=g)
+    lens[0], lens[1] = 0, L
+    mask = (torch.arange(L)[None] < lens[:, None]).to(torch.float64)
+    yy = y[rows].view(n, L, -1)
+    O = _ref(yy[..., :heads * dk], yy[..., heads * dk:heads * (dk + dv)], mask, heads, dk, dv)
+    want = R.scaled_dp_attention(q.view(1, 1, H).expand(n, 1, H), O, O, mask.view(n, 1, L)).view(n, H)
+    p_ = {"bf16x6": L_.GEMM_BF16X6, "f32": L_.GEMM_F32, "bf16": L_.GEMM_BF16}[prec]
+    out = torch.full((n, H), float("nan"), device="cuda")
+    K.mha_user_pool_fwd(y.float().cuda(), rows.cuda(), mask.cuda(), n, L, heads, dk, dv, q.float().cuda(), out,
+                        prec=p_)
+    err = (out.double().cpu() - want).abs().max().item()
+    scale = want.abs().max().item()
+    tol = 3e-2 if prec == "bf16" else 2e-5
+    print("user pool L=%d dk=%d dv=%d %s: max |err| %.3e of %.3e" % (L, dk, dv, prec, err, scale))
+    assert err <= tol * scale
+    assert out[0].abs().max().item() == 0.0   # an empty history: zero user vector (XSoftmax)
