@@ -182,6 +182,21 @@ int nr_segment_rows_sum(const float* src, int64_t lds, int64_t width, int64_t T,
                         const int32_t* counts, int64_t rows_max, float* work, float* dst,
                         int64_t ldd, hipStream_t stream);
 
+/* dst rows [V, width] whose id is absent from the batch of the last nr_unique_rows call on `work`
+ * (and the pad row) set to zero; the present rows are left for the distinct-row scatter GEMM that
+ * writes every one of them (nr_gemm_f32_ws NR_EPI_SCATTER_ZEROED with a workspace, bf16x6): the word
+ * table's dense gradient (nn.Embedding backward, BERT.py:39) without a full zero fill.  counts: that
+ * call's counts.  width % 4 == 0, dst 16-B aligned. */
+int nr_unique_rows_zero_absent(const int32_t* work, const int32_t* counts, int64_t V, int64_t pad_row, float* dst,
+                               int64_t ldd, int64_t width, hipStream_t stream);
+
+/* nr_segment_rows_sum for the segments of two or more tokens only: a one-token segment's dst row is
+ * left as it is (its producer wrote it there: nr_mha_pool_bwd with seg_off).  Same arguments,
+ * workspace and alignment rules as nr_segment_rows_sum. */
+int nr_segment_rows_sum_multi(const float* src, int64_t lds, int64_t width, int64_t T, const int32_t* seg_off,
+                              const int32_t* seg_tok, const int32_t* seg_of, const int32_t* counts,
+                              int64_t rows_max, float* work, float* dst, int64_t ldd, hipStream_t stream);
+
 /* The CNN encoder's k = 3 convolution per distinct row (CNN.py:41, Conv1d(E -> H, k = 3, pad = 1)).
  * nr_segment_rows_sum_conv3: dst[u][tap*tap_width + c] = sum over the CSR tokens t of distinct row u
  * of src[t + 1 - tap][c] for tap in {0, 1, 2}, zero when t + 1 - tap leaves t's title of L tokens
@@ -308,7 +323,13 @@ int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows, const voi
  * ws (optional, forms with o only): ws_copies x ceil4(3*heads*dv + heads*(dk+dv)) floats, ZERO on entry
  * and left zero on return -- workgroups spread their dgamma / dbeta / dq / dbias atomics over the
  * copies (one address per title would serialise them at L2) and a last kernel adds the copy sums
- * into the outputs. */
+ * into the outputs.
+ * dy rows are addressed by 32-bit byte offsets: dy_rows (rows of the dy buffer, >= nseq*L) *
+ * lddy * 4 < 2^32.  seg_off (optional; with yrows): the CSR offsets of nr_unique_rows over the
+ * gradient-carrying tokens -- a token alone in its distinct row's segment writes its gradient row
+ * straight to dy row dyu_row0 + yrows[t] (the per-distinct-row sum, which nr_segment_rows_sum_multi
+ * then skips), a masked token writes nothing; dsto: [nseq*L] uint32 scratch (the split form's LN
+ * pass stores each token's row offset there for the attention pass). */
 int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const void* mask,
                     int32_t mask_dtype, int64_t nseq,
                     int32_t L, int32_t heads, int32_t dk, int32_t dv, const float* gamma,
@@ -318,7 +339,8 @@ int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows, const voi
                     int64_t ldn, const float* dz, int64_t lddz, const float* o, int64_t ldo,
                     float* dob, int64_t lddob, float* dy, int64_t lddy,
                     float* dbias, float* dq, float* dgamma, float* dbeta, float* ws,
-                    int32_t ws_copies, int32_t prec, hipStream_t stream);
+                    int32_t ws_copies, const int32_t* seg_off, int64_t dyu_row0, int64_t dy_rows,
+                    uint32_t* dsto, int32_t prec, hipStream_t stream);
 
 /* ------------------------------------------------------------------ pooling */
 

@@ -335,27 +335,44 @@ __global__ __launch_bounds__(1024) void segsum_pieces_kernel(const float* __rest
                                                              const int32_t* __restrict__ seg_of,
                                                              const int32_t* __restrict__ counts,
                                                              float4* __restrict__ part, float* __restrict__ dst,
-                                                             int64_t ldd) {
+                                                             int64_t ldd, int skip_single) {
   const int64_t T = counts[3];   // positions in the CSR
   const int64_t b = blockIdx.x, p0 = b * SEG_RANGE;
   if (p0 >= T) return;
   const int64_t p1 = p0 + SEG_RANGE < T ? p0 + SEG_RANGE : T;
-  const int n = (int)(p1 - p0);
+  int n = (int)(p1 - p0);
   __shared__ int32_t s_tok[SEG_RANGE], s_seg[SEG_RANGE + 1];
   __shared__ uint8_t s_ok[TAPS ? SEG_RANGE : 1];   // TAPS: bit j = src row t + 1 - j inside the title
   __shared__ int64_t s_dst[SEG_RANGE];   // at a piece's last position: its float4 destination
+  __shared__ int s_n;
   const int tid = threadIdx.x;
-  if (tid < n) {
-    const int32_t t = seg_tok[p0 + tid];
-    s_tok[tid] = t;
-    s_seg[tid] = seg_of[p0 + tid];
-    if (TAPS) {
-      const int pos = t % L;
-      s_ok[tid] = (uint8_t)((pos + 1 < L ? 1 : 0) | 2 | (pos > 0 ? 4 : 0));
+  if (tid < SEG_RANGE) {   // wave 0 (SEG_RANGE = 64 = one wave): the range's positions, compacted
+    int32_t t = 0, u = -1;
+    bool keep = tid < n;
+    if (keep) {
+      t = seg_tok[p0 + tid];
+      u = seg_of[p0 + tid];
+      // skip_single: a one-token segment's row was written by the producer itself (nr_mha_pool_bwd
+      // with seg_off): its position is dropped (a segment of one token is never cut by a range)
+      if (skip_single) keep = seg_off[u + 1] - seg_off[u] != 1;
+    }
+    const uint64_t kb = __ballot(keep);
+    const int at = __popcll(kb & ((1ull << tid) - 1ull));
+    if (keep) {
+      s_tok[at] = t;
+      s_seg[at] = u;
+      if (TAPS) {
+        const int pos = t % L;
+        s_ok[at] = (uint8_t)((pos + 1 < L ? 1 : 0) | 2 | (pos > 0 ? 4 : 0));
+      }
+    }
+    if (tid == 0) {
+      s_n = __popcll(kb);
+      s_seg[__popcll(kb)] = -1;
     }
   }
-  if (tid == 0) s_seg[n] = -1;
   __syncthreads();
+  n = s_n;
   if (tid < n && s_seg[tid + 1] != s_seg[tid]) {   // last position of a piece
     const int32_t u = s_seg[tid];
     const int64_t gb = seg_off[u], ge = seg_off[u + 1];
@@ -546,6 +563,37 @@ extern "C" int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t 
   return NR_OK;
 }
 
+namespace {
+// Rows of a [V, width] matrix whose id is absent from the last nr_unique_rows call on `work` (its
+// presence scan pos[] is left there), and the pad row, set to zero; present rows are left alone.
+__global__ __launch_bounds__(256) void zero_absent_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ counts,
+                                                          int64_t V, int64_t pad_row, float* __restrict__ dst, int64_t ldd,
+                                                          int64_t w4) {
+  const int32_t U = counts[0];
+  for (int64_t v = blockIdx.x; v < V; v += gridDim.x) {
+    const int32_t next = v + 1 < V ? pos[v + 1] : U;
+    if (next > pos[v] && v != pad_row) continue;   // present: the scatter GEMM writes this row
+    float4* row = reinterpret_cast<float4*>(dst + v * ldd);
+    for (int64_t j = threadIdx.x; j < w4; j += 256) row[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+}  // namespace
+
+extern "C" int nr_unique_rows_zero_absent(const int32_t* work, const int32_t* counts, int64_t V, int64_t pad_row,
+                                          float* dst, int64_t ldd, int64_t width, hipStream_t stream) {
+  if (V < 1 || V > 0x7fffffff || width < 0 || (width & 3) || (ldd & 3) || ldd < width) return NR_EINVAL(0);
+  if (!work || !counts || !dst) return NR_EINVAL(1);
+  if (reinterpret_cast<uintptr_t>(dst) & 15) return NR_EINVAL(2);
+  if (width == 0) return NR_OK;
+  const int64_t V4 = (V + 3) & ~int64_t(3);
+  const int32_t* pos = work + CTRL_WORDS + 3 * V4;
+  const int64_t blocks = V < 2048 ? V : 2048;
+  hipLaunchKernelGGL(zero_absent_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, pos, counts, V, pad_row, dst, ldd,
+                     width / 4);
+  NR_LAUNCH_CHECK();
+  return NR_OK;
+}
+
 extern "C" int64_t nr_unique_rows_workspace(int64_t V) {
   const int64_t V4 = (V + 3) & ~int64_t(3);
   return CTRL_WORDS + 4 * V4 + 2 * ((V + scan_tile_n<SCAN_THREADS>() - 1) / scan_tile_n<SCAN_THREADS>());
@@ -558,7 +606,7 @@ extern "C" int64_t nr_segment_rows_sum_workspace(int64_t T, int64_t width) {
 namespace {
 int segsum_launch(bool taps, const float* src, int64_t lds, int64_t width, int64_t wt4, int L, int64_t T,
                   const int32_t* seg_off, const int32_t* seg_tok, const int32_t* seg_of, const int32_t* counts,
-                  int64_t rows_max, float* work, float* dst, int64_t ldd, hipStream_t stream) {
+                  int64_t rows_max, float* work, float* dst, int64_t ldd, hipStream_t stream, int skip_single = 0) {
   if (rows_max == 0 || width == 0) return NR_OK;
   const int64_t w4 = width / 4;
   if (T > 0) {
@@ -566,10 +614,10 @@ int segsum_launch(bool taps, const float* src, int64_t lds, int64_t width, int64
     const dim3 block((unsigned)(w4 >= 1024 ? 1024 : (w4 < SEG_RANGE ? SEG_RANGE : (w4 + 63) / 64 * 64)));
     if (taps)
       hipLaunchKernelGGL(segsum_pieces_kernel<true>, grid, block, 0, stream, src, lds, w4, wt4, L, seg_off, seg_tok,
-                         seg_of, counts, reinterpret_cast<float4*>(work), dst, ldd);
+                         seg_of, counts, reinterpret_cast<float4*>(work), dst, ldd, skip_single);
     else
       hipLaunchKernelGGL(segsum_pieces_kernel<false>, grid, block, 0, stream, src, lds, w4, wt4, L, seg_off, seg_tok,
-                         seg_of, counts, reinterpret_cast<float4*>(work), dst, ldd);
+                         seg_of, counts, reinterpret_cast<float4*>(work), dst, ldd, skip_single);
   }
   const int64_t fb = (rows_max + FIX_THREADS - 1) / FIX_THREADS;
   hipLaunchKernelGGL(segsum_fix_kernel, dim3((unsigned)(fb < FIX_BLOCKS ? fb : FIX_BLOCKS)), dim3(FIX_THREADS), 0,
@@ -589,6 +637,17 @@ extern "C" int nr_segment_rows_sum(const float* src, int64_t lds, int64_t width,
   if (misaligned(src) || misaligned(dst) || misaligned(work)) return NR_EINVAL(2);
   return segsum_launch(false, src, lds, width, 0, 1, T, seg_off, seg_tok, seg_of, counts, rows_max, work, dst, ldd,
                        stream);
+}
+
+extern "C" int nr_segment_rows_sum_multi(const float* src, int64_t lds, int64_t width, int64_t T,
+                                         const int32_t* seg_off, const int32_t* seg_tok, const int32_t* seg_of,
+                                         const int32_t* counts, int64_t rows_max, float* work, float* dst,
+                                         int64_t ldd, hipStream_t stream) {
+  if (width < 0 || (width & 3) || (lds & 3) || (ldd & 3) || rows_max < 0 || T < 0) return NR_EINVAL(0);
+  if (!src || !seg_off || !seg_tok || !seg_of || !counts || !dst || (T > 0 && !work)) return NR_EINVAL(1);
+  if (misaligned(src) || misaligned(dst) || misaligned(work)) return NR_EINVAL(2);
+  return segsum_launch(false, src, lds, width, 0, 1, T, seg_off, seg_tok, seg_of, counts, rows_max, work, dst, ldd,
+                       stream, 1);
 }
 
 extern "C" int nr_segment_rows_sum_conv3(const float* src, int64_t lds, int64_t tap_width, int32_t L, int64_t T,

@@ -44,6 +44,11 @@ struct MPArgs {
   float* stats; float* probs;         // [T][2], [T]
   const float* dz; int64_t lddz;      // bwd: optional grad of Z
   float* dy; int64_t lddy;            // bwd: [T][heads*dk + heads*dv]
+  // bwd, optional: the CSR offsets of the distinct rows' gradient-carrying tokens (nr_unique_rows):
+  // a token alone in its row's segment writes its dy row straight to row dyu_row0 + yrows[t] of dy
+  // (the per-distinct-row sum the segment sum would form), masked tokens write nothing
+  const int32_t* seg_off; int64_t dyu_row0;
+  uint32_t* dsto;                     // split bwd with seg_off: per-token dy byte offsets (LN pass writes)
   float* dbias; float* dq; float* dgamma; float* dbeta;
   float* o; int64_t ldo;              // fwd: optional saved attention output O (pre-LN); bwd: its input
   float* dob; int64_t lddob;          // split bwd: dO rows (kernel 1 writes, kernel 2 reads)
@@ -73,6 +78,22 @@ __device__ __forceinline__ uint32_t yrow_off(const MPArgs& g, int l) {
 
 __device__ __forceinline__ float ld_off(const float* base, uint32_t byte_off) {
   return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + byte_off);
+}
+
+__device__ __forceinline__ void st_off(float* base, uint32_t byte_off, float v) {
+  *reinterpret_cast<float*>(reinterpret_cast<char*>(base) + byte_off) = v;
+}
+
+// Byte offset (from dy) of the gradient row of token t = seq * L + l, ~0 for no write (see
+// MPArgs::seg_off); requires (rows of dy) * lddy * 4 < 2^32
+__device__ __forceinline__ uint32_t dy_row_off(const MPArgs& g, int64_t seq, int l, uint64_t bits) {
+  if (l >= g.L) return ~0u;
+  const int64_t t = seq * g.L + l;
+  if (!g.seg_off) return (uint32_t)(t * g.lddy * 4);
+  if (!((bits >> l) & 1ull)) return ~0u;   // masked: exact zero, outside the CSR
+  const int64_t u = g.yrows[t];
+  const int64_t row = g.seg_off[u + 1] - g.seg_off[u] == 1 ? g.dyu_row0 + u : t;
+  return (uint32_t)(row * g.lddy * 4);
 }
 
 __device__ __forceinline__ const float* yrow(const MPArgs& g, int l) {
@@ -464,10 +485,11 @@ struct DoSource {
 // to cs[] (dbias: cs[vb] for the value columns, cs[DV/32 + kb] for the key columns).
 template <int DK, int DV, int NP>
 __device__ __forceinline__ void head_bwd(const MPArgs& g, int64_t seq, int head, uint64_t bits, float* tw,
-                                         const DoSource<DV>& dO, float (&cs)[DV / 32 + DK / 32]) {
+                                         const DoSource<DV>& dO, float (&cs)[DV / 32 + DK / 32],
+                                         const uint32_t* dsto) {
   const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
   const int nq = g.heads * DK;
-  float* dyt = g.dy + seq * g.L * g.lddy;   // the title's dy rows (wave-uniform base)
+
   float p[16];
   head_probs<DK, NP>(g, seq, head, bits, p);
   // phase fences: keep each phase's loads inside it (hoisting them all to the top costs more
@@ -495,7 +517,7 @@ __device__ __forceinline__ void head_bwd(const MPArgs& g, int64_t seq, int head,
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int i = crow(r, h);
-        if (i < g.L) dyt[(uint32_t)(i * (int)g.lddy + nq + head * DV + vb * 32 + c)] = acc[r];
+        if (i < g.L && dsto[i] != ~0u) st_off(g.dy, dsto[i] + 4u * (uint32_t)(nq + head * DV + vb * 32 + c), acc[r]);
         sum += acc[r];
       }
       cs[vb] += sum;
@@ -571,7 +593,7 @@ __device__ __forceinline__ void head_bwd(const MPArgs& g, int64_t seq, int head,
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int j = crow(r, h);
-      if (j < g.L) dyt[(uint32_t)(j * (int)g.lddy + head * DK + kb * 32 + c)] = acc[r];
+      if (j < g.L && dsto[j] != ~0u) st_off(g.dy, dsto[j] + 4u * (uint32_t)(head * DK + kb * 32 + c), acc[r]);
       sum += acc[r];
     }
     cs[DV / 32 + kb] += sum;
@@ -633,14 +655,16 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
     st[2 * tid + 1] = tid < g.L ? g.stats[2 * (seq * g.L + tid) + 1] : 0.f;
   }
   __syncthreads();
-  pool_ln_bwd<NH64>(g, seq, os, ps, ds, st, red, kb, nullptr, 0);
+  __shared__ uint32_t s_dsto[32];
+  if (tid < 32) s_dsto[tid] = dy_row_off(g, seq, tid, bits);
+  pool_ln_bwd<NH64>(g, seq, os, ps, ds, st, red, kb, nullptr, 0);   // (its barriers publish s_dsto)
   float* tw = ts + w * 32 * 33;
   for (int head = w; head < g.heads; head += nw) {
     DoSource<DV> dO{os + head * DV, SO, g.L, false};
     float cs[DV / 32 + DK / 32];
 #pragma unroll
     for (int i = 0; i < DV / 32 + DK / 32; ++i) cs[i] = 0.f;
-    head_bwd<DK, DV, NP>(g, seq, head, bits, tw, dO, cs);
+    head_bwd<DK, DV, NP>(g, seq, head, bits, tw, dO, cs, s_dsto);
     flush_dbias<DK, DV>(g, head, cs);
   }
 }
@@ -680,6 +704,7 @@ __global__ __launch_bounds__(256) void mha_ln_bwd_kernel(MPArgs g) {
     dnv[k] = g.news[seq * g.ldn + lane + 64 * k];
   }
   if (tid < 32) sps[tid] = tid < L ? g.probs[seq * L + tid] : 0.f;
+  if (g.dsto && tid < L) g.dsto[seq * L + tid] = dy_row_off(g, seq, tid, token_bits(g, seq));
   // (1) normalise in place (x -> x_hat), dp_l = dnews · Z_l, keep-bits kept per row
   static_assert(NH64 <= 32, "keep-bits of a row fit one word");
   uint32_t kbit[RW];
@@ -775,8 +800,9 @@ __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
   const int head = blockIdx.y * nw + w;
   if (head >= g.heads) return;   // no block-wide barrier below
   uint32_t* rows = reinterpret_cast<uint32_t*>(sm) + 32 * w;   // this wave's staged row offsets (yrow)
-  float* tw = sm + 32 * nw + w * 32 * 33;                     // this wave's transpose tile
-  float* dot = sm + 32 * nw + nw * 32 * 33 + w * 32 * (DV + 1);   // this wave's dO slice [32][DV+1]
+  uint32_t* dsts = reinterpret_cast<uint32_t*>(sm) + 32 * nw + 32 * w;   // ... and dy row offsets
+  float* tw = sm + 64 * nw + w * 32 * 33;                     // this wave's transpose tile
+  float* dot = sm + 64 * nw + nw * 32 * 33 + w * 32 * (DV + 1);   // this wave's dO slice [32][DV+1]
   float cs[DV / 32 + DK / 32];
 #pragma unroll
   for (int i = 0; i < DV / 32 + DK / 32; ++i) cs[i] = 0.f;
@@ -786,6 +812,8 @@ __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
     // every global load of the prologue in flight together: row ids, mask, the head's dO slice
     const uint32_t roff = lane < 32 ? row_byte_off(g, seq * g.L + (lane < g.L ? lane : 0)) : 0u;
     const uint64_t bits = token_bits(g, seq);
+    uint32_t doff = ~0u;
+    if (lane < g.L) doff = g.dsto ? g.dsto[seq * g.L + lane] : (uint32_t)((seq * g.L + lane) * g.lddy * 4);
     constexpr int F4 = DV / 4;                 // float4 per dO row
     constexpr int PER = 32 * F4 / 64;          // per lane
     float4 v[PER];
@@ -799,7 +827,10 @@ __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
         if (r >= g.L) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
-    if (lane < 32) rows[lane] = roff;
+    if (lane < 32) {
+      rows[lane] = roff;
+      dsts[lane] = doff;
+    }
 #pragma unroll
     for (int i = 0; i < PER; ++i) {   // dO slice into LDS, rows >= L zero
       const int e = lane + 64 * i, r = e / F4, c4 = e % F4;
@@ -808,7 +839,7 @@ __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
     }
     wave_lds_fence();
     DoSource<DV> dO{dot, DV + 1, g.L, false};
-    head_bwd<DK, DV, NP>(g, seq, head, bits, tw, dO, cs);
+    head_bwd<DK, DV, NP>(g, seq, head, bits, tw, dO, cs, dsts);
     wave_lds_fence();   // the next title's row indices / dO overwrite these
   }
   flush_dbias<DK, DV>(g, head, cs);
@@ -840,7 +871,7 @@ size_t bwd_smem(int H, int nw) {
   return (size_t)(32 + 32 * (H + 1) + 32 + 32 + 64 + 2 * 32 * (H / 64) + (tiles > red ? tiles : red)) * sizeof(float);
 }
 
-size_t head_bwd_smem(int nw, int dv) { return (size_t)(32 * nw + nw * 32 * 33 + nw * 32 * (dv + 1)) * sizeof(float); }
+size_t head_bwd_smem(int nw, int dv) { return (size_t)(64 * nw + nw * 32 * 33 + nw * 32 * (dv + 1)) * sizeof(float); }
 
 enum Pass { FWD = 0, BWD_FUSED = 1, BWD_SPLIT = 2 };
 
@@ -1164,12 +1195,16 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
                                const float* stats, const float* probs, const float* dnews, int64_t ldn,
                                const float* dz, int64_t lddz, const float* o, int64_t ldo, float* dob,
                                int64_t lddob, float* dy, int64_t lddy, float* dbias, float* dq, float* dgamma,
-                               float* dbeta, float* ws, int32_t ws_copies, int32_t prec, hipStream_t stream) {
+                               float* dbeta, float* ws, int32_t ws_copies, const int32_t* seg_off,
+                               int64_t dyu_row0, int64_t dy_rows, uint32_t* dsto, int32_t prec, hipStream_t stream) {
   if (L < 1 || L > 32 || heads < 1 || heads > 12) return NR_EINVAL(0);
   if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(4);
   if (!y || !mask || !gamma || !beta || !q || !stats || !probs || !dnews || !dy || !dbias || !dq || !dgamma ||
       !dbeta)
     return NR_EINVAL(1);
+  // dy rows addressed by 32-bit byte offsets from dy
+  if (dy_rows < nseq * L || dy_rows * lddy * 4 >= ((int64_t)1 << 32)) return NR_EINVAL(6);
+  if (seg_off && (!yrows || !dsto || dyu_row0 < nseq * L || dyu_row0 > dy_rows)) return NR_EINVAL(7);
   if ((ldy & 3) || !al16(y)) return NR_EINVAL(2);
   if (nseq == 0) return NR_OK;
   MPArgs g{};
@@ -1181,6 +1216,7 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
   g.probs = const_cast<float*>(probs); g.dz = dz; g.lddz = lddz; g.dy = dy; g.lddy = lddy; g.dbias = dbias;
   g.dq = dq; g.dgamma = dgamma; g.dbeta = dbeta;
   g.o = const_cast<float*>(o); g.ldo = ldo; g.dob = dob; g.lddob = lddob;
+  g.seg_off = seg_off; g.dyu_row0 = dyu_row0; g.dsto = seg_off ? dsto : nullptr;
   // o with dob: the split backward (dO through dob); o without dob: the fused backward on the saved O
   if (o && ((dob && lddob < (int64_t)heads * dv) || ldo < (int64_t)heads * dv || (ldo & 3) || !al16(o)))
     return NR_EINVAL(3);

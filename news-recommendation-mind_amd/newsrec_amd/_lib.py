@@ -66,6 +66,9 @@ _SIGS = {
                        c_ptr],
     "nr_segment_rows_sum": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
                             c_ptr],
+    "nr_segment_rows_sum_multi": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
+                                  c_ptr],
+    "nr_unique_rows_zero_absent": [c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr],
     "nr_segment_rows_sum_workspace": [c_i64, c_i64],
     "nr_unique_rows_workspace": [c_i64],
     "nr_segment_rows_sum_conv3": [c_ptr, c_i64, c_i64, c_i32, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr,
@@ -117,7 +120,8 @@ _SIGS = {
                         c_ptr],
     "nr_mha_pool_bwd": [c_ptr, c_i64, c_ptr, c_ptr, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_ptr, c_ptr, c_f32, c_u64,
                         c_u64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64,
-                        c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i32, c_i32, c_ptr],
+                        c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i32, c_ptr, c_i64, c_i64, c_ptr,
+                        c_i32, c_ptr],
     "nr_form_train_batch": [c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_i64,
                             c_i32, c_i32, c_i32, c_i32, c_u64, c_u64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
                             c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],

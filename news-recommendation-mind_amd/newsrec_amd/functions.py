@@ -339,6 +339,11 @@ PROJ_DGRAD_KC = False
 PROJ_WGRAD_WS = True
 # the table dgrad's stream-K tail through the GEMM workspace + an ordered reduction (no fp32 atomics)
 PROJ_DGRAD_TAIL_WS = True
+# the MHA news backward writes the gradient row of a token alone in its distinct row's segment
+# straight into the per-distinct-row sums (the segment sum then covers the rows of 2+ tokens)
+SINGLE_ROWS_DIRECT = True
+# the word-table gradient: only the rows absent from the batch (and the pad row) zero-filled
+ABSENT_ROWS_ZERO = True
 # CNN word attention (tanh key projection + learned-query pooling) fused per title, forward and
 # backward (nr_cnn_keypool_*; False: the key GEMM + pooling kernels the parity tests compare with).
 FUSED_KEYPOOL = True
@@ -562,16 +567,21 @@ class MHANewsFn(_GradAwareFn):
         NY = NQ + H
         dnews = dnews.contiguous()
         dq, dgamma, dbeta, db, dw = _backward_zeros(ctx, table.device, (H,), (H,), (H,), (NY,), (NY, E))
-        dY = _empty(T, NY, table)
         dz = dtok.contiguous() if dtok is not None else None
         ur = ctx.ur
+        # one buffer: per-token gradient rows [0, T), then the per-distinct-row sums [T, T + cap); with
+        # SINGLE_ROWS_DIRECT a token alone in its row's segment writes its row straight to the sums
+        direct = fused and ur is not None and SINGLE_ROWS_DIRECT
+        dYall = _empty(T + (ur.cap if ur is not None else 0), NY, table)
+        dY = dYall[:T]
         if fused:
             dob = _empty(T, H, table) if O is not None and not FUSED_SAVED_BWD else None
             ws = _grad_copies(table.device, 3 * H + NY) if O is not None else None
-            K.mha_pool_bwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, stats, probs, dnews, dY, db, dq,
+            K.mha_pool_bwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, stats, probs, dnews,
+                           dYall if direct else dY, db, dq,
                            dgamma, dbeta, p_drop=p_drop, seed=seed, offset=0 if ctx.rng is not None else offset,
                            dz=dz, yrows=ur.inv if ur else None, rng=ctx.rng, o=O, dob=dob, ws=ws,
-                           ws_copies=GRAD_COPIES if ws is not None else 0)
+                           ws_copies=GRAD_COPIES if ws is not None else 0, seg=ur if direct else None, dyu_row0=T)
         else:
             dO = _empty(T, H, table)
             K.attn_pool_bwd(O, query, mask, n, seq_len, probs, dnews, dO, dq, gamma=gamma, beta=beta, stats=stats,
@@ -582,11 +592,20 @@ class MHANewsFn(_GradAwareFn):
         dtable = None
         if ur is not None:
             # per-distinct-row gradient, then the two GEMMs over U rows instead of T tokens
-            dYu = _empty(ur.cap, NY, table)
-            ur.segment_sum(dY, dYu)
+            dYu = dYall[T:]
+            if direct:
+                ur.segment_sum_multi(dY, dYu)
+            else:
+                ur.segment_sum(dY, dYu)
             inflight = False
             if ctx.needs_input_grad[0]:
-                dtable = torch.zeros(V, E, device=table.device)
+                if PROJ_DGRAD_TAIL_WS and ABSENT_ROWS_ZERO and ctx.prec == L.GEMM_BF16X6 and 0 <= pad_row < V:
+                    # every present row is stored by the dgrad (its tail through the workspace, no
+                    # atomics): zero only the absent rows and the pad row instead of the whole table
+                    dtable = torch.empty(V, E, device=table.device)
+                    ur.zero_absent_rows(dtable, pad_row)
+                else:
+                    dtable = torch.zeros(V, E, device=table.device)
                 # distinct rows (M = U, not U_pad: no duplicate pad ids): plain row stores
                 wt = K.transpose(w_cat) if PROJ_DGRAD_KC else None   # kept alive by the closure
 

@@ -208,6 +208,9 @@ def score_nll_status(dev, clear=True):
     return bad
 
 
+_UR_GEN = {}   # (device, vocab) -> calls of nr_unique_rows on that workspace (UniqueRows.zero_absent_rows)
+
+
 class UniqueRows:
     """Distinct ids of a token batch (``nr_unique_rows``), sizes left on the device.
 
@@ -226,6 +229,10 @@ class UniqueRows:
         # ctrl[4] | cnt_all | cnt_csr are the counters (dedup.hip); cursor | pos | tile totals scratch
         work = self_cleaning_workspace(dev, f"nr_unique_rows/{vocab}", L.load().nr_unique_rows_workspace(vocab),
                                        clean=4 + 2 * ((vocab + 3) // 4 * 4))
+        # the workspace keeps this call's presence scan until the next call on it (zero_absent_rows)
+        key = (torch.device(dev), vocab)
+        _UR_GEN[key] = self._gen = _UR_GEN.get(key, 0) + 1
+        self._key, self._work = key, work
         self.uids = torch.empty(self.cap, device=dev, dtype=torch.int64)
         self.inv = torch.empty(T, device=dev, dtype=torch.int64)
         self.seg_off = torch.empty(self.cap + 1, **i32)
@@ -252,6 +259,32 @@ class UniqueRows:
                L.ptr(self.seg_tok), L.ptr(self.seg_of), L.ptr(self.counts), self.cap, L.ptr(work), L.ptr(dst),
                dst.stride(0), L.stream_ptr(src))
 
+
+    def zero_absent_rows(self, dst, pad_row):
+        """Zero the rows of dst [vocab, W] whose id is absent from this batch, and the pad row (the
+        present rows are left for the distinct-row scatter GEMM).  Falls back to a full zero fill when
+        another UniqueRows call on the same vocabulary has since replaced this one's presence scan."""
+        _f32(dst)
+        if dst.dim() != 2 or dst.shape[0] != self.vocab or dst.stride(1) != 1:
+            raise L.HipError("zero_absent_rows: dst must be a row-major [vocab, W] matrix")
+        if _UR_GEN.get(self._key) != self._gen:
+            dst.zero_()
+            return
+        L.call("nr_unique_rows_zero_absent", L.ptr(self._work), L.ptr(self.counts), self.vocab, int(pad_row),
+               L.ptr(dst), dst.stride(0), dst.shape[1], L.stream_ptr(dst))
+
+    def segment_sum_multi(self, src, dst):
+        """segment_sum for the distinct rows of two or more CSR tokens; a one-token row of dst is left
+        as it is (its producer wrote it: mha_pool_bwd with seg=)."""
+        _f32(src, dst)
+        _rows_ok(src, self.T, src.shape[1], "segment_sum src")
+        _rows_ok(dst, self.cap, src.shape[1], "segment_sum dst")
+        width = src.shape[1]
+        nbytes = L.load().nr_segment_rows_sum_workspace(self.T, width)
+        work = torch.empty(max(1, nbytes // 4), device=src.device, dtype=torch.float32)
+        L.call("nr_segment_rows_sum_multi", L.ptr(src), src.stride(0), width, self.T, L.ptr(self.seg_off),
+               L.ptr(self.seg_tok), L.ptr(self.seg_of), L.ptr(self.counts), self.cap, L.ptr(work), L.ptr(dst),
+               dst.stride(0), L.stream_ptr(src))
 
     def segment_sum_conv3(self, src, dst, tap_width, seq_len):
         """dst[u][tap*tap_width + c] = Σ src[t + 1 - tap][c] over the tokens t of distinct row u (taps
@@ -856,11 +889,14 @@ def mha_pool_fwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, news, st
 
 def mha_pool_bwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, dbias, dq,
                  dgamma, dbeta, p_drop=0.0, seed=0, offset=0, dz=None, yrows=None, rng=None, o=None, dob=None,
-                 prec=None, ws=None, ws_copies=0):
+                 prec=None, ws=None, ws_copies=0, seg=None, dyu_row0=0):
     """``o`` (the forward's ``oout``) with ``dob`` [T, heads*dv] (its dO workspace) selects the split
     backward, ``o`` without ``dob`` the fused backward on the saved O (dO kept in LDS); ``ws`` (forms
     with ``o``) a zeroed [ws_copies, >= 3*heads*dv + heads*(dk+dv)] buffer that spreads the
-    parameter-gradient atomics (left zero)."""
+    parameter-gradient atomics (left zero).  ``seg`` (a UniqueRows built with the token mask, with
+    ``yrows`` = its inv): tokens alone in their distinct row's segment write their gradient row to dy
+    row ``dyu_row0`` + u of ``dy`` (the whole buffer) directly (then ``seg.segment_sum_multi``), masked
+    tokens write nothing."""
     _rng_ok(rng)
     H = heads * dv
     _f32(y, gamma, beta, q, stats, probs, dnews, dy, dbias, dq, dgamma, dbeta, dz)
@@ -875,12 +911,22 @@ def mha_pool_bwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, stats, p
         w = (3 * heads * dv + heads * (dk + dv) + 3) // 4 * 4
         if o is None or ws_copies < 1 or ws.numel() < ws_copies * w or not ws.is_contiguous():
             raise L.HipError("mha_pool_bwd: ws needs the saved O and ws_copies x %d contiguous floats" % w)
+    dy_rows = dy.shape[0]
+    dsto = None
+    if seg is not None:
+        if yrows is None or seg.all_tokens or seg.T != nseq * seq_len:
+            raise L.HipError("mha_pool_bwd: seg needs yrows and the token-masked UniqueRows of these tokens")
+        # dy: the whole buffer -- token rows [0, T), the distinct-row sums at rows [dyu_row0, + cap)
+        if dyu_row0 < nseq * seq_len or dy.shape[0] < dyu_row0 + seg.cap:
+            raise L.HipError("mha_pool_bwd: dy must hold the distinct-row rows [dyu_row0, dyu_row0 + cap)")
+        dsto = torch.empty(nseq * seq_len, device=dy.device, dtype=torch.int32)
     mp, mdt = mask_arg(mask, nseq * seq_len)
     L.call("nr_mha_pool_bwd", L.ptr(y), y.stride(0), L.ptr(yrows), mp, mdt, nseq, seq_len, heads, dk, dv, L.ptr(gamma),
            L.ptr(beta), p_drop, seed, offset, L.ptr(rng), L.ptr(q), L.ptr(stats), L.ptr(probs), L.ptr(dnews), dnews.stride(0),
            L.ptr(dz), dz.stride(0) if dz is not None else 0, L.ptr(o), o.stride(0) if o is not None else 0,
            L.ptr(dob), dob.stride(0) if dob is not None else 0, L.ptr(dy), dy.stride(0), L.ptr(dbias), L.ptr(dq),
-           L.ptr(dgamma), L.ptr(dbeta), L.ptr(ws), int(ws_copies), _prec(prec), L.stream_ptr(y))
+           L.ptr(dgamma), L.ptr(dbeta), L.ptr(ws), int(ws_copies), L.ptr(seg.seg_off) if seg is not None else None,
+           int(dyu_row0), int(dy_rows), L.ptr(dsto), _prec(prec), L.stream_ptr(y))
 
 
 # ---------------------------------------------------------------------- BERT towers

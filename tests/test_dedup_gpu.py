@@ -218,3 +218,94 @@ def test_mha_news_dedup_vs_tokenwise(monkeypatch):
         torch.testing.assert_close(res[1][0], res[0][0], rtol=1e-5, atol=1e-5)
     for a, c in zip(res[0][1:], res[1][1:]):   # backward: same sums, different fp32 order
         torch.testing.assert_close(c, a, rtol=1e-4, atol=5e-5)
+
+
+def test_segment_sum_multi_leaves_single_rows():
+    """nr_segment_rows_sum_multi: the rows of two or more CSR tokens are summed as by
+    nr_segment_rows_sum (same order: bitwise), a one-token row keeps what its producer wrote; pad rows
+    and rows without a gradient-carrying token are zero."""
+    g = torch.Generator().manual_seed(4)
+    T, V, W = 3000, 900, 1152
+    ids = torch.randint(0, V, (T,), generator=g).cuda()
+    gm = (torch.rand(T, generator=g) < 0.7).long().cuda()
+    ur = K.UniqueRows(ids, V, grad_mask=gm)
+    src = torch.randn(T, W, device="cuda")
+    full = torch.empty(ur.cap, W, device="cuda")
+    ur.segment_sum(src, full)
+    dst = torch.full((ur.cap, W), 7.0, device="cuda")
+    ur.segment_sum_multi(src, dst)
+    torch.cuda.synchronize()
+    up = int(ur.counts[1].item())   # rows [0, U_pad) are the sums' extent
+    seg = ur.seg_off[:up + 1].long()
+    single = (seg[1:] - seg[:-1]) == 1
+    assert single.any() and (~single).any()
+    assert torch.equal(dst[:up][~single], full[:up][~single])
+    assert (dst[:up][single] == 7.0).all()
+
+
+@pytest.mark.parametrize("form", ["split", "fused_saved", "recompute"])
+def test_mha_pool_bwd_single_rows_direct(form):
+    """nr_mha_pool_bwd with seg_off: a token alone in its distinct row's segment writes its gradient
+    row straight to the per-distinct-row sums; with nr_segment_rows_sum_multi the sums equal the
+    per-token backward + nr_segment_rows_sum, bitwise -- ragged masks, dropout, the three backward
+    forms."""
+    torch.manual_seed(3)
+    n, Lq, heads, dk, dv = 80, 30, 12, 64, 32
+    T, NY, H = n * Lq, heads * (dk + dv), heads * dv
+    ids = _ids(T, 700, 13).cuda()
+    mask = (torch.rand(n, Lq, device="cuda") < 0.75).long()
+    mask[:, 0] = 1
+    ur = K.UniqueRows(ids, 700, grad_mask=mask)
+    Yu = torch.randn(ur.cap, NY, device="cuda") * 0.3
+    gamma = 1 + 0.1 * torch.randn(H, device="cuda")
+    beta = 0.1 * torch.randn(H, device="cuda")
+    q = torch.randn(H, device="cuda")
+    news = torch.empty(n, H, device="cuda")
+    stats = torch.empty(T, 2, device="cuda")
+    probs = torch.empty(T, device="cuda")
+    O = torch.empty(T, H, device="cuda") if form != "recompute" else None
+    K.mha_pool_fwd(Yu, mask, n, Lq, heads, dk, dv, gamma, beta, q, news, stats, probs, p_drop=0.2, seed=5,
+                   offset=9, yrows=ur.inv, oout=O)
+    dnews = torch.randn(n, H, device="cuda")
+    outs = []
+    for direct in (False, True):
+        dyall = torch.full((T + ur.cap, NY), float("nan"), device="cuda")
+        dob = torch.empty(T, H, device="cuda") if form == "split" else None
+        db, dq, dg, dbt = (torch.zeros(NY, device="cuda"), torch.zeros(H, device="cuda"),
+                           torch.zeros(H, device="cuda"), torch.zeros(H, device="cuda"))
+        K.mha_pool_bwd(Yu, mask, n, Lq, heads, dk, dv, gamma, beta, q, stats, probs, dnews,
+                       dyall if direct else dyall[:T], db, dq, dg, dbt, p_drop=0.2, seed=5, offset=9, yrows=ur.inv,
+                       o=O, dob=dob, seg=ur if direct else None, dyu_row0=T)
+        dyu = dyall[T:]
+        (ur.segment_sum_multi if direct else ur.segment_sum)(dyall[:T], dyu)
+        outs.append((dyu.clone(), db, dq, dg, dbt))
+    torch.cuda.synchronize()
+    U = int(ur.counts[1].item())
+    assert not torch.isnan(outs[1][0][:U]).any()
+    assert torch.equal(outs[0][0][:U], outs[1][0][:U])
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)   # atomics: order-level differences
+
+
+def test_zero_absent_rows():
+    """UniqueRows.zero_absent_rows: rows of ids absent from the batch and the pad row become zero,
+    present rows keep their contents; after another nr_unique_rows call on the same vocabulary the
+    presence scan is gone and the whole matrix is zeroed instead."""
+    g = torch.Generator().manual_seed(8)
+    V, W, T = 5000, 768, 4000
+    ids = torch.randint(0, V, (T,), generator=g).cuda()
+    ids[:7] = 0
+    ur = K.UniqueRows(ids, V, fill_row=0)
+    dst = torch.full((V, W), 3.0, device="cuda")
+    ur.zero_absent_rows(dst, 0)
+    torch.cuda.synchronize()
+    present = torch.zeros(V, dtype=torch.bool)
+    present[ids.cpu()] = True
+    present[0] = False
+    d = dst.cpu()
+    assert (d[present] == 3.0).all() and (d[~present] == 0.0).all()
+    K.UniqueRows(ids[:100].contiguous(), V)   # replaces the workspace's scan
+    dst.fill_(3.0)
+    ur.zero_absent_rows(dst, 0)
+    torch.cuda.synchronize()
+    assert (dst == 0.0).all()

@@ -91,3 +91,36 @@ def test_nrms_training_forward_saves_for_the_split_backward(monkeypatch):
         model.forward_loss(x)
     assert calls and not any(ok for _, ok in calls), calls
     _check(g, model)
+
+
+def test_probe_replays_with_a_hook_owned_table_gradient():
+    """functions.PROBE (bench.py's per-launch GEMM timing) keeps each projection GEMM as a closure over
+    the operands it launched with: when TABLE_GRAD_HOOK takes the word-table gradient (a data-parallel
+    all-reduce owns it), the dgrad closure still holds that buffer -- the replays run, and the buffer
+    is restored bitwise afterwards (the closure had looked the name up late and replayed
+    into None)."""
+    from newsrec_amd import functions as F
+    g, model, x = _setup("nrms")
+    model.train()
+    taken = {}
+
+    def hook(table, dtable):
+        taken["g"] = dtable
+        return True
+
+    F.TABLE_GRAD_HOOK.set(hook)
+    F.PROBE.enable()
+    try:
+        _, loss = model.forward_loss(x)
+        loss.backward()
+        torch.cuda.synchronize()
+        assert "g" in taken
+        before = taken["g"].clone()
+        res = F.PROBE.time(reps=2, warm=1)
+        torch.cuda.synchronize()
+    finally:
+        F.PROBE.disable()
+        F.TABLE_GRAD_HOOK.set(None)
+    assert {"proj_fwd_ms", "proj_dgrad_ms", "proj_wgrad_ms"} <= set(res), res
+    assert all(res[k] > 0 for k in ("proj_fwd_ms", "proj_dgrad_ms", "proj_wgrad_ms"))
+    assert torch.equal(taken["g"], before)
