@@ -569,12 +569,27 @@ namespace {
 __global__ __launch_bounds__(256) void zero_absent_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ counts,
                                                           int64_t V, int64_t pad_row, float* __restrict__ dst, int64_t ldd,
                                                           int64_t w4) {
-  const int32_t U = counts[0];
-  for (int64_t v = blockIdx.x; v < V; v += gridDim.x) {
-    const int32_t next = v + 1 < V ? pos[v + 1] : U;
-    if (next > pos[v] && v != pad_row) continue;   // present: the scatter GEMM writes this row
-    float4* row = reinterpret_cast<float4*>(dst + v * ldd);
-    for (int64_t j = threadIdx.x; j < w4; j += 256) row[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // 64 rows per workgroup: wave 0 tests them (coalesced scan reads) and lists the absent ones in LDS,
+  // then the workgroup zeroes the listed rows together
+  __shared__ int32_t rows[64];
+  __shared__ int nrow;
+  const int64_t v0 = (int64_t)blockIdx.x * 64;
+  if (threadIdx.x < 64) {
+    const int64_t v = v0 + threadIdx.x;
+    bool absent = false;
+    if (v < V) {
+      const int32_t next = v + 1 < V ? pos[v + 1] : counts[0];
+      absent = !(next > pos[v]) || v == pad_row;
+    }
+    const uint64_t bl = __ballot(absent);
+    if (absent) rows[__popcll(bl & ((1ull << threadIdx.x) - 1ull))] = (int32_t)(v - v0);
+    if (threadIdx.x == 0) nrow = __popcll(bl);
+  }
+  __syncthreads();
+  const int n = nrow;
+  for (int64_t e = threadIdx.x; e < (int64_t)n * w4; e += 256) {
+    const int r = (int)(e / w4);
+    reinterpret_cast<float4*>(dst + (v0 + rows[r]) * ldd)[e - r * w4] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 }  // namespace
@@ -587,9 +602,8 @@ extern "C" int nr_unique_rows_zero_absent(const int32_t* work, const int32_t* co
   if (width == 0) return NR_OK;
   const int64_t V4 = (V + 3) & ~int64_t(3);
   const int32_t* pos = work + CTRL_WORDS + 3 * V4;
-  const int64_t blocks = V < 2048 ? V : 2048;
-  hipLaunchKernelGGL(zero_absent_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, pos, counts, V, pad_row, dst, ldd,
-                     width / 4);
+  hipLaunchKernelGGL(zero_absent_kernel, dim3((unsigned)((V + 63) / 64)), dim3(256), 0, stream, pos, counts, V, pad_row,
+                     dst, ldd, width / 4);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

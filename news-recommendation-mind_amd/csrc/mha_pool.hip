@@ -155,6 +155,24 @@ __device__ __forceinline__ void load_krow(const MPArgs& g, int64_t seq, int head
   }
 }
 
+// Block kb (features 32 kb .. 32 kb + 31) of the wave's key rows into the transpose tile tw[row][33]
+// from the lanes' half-rows in load_krow's order (lane (c, h) holds row c; rows past L are zero there)
+template <int DK, int NP>
+__device__ __forceinline__ void stage_kblock(const float (&a)[DK / 2], int kb, float* tw) {
+  const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+  if constexpr (NP > 0) {   // a[8t + u] = K[c][16t + 8h + u]: steps t = 2kb, 2kb + 1
+#pragma unroll
+    for (int t = 2 * kb; t < 2 * kb + 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) tw[c * 33 + 16 * t + 8 * h + u - 32 * kb] = a[8 * t + u];
+  } else {                  // a[4m + q] = K[c][8m + 4h + q]: chunks m = 4kb .. 4kb + 3
+#pragma unroll
+    for (int m = 4 * kb; m < 4 * kb + 4; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tw[c * 33 + 8 * m + 4 * h + q - 32 * kb] = a[4 * m + q];
+  }
+}
+
 // S and P of one head for this lane's row c = lane & 31 from its key half-row a[];
 // returns P in p[16] (C layout).
 template <int DK, int NP>
@@ -195,13 +213,6 @@ __device__ __forceinline__ void head_probs_from(const MPArgs& g, uint64_t bits, 
   const float inv = sum > 0.f ? 1.f / sum : 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) p[r] *= inv;
-}
-
-template <int DK, int NP>
-__device__ __forceinline__ void head_probs(const MPArgs& g, int64_t seq, int head, uint64_t bits, float (&p)[16]) {
-  float a[DK / 2];
-  load_krow<DK, NP>(g, seq, head, a);
-  head_probs_from<DK, NP>(g, bits, a, p);
 }
 
 // V operand of O = P V: lane (c, h) needs V[crow(s, h)][vb*32 + c] (rows past L -> 0)
@@ -491,7 +502,9 @@ __device__ __forceinline__ void head_bwd(const MPArgs& g, int64_t seq, int head,
   const int nq = g.heads * DK;
 
   float p[16];
-  head_probs<DK, NP>(g, seq, head, bits, p);
+  float ka[DK / 2];   // this lane's key half-row, kept for dK = W K (staged through tw, not re-loaded)
+  load_krow<DK, NP>(g, seq, head, ka);
+  head_probs_from<DK, NP>(g, bits, ka, p);
   // phase fences: keep each phase's loads inside it (hoisting them all to the top costs more
   // registers than the latency they would hide; the split kernel runs 4 waves per SIMD)
   __builtin_amdgcn_sched_barrier(0);
@@ -575,16 +588,15 @@ __device__ __forceinline__ void head_bwd(const MPArgs& g, int64_t seq, int head,
 #pragma unroll
   for (int r = 0; r < 16; ++r) dsv[r] += tw[crow(r, h) * 33 + c];
   wave_lds_fence();
-  // dKp = W Kp  -> dY[:, head*DK ..]
+  // dKp = W Kp  -> dY[:, head*DK ..]; K's 32-feature block kb from the lanes' key rows through tw
 #pragma unroll
   for (int kb = 0; kb < DK / 32; ++kb) {
+    stage_kblock<DK, NP>(ka, kb, tw);
+    wave_lds_fence();
     float bk[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int k = crow(s, h);
-      const float v = ld_off(g.y, yrow_off(g, k < g.L ? k : 0) + 4u * (uint32_t)(head * DK + kb * 32 + c));
-      bk[s] = k < g.L ? v : 0.f;
-    }
+    for (int s = 0; s < 16; ++s) bk[s] = tw[crow(s, h) * 33 + c];
+    wave_lds_fence();
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
