@@ -40,6 +40,7 @@ TRAIN_IMPR_SYNTH = 262144          # train impressions resident for the syntheti
 FP32_MFMA_PEAK_TF = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = f32 vector peak
 BF16_MFMA_PEAK_TF = 2500.0         # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
 HBM_PEAK_GBS = 8000.0
+EVAL_BATCH_IMPR = 8192             # impressions per fast-eval predict batch (the host loop's launches amortised)
 
 
 def synth_batch(gen, device, b=B, c=C, nh=NH, l=L, full=True):
@@ -245,7 +246,7 @@ def fast_eval_leg(model, dev, world, rank, n_impr):
     table = EV.encode_news_table(model, st)
     sync()
     t1 = time.perf_counter()
-    preds, labels, grp = EV.eval_fast(model, st, batch_impr=2048, news_table=table)
+    preds, labels, grp = EV.eval_fast(model, st, batch_impr=EVAL_BATCH_IMPR, news_table=table)
     sync()
     t2 = time.perf_counter()
     res = EV.cal_metric_packed(preds, labels, grp, ["auc", "mean_mrr", "ndcg@5;10"]) if rank == 0 else None

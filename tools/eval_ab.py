@@ -1,6 +1,6 @@
 """A/B of the fast-eval leg (bench.fast_eval_leg: MIND-large-shaped dev split, news-table encode,
-predict, metrics) under module switches of newsrec_amd.encoders, interleaved in one process.
-python tools/eval_ab.py USER_POOL_FUSED=0 USER_POOL_FUSED=1 [--rounds 2]"""
+predict, metrics) under module switches of newsrec_amd.encoders (NAME=v) or bench (bench.NAME=v),
+interleaved in one process.  python tools/eval_ab.py USER_POOL_FUSED=0 USER_POOL_FUSED=1 [--rounds 2]"""
 import argparse
 import json
 import os
@@ -28,7 +28,9 @@ def main():
         for v in a.variants:
             for kv in v.split(","):
                 k, val = kv.split("=")
-                setattr(E, k, bool(int(val)))
+                mod, name = (bench, k.split(".", 1)[1]) if k.startswith("bench.") else (E, k)
+                cur = getattr(mod, name)
+                setattr(mod, name, bool(int(val)) if isinstance(cur, bool) else type(cur)(val))
             out = bench.fast_eval_leg(model, dev, 1, 0, bench.DEV_IMPR_LARGE)
             res[v].append({k: out[k] for k in ("predict_ms", "end_to_end_ms", "end_to_end_candidates_per_s",
                                                "metrics_random_model")})
