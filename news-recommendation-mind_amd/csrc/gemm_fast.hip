@@ -224,7 +224,11 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
     // (re-measured in round 4 on the k-contiguous CNN dgrad, bf16: 59 us here, 95 us with kmin = 480,
     // profiles/r04_h_gemm_ab.json)
     const int kmin = 512;
-    const bool tailed = zeroed && splits == 1 && K >= kmin && N >= 256 && big_bn(M, N, K, 1, false, false, kmin) >= 0;
+    // the stream-K tail through the workspace (bf16x6, below) makes the big kernel pay for contractions
+    // down to 256 too: the CNN table dgrad (K = 480) left the 128 x 128 kernel with it
+    const bool ws_tail = zeroed && prec == NR_GEMM_BF16X6 && work != nullptr;
+    const int kmin_t = ws_tail ? 256 : kmin;
+    const bool tailed = zeroed && splits == 1 && K >= kmin_t && N >= 256 && big_bn(M, N, K, 1, false, false, kmin_t) >= 0;
     // bf16 split-K (atomic) launches take the big kernel too: its fewer, larger units halve the operand
     // re-reads and keep three k-tiles of loads in flight (CNN conv weight gradient 200 -> 138 us)
     const int bb = big_bn(M, N, K, splits, resplit, m_dev != nullptr, kmin);

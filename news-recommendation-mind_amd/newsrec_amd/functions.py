@@ -846,14 +846,19 @@ class CNNNewsRowsFn(_GradAwareFn):
         dtable = None
         inflight = False
         if ctx.needs_input_grad[0]:
-            dtable = torch.zeros(V, E, device=dev)
+            if PROJ_DGRAD_TAIL_WS and ABSENT_ROWS_ZERO and ctx.prec == L.GEMM_BF16X6 and 0 <= pad_row < V:
+                # the dgrad stores every present row (its tail through the workspace): zero the rest
+                dtable = torch.empty(V, E, device=dev)
+                ur.zero_absent_rows(dtable, pad_row)
+            else:
+                dtable = torch.zeros(V, E, device=dev)
             if CNN_DGRAD_KC:   # the weights transposed (1.5 MB, by the pack launch) so both operands are k-contiguous
                 w_b = K.operand(w3tt if w3tt is not None else w3t.t().contiguous(), L.KCONTIG)
             else:
                 w_b = K.operand(w3t, L.MNCONTIG)
             K.gemm_dyn(ur.cap, E, 3 * Hp, K.operand(S, L.KCONTIG), w_b, dtable,
                        m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(ur.uids, L.ROWS_GATHER),
-                       pad_row=pad_row)
+                       pad_row=pad_row, workspace=PROJ_DGRAD_TAIL_WS)
             if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
                 dtable = None
                 inflight = True
