@@ -40,7 +40,7 @@ TRAIN_IMPR_SYNTH = 262144          # train impressions resident for the syntheti
 FP32_MFMA_PEAK_TF = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 = f32 vector peak
 BF16_MFMA_PEAK_TF = 2500.0         # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
 HBM_PEAK_GBS = 8000.0
-EVAL_BATCH_IMPR = 8192             # impressions per fast-eval predict batch (the host loop's launches amortised)
+EVAL_BATCH_IMPR = 16384            # impressions per fast-eval predict batch (the host loop's launches amortised)
 
 
 def synth_batch(gen, device, b=B, c=C, nh=NH, l=L, full=True):
