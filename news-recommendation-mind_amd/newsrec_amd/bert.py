@@ -33,6 +33,10 @@ from .functions import _empty, _gemm_backward, _proj_wgrad, _zeros_views
 # the bf16-MFMA attention forward stores its dropout keep bits for the backward (False: the backward
 # re-hashes every probability's counter, the same masks)
 ATTN_KEEP_BITS = True
+# input-gradient GEMMs (dX = dY W) on the k-contiguous weight (W transposed per layer and backward by
+# nr_transpose_f32) instead of the MN-contiguous one: XFormer step 68.6-68.9 vs 68.1 ms
+# (profiles/r05_z_xformer_dgrad_kc_ab.jsonl), off
+DGRAD_KC = False
 
 
 class BertConfig:
@@ -134,6 +138,16 @@ class _Segment:
         self.ids = ids.reshape(-1).contiguous()
         m = mask.reshape(-1)
         self.mask = m if m.is_contiguous() else m.contiguous()
+
+
+def _wdgrad(w, keep):
+    """B operand of dX = dY W for an nn.Linear weight W [out, in]: W itself (MN-contiguous) or its
+    transpose (k-contiguous, DGRAD_KC; appended to ``keep``, which holds it until the GEMM is enqueued)."""
+    if DGRAD_KC:
+        t = K.transpose(w)
+        keep.append(t)
+        return K.operand(t, L.KCONTIG)
+    return K.operand(w, L.MNCONTIG)
 
 
 class BertFn(torch.autograd.Function):
@@ -269,20 +283,21 @@ class BertFn(torch.autograd.Function):
             # fused [3H, H] / [3H] wgrad outputs
             dwqkv, dbqkv, *grest = _zeros_views(dev, (3 * H, H), (3 * H,), *[tuple(t.shape) for t in lp[li][6:]])
             g = [dwqkv[:H], dbqkv[:H], dwqkv[H:2 * H], dbqkv[H:2 * H], dwqkv[2 * H:], dbqkv[2 * H:]] + grest
+            keep = []   # the layer's transposed weights (DGRAD_KC)
             dh1 = _empty(T, H, word)
             do = _empty(T, H, word)
             K.bert_add_ln_bwd(o, h1, l2w, st2, dh, dh1, do, g[14], g[15], **dsite_seg(3 + 3 * li, p_h, 0))
             dU = _empty(T, I, word)
-            K.gemm(T, I, H, K.operand(do, L.KCONTIG), K.operand(wo2, L.MNCONTIG), dU, epilogue=L.EPI_GELU_GRAD,
+            K.gemm(T, I, H, K.operand(do, L.KCONTIG), _wdgrad(wo2, keep), dU, epilogue=L.EPI_GELU_GRAD,
                    c_rows=K.operand(U, L.KCONTIG))
             _proj_wgrad(do, K.operand(G, L.MNCONTIG), g[12], g[13], T)
-            K.gemm(T, H, I, K.operand(dU, L.KCONTIG), K.operand(wi, L.MNCONTIG), dh1, epilogue=L.EPI_ACCUM)
+            K.gemm(T, H, I, K.operand(dU, L.KCONTIG), _wdgrad(wi, keep), dh1, epilogue=L.EPI_ACCUM)
             _proj_wgrad(dU, K.operand(h1, L.MNCONTIG), g[10], g[11], T)
             dx = _empty(T, H, word)
             da = _empty(T, H, word)
             K.bert_add_ln_bwd(a, x, l1w, st1, dh1, dx, da, g[8], g[9], **dsite_seg(2 + 3 * li, p_h, 0))
             dcx = _empty(T, H, word)
-            K.gemm(T, H, H, K.operand(da, L.KCONTIG), K.operand(wo, L.MNCONTIG), dcx)
+            K.gemm(T, H, H, K.operand(da, L.KCONTIG), _wdgrad(wo, keep), dcx)
             _proj_wgrad(da, K.operand(cx, L.MNCONTIG), g[6], g[7], T)
             dqkv = _empty(T, 3 * H, word)
             for s, r0, kp in zip(segs, r0s, ctx.keeps[li]):
@@ -290,7 +305,7 @@ class BertFn(torch.autograd.Function):
                 K.bert_attn_bwd(qkv[r0:r0 + n], heads, s.mask, s.nseq, s.L, cx[r0:r0 + n],
                                 ml[r0 * heads * 2:(r0 + n) * heads * 2], dcx[r0:r0 + n], dqkv[r0:r0 + n],
                                 keep=kp, **dsite_seg(1 + 3 * li, p_a, r0))
-            K.gemm(T, H, 3 * H, K.operand(dqkv, L.KCONTIG), K.operand(wqkv, L.MNCONTIG), dx, epilogue=L.EPI_ACCUM)
+            K.gemm(T, H, 3 * H, K.operand(dqkv, L.KCONTIG), _wdgrad(wqkv, keep), dx, epilogue=L.EPI_ACCUM)
             _proj_wgrad(dqkv, K.operand(x, L.MNCONTIG), dwqkv, dbqkv, T)
             for k in range(16):
                 grads[5 + 16 * li + k] = g[k]
