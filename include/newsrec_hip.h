@@ -186,9 +186,10 @@ int nr_segment_rows_sum(const float* src, int64_t lds, int64_t width, int64_t T,
  * (and the pad row) set to zero; the present rows are left for the distinct-row scatter GEMM that
  * writes every one of them (nr_gemm_f32_ws NR_EPI_SCATTER_ZEROED with a workspace, bf16x6): the word
  * table's dense gradient (nn.Embedding backward, BERT.py:39) without a full zero fill.  counts: that
- * call's counts.  width % 4 == 0, dst 16-B aligned. */
+ * call's counts.  width % 4 == 0, dst 16-B aligned.  flags (nullable, uint8 [V]): 1 for a present row,
+ * 0 for a zeroed one -- the per-row flags nr_adam_multi's row_touched reads to skip zero rows. */
 int nr_unique_rows_zero_absent(const int32_t* work, const int32_t* counts, int64_t V, int64_t pad_row, float* dst,
-                               int64_t ldd, int64_t width, hipStream_t stream);
+                               int64_t ldd, int64_t width, uint8_t* flags, hipStream_t stream);
 
 /* nr_segment_rows_sum for the segments of two or more tokens only: a one-token segment's dst row is
  * left as it is (its producer wrote it there: nr_mha_pool_bwd with seg_off).  Same arguments,

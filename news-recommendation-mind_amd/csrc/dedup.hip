@@ -568,9 +568,10 @@ namespace {
 // presence scan pos[] is left there), and the pad row, set to zero; present rows are left alone.
 __global__ __launch_bounds__(256) void zero_absent_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ counts,
                                                           int64_t V, int64_t pad_row, float* __restrict__ dst, int64_t ldd,
-                                                          int64_t w4) {
+                                                          int64_t w4, uint8_t* __restrict__ flags) {
   // 64 rows per workgroup: wave 0 tests them (coalesced scan reads) and lists the absent ones in LDS,
-  // then the workgroup zeroes the listed rows together
+  // then the workgroup zeroes the listed rows together; flags (optional): 1 for a row the dgrad
+  // stores, 0 for one zeroed here (Adam's per-row "gradient may be non-zero" flags)
   __shared__ int32_t rows[64];
   __shared__ int nrow;
   const int64_t v0 = (int64_t)blockIdx.x * 64;
@@ -581,6 +582,7 @@ __global__ __launch_bounds__(256) void zero_absent_kernel(const int32_t* __restr
       const int32_t next = v + 1 < V ? pos[v + 1] : counts[0];
       absent = !(next > pos[v]) || v == pad_row;
     }
+    if (flags && v < V) flags[v] = absent ? 0 : 1;
     const uint64_t bl = __ballot(absent);
     if (absent) rows[__popcll(bl & ((1ull << threadIdx.x) - 1ull))] = (int32_t)(v - v0);
     if (threadIdx.x == 0) nrow = __popcll(bl);
@@ -595,15 +597,16 @@ __global__ __launch_bounds__(256) void zero_absent_kernel(const int32_t* __restr
 }  // namespace
 
 extern "C" int nr_unique_rows_zero_absent(const int32_t* work, const int32_t* counts, int64_t V, int64_t pad_row,
-                                          float* dst, int64_t ldd, int64_t width, hipStream_t stream) {
+                                          float* dst, int64_t ldd, int64_t width, uint8_t* flags,
+                                          hipStream_t stream) {
   if (V < 1 || V > 0x7fffffff || width < 0 || (width & 3) || (ldd & 3) || ldd < width) return NR_EINVAL(0);
   if (!work || !counts || !dst) return NR_EINVAL(1);
   if (reinterpret_cast<uintptr_t>(dst) & 15) return NR_EINVAL(2);
-  if (width == 0) return NR_OK;
+  if (width == 0 && !flags) return NR_OK;
   const int64_t V4 = (V + 3) & ~int64_t(3);
   const int32_t* pos = work + CTRL_WORDS + 3 * V4;
   hipLaunchKernelGGL(zero_absent_kernel, dim3((unsigned)((V + 63) / 64)), dim3(256), 0, stream, pos, counts, V, pad_row,
-                     dst, ldd, width / 4);
+                     dst, ldd, width / 4, flags);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

@@ -68,7 +68,7 @@ _SIGS = {
                             c_ptr],
     "nr_segment_rows_sum_multi": [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_i64,
                                   c_ptr],
-    "nr_unique_rows_zero_absent": [c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr],
+    "nr_unique_rows_zero_absent": [c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_ptr],
     "nr_segment_rows_sum_workspace": [c_i64, c_i64],
     "nr_unique_rows_workspace": [c_i64],
     "nr_segment_rows_sum_conv3": [c_ptr, c_i64, c_i64, c_i32, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr,

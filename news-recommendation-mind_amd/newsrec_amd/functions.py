@@ -344,6 +344,8 @@ PROJ_DGRAD_TAIL_WS = True
 SINGLE_ROWS_DIRECT = True
 # the word-table gradient: only the rows absent from the batch (and the pad row) zero-filled
 ABSENT_ROWS_ZERO = True
+# ... and those rows flagged for Adam, which then skips reading them (optim.FusedAdam, row_touched)
+WORD_ROW_FLAGS = True
 # CNN word attention (tanh key projection + learned-query pooling) fused per title, forward and
 # backward (nr_cnn_keypool_*; False: the key GEMM + pooling kernels the parity tests compare with).
 FUSED_KEYPOOL = True
@@ -451,13 +453,33 @@ class _LocalRowGrad:
         else:
             self.prev[key] = rows.reshape(-1).clone()
         table.grad = buf
-        table._nr_row_touched = (buf, flags)
+        table._nr_row_touched = (buf, flags, buf._version)   # (optim: valid while buf is unmodified)
         return True
 
     def clear(self):
         self.buf.clear()
         self.prev.clear()
         self.flags.clear()
+
+
+def _zero_absent_word_rows(table, dtable, ur, pad_row):
+    """Zero dtable's rows of ids absent from the batch (and the pad row).  Returns Adam's per-row
+    flags (1 = the dgrad stores the row) when the gradient will become ``table.grad`` as it is: a leaf
+    table whose ``.grad`` is None (no accumulation into an older gradient) in a single process (a
+    dense all-reduce would add other ranks' rows).  None otherwise."""
+    track = WORD_ROW_FLAGS and _is_param_leaf(table) and table.grad is None and not _multi_rank()
+    flags = torch.empty(dtable.shape[0], dtype=torch.uint8, device=dtable.device) if track else None
+    return flags if ur.zero_absent_rows(dtable, pad_row, flags) else None
+
+
+def _word_row_flags(table, dtable, flags):
+    """Publish (or clear) the word table's row flags for optim.FusedAdam, keyed by the gradient
+    buffer's address and version counter: they apply only while ``table.grad`` is exactly that buffer,
+    unmodified (autograd installs a lone returned gradient as it is; a copy changes the address, an
+    in-place accumulation -- another use of the table in the graph, a second backward -- the version)."""
+    if _is_param_leaf(table):
+        table._nr_row_touched = ((dtable.data_ptr(), flags, dtable._version)
+                                 if dtable is not None and flags is not None else None)
 
 
 def _multi_rank():
@@ -558,6 +580,8 @@ class MHANewsFn(_GradAwareFn):
     @_gemm_backward
     def backward(ctx, dnews, dtok):
         table, ids, mask, w_cat, gamma, beta, query, Y, O, probs, stats = ctx.saved_tensors
+        _word_row_flags(ctx.table_ref, None, None)
+        rflags = None
         heads, dk, dv, seq_len, pad_row, p_drop, seed, offset, fused = ctx.cfg
         T = ids.numel()
         n = T // seq_len
@@ -603,7 +627,7 @@ class MHANewsFn(_GradAwareFn):
                     # every present row is stored by the dgrad (its tail through the workspace, no
                     # atomics): zero only the absent rows and the pad row instead of the whole table
                     dtable = torch.empty(V, E, device=table.device)
-                    ur.zero_absent_rows(dtable, pad_row)
+                    rflags = _zero_absent_word_rows(ctx.table_ref, dtable, ur, pad_row)
                 else:
                     dtable = torch.zeros(V, E, device=table.device)
                 # distinct rows (M = U, not U_pad: no duplicate pad ids): plain row stores
@@ -619,6 +643,7 @@ class MHANewsFn(_GradAwareFn):
                 if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
                     dtable = None
                     inflight = True   # the table's all-reduce runs beside the weight gradient
+                _word_row_flags(ctx.table_ref, dtable, rflags)
             prec = ctx.prec
 
             def wgrad(max_cus=0):
@@ -675,6 +700,7 @@ class CNNNewsFn(torch.autograd.Function):
     @_gemm_backward
     def backward(ctx, dnews, dC_out):
         table, ids, mask, w3, wq, query, C, Kq, probs = ctx.saved_tensors
+        _word_row_flags(ctx.table_ref, None, None)
         seq_len, pad_row = ctx.cfg
         T = ids.numel()
         n = T // seq_len
@@ -809,6 +835,8 @@ class CNNNewsRowsFn(_GradAwareFn):
     @_gemm_backward
     def backward(ctx, dnews, dC_out):
         table, ids, mask, w3t, wq, bq, query, C, Kq, probs, w3tt = ctx.saved_tensors
+        _word_row_flags(ctx.table_ref, None, None)
+        rflags = None
         seq_len, pad_row, H, fused = ctx.cfg
         ur = ctx.ur
         T = ids.numel()
@@ -849,7 +877,7 @@ class CNNNewsRowsFn(_GradAwareFn):
             if PROJ_DGRAD_TAIL_WS and ABSENT_ROWS_ZERO and ctx.prec == L.GEMM_BF16X6 and 0 <= pad_row < V:
                 # the dgrad stores every present row (its tail through the workspace): zero the rest
                 dtable = torch.empty(V, E, device=dev)
-                ur.zero_absent_rows(dtable, pad_row)
+                rflags = _zero_absent_word_rows(ctx.table_ref, dtable, ur, pad_row)
             else:
                 dtable = torch.zeros(V, E, device=dev)
             if CNN_DGRAD_KC:   # the weights transposed (1.5 MB, by the pack launch) so both operands are k-contiguous
@@ -862,6 +890,7 @@ class CNNNewsRowsFn(_GradAwareFn):
             if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
                 dtable = None
                 inflight = True
+            _word_row_flags(ctx.table_ref, dtable, rflags)
         K.gemm_dyn(3 * Hp, E, ur.cap, K.operand(S, L.MNCONTIG),
                    K.operand(table, L.MNCONTIG, rows=ur.uids, mapping=L.ROWS_GATHER), dw3t, k_dev=ur.u_pad,
                    epilogue=L.EPI_ATOMIC, split_k=_split_k(3 * Hp, E, ur.cap),

@@ -260,18 +260,25 @@ class UniqueRows:
                dst.stride(0), L.stream_ptr(src))
 
 
-    def zero_absent_rows(self, dst, pad_row):
+    def zero_absent_rows(self, dst, pad_row, flags=None):
         """Zero the rows of dst [vocab, W] whose id is absent from this batch, and the pad row (the
-        present rows are left for the distinct-row scatter GEMM).  Falls back to a full zero fill when
-        another UniqueRows call on the same vocabulary has since replaced this one's presence scan."""
+        present rows are left for the distinct-row scatter GEMM).  flags (uint8 [vocab], optional)
+        receives 1 for a present row, 0 for a zeroed one.  Falls back to a full zero fill when
+        another UniqueRows call on the same vocabulary has since replaced this one's presence scan;
+        returns False then (flags not written), True otherwise."""
         _f32(dst)
         if dst.dim() != 2 or dst.shape[0] != self.vocab or dst.stride(1) != 1:
             raise L.HipError("zero_absent_rows: dst must be a row-major [vocab, W] matrix")
+        if flags is not None and (flags.dtype != torch.uint8 or flags.numel() != self.vocab or
+                                  not flags.is_contiguous() or flags.device != dst.device):
+            raise L.HipError("zero_absent_rows: flags must be a contiguous uint8 [vocab] tensor on dst's device")
         if _UR_GEN.get(self._key) != self._gen:
             dst.zero_()
-            return
+            return False
         L.call("nr_unique_rows_zero_absent", L.ptr(self._work), L.ptr(self.counts), self.vocab, int(pad_row),
-               L.ptr(dst), dst.stride(0), dst.shape[1], L.stream_ptr(dst))
+               L.ptr(dst), dst.stride(0), dst.shape[1], L.ptr(flags) if flags is not None else None,
+               L.stream_ptr(dst))
+        return True
 
     def segment_sum_multi(self, src, dst):
         """segment_sum for the distinct rows of two or more CSR tokens; a one-token row of dst is left

@@ -69,9 +69,13 @@ class FusedAdam(torch.optim.Optimizer):
             ent = (p, g, st["exp_avg"], st["exp_avg_sq"], lr, st["step"])
             # a row-sparse table gradient (functions.LOCAL_ROW_GRAD) carries per-row "touched" flags:
             # the kernel skips reading the rows known to be zero
+            # rt = (that buffer or its address, flags, its version counter when published): the flags
+            # hold only while p.grad is that buffer, unmodified since (functions._word_row_flags)
             rt = getattr(p, "_nr_row_touched", None)
-            if rt is not None and p.grad.data_ptr() == rt[0].data_ptr():
-                ent = ent + (rt[1],)
+            if rt is not None:
+                ptr = rt[0] if isinstance(rt[0], int) else rt[0].data_ptr()
+                if p.grad.data_ptr() == ptr and (len(rt) < 3 or p.grad._version == rt[2]):
+                    ent = ent + (rt[1],)
             batches.setdefault(key, []).append(ent)
         for (betas, eps, wd), entries in batches.items():
             K.adam_multi(entries, betas[0], betas[1], eps, wd, grad_scale, advance_steps=self.capturable)

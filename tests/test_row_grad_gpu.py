@@ -55,7 +55,7 @@ def test_adam_skips_untouched_rows_exactly():
     h = F._LocalRowGrad()
     rows = torch.randint(0, V, (32,), device="cuda")
     assert h(table, rows, torch.randn(32, E, device="cuda"))
-    buf, flags = table._nr_row_touched
+    buf, flags, _ = table._nr_row_touched
     assert int(flags.sum()) == len(set(rows.tolist()))
     m0 = torch.randn(V, E, device="cuda").abs() * 0.01
     v0 = torch.randn(V, E, device="cuda").abs() * 0.001
@@ -186,3 +186,71 @@ def test_transpose(rows, cols):
     from newsrec_amd import kernels as K
     src = torch.randn(rows, cols + 3, device="cuda")[:, :cols]
     assert torch.equal(K.transpose(src), src.t().contiguous())
+
+
+def _word_table_step(cfg, mode):
+    """The golden model's word-table gradient, FusedAdam stepped once on it; returns the table, its
+    gradient, its published row flags (or None) and whether Adam matched the dense update bitwise.
+    mode "one": one forward + backward; "passes": a second backward over a batch with other history
+    ids accumulated into .grad; "uses": both batches' losses summed, one backward (the table used
+    twice in one graph, autograd summing the two gradients)."""
+    from golden_util import Golden
+    from model_util import build_model, load_golden_params
+    from newsrec_amd import kernels as K
+    from newsrec_amd.optim import FusedAdam
+    g = Golden(cfg)
+    model = build_model(g.encN, g.encU, g.hidden, vocab=int(g["meta.vocab"]))
+    load_golden_params(model, g)
+    if g.encU == "lstur":
+        model.encoderU.keep_override = torch.from_numpy(g["in.lstur_keep"])
+    model.train()
+    x = g.inputs("cuda")
+    table = model.embedding.bert_word_embedding.weight
+    his = x["his_encoded_index"]
+    gen = torch.Generator().manual_seed(5)
+    x2 = dict(x, his_encoded_index=torch.randint(1, table.shape[0], his.shape, generator=gen).cuda() * (his != 0))
+    if mode == "one":
+        model.forward_loss(x)[1].backward()
+    elif mode == "passes":
+        model.forward_loss(x)[1].backward()
+        model.forward_loss(x2)[1].backward()
+    else:
+        (model.forward_loss(x)[1] + model.forward_loss(x2)[1]).backward()
+    rt = table._nr_row_touched
+    grad = table.grad.detach().clone()
+    p0 = table.detach().clone()
+    opt = FusedAdam([table], lr=1e-3)
+    opt.step()
+    st = opt.state[table]
+    p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
+    K.adam_multi([(p, grad, m, v, 1e-3, 1)], 0.9, 0.999, 1e-8, 0.0, 1.0)
+    torch.cuda.synchronize()
+    same = (torch.equal(table.detach(), p) and torch.equal(st["exp_avg"], m) and torch.equal(st["exp_avg_sq"], v))
+    return table, grad, rt, same
+
+
+@pytest.mark.parametrize("cfg", ["nrms", "cnn_attn"])
+def test_word_table_row_flags(cfg):
+    """The word-table gradient's row flags (nr_unique_rows_zero_absent): published for the gradient
+    autograd installs as it is, set for every non-zero row and not for the pad row, and FusedAdam
+    reading them is bitwise the dense update."""
+    table, grad, rt, same = _word_table_step(cfg, "one")
+    assert rt is not None and rt[0] == table.grad.data_ptr() and rt[2] == table.grad._version
+    flags = rt[1].bool().cpu()
+    nz = (grad != 0).any(1).cpu()
+    assert not (nz & ~flags).any()
+    assert int(flags[0]) == 0 and int(flags.sum()) >= int(nz.sum()) > 0
+    assert same
+
+
+@pytest.mark.parametrize("mode", ["passes", "uses"])
+@pytest.mark.parametrize("cfg", ["nrms", "cnn_attn"])
+def test_word_table_row_flags_accumulated(cfg, mode):
+    """Gradients of two batches summed into the table's .grad -- a second backward pass (the flags
+    are not published: .grad exists), or two uses of the table in one graph (each backward publishes,
+    autograd adds the two gradients: a copy changes the address, an in-place add the version) --
+    the flags no longer describe .grad, FusedAdam must not use them: bitwise the dense update."""
+    table, grad, rt, same = _word_table_step(cfg, mode)
+    if rt is not None:
+        assert not (rt[0] == table.grad.data_ptr() and rt[2] == table.grad._version)
+    assert same
