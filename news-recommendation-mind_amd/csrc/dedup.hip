@@ -421,11 +421,12 @@ __global__ __launch_bounds__(1024) void segsum_pieces_kernel(const float* __rest
   }
 }
 
-// Pass 2: workgroups stride over the distinct rows in chunks of FIX_THREADS and compact the
-// rows that need work into LDS: segments cut by a range boundary (sum their pieces in range
-// order), empty segments and pad rows [U, U_pad) (zero).  Whole segments were written by pass
-// 1.  One wave per row for short cuts; a cut with many pieces (a long segment) takes the whole
-// workgroup, pieces split over thread groups and combined in LDS.
+// Pass 2: workgroup b takes the distinct rows u = b (mod grid) -- rows of neighbouring ids, e.g. the
+// [CLS] / [SEP] of every title, land on different workgroups -- and compacts the rows that need
+// work into LDS: segments cut by a range boundary (sum their pieces in range order), empty
+// segments and pad rows [U, U_pad) (zero).  Whole segments were written by pass 1.  One wave per
+// row for short cuts; a cut with many pieces (a long segment) takes the whole workgroup, pieces
+// split over thread groups and combined in LDS.
 constexpr int FIX_THREADS = 1024;
 constexpr int FIX_BLOCKS = 256;
 constexpr int FIX_WAVE_PIECES = 8;
@@ -447,11 +448,11 @@ __global__ __launch_bounds__(FIX_THREADS) void segsum_fix_kernel(int64_t w4, con
   const int64_t gw = w4 < FIX_THREADS ? w4 : FIX_THREADS;
   const int g = (int)(tid / gw);
   const int64_t j0 = tid - (int64_t)g * gw;
-  for (int64_t c0 = (int64_t)blockIdx.x * FIX_THREADS; c0 < Up; c0 += (int64_t)gridDim.x * FIX_THREADS) {
+  for (int64_t c0 = 0; c0 < Up; c0 += (int64_t)gridDim.x * FIX_THREADS) {
     if (tid == 0) nw_todo = nb_todo = 0;
     __syncthreads();
     {
-      const int64_t u = c0 + tid;
+      const int64_t u = c0 + (int64_t)tid * gridDim.x + blockIdx.x;
       if (u < Up) {
         bool wave_item = false, block_item = false;
         if (u >= U) {
@@ -500,12 +501,12 @@ __global__ __launch_bounds__(FIX_THREADS) void segsum_fix_kernel(int64_t w4, con
             s = part[(b * 2 + (sb > b0 * SEG_RANGE ? 1 : 0)) * w4 + j];
             b += G;
           }
-          for (; b + 3 * G <= b1; b += 4 * G) {   // later pieces: slot 0, four loads in flight
-            const float4 x0 = part[(b * 2) * w4 + j];
-            const float4 x1 = part[((b + G) * 2) * w4 + j];
-            const float4 x2 = part[((b + 2 * G) * 2) * w4 + j];
-            const float4 x3 = part[((b + 3 * G) * 2) * w4 + j];
-            s = f4add(s, x0); s = f4add(s, x1); s = f4add(s, x2); s = f4add(s, x3);
+          for (; b + 7 * G <= b1; b += 8 * G) {   // later pieces: slot 0, eight loads in flight
+            float4 x[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) x[q] = part[((b + q * G) * 2) * w4 + j];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) s = f4add(s, x[q]);
           }
           for (; b <= b1; b += G) s = f4add(s, part[(b * 2) * w4 + j]);
         }
@@ -636,7 +637,7 @@ int segsum_launch(bool taps, const float* src, int64_t lds, int64_t width, int64
       hipLaunchKernelGGL(segsum_pieces_kernel<false>, grid, block, 0, stream, src, lds, w4, wt4, L, seg_off, seg_tok,
                          seg_of, counts, reinterpret_cast<float4*>(work), dst, ldd, skip_single);
   }
-  const int64_t fb = (rows_max + FIX_THREADS - 1) / FIX_THREADS;
+  const int64_t fb = (rows_max + 255) / 256;   // a quarter of each workgroup's threads hold a row
   hipLaunchKernelGGL(segsum_fix_kernel, dim3((unsigned)(fb < FIX_BLOCKS ? fb : FIX_BLOCKS)), dim3(FIX_THREADS), 0,
                      stream, w4, seg_off, counts, reinterpret_cast<const float4*>(work), dst, ldd);
   NR_LAUNCH_CHECK();
