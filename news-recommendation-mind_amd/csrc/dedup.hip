@@ -567,32 +567,36 @@ extern "C" int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t 
 namespace {
 // Rows of a [V, width] matrix whose id is absent from the last nr_unique_rows call on `work` (its
 // presence scan pos[] is left there), and the pad row, set to zero; present rows are left alone.
+// rows per workgroup: 16 -> 7.5 us for the bench batch's word-table gradient, 11.6 us at 64 (8: 7.7, 32:
+// 7.7; profiles/r05_af_ab_zero_absent_rows.json)
+constexpr int ZA_ROWS = 16;
 __global__ __launch_bounds__(256) void zero_absent_kernel(const int32_t* __restrict__ pos, const int32_t* __restrict__ counts,
                                                           int64_t V, int64_t pad_row, float* __restrict__ dst, int64_t ldd,
                                                           int64_t w4, uint8_t* __restrict__ flags) {
-  // 64 rows per workgroup: wave 0 tests them (coalesced scan reads) and lists the absent ones in LDS,
-  // then the workgroup zeroes the listed rows together; flags (optional): 1 for a row the dgrad
-  // stores, 0 for one zeroed here (Adam's per-row "gradient may be non-zero" flags)
-  __shared__ int32_t rows[64];
+  // flags (optional): 1 for a row the dgrad stores, 0 for one zeroed here (Adam's per-row
+  // "gradient may be non-zero" flags)
+  // ZA_ROWS rows per workgroup: the first ZA_ROWS lanes test them (coalesced scan reads) and list the
+  // absent ones in LDS, then the workgroup zeroes the listed rows together
+  __shared__ int32_t rows[ZA_ROWS];
   __shared__ int nrow;
-  const int64_t v0 = (int64_t)blockIdx.x * 64;
+  const int64_t v0 = (int64_t)blockIdx.x * ZA_ROWS;
   if (threadIdx.x < 64) {
     const int64_t v = v0 + threadIdx.x;
     bool absent = false;
-    if (v < V) {
+    if (threadIdx.x < ZA_ROWS && v < V) {
       const int32_t next = v + 1 < V ? pos[v + 1] : counts[0];
       absent = !(next > pos[v]) || v == pad_row;
+      if (flags) flags[v] = absent ? 0 : 1;
     }
-    if (flags && v < V) flags[v] = absent ? 0 : 1;
     const uint64_t bl = __ballot(absent);
     if (absent) rows[__popcll(bl & ((1ull << threadIdx.x) - 1ull))] = (int32_t)(v - v0);
     if (threadIdx.x == 0) nrow = __popcll(bl);
   }
   __syncthreads();
-  const int n = nrow;
-  for (int64_t e = threadIdx.x; e < (int64_t)n * w4; e += 256) {
-    const int r = (int)(e / w4);
-    reinterpret_cast<float4*>(dst + (v0 + rows[r]) * ldd)[e - r * w4] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int n = nrow, n4 = (int)w4;
+  for (int e = threadIdx.x; e < n * n4; e += 256) {
+    const int r = e / n4;
+    reinterpret_cast<float4*>(dst + (v0 + rows[r]) * ldd)[e - r * n4] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 }  // namespace
@@ -600,13 +604,15 @@ __global__ __launch_bounds__(256) void zero_absent_kernel(const int32_t* __restr
 extern "C" int nr_unique_rows_zero_absent(const int32_t* work, const int32_t* counts, int64_t V, int64_t pad_row,
                                           float* dst, int64_t ldd, int64_t width, uint8_t* flags,
                                           hipStream_t stream) {
-  if (V < 1 || V > 0x7fffffff || width < 0 || (width & 3) || (ldd & 3) || ldd < width) return NR_EINVAL(0);
+  if (V < 1 || V > 0x7fffffff || width < 0 || width > (int64_t)(0x7fffffff / 64) * 4 || (width & 3) || (ldd & 3) ||
+      ldd < width)
+    return NR_EINVAL(0);
   if (!work || !counts || !dst) return NR_EINVAL(1);
   if (reinterpret_cast<uintptr_t>(dst) & 15) return NR_EINVAL(2);
   if (width == 0 && !flags) return NR_OK;
   const int64_t V4 = (V + 3) & ~int64_t(3);
   const int32_t* pos = work + CTRL_WORDS + 3 * V4;
-  hipLaunchKernelGGL(zero_absent_kernel, dim3((unsigned)((V + 63) / 64)), dim3(256), 0, stream, pos, counts, V, pad_row,
+  hipLaunchKernelGGL(zero_absent_kernel, dim3((unsigned)((V + ZA_ROWS - 1) / ZA_ROWS)), dim3(256), 0, stream, pos, counts, V, pad_row,
                      dst, ldd, width / 4, flags);
   NR_LAUNCH_CHECK();
   return NR_OK;
