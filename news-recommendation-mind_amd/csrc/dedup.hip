@@ -25,16 +25,20 @@ namespace {
 
 constexpr int SEG_RANGE = 64;   // CSR positions per segment-sum workgroup
 constexpr int SEG_BATCH = 8;   // row loads in flight per thread (16 measured equal: 1.4273 vs 1.4259 ms per NRMS step)
-constexpr int CNT_THREADS = 1024;
-constexpr int HASH_SLOTS = 2048;
+// tokens per count / fill workgroup: 512 -> 7.7 + 8.3 us for the bench batch, 1024: 8.4 + 8.9, 256: 9.0 +
+// 9.8 (profiles/r05_ag_ab_count_fill_threads.json)
+constexpr int CNT_THREADS = 512;
+constexpr int HASH_BITS = 10;   // 2 slots per token
+constexpr int HASH_SLOTS = 1 << HASH_BITS;
+static_assert(HASH_SLOTS == 2 * CNT_THREADS, "hash table: two slots per token of the workgroup");
 
-// Per-workgroup aggregation of equal ids: an open-addressing hash table in LDS (1024 tokens ->
-// 2048 slots) collects (id, count); one global atomic per distinct id of the block.  Frequent
+// Per-workgroup aggregation of equal ids: an open-addressing hash table in LDS (512 tokens ->
+// 1024 slots) collects (id, count); one global atomic per distinct id of the block.  Frequent
 // ids (padding, [CLS], [SEP]: once per title) would otherwise serialise thousands of
 // same-address atomics at one L2 channel.  Returns the slot; `rank` = the token's arrival
 // order among the block's tokens of that id counted in `hcnt` (unique, order not fixed).
 __device__ __forceinline__ int hash_slot(int32_t* hkey, int32_t v) {
-  uint32_t h = ((uint32_t)v * 0x9E3779B1u) >> (32 - 11);   // 11 bits: HASH_SLOTS
+  uint32_t h = ((uint32_t)v * 0x9E3779B1u) >> (32 - HASH_BITS);
   for (;;) {
     const int32_t old = atomicCAS(&hkey[h], -1, v);
     if (old == -1 || old == v) return (int)h;
