@@ -51,9 +51,9 @@ __device__ __forceinline__ bool grad_on(const void* gm, int dt, int64_t t) {
 }
 
 // Workspace (nr_unique_rows_workspace): ctrl[4] | cnt_all[V] | cnt_csr[V] | cursor[V] | pos[V] | tot[2 nb].
-// ctrl, cnt_all and cnt_csr are zero on entry and left zero on return (fill_kernel, the last pass,
-// clears the counters and the flag), so a call needs no zero-fill launch; cursor / pos / tot are
-// rewritten every call.
+// ctrl, cnt_all, cnt_csr and tot are zero on entry and left zero on return (fill_kernel, the last
+// pass, clears the counters, the tile totals and the flag), so a call needs no zero-fill launch;
+// cursor / pos are rewritten every call.
 constexpr int CTRL_BAD = 1;    // an id fell outside [0, V)
 constexpr int CTRL_WORDS = 4;
 
@@ -177,13 +177,22 @@ __device__ __forceinline__ void scan_finish(int32_t U, int32_t Tv, const int32_t
   }
 }
 
-// cnt_all[v]: tokens of id v (distinctness), cnt_csr[v]: those with grad_mask set (segments)
+// cnt_all[v]: tokens of id v (distinctness), cnt_csr[v]: those with grad_mask set (segments);
+// tot[2 b], tot[2 b + 1]: the distinct ids and the segment positions of vocabulary tile b (the first
+// block to count an id sees it at zero), per block collected in LDS up to COUNT_TILES_LDS tiles, so the
+// scan reads the totals of the tiles before its own instead of re-reading their counters.
+constexpr int COUNT_TILES_LDS = 256;
 __global__ __launch_bounds__(CNT_THREADS) void count_kernel(const int64_t* __restrict__ ids, int64_t T, int64_t V,
                                                             const void* gm, int gm_dt, int32_t* __restrict__ ctrl,
                                                             int32_t* __restrict__ cnt_all,
-                                                            int32_t* __restrict__ cnt_csr) {
+                                                            int32_t* __restrict__ cnt_csr, int32_t* __restrict__ tot,
+                                                            int nb, int tile_n) {
   __shared__ int32_t hkey[HASH_SLOTS], hall[HASH_SLOTS], hcsr[HASH_SLOTS];
+  __shared__ int32_t th[2 * COUNT_TILES_LDS];
+  const bool lds_tiles = nb <= COUNT_TILES_LDS;
   for (int i = threadIdx.x; i < HASH_SLOTS; i += blockDim.x) { hkey[i] = -1; hall[i] = 0; hcsr[i] = 0; }
+  if (lds_tiles)
+    for (int i = threadIdx.x; i < 2 * nb; i += blockDim.x) th[i] = 0;
   __syncthreads();
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < T) {
@@ -197,21 +206,27 @@ __global__ __launch_bounds__(CNT_THREADS) void count_kernel(const int64_t* __res
     }
   }
   __syncthreads();
+  int32_t* tt = lds_tiles ? th : tot;
   for (int i = threadIdx.x; i < HASH_SLOTS; i += blockDim.x)
     if (hkey[i] >= 0) {
-      atomicAdd(&cnt_all[hkey[i]], hall[i]);
-      if (hcsr[i]) atomicAdd(&cnt_csr[hkey[i]], hcsr[i]);
+      const int32_t k = hkey[i], b = k / tile_n;
+      if (atomicAdd(&cnt_all[k], hall[i]) == 0) atomicAdd(&tt[2 * b], 1);
+      if (hcsr[i]) {
+        atomicAdd(&cnt_csr[k], hcsr[i]);
+        atomicAdd(&tt[2 * b + 1], hcsr[i]);
+      }
     }
+  if (lds_tiles) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * nb; i += blockDim.x)
+      if (th[i]) atomicAdd(&tot[i], th[i]);
+  }
 }
 
-// The scan over tiles of 16 x 256 entries, one workgroup per tile (ceil(V / 4096) CUs):
-//   scan_down:   each tile finds the totals of the tiles before it and runs scan_tile; the last tile
-//                writes counts and the pad entries.  Up to SCAN_OWN_MAX ids a tile sums the counters
-//                before it itself (<= 56 K int32 reads: one launch);
-//   scan_reduce: larger vocabularies first reduce per-tile totals -> tot[2b], tot[2b + 1], which
-//                scan_down then adds up.
+// The scan over tiles of 16 x 256 entries, one workgroup per tile (ceil(V / 4096) CUs): each tile
+// adds up the totals count_kernel left for the tiles before it and runs scan_tile; the last tile
+// writes counts and the pad entries.
 constexpr int SCAN_THREADS = 256;
-constexpr int SCAN_OWN_MAX = 16 * scan_tile_n<SCAN_THREADS>();
 
 // block-wide sums of two values (every thread gets both)
 __device__ __forceinline__ void block_sum2(int32_t& a, int32_t& b, int32_t* red) {
@@ -229,27 +244,6 @@ __device__ __forceinline__ void block_sum2(int32_t& a, int32_t& b, int32_t* red)
   __syncthreads();
 }
 
-__global__ __launch_bounds__(SCAN_THREADS) void scan_reduce_kernel(const int32_t* __restrict__ cnt_all,
-                                                                   const int32_t* __restrict__ cnt_csr, int64_t V,
-                                                                   int32_t* __restrict__ tot) {
-  __shared__ int32_t red[2 * SCAN_THREADS / 64];
-  constexpr int TILE = scan_tile_n<SCAN_THREADS>();
-  const int64_t base = (int64_t)blockIdx.x * TILE;
-  const int nv = (int)(V - base < TILE ? V - base : TILE);
-  int32_t fu = 0, fc = 0;
-#pragma unroll
-  for (int k = 0; k < SCAN_PER; ++k) {   // coalesced: the order inside the tile is irrelevant to a sum
-    const int i = threadIdx.x + k * SCAN_THREADS;
-    if (i < nv) {
-      fu += cnt_all[base + i] > 0 ? 1 : 0;
-      fc += cnt_csr[base + i];
-    }
-  }
-  block_sum2(fu, fc, red);
-  if (threadIdx.x == 0) { tot[2 * blockIdx.x] = fu; tot[2 * blockIdx.x + 1] = fc; }
-}
-
-template <bool OWN_PREFIX>
 __global__ __launch_bounds__(SCAN_THREADS) void scan_down_kernel(const int32_t* __restrict__ ctrl,
                                                                  const int32_t* __restrict__ cnt_all,
                                                                  const int32_t* __restrict__ cnt_csr, int64_t V,
@@ -265,18 +259,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void scan_down_kernel(const int32_t* 
   const int64_t base = (int64_t)b * TILE;
   const int nv = (int)(V - base < TILE ? V - base : TILE);
   int32_t ubase = 0, cbase = 0;   // totals of the tiles before this one
-  if constexpr (OWN_PREFIX) {   // the counters themselves: int4 loads (both arrays 16-B aligned, base % 4096 == 0)
-    const int4* a4 = reinterpret_cast<const int4*>(cnt_all);
-    const int4* c4 = reinterpret_cast<const int4*>(cnt_csr);
-#pragma unroll 4
-    for (int64_t q = threadIdx.x; q < base / 4; q += SCAN_THREADS) {
-      const int4 a = a4[q], c = c4[q];
-      ubase += (a.x > 0) + (a.y > 0) + (a.z > 0) + (a.w > 0);
-      cbase += c.x + c.y + c.z + c.w;
-    }
-  } else {
-    for (int j = threadIdx.x; j < b; j += SCAN_THREADS) { ubase += tot[2 * j]; cbase += tot[2 * j + 1]; }
-  }
+  for (int j = threadIdx.x; j < b; j += SCAN_THREADS) { ubase += tot[2 * j]; cbase += tot[2 * j + 1]; }
   block_sum2(ubase, cbase, red);
   int32_t tu, tc;
   scan_tile<SCAN_THREADS>(tile, wu, wc, cnt_all, cnt_csr, base, nv, ubase, cbase, pos, cursor, uids, seg_off, tu, tc);
@@ -293,10 +276,14 @@ __global__ __launch_bounds__(CNT_THREADS) void fill_kernel(const int64_t* __rest
                                                            int32_t* __restrict__ cursor, int64_t* __restrict__ inv,
                                                            int32_t* __restrict__ seg_tok,
                                                            int32_t* __restrict__ seg_of, int32_t* __restrict__ ctrl,
-                                                           int4* __restrict__ counters, int64_t n_counter4) {
-  // the call's last pass: both counters (2 x ceil4(V) int32, contiguous) and the flag back to zero
+                                                           int4* __restrict__ counters, int64_t n_counter4,
+                                                           int32_t* __restrict__ tot, int64_t n_tot) {
+  // the call's last pass: both counters (2 x ceil4(V) int32, contiguous), the tile totals and the
+  // flag back to zero
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n_counter4; q += (int64_t)gridDim.x * blockDim.x)
     counters[q] = make_int4(0, 0, 0, 0);
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n_tot; q += (int64_t)gridDim.x * blockDim.x)
+    tot[q] = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) ctrl[CTRL_BAD] = 0;
   __shared__ int32_t hkey[HASH_SLOTS], hcnt[HASH_SLOTS];
   for (int i = threadIdx.x; i < HASH_SLOTS; i += blockDim.x) { hkey[i] = -1; hcnt[i] = 0; }
@@ -547,23 +534,18 @@ extern "C" int nr_unique_rows(const int64_t* ids, int64_t T, int64_t V, int64_t 
   int32_t* cnt_csr = cnt_all + V4;
   int32_t* cursor = cnt_csr + V4;
   int32_t* pos = cursor + V4;
-  int32_t* tot = pos + V4;   // [nb][2] tile totals (large vocabularies)
+  int32_t* tot = pos + V4;   // [nb][2] tile totals (count_kernel; zero on entry, cleared by fill_kernel)
   const int64_t nb = (V + scan_tile_n<SCAN_THREADS>() - 1) / scan_tile_n<SCAN_THREADS>();
   // at least one count workgroup
   const unsigned gb = (unsigned)(T > 0 ? (T + CNT_THREADS - 1) / CNT_THREADS : 1);
+  constexpr int TILE = scan_tile_n<SCAN_THREADS>();
   hipLaunchKernelGGL(count_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, grad_mask, mask_dtype, ctrl,
-                     cnt_all, cnt_csr);
-  if (V <= SCAN_OWN_MAX) {
-    hipLaunchKernelGGL(scan_down_kernel<true>, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, stream, ctrl, cnt_all,
-                       cnt_csr, V, tot, pos, cursor, uids, seg_off, counts, fill_row);
-  } else {
-    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, stream, cnt_all, cnt_csr, V, tot);
-    hipLaunchKernelGGL(scan_down_kernel<false>, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, stream, ctrl, cnt_all,
-                       cnt_csr, V, tot, pos, cursor, uids, seg_off, counts, fill_row);
-  }
-  // fill runs even for T = 0: it is the pass that clears the counters and the flag
+                     cnt_all, cnt_csr, tot, (int)nb, TILE);
+  hipLaunchKernelGGL(scan_down_kernel, dim3((unsigned)nb), dim3(SCAN_THREADS), 0, stream, ctrl, cnt_all, cnt_csr, V,
+                     tot, pos, cursor, uids, seg_off, counts, fill_row);
+  // fill runs even for T = 0: it is the pass that clears the counters, the tile totals and the flag
   hipLaunchKernelGGL(fill_kernel, dim3(gb), dim3(CNT_THREADS), 0, stream, ids, T, V, grad_mask, mask_dtype, pos,
-                     cursor, inv, seg_tok, seg_of, ctrl, reinterpret_cast<int4*>(cnt_all), 2 * V4 / 4);
+                     cursor, inv, seg_tok, seg_of, ctrl, reinterpret_cast<int4*>(cnt_all), 2 * V4 / 4, tot, 2 * nb);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

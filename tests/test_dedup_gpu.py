@@ -21,7 +21,7 @@ def _ids(T, V, seed, pad_frac=0.4):
 
 # V <= 65536: count + fused scan (one launch); 200000: the multi-tile scan (two more launches)
 @pytest.mark.parametrize("T,V", [(1, 5), (37, 7), (1000, 30522), (52800, 30522), (4096, 100), (60000, 200000),
-                                 (20000, 65536), (5000, 900000)])
+                                 (20000, 65536), (5000, 900000), (3000, 1200000)])
 def test_unique_rows(T, V):
     ids = _ids(T, V, T + V)
     ur = K.UniqueRows(ids.cuda(), V, fill_row=0)
