@@ -874,8 +874,14 @@ class CNNNewsRowsFn(_GradAwareFn):
         dtable = None
         inflight = False
         if ctx.needs_input_grad[0]:
-            if PROJ_DGRAD_TAIL_WS and ABSENT_ROWS_ZERO and ctx.prec == L.GEMM_BF16X6 and 0 <= pad_row < V:
-                # the dgrad stores every present row (its tail through the workspace): zero the rest
+            # the dgrad stores every present row -- bf16x6: its stream-K tail through the workspace;
+            # bf16: as plain scatter stores (NR_EPI_SCATTER_STORE: no atomic tail, which would need
+            # zeroed rows) -- so only the absent rows and the pad row are zeroed
+            epi = L.EPI_SCATTER_ZEROED
+            if ABSENT_ROWS_ZERO and 0 <= pad_row < V and ((PROJ_DGRAD_TAIL_WS and ctx.prec == L.GEMM_BF16X6) or
+                                                          ctx.prec == L.GEMM_BF16):
+                if ctx.prec == L.GEMM_BF16:
+                    epi = L.EPI_SCATTER_STORE
                 dtable = torch.empty(V, E, device=dev)
                 rflags = _zero_absent_word_rows(ctx.table_ref, dtable, ur, pad_row)
             else:
@@ -885,7 +891,7 @@ class CNNNewsRowsFn(_GradAwareFn):
             else:
                 w_b = K.operand(w3t, L.MNCONTIG)
             K.gemm_dyn(ur.cap, E, 3 * Hp, K.operand(S, L.KCONTIG), w_b, dtable,
-                       m_dev=ur.n_rows, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(ur.uids, L.ROWS_GATHER),
+                       m_dev=ur.n_rows, epilogue=epi, c_rows=K.rows_map(ur.uids, L.ROWS_GATHER),
                        pad_row=pad_row, workspace=PROJ_DGRAD_TAIL_WS)
             if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
                 dtable = None

@@ -188,7 +188,7 @@ def test_transpose(rows, cols):
     assert torch.equal(K.transpose(src), src.t().contiguous())
 
 
-def _word_table_step(cfg, mode):
+def _word_table_step(cfg, mode, prec=None):
     """The golden model's word-table gradient, FusedAdam stepped once on it; returns the table, its
     gradient, its published row flags (or None) and whether Adam matched the dense update bitwise.
     mode "one": one forward + backward; "passes": a second backward over a batch with other history
@@ -209,13 +209,16 @@ def _word_table_step(cfg, mode):
     his = x["his_encoded_index"]
     gen = torch.Generator().manual_seed(5)
     x2 = dict(x, his_encoded_index=torch.randint(1, table.shape[0], his.shape, generator=gen).cuda() * (his != 0))
-    if mode == "one":
-        model.forward_loss(x)[1].backward()
-    elif mode == "passes":
-        model.forward_loss(x)[1].backward()
-        model.forward_loss(x2)[1].backward()
-    else:
-        (model.forward_loss(x)[1] + model.forward_loss(x2)[1]).backward()
+    import contextlib
+    from newsrec_amd import _lib as L
+    with (K.gemm_precision(getattr(L, prec)) if prec else contextlib.nullcontext()):
+        if mode == "one":
+            model.forward_loss(x)[1].backward()
+        elif mode == "passes":
+            model.forward_loss(x)[1].backward()
+            model.forward_loss(x2)[1].backward()
+        else:
+            (model.forward_loss(x)[1] + model.forward_loss(x2)[1]).backward()
     rt = table._nr_row_touched
     grad = table.grad.detach().clone()
     p0 = table.detach().clone()
@@ -229,12 +232,12 @@ def _word_table_step(cfg, mode):
     return table, grad, rt, same
 
 
-@pytest.mark.parametrize("cfg", ["nrms", "cnn_attn"])
-def test_word_table_row_flags(cfg):
+@pytest.mark.parametrize("cfg,prec", [("nrms", None), ("cnn_attn", None), ("cnn_attn", "GEMM_BF16")])
+def test_word_table_row_flags(cfg, prec):
     """The word-table gradient's row flags (nr_unique_rows_zero_absent): published for the gradient
     autograd installs as it is, set for every non-zero row and not for the pad row, and FusedAdam
-    reading them is bitwise the dense update."""
-    table, grad, rt, same = _word_table_step(cfg, "one")
+    reading them is bitwise the dense update (bf16: the CNN dgrad's plain scatter stores)."""
+    table, grad, rt, same = _word_table_step(cfg, "one", prec)
     assert rt is not None and rt[0] == table.grad.data_ptr() and rt[2] == table.grad._version
     flags = rt[1].bool().cpu()
     nz = (grad != 0).any(1).cpu()
