@@ -418,21 +418,24 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs g) {
 }
 
 // D[t][h] = Σ_d dctx[t][h*64+d] * ctx[t][h*64+d]   (one thread per (token, head))
+// D[t][h] = dctx[t, h-th 64 columns] . ctx[t, same]: one float4 of one token per thread (coalesced
+// rows), the 16 lanes of a head's 64 columns reduced by shuffles (was one thread per (token, head)
+// reading its 256-B slices: 64 cache lines per wave instruction, 2.3 TB/s on the user sequence)
 __global__ void __launch_bounds__(256) attn_dsum_kernel(const float* dctx, int64_t ldd, const float* ctx, int64_t ldc,
                                                         int64_t T, int heads, float* D) {
+  const int c4 = heads * (kHD / 4);   // float4 per token row
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= T * heads) return;
-  const int64_t t = i / heads;
-  const int h = (int)(i - t * heads);
-  const float* a = dctx + t * ldd + h * kHD;
-  const float* b = ctx + t * ldc + h * kHD;
+  const int64_t t = i / c4;
+  const int c = (int)(i - t * c4);
   float s = 0.f;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const float4 x = ld4(a + 4 * j), y = ld4(b + 4 * j);
-    s += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+  if (t < T) {
+    const float4 x = ld4(dctx + t * ldd + 4 * c), y = ld4(ctx + t * ldc + 4 * c);
+    s = x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
   }
-  D[i] = s;
+  // a head's 16 float4 are 16 consecutive threads (c4 is a multiple of 16, so they share a wave)
+#pragma unroll
+  for (int d = 8; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+  if (t < T && (c & 15) == 0) D[t * heads + (c >> 4)] = s;
 }
 
 // dK, dV: a wave owns 32 keys; query tiles (Q, dctx, stats) staged in LDS.
@@ -1431,8 +1434,8 @@ extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int
   if (!prec_ok(prec)) return NR_EINVAL(6);
   if (nseq == 0) return NR_OK;
   const int64_t T = nseq * L;
-  hipLaunchKernelGGL(attn_dsum_kernel, dim3((unsigned)((T * heads + 255) / 256)), dim3(256), 0, stream, dctx, ldd, ctx,
-                     ldc, T, heads, work);
+  hipLaunchKernelGGL(attn_dsum_kernel, dim3((unsigned)((T * heads * (kHD / 4) + 255) / 256)), dim3(256), 0, stream, dctx,
+                     ldd, ctx, ldc, T, heads, work);
   NR_LAUNCH_CHECK();
   g.dctx = dctx; g.ldd = ldd; g.Dq = work; g.dqkv = dqkv; g.lddq = lddq;
   // the f32 kernels re-hash (their forward stored no bits: the same masks either way)
