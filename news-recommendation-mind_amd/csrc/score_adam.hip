@@ -324,19 +324,43 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
     // are distinct allocations; without the explicit order the stores of one float4 would have
     // to land before the next one's loads could be issued)
     float4 pp[4], gg[4], mm[4], vv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t i = base / 4 + u * 256 + threadIdx.x;
-      pp[u] = adam_ld(e.p, i);
+    if (e.rt && e.n <= (int64_t)0x1fffffff) {
       // rows flagged untouched hold zeros: skip their gradient read (a float4 that reaches into a
       // touched row is read whole -- the untouched part reads as the zeros it holds).  The float4
-      // spans rows (4i) / rlen .. (4i + 3) / rlen: all of them when rows are shorter than 4
-      bool rd = !e.rt;
-      if (!rd)
-        for (int64_t r = (4 * i) / e.rlen; r <= (4 * i + 3) / e.rlen && !rd; ++r) rd = e.rt[r] != 0;
-      gg[u] = rd ? adam_ld(e.g, i) : make_float4(0.f, 0.f, 0.f, 0.f);
-      mm[u] = adam_ld(e.m, i);
-      vv[u] = adam_ld(e.v, i);
+      // spans rows (4i) / rlen .. (4i + 3) / rlen (up to four when rows are shorter than 4).  All
+      // the thread's flags first, then the gradient through a buffer descriptor: a skipped float4
+      // gets an out-of-range offset, which the range check answers with zeros without a memory
+      // access -- no branch around the load, no flag -> load round trip per float4
+      bool rd[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = base / 4 + u * 256 + threadIdx.x;
+        const int64_t r0 = (4 * i) / e.rlen, r1 = (4 * i + 3) / e.rlen;   // (clamped: no branch, one batch)
+        rd[u] = ((uint32_t)e.rt[r0] | (uint32_t)e.rt[r0 + 1 < r1 ? r0 + 1 : r1] |
+                 (uint32_t)e.rt[r0 + 2 < r1 ? r0 + 2 : r1] | (uint32_t)e.rt[r1]) != 0;
+      }
+      const auto grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(e.g), 0, (int)(e.n * 4), 0x00020000);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = base / 4 + u * 256 + threadIdx.x;
+        pp[u] = adam_ld(e.p, i);
+        const uint32_t off = rd[u] ? (uint32_t)(i * 16) : 0x80000000u;
+        gg[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(grs, (int)off, 0, 0));
+        mm[u] = adam_ld(e.m, i);
+        vv[u] = adam_ld(e.v, i);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = base / 4 + u * 256 + threadIdx.x;
+        pp[u] = adam_ld(e.p, i);
+        bool rd = !e.rt;   // (a gradient over 2^29 elements with row flags: the per-float4 test)
+        if (!rd)
+          for (int64_t r = (4 * i) / e.rlen; r <= (4 * i + 3) / e.rlen && !rd; ++r) rd = e.rt[r] != 0;
+        gg[u] = rd ? adam_ld(e.g, i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        mm[u] = adam_ld(e.m, i);
+        vv[u] = adam_ld(e.v, i);
+      }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
