@@ -152,7 +152,7 @@ def _wdgrad(w, keep):
 
 class BertFn(torch.autograd.Function):
     """The BertModel forward over concatenated segments -> (last_hidden [T, H], pooled [S, H]).
-    ``drop`` = list of per-site (seed, offset, rng) or None (eval / p = 0)."""
+    ``drop`` = list of per-site (seed, offset, rng, offset inside rng's range) or None (eval / p = 0)."""
 
     @staticmethod
     def forward(ctx, cfg, segs, drop, *params):
@@ -179,8 +179,8 @@ class BertFn(torch.autograd.Function):
         def dsite(k):
             if drop is None:
                 return dict(p_drop=0.0)
-            seed, off, rng = drop[k]
-            return dict(seed=seed, offset=0 if rng is not None else off, rng=rng)
+            seed, off, rng, rel = drop[k]
+            return dict(seed=seed, offset=rel if rng is not None else off, rng=rng)
 
         def dsite_seg(k, p, extra):
             d = dsite(k)
@@ -383,11 +383,16 @@ class BertModel(nn.Module):
         if not self.training or (c.hidden_dropout_prob <= 0 and c.attention_probs_dropout_prob <= 0):
             return None
         H = c.hidden_size
-        sites = [self._rng.take(T * H, device)]
-        for _ in range(c.num_hidden_layers):
-            sites.append(self._rng.take(T * 64, device))   # attention: per (seq, head) keys, q*L + k
-            sites.append(self._rng.take(T * H, device))
-            sites.append(self._rng.take(T * H, device))
+        # counter ranges of the 1 + 3 x layers sites (attention: per (seq, head) keys, q*L + k), taken
+        # as ONE snapshot (one nr_rng_take launch per step instead of 37); a site's kernels add its
+        # start inside the range to the snapshot's device offset -- the same counters, hence masks,
+        # as one take per site
+        sizes = [T * H] + [T * 64, T * H, T * H] * c.num_hidden_layers
+        seed, off, snap = self._rng.take(sum(sizes), device)
+        sites, rel = [], 0
+        for n in sizes:
+            sites.append((seed, off + rel, snap, rel))
+            rel += n
         return sites
 
     def encode_segments(self, segments):
