@@ -39,7 +39,7 @@ uids = torch.randperm(V - 1, device=dev)[:24600] + 1; dT = torch.zeros(V, E, dev
 dYc = torch.randn(52800, 1152, device=dev); WT = W.t().contiguous()
 ux = torch.randn(1600, 384, device=dev); uw = torch.randn(768, 384, device=dev) / 20; ub = torch.randn(768, device=dev)
 uy = torch.empty(1600, 768, device=dev); udy = torch.randn(1600, 768, device=dev); udx = torch.empty(1600, 384, device=dev)
-udw = torch.zeros(768, 384, device=dev); uwT = uw.t().contiguous(); m_dev = torch.tensor([24600], dtype=torch.int32, device=dev)
+udw = torch.zeros(768, 384, device=dev); udb = torch.zeros(768, device=dev); uwT = uw.t().contiguous(); m_dev = torch.tensor([24600], dtype=torch.int32, device=dev)
 adam_p = [torch.randn(30522, 768, device=dev), torch.randn(1152, 768, device=dev), torch.randn(768, 384, device=dev)]
 adam_s = [(q, torch.randn_like(q), torch.zeros_like(q), torch.zeros_like(q)) for q in adam_p]
 def adam_step(p):
@@ -56,6 +56,10 @@ cases = {
  "user_dgrad": (2*1600*768*384, lambda p: K.gemm(1600, 384, 768, K.operand(udy, L.KCONTIG), K.operand(uw, L.MNCONTIG), udx, prec=p)),
  "user_dgrad_kc": (2*1600*768*384, lambda p: K.gemm(1600, 384, 768, K.operand(udy, L.KCONTIG), K.operand(uwT, L.KCONTIG), udx, prec=p)),
  "user_wgrad": (2*1600*768*384, lambda p: K.gemm(768, 384, 1600, K.operand(udy, L.MNCONTIG), K.operand(ux, L.MNCONTIG), udw, epilogue=L.EPI_ATOMIC, split_k=F._split_k(768, 384, 1600), prec=p)),
+ "user_wgrad_s25": (2*1600*768*384, lambda p: K.gemm(768, 384, 1600, K.operand(udy, L.MNCONTIG), K.operand(ux, L.MNCONTIG), udw, epilogue=L.EPI_ATOMIC, split_k=25, prec=p)),
+ "user_wgrad_s25_cs": (2*1600*768*384, lambda p: K.gemm(768, 384, 1600, K.operand(udy, L.MNCONTIG), K.operand(ux, L.MNCONTIG), udw, epilogue=L.EPI_ATOMIC, split_k=25, prec=p, colsum=udb)),
+ "user_wgrad_cs": (2*1600*768*384, lambda p: K.gemm(768, 384, 1600, K.operand(udy, L.MNCONTIG), K.operand(ux, L.MNCONTIG), udw, epilogue=L.EPI_ATOMIC, split_k=F._split_k(768, 384, 1600), prec=p, colsum=udb)),
+ "user_wgrad_s50": (2*1600*768*384, lambda p: K.gemm(768, 384, 1600, K.operand(udy, L.MNCONTIG), K.operand(ux, L.MNCONTIG), udw, epilogue=L.EPI_ATOMIC, split_k=50, prec=p)),
  "nrms_proj_wgrad": (2*U*E*1152, lambda p: K.gemm_dyn(1152, E, U, K.operand(dY, L.MNCONTIG), K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dW, epilogue=L.EPI_ATOMIC, split_k=F._split_k(1152, E, U), prec=p)),
  "cnn_tap_proj": (2*U*E*480, lambda p: K.gemm_dyn(U, 480, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(w3, L.KCONTIG), P, prec=p)),
  "bert_qkv": (2*T*768*2304, lambda p: K.gemm(T, 2304, 768, K.operand(x, L.KCONTIG), K.operand(wqkv, L.KCONTIG), qkv, prec=p)),
