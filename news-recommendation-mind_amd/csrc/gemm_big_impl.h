@@ -341,6 +341,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
       p = p < g.tail ? p : g.tail;
       const int64_t pmax = g.K / 128;   // >= 8 k-tiles per piece
       p = p < pmax ? p : (int)pmax;
+      // pieces through the workspace: one partial tile each, at most tail_cap of them
+      if (TR && g.slab && p * r > g.tail_cap) p = g.tail_cap / r;
       if (p > 1) {
         kc_tail = ((g.K + p - 1) / p + 31) / 32 * 32;
         pieces = (int)((g.K + kc_tail - 1) / kc_tail);

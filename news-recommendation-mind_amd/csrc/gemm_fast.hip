@@ -258,13 +258,17 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
                         (reinterpret_cast<uintptr_t>(work) & 15) == 0;
       const bool fold = slab && colsum && am == MN_PLAIN;
       // the stream-K tail's pieces through the workspace too (tail_slab_tr / tail_reduce_kernel): one
-      // 256 x 256 partial tile per tail unit, at most one unit per CU (bf16x6: one 147 KB workgroup per
-      // CU; the bf16 kernel's smaller LDS image admits two, so it keeps the atomic tail)
+      // 256 x 256 partial tile per tail unit; the kernel's plan keeps the pieces within the tiles the
+      // workspace holds (Args::tail_cap), so a grid of more than one workgroup per CU cannot overrun it
+      // (bf16x6: one 147 KB workgroup per CU; the bf16 kernel keeps the atomic tail)
       const int cus = device_cus();
-      const bool tail_ws = tailed && prec == NR_GEMM_BF16X6 && work && cus > 0 &&
-                           work_elems >= (int64_t)TAIL_WS_HDR + (int64_t)cus * 65536 &&
+      const int64_t cap_tiles = work_elems > TAIL_WS_HDR ? (work_elems - TAIL_WS_HDR) / 65536 : 0;
+      const bool tail_ws = tailed && prec == NR_GEMM_BF16X6 && work && cus > 0 && cap_tiles >= cus &&
                            (reinterpret_cast<uintptr_t>(work) & 15) == 0;
-      if (tail_ws) gb.slab = work;
+      if (tail_ws) {
+        gb.slab = work;
+        gb.tail_cap = (int)(cap_tiles < 0x7fffffff ? cap_tiles : 0x7fffffff);
+      }
       if (slab) {
         gb.slab = work;
         gb.slab_ld = sld;

@@ -76,6 +76,9 @@ struct Args {
   const int32_t* mdyn;   // device-resident M (<= M), or null
   const int32_t* kdyn;   // device-resident K (<= K), or null
   int tail;  // big kernel, NR_EPI_SCATTER_ZEROED: max K pieces of the last partial round's tiles (0 = off)
+  // big kernel, the stream-K tail through the workspace (slab with tail): partial tiles the workspace
+  // holds; the plan keeps rem * pieces <= tail_cap whatever the grid (occupancy > 1 per CU included)
+  int tail_cap = 0;
   int max_cus;   // persistent grid limited to this many CUs (0 = all): leaves CUs to a concurrent collective
   // big kernel, split-K NR_EPI_ATOMIC: each split stores its partial tile to slab + split * slab_stride
   // ([M][slab_ld], plain stores) and splitk_reduce adds the splits into C -- instead of fp32 atomics

@@ -1061,6 +1061,7 @@ __global__ __launch_bounds__(768) void mha_user_pool_fwd_kernel(MPArgs g) {
 }
 
 size_t user_pool_smem(int H, int L) { return (size_t)(64 + L * (H + 1) + 64) * sizeof(float); }
+constexpr size_t NR_MAX_LDS = 160 * 1024;   // gfx950: LDS per CU, the most one workgroup may allocate
 
 // One wave per head (twelve per impression, three per SIMD at 167 VGPRs: one workgroup per CU).  Six
 // waves of two heads each, two workgroups per CU (O held for the L real slots, 77.5 KB at L = 50),
@@ -1194,6 +1195,9 @@ extern "C" int nr_mha_user_pool_fwd(const float* y, int64_t ldy, int64_t y_rows,
   g.np = prec == NR_GEMM_BF16X6 ? 3 : prec == NR_GEMM_BF16 ? 1 : 0;
   const int nh64 = heads * dv / 64;
   if ((heads * dv) % 64) return NR_EINVAL(9);
+  // O [L][H + 1] stays in LDS: at H = 768 that caps L at 53 (the caller falls back to the two-launch
+  // path, kernels.mha_user_pool_supported)
+  if (user_pool_smem(heads * dv, L) > NR_MAX_LDS) return NR_EINVAL(10);
   if (dk == 32 && dv == 32 && nh64 == 6) return launch_user_pool<32, 32, 6>(g, stream);
   if (dk == 64 && dv == 32 && nh64 == 6) return launch_user_pool<64, 32, 6>(g, stream);
   if (dk == 64 && dv == 64 && nh64 == 12) return launch_user_pool<64, 64, 12>(g, stream);

@@ -12,6 +12,7 @@ call uses the same functions with the embeddings as the "table" and identity row
 import functools
 import os
 import threading
+import weakref
 
 import torch
 
@@ -473,13 +474,31 @@ def _zero_absent_word_rows(table, dtable, ur, pad_row):
 
 
 def _word_row_flags(table, dtable, flags):
-    """Publish (or clear) the word table's row flags for optim.FusedAdam, keyed by the gradient
-    buffer's address and version counter: they apply only while ``table.grad`` is exactly that buffer,
-    unmodified (autograd installs a lone returned gradient as it is; a copy changes the address, an
-    in-place accumulation -- another use of the table in the graph, a second backward -- the version)."""
+    """Publish (or clear) the word table's row flags for optim.FusedAdam.  The backward only leaves
+    them pending, keyed by the gradient buffer's address and version counter; the table's
+    post-accumulate-grad hook (_row_flag_hook) turns them into flags bound to the very ``.grad``
+    tensor autograd installed (a weak reference to it), and only if that is the buffer, unmodified
+    (autograd installs a lone returned gradient as it is; a copy changes the address, an in-place
+    accumulation -- another use of the table in the graph, a second backward -- the version).  So the
+    flags die with that gradient: after zero_grad(set_to_none) a new gradient the caching allocator
+    places at the same address is a different tensor and never picks them up."""
     if _is_param_leaf(table):
-        table._nr_row_touched = ((dtable.data_ptr(), flags, dtable._version)
+        table._nr_row_touched = None
+        table._nr_row_pending = ((dtable.data_ptr(), flags, dtable._version)
                                  if dtable is not None and flags is not None else None)
+        if getattr(table, "_nr_row_hook", None) is None:
+            table._nr_row_hook = table.register_post_accumulate_grad_hook(_row_flag_hook)
+
+
+def _row_flag_hook(p):
+    """Post-accumulate-grad hook of a table with published row flags (see _word_row_flags)."""
+    pend = getattr(p, "_nr_row_pending", None)
+    p._nr_row_pending = None
+    g = p.grad
+    if pend is not None and g is not None and g.data_ptr() == pend[0] and g._version == pend[2]:
+        p._nr_row_touched = (weakref.ref(g), pend[1], g._version)
+    elif isinstance(getattr(p, "_nr_row_touched", None), tuple) and isinstance(p._nr_row_touched[0], weakref.ref):
+        p._nr_row_touched = None
 
 
 def _multi_rank():

@@ -143,7 +143,7 @@ _SELF_CLEANING = {}
 _RETIRED = []   # outgrown buffers stay allocated: a captured graph may still address them
 
 
-_CLEAN_WORDS = {}   # (device, name) -> leading words the kernels leave zero (the rest is scratch)
+_CLEAN_WORDS = {}   # (device, name) -> [(start, end)] word spans the kernels leave zero (the rest is scratch)
 
 
 def self_cleaning_workspace(dev, name, n, clean=None):
@@ -151,7 +151,8 @@ def self_cleaning_workspace(dev, name, n, clean=None):
     kernels whose counters start at zero and that leave them zero again (nr_unique_rows,
     nr_score_nll_fwd): no zero-fill launch per call.  ``clean``: how many leading words are such
     counters (default all; nr_unique_rows' scan outputs and the NLL head's per-impression terms that
-    follow are scratch), for ``self_cleaning_check``.
+    follow are scratch), or a list of (start, end) word spans when the counters are not one prefix
+    (nr_unique_rows' tile totals sit after its scratch arrays), for ``self_cleaning_check``.
 
     Created (or grown) by an eager call, never inside a graph capture: a buffer first zero-filled
     during a capture would only be zero once that graph had replayed.  Steps run one at a time on
@@ -164,7 +165,11 @@ def self_cleaning_workspace(dev, name, n, clean=None):
         if ws is not None:
             _RETIRED.append(ws)
         ws = _SELF_CLEANING[key] = torch.zeros(max(int(n), 4), device=dev, dtype=torch.int32)
-    _CLEAN_WORDS[key] = int(n if clean is None else clean)
+    if clean is None:
+        clean = [(0, int(n))]
+    elif not isinstance(clean, (list, tuple)):
+        clean = [(0, int(clean))]
+    _CLEAN_WORDS[key] = [(int(a), int(b)) for a, b in clean]
     return ws
 
 
@@ -187,11 +192,12 @@ def self_cleaning_check(dev=None, reset=False):
     for (d, name), ws in _SELF_CLEANING.items():
         if dev is not None and d != _dev_key(dev):
             continue
-        w = ws[:_CLEAN_WORDS.get((d, name), ws.numel())].clone()
-        if bool((w != 0).any().item()):
+        spans = _CLEAN_WORDS.get((d, name), [(0, ws.numel())])
+        if any(bool((ws[a:b] != 0).any().item()) for a, b in spans):
             bad.append(name)
             if reset:
-                ws[:w.numel()].zero_()
+                for a, b in spans:
+                    ws[a:b].zero_()
     return bad
 
 
@@ -226,9 +232,12 @@ class UniqueRows:
         self.T, self.vocab = T, vocab
         self.cap = max(32, _ceil32(min(T, vocab)))
         i32 = dict(device=dev, dtype=torch.int32)
-        # ctrl[4] | cnt_all | cnt_csr are the counters (dedup.hip); cursor | pos | tile totals scratch
-        work = self_cleaning_workspace(dev, f"nr_unique_rows/{vocab}", L.load().nr_unique_rows_workspace(vocab),
-                                       clean=4 + 2 * ((vocab + 3) // 4 * 4))
+        # ctrl[4] | cnt_all | cnt_csr | cursor | pos | tot (dedup.hip): ctrl, the two counter arrays and
+        # the vocabulary tiles' totals are zero on entry and left zero; cursor and pos are scratch
+        nwords = L.load().nr_unique_rows_workspace(vocab)
+        v4 = (vocab + 3) // 4 * 4
+        work = self_cleaning_workspace(dev, f"nr_unique_rows/{vocab}", nwords,
+                                       clean=[(0, 4 + 2 * v4), (4 + 4 * v4, nwords)])
         # the workspace keeps this call's presence scan until the next call on it (zero_absent_rows)
         key = (torch.device(dev), vocab)
         _UR_GEN[key] = self._gen = _UR_GEN.get(key, 0) + 1
@@ -456,10 +465,19 @@ def mha_attn_fwd(qk, v, mask, nseq, seq_len, heads, dk, dv, out, rows=None):
 
 
 MHA_USER_POOL_SHAPES = {(32, 32, 384), (64, 32, 384), (64, 64, 768)}
+# gfx950: 160 KB of LDS per CU, the most one workgroup may allocate (mha_pool.hip NR_MAX_LDS)
+MAX_LDS_BYTES = 160 * 1024
+
+
+def mha_user_pool_smem(seq_len, H):
+    """Dynamic LDS of mha_user_pool_fwd_kernel (mha_pool.hip user_pool_smem): row offsets, O [L][H+1],
+    the pooling scores."""
+    return (64 + seq_len * (H + 1) + 64) * 4
 
 
 def mha_user_pool_supported(seq_len, heads, dk, dv):
-    return seq_len <= 64 and heads <= 12 and (dk, dv, heads * dv) in MHA_USER_POOL_SHAPES
+    return (seq_len <= 64 and heads <= 12 and (dk, dv, heads * dv) in MHA_USER_POOL_SHAPES
+            and mha_user_pool_smem(seq_len, heads * dv) <= MAX_LDS_BYTES)
 
 
 def mha_user_pool_fwd(y, rows, mask, nseq, seq_len, heads, dk, dv, q, out, prec=None):

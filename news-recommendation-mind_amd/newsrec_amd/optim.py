@@ -1,5 +1,7 @@
 """Adam on the HIP ``nr_adam`` kernel — a drop-in for the ``torch.optim.Adam`` that
 utils/Manager.py:404-413 builds (two param groups, default betas/eps, no weight decay)."""
+import weakref
+
 import torch
 
 from . import kernels as K
@@ -69,12 +71,16 @@ class FusedAdam(torch.optim.Optimizer):
             ent = (p, g, st["exp_avg"], st["exp_avg_sq"], lr, st["step"])
             # a row-sparse table gradient (functions.LOCAL_ROW_GRAD) carries per-row "touched" flags:
             # the kernel skips reading the rows known to be zero
-            # rt = (that buffer or its address, flags, its version counter when published): the flags
-            # hold only while p.grad is that buffer, unmodified since (functions._word_row_flags)
+            # rt = (that buffer, or a weak reference to the .grad tensor they were bound to, flags, its
+            # version counter): the flags hold only while p.grad is that tensor, unmodified since
+            # (functions._LocalRowGrad, functions._word_row_flags)
             rt = getattr(p, "_nr_row_touched", None)
             if rt is not None:
-                ptr = rt[0] if isinstance(rt[0], int) else rt[0].data_ptr()
-                if p.grad.data_ptr() == ptr and (len(rt) < 3 or p.grad._version == rt[2]):
+                if isinstance(rt[0], weakref.ref):
+                    ok = rt[0]() is p.grad
+                else:
+                    ok = p.grad.data_ptr() == rt[0].data_ptr()
+                if ok and p.grad._version == rt[2]:
                     ent = ent + (rt[1],)
             batches.setdefault(key, []).append(ent)
         for (betas, eps, wd), entries in batches.items():

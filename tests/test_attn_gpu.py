@@ -144,3 +144,39 @@ def test_mha_user_pool(L, heads, dk, dv, prec):
     print("user pool L=%d dk=%d dv=%d %s: max |err| %.3e of %.3e" % (L, dk, dv, prec, err, scale))
     assert err <= tol * scale
     assert out[0].abs().max().item() == 0.0   # an empty history: zero user vector (XSoftmax)
+
+
+def test_mha_user_pool_lds_cap_falls_back():
+    """At H = 768 the fused user pool's O [L][H + 1] exceeds the 160 KB LDS from L = 54 on: the entry
+    refuses the launch (NR_EINVAL(10), never a failed hipFuncSetAttribute), mha_user_pool_supported says
+    no, and MHA_User_Encoder.forward_rows takes the two-launch path with the same result as the
+    fp64 restatement."""
+    from newsrec_amd import _lib as L_
+    from newsrec_amd.encoders import MHA_User_Encoder
+    L, heads, dk, dv = 64, 12, 64, 64
+    H = heads * dv
+    assert not K.mha_user_pool_supported(L, heads, dk, dv)
+    assert K.mha_user_pool_supported(53, heads, dk, dv) and not K.mha_user_pool_supported(54, heads, dk, dv)
+    g = torch.Generator().manual_seed(7)
+    n, nrow = 9, 100
+    y = torch.randn(nrow, heads * (dk + dv), generator=g, dtype=torch.float64)
+    rows = torch.randint(0, nrow, (n * L,), generator=g)
+    lens = torch.randint(0, L + 1, (n,), generator=g)
+    lens[0], lens[1] = 0, L
+    mask = (torch.arange(L)[None] < lens[:, None]).to(torch.float64)
+    out = torch.empty(n, H, device="cuda")
+    with pytest.raises(L_.HipError):
+        K.mha_user_pool_fwd(y.float().cuda(), rows.cuda(), mask.cuda(), n, L, heads, dk, dv,
+                            torch.randn(H, device="cuda"), out)
+
+    class _M:
+        hidden_dim, head_num, dropout_p = H, heads, 0.2
+    enc = MHA_User_Encoder(_M()).cuda()
+    assert enc.mha.key_dim == dk and enc.mha.value_dim == dv
+    q = enc.query_news.detach().double().cpu().view(-1)
+    yy = y[rows].view(n, L, -1)
+    O = _ref(yy[..., :heads * dk], yy[..., heads * dk:], mask, heads, dk, dv)
+    want = R.scaled_dp_attention(q.view(1, 1, H).expand(n, 1, H), O, O, mask.view(n, 1, L)).view(n, H)
+    got = enc.forward_rows(y.float().cuda(), rows.view(n, L).cuda(), mask.view(n, L, 1).cuda(), n, L)
+    err = (got.view(n, H).double().cpu() - want).abs().max().item()
+    assert err <= 2e-5 * want.abs().max().item()

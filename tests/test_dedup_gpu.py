@@ -96,6 +96,26 @@ def test_unique_rows_repeated_calls_and_empty(V):
     ws = K._SELF_CLEANING[(torch.device("cuda", 0), f"nr_unique_rows/{V}")]
     V4 = (V + 3) // 4 * 4
     assert int(ws[:4 + 2 * V4].abs().sum()) == 0   # ctrl words + both counters back to zero
+    assert int(ws[4 + 4 * V4:].abs().sum()) == 0    # the vocabulary tiles' totals too
+    assert K.self_cleaning_check("cuda") == []
+
+
+def test_unique_rows_dirty_tile_totals_detected():
+    """The tile totals (tot, after the scratch arrays) must be zero on entry like the counters: a call
+    stopped between count and fill would leave them set.  self_cleaning_check reports that and
+    reset=True clears them, after which the next call is exact again."""
+    V = 30522
+    K.UniqueRows(_ids(100, V, 1).cuda(), V)
+    ws = K._SELF_CLEANING[(torch.device("cuda", 0), f"nr_unique_rows/{V}")]
+    V4 = (V + 3) // 4 * 4
+    ws[4 + 4 * V4] = 7                                  # a stale tile total
+    assert f"nr_unique_rows/{V}" in K.self_cleaning_check("cuda", reset=True)
+    assert K.self_cleaning_check("cuda") == []
+    ids = _ids(5000, V, 2)
+    ur = K.UniqueRows(ids.cuda(), V)
+    torch.cuda.synchronize()
+    ref = np.unique(ids.numpy())
+    assert ur.counts.tolist()[0] == len(ref) and (ur.uids[:len(ref)].cpu().numpy() == ref).all()
 
 
 @pytest.mark.parametrize("T,V,W", [(300, 50, 1152), (52800, 30522, 1152), (33, 4, 4)])

@@ -222,16 +222,20 @@ def test_xformer_bf16x6_gemms_vs_oracle():
                  rel=5e-3)
 
 
-def test_xformer_12_layers_step_vs_oracle():
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+def test_xformer_12_layers_step_vs_oracle(p_drop):
     """configs[4] at full BERT-base depth: XFormer (12 layers, 768 wide, 12 heads, 3072 FFN, V = 30522)
     over B = 2 impressions -- 5 candidate titles each and the 501-token user sequence (CLS + 10
     word-pieces of each of 50 history titles, XFormer.py:80-89) -- one train step through the bench's
     path (forward_loss, backward, FusedAdam with the two parameter groups) against the fp32 oracle:
     logits within 1e-3, EVERY gradient within 1e-3 of its max magnitude, every parameter after Adam
     within 2 lr (all but a rounding-level handful within 1e-3 lr).  Gradients are checked against the
-    oracle run in float64 (see below).  Dropout 0 (BertFn's dropout sites are checked against their
-    kernels in tests/test_bert_gpu.py).  The key biases' gradient is zero in exact arithmetic (softmax
-    cancels q . b_k), so it is held to its attention block's gradient scale."""
+    oracle run in float64 (see below).  At p = 0.1 -- the dropout the bench times (bench.py xformer
+    leg: BERT's own hidden / attention-probability dropout) -- the oracle replays the step's device
+    masks at all 37 sites (R.BertDropout: embeddings, and per layer the attention probabilities and
+    both dense outputs), from the forward's single counter snapshot.  The key biases' gradient is zero
+    in exact arithmetic (softmax cancels q . b_k), so it is held to its attention block's gradient
+    scale."""
     import bench
     from newsrec_amd import _lib as Lb, kernels as Kn
     from newsrec_amd.bert import BertConfig
@@ -240,7 +244,7 @@ def test_xformer_12_layers_step_vs_oracle():
     assert Kn.get_gemm_precision() == Lb.GEMM_BF16X6
     torch.manual_seed(5)
     Bx, Cx, N, Lt = 2, 5, 50, 30
-    bc = BertConfig(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    bc = BertConfig(hidden_dropout_prob=p_drop, attention_probs_dropout_prob=p_drop)
     # built and initialised on the host (CPU generator: the draw -- and so the conditioning of every
     # gradient against the float64 oracle, fp32 error <= 2e-5 of max -- is the same on every box)
     model = XFormer(ManagerConfig("bert", "xformer", 768, bert_dim=768), bert_config=bc)
@@ -273,26 +277,34 @@ def test_xformer_12_layers_step_vs_oracle():
     model.train()
     opt = get_optim(model)
     opt.zero_grad(set_to_none=True)
+    rng = model.bert._rng
+    seed, off0 = rng.seed, rng.offset       # the forward's dropout counter range starts here
     logits, loss = model.forward_loss(xg)
     loss.backward(bench._one(loss))
     opt.step()
     torch.cuda.synchronize()
+    T = Bx * Cx * Lt + Bx * 501
+    drop = R.BertDropout(seed, off0, T, 768, 12, 12, p_drop, p_drop) if p_drop > 0 else None
+    if drop is not None:
+        assert rng.offset == off0 + T * 768 + 12 * T * (64 + 2 * 768)   # one range, all 37 sites
+        kd = drop.attn(0, Bx * Cx * Lt, Bx, 501).float().mean().item()
+        assert abs(kd - (1 - p_drop)) < 0.01
     base, bert = R.adam_groups(P)
     ropt = torch.optim.Adam([{"params": [P[k] for k in base], "lr": 1e-4},
                              {"params": [P[k] for k in bert], "lr": 6e-6}])
-    want = R.xformer_forward(P, x, True, 12)
+    want = R.xformer_forward(P, x, True, 12, drop=drop)
     want_loss = R.nll_loss(want, x["label"])
     want_loss.backward()
     ropt.step()
     err = (logits.detach().cpu() - want.detach()).abs().max().item()
-    print("XFormer 12 layers B=2: logit std %.3f, max |logit err| %.3e, loss %.6f vs %.6f"
-          % (want.detach().std().item(), err, loss.item(), want_loss.item()))
+    print("XFormer 12 layers B=2 p=%.1f: logit std %.3f, max |logit err| %.3e, loss %.6f vs %.6f"
+          % (p_drop, want.detach().std().item(), err, loss.item(), want_loss.item()))
     assert want.detach().std().item() > 0.05
     assert err <= 1e-3
     assert abs(loss.item() - want_loss.item()) <= 1e-3
     # gradients against the oracle in float64 (the exact values to ~1e-15): every one within 1e-3 of its
     # max magnitude (the fp32 oracle's own error is <= 2e-5 of it at this init)
-    R.nll_loss(R.xformer_forward(P64, x, True, 12), x["label"]).backward()
+    R.nll_loss(R.xformer_forward(P64, x, True, 12, drop=drop), x["label"]).backward()
     ps = dict(model.named_parameters())
     worst, worst32 = 0.0, 0.0
     for n in P:
@@ -308,8 +320,8 @@ def test_xformer_12_layers_step_vs_oracle():
         e32 = (g32.double() - want_g).abs().max().item()
         worst, worst32 = max(worst, gerr / scale), max(worst32, e32 / scale)
         assert gerr <= 1e-3 * scale, (n, gerr, e32, scale)
-    print("XFormer 12 layers: worst gradient error / max %.3e over %d tensors (fp32 oracle %.3e)"
-          % (worst, len(P), worst32))
+    print("XFormer 12 layers p=%.1f: worst gradient error / max %.3e over %d tensors (fp32 oracle %.3e)"
+          % (p_drop, worst, len(P), worst32))
     # parameters after Adam: within 2 lr of the oracle's step (Adam's first update is lr * g / (|g| + eps),
     # about lr * sign(g): an element whose exact gradient is within the rounding error of zero may step
     # either way, so elementwise agreement with the oracle's step is not the test), and the GPU step
