@@ -185,6 +185,7 @@ class GraphedStep:
             self.wgraph.replay()
             self.sync.exchange(self.packed, self.rec, works)
             self.opt_graph.replay()
+            self.sync.after_step()   # shard_tables: all-gather the updated table slabs (else nothing)
 
 
 _ONES = {}
@@ -218,6 +219,8 @@ def train_step(model, opt, x, sync):
     loss = forward_backward(model, opt, x)
     scale = sync() if sync is not None else 1.0
     opt.step(grad_scale=scale)
+    if sync is not None:
+        sync.after_step()
     return loss
 
 
@@ -263,6 +266,9 @@ def fast_eval_leg(model, dev, world, rank, n_impr):
             "metrics_random_model": res}
 
 
+SHARD_TABLES = False   # --shard-table: the word tables' Adam sharded by rows across ranks (GradSync)
+
+
 def _dp_setup(model, world):
     """Data parallel (N > 1): rank 0's parameters broadcast (DDP's construction, twotower.py:49-50) and
     a GradSync for the model (its gradient hooks are process-wide: one live GradSync at a time)."""
@@ -272,7 +278,7 @@ def _dp_setup(model, world):
     with torch.no_grad():
         for p in model.parameters():
             dist.broadcast(p, 0)
-    return GradSync(model)
+    return GradSync(model, shard_tables=SHARD_TABLES)
 
 
 def _timed(step_fn, steps, world, dev):
@@ -507,7 +513,12 @@ def main():
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the train step as HIP graphs (auto = on; N > 1: forward/backward and "
                          "optimizer graphs with the RCCL collectives between them)")
+    ap.add_argument("--shard-table", action="store_true",
+                    help="N > 1: shard the word tables' Adam by rows (reduce-scatter + slab Adam + all-gather) "
+                         "instead of the DDP all-reduce + replicated Adam")
     a = ap.parse_args()
+    global SHARD_TABLES
+    SHARD_TABLES = bool(a.shard_table)
 
     # one rank per GPU over RCCL; NR_DIST_BACKEND=gloo lets a 1-GPU box rehearse the N > 1 path
     backend = os.environ.get("NR_DIST_BACKEND", "nccl")
@@ -555,7 +566,7 @@ def main():
                 dist.broadcast(p, 0)
     use_graph = a.graph in ("on", "auto")
     opt = make_optim(model, capturable=use_graph)
-    sync = GradSync(model) if world > 1 else None
+    sync = GradSync(model, shard_tables=SHARD_TABLES) if world > 1 else None
     gen = torch.Generator().manual_seed(1234 + rank)
     feed = DeviceFeed(dev, world, rank) if a.data == "device" else \
         ResidentFeed([synth_batch(gen, dev) for _ in range(4)])
@@ -731,7 +742,11 @@ def dp_check(model, opt, world, dev):
     sums = []
     with torch.no_grad():
         for p in model.parameters():
-            ts = [p] + [opt.state[p][k] for k in ("exp_avg", "exp_avg_sq") if k in opt.state.get(p, {})]
+            # a sharded table's moments exist for the rank's own rows only (GradSync shard_tables):
+            # nothing to compare across ranks; its parameter is
+            sharded = getattr(p, "_nr_shard", None) is not None
+            ts = [p] + [opt.state[p][k] for k in ("exp_avg", "exp_avg_sq")
+                        if k in opt.state.get(p, {}) and not sharded]
             for t in ts:
                 d = t.detach().double()
                 sums.append(d.sum())
@@ -744,7 +759,8 @@ def dp_check(model, opt, world, dev):
     rel = float(diff.max().item())
     exact = bool((allv == ref).all().item())
     return {"dp_in_sync": rel <= 1e-9, "dp_bitwise_equal": exact, "dp_max_rel_diff": rel,
-            "dp_checksums": int(vec.numel()), "dp_world_size": dist.get_world_size()}
+            "dp_checksums": int(vec.numel()), "dp_world_size": dist.get_world_size(),
+            "dp_shard_tables": any(getattr(p, "_nr_shard", None) is not None for p in model.parameters())}
 
 
 if __name__ == "__main__":

@@ -27,7 +27,7 @@ from torch import nn
 
 from . import _lib as L
 from . import kernels as K
-from .functions import _empty, _gemm_backward, _proj_wgrad, _zeros_views
+from .functions import _empty, _gemm_backward, _proj_wgrad, _zeros_views, table_grad_buffer
 
 
 # the bf16-MFMA attention forward stores its dropout keep bits for the backward (False: the backward
@@ -319,7 +319,7 @@ class BertFn(torch.autograd.Function):
             K.bert_embed_bwd(word, pos, typ[0], s.ids, s.nseq, s.L, elw, st_e[r0:r0 + n], dh[r0:r0 + n],
                              ds[r0:r0 + n], delw, delb, **dsite_seg(0, p_h, r0 * H))
             ids_all.append(s.ids)
-        dword = z(word)
+        dword = table_grad_buffer(word, word.shape[0], word.shape[1], dev, zero=True)   # (dist shard padding)
         K.embedding_bwd(ds, torch.cat(ids_all) if len(ids_all) > 1 else ids_all[0], dword,
                         padding_idx=c.pad_token_id)
         for s, r0 in zip(segs, r0s):

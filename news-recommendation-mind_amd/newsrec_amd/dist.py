@@ -130,6 +130,18 @@ class GradSync:
       bucket (a few large collectives over xGMI instead of one per parameter); a gradient of
       >= ``inplace_mb`` MB is all-reduced in place, never copied into a bucket.
 
+    ``shard_tables`` (N > 1): the word tables' optimizer step is sharded by rows instead of
+    replicated (ZeRO-1 for the two [V, 768] tables, BERT.py:16-21 / XFormer.py:44-48's
+    word_embeddings): each rank owns a slab of ceil(V / world) rows, its gradient is
+    reduce-scattered in place (every rank receives the complete sum of its own slab), FusedAdam
+    updates that slab with moments for those rows only, and ``after_step`` all-gathers the updated
+    slabs in place.  The wire bytes equal the all-reduce's (a ring all-reduce IS a reduce-scatter +
+    an all-gather), while the table's Adam stream (28 B per element: 657 MB for the NRMS word table)
+    and its moments (188 MB) drop world-fold per rank; every rank ends with the same bytes of every
+    row, so replicas stay bitwise identical.  The parameter is re-homed into a buffer padded to
+    world x slab rows (``p.data`` a view of it) and its gradient comes padded as well
+    (functions.table_grad_buffer), so neither collective copies.  Dense all-reduce stays the default.
+
     ``deferred`` (a train step replayed as HIP graphs, bench.GraphedStep at N > 1): no collective
     is ever captured; they run between graphs.  The news tower's projection weight-gradient GEMM
     (WGRAD_DEFER_HOOK) is taken out of the backward, so the step is three graphs:
@@ -146,7 +158,7 @@ class GradSync:
     """
 
     def __init__(self, model, group=None, overlap_tables=True, sparse_tables=True, bucket_mb=128, inplace_mb=16,
-                 deferred=False, collective_cus=16, rows_add=None):
+                 deferred=False, collective_cus=16, rows_add=None, shard_tables=False):
         self.model = model
         # the ordered row-sparse sum (nr_rows_add_ordered); host-only tests of this plumbing on CPU
         # tensors inject their own
@@ -164,11 +176,53 @@ class GradSync:
         self._rec = []
         self._runs = []
         self._deferred = False
+        self.shards = {}   # id(param) -> (param, padded storage, first row, slab rows)
+        if shard_tables and self.world > 1:
+            for name, p in model.named_parameters():
+                if "word_embedding" in name and p.dim() == 2 and p.is_contiguous():
+                    self._shard_param(p)
         if self.overlap:
             functions.TABLE_GRAD_HOOK.set(self._table_hook)
         if self.use_sparse:
             functions.SPARSE_GRAD_HOOK.set(self._sparse_hook)
         self.deferred = deferred
+
+    def _shard_param(self, p):
+        """Re-home p's rows into a buffer of world x slab rows (p.data a view of it) and mark the slab
+        this rank's optimizer updates (optim.FusedAdam reads p._nr_shard = (first row, rows))."""
+        V, E = p.shape
+        S = -(-V // self.world)
+        r = dist.get_rank(self.group)
+        with torch.no_grad():
+            padded = torch.zeros(self.world * S, E, device=p.device, dtype=p.dtype)
+            padded[:V].copy_(p.data)
+            p.data = padded[:V]
+        row0 = r * S
+        p._nr_shard = (row0, max(0, min(S, V - row0)))
+        p._nr_grad_rows = self.world * S
+        self.shards[id(p)] = (p, padded, row0, S)
+
+    def _padded_grad(self, p, g):
+        """g ([V, E], p's gradient) as the [world x slab, E] tensor it is the head of: the buffer
+        functions.table_grad_buffer allocated padded (the reduce-scatter runs on it in place)."""
+        _, padded, _, S = self.shards[id(p)]
+        rows, E = padded.shape
+        if (g.stride() != (E, 1) or
+                g.untyped_storage().nbytes() < (g.storage_offset() + rows * E) * g.element_size()):
+            raise RuntimeError("GradSync(shard_tables): the table gradient is not padded to %d rows "
+                               "(functions.table_grad_buffer)" % rows)
+        return g.as_strided((rows, E), (E, 1))
+
+    def _reduce_scatter(self, p, g):
+        full = self._padded_grad(p, g)
+        _, _, row0, S = self.shards[id(p)]
+        return dist.reduce_scatter_tensor(full[row0:row0 + S], full, group=self.group, async_op=True)
+
+    def after_step(self):
+        """After the optimizer step: all-gather every sharded table's updated slabs in place (each
+        rank's slab of its padded storage), so every rank holds every row again."""
+        for p, padded, row0, S in self.shards.values():
+            dist.all_gather_into_tensor(padded, padded[row0:row0 + S], group=self.group)
 
     @property
     def deferred(self):
@@ -211,6 +265,12 @@ class GradSync:
     def _table_hook(self, table, dtable):
         if self.deferred:          # an ordinary gradient: all-reduced in exchange()
             return False
+        if id(table) in self.shards:
+            if table.grad is not None:
+                raise RuntimeError("GradSync(shard_tables): accumulating into a sharded table's .grad is "
+                                   "not supported; call optimizer.zero_grad(set_to_none=True) before backward")
+            self.pending.append((table, dtable, self._reduce_scatter(table, dtable)))
+            return True
         work = dist.all_reduce(dtable, group=self.group, async_op=True)
         self.pending.append((table, dtable, work))
         return True
@@ -275,6 +335,9 @@ class GradSync:
             functions.WGRAD_DEFER_HOOK.set(None)
         if self.use_sparse:
             functions.SPARSE_GRAD_HOOK.set(None)
+        for p, _, _, _ in self.shards.values():   # p keeps its padded storage (a view, same values)
+            del p._nr_shard, p._nr_grad_rows
+        self.shards.clear()
         self._dense.clear()       # the row-sparse buffers (526 MB for the LSTUR user table)
         self._touched.clear()
         self._gather_bufs.clear()
@@ -296,7 +359,8 @@ class GradSync:
         return out
 
     def _dense_params(self, skip):
-        return [p for p in self.model.parameters() if p.grad is not None and id(p) not in skip]
+        return [p for p in self.model.parameters()
+                if p.grad is not None and id(p) not in skip and id(p) not in self.shards]
 
     # ---- deferred (graph) mode
     def take_sparse(self):
@@ -321,6 +385,13 @@ class GradSync:
                 raise RuntimeError("GradSync: a deferred weight gradient is not any parameter's .grad "
                                    "(autograd copied it); its GEMM would write a detached buffer")
         early, packed = [], []
+        for p, _, _, _ in self.shards.values():
+            if p.grad is not None:   # the sharded tables: reduce-scattered in place by issue()
+                g = p.grad
+                a, b = g.data_ptr(), g.data_ptr() + g.numel() * g.element_size()
+                if any(a < e and s < b for s, e in spans):
+                    raise RuntimeError("GradSync(shard_tables): a deferred GEMM writes a sharded table's gradient")
+                early.append(([p], g, "shard"))
         for bucket, inplace in self._buckets(self._dense_params(skip)):
             if inplace:
                 g = bucket[0].grad
@@ -340,8 +411,10 @@ class GradSync:
         return early + packed, rec
 
     def issue(self, early):
-        """Start the all-reduce of the buckets complete after graph 1 (async, RCCL's stream)."""
-        return [dist.all_reduce(flat, group=self.group, async_op=True) for _, flat, _ in early]
+        """Start the all-reduce of the buckets complete after graph 1 (async, RCCL's stream); the
+        sharded tables' gradients are reduce-scattered in place instead."""
+        return [self._reduce_scatter(b[0], flat) if kind == "shard" else
+                dist.all_reduce(flat, group=self.group, async_op=True) for b, flat, kind in early]
 
     def _sparse_buffer_noreset(self, table):
         buf = self._dense.get(id(table))
@@ -353,7 +426,7 @@ class GradSync:
     def exchange(self, packed, rec, works=()):
         """Eager, between the graphs: the remaining collectives of the step, then wait for all of
         them (``works``: those ``issue`` started)."""
-        works = list(works) + [dist.all_reduce(flat, group=self.group, async_op=True) for _, flat, _ in packed]
+        works = list(works) + self.issue(packed)
         gathers = [(table,) + self._gather(table, rows, grads) for table, rows, grads in rec]
         for table, ids, gs, w1, w2 in gathers:
             w1.wait()

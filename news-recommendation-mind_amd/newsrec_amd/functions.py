@@ -382,6 +382,18 @@ def _is_param_leaf(t):
 TABLE_GRAD_HOOK = _TableGradHook()
 
 
+def table_grad_buffer(table, V, E, device, zero):
+    """The dense [V, E] gradient of a word table.  A table whose rows are sharded across ranks for
+    its optimizer step (dist.GradSync(shard_tables=True) sets ``_nr_grad_rows`` = world x slab rows)
+    gets a view of a buffer padded to that many rows, so the reduce-scatter runs on the gradient in
+    place (no 94 MB copy into a padded send buffer); every other table a plain [V, E] tensor."""
+    rows = int(getattr(table, "_nr_grad_rows", 0) or 0) if table is not None else 0
+    alloc = torch.zeros if zero else torch.empty
+    if rows > V:
+        return alloc(rows, E, device=device)[:V]
+    return alloc(V, E, device=device)
+
+
 class _SparseGradHook:
     """Optional callback ``hook(table_param, rows [n] int64, grads [n, E]) -> bool`` for tables whose
     step gradient touches only a few rows (LSTUR's user table: B rows of 876,957).  Returning True
@@ -645,10 +657,10 @@ class MHANewsFn(_GradAwareFn):
                 if PROJ_DGRAD_TAIL_WS and ABSENT_ROWS_ZERO and ctx.prec == L.GEMM_BF16X6 and 0 <= pad_row < V:
                     # every present row is stored by the dgrad (its tail through the workspace, no
                     # atomics): zero only the absent rows and the pad row instead of the whole table
-                    dtable = torch.empty(V, E, device=table.device)
+                    dtable = table_grad_buffer(ctx.table_ref, V, E, table.device, zero=False)
                     rflags = _zero_absent_word_rows(ctx.table_ref, dtable, ur, pad_row)
                 else:
-                    dtable = torch.zeros(V, E, device=table.device)
+                    dtable = table_grad_buffer(ctx.table_ref, V, E, table.device, zero=True)
                 # distinct rows (M = U, not U_pad: no duplicate pad ids): plain row stores
                 wt = K.transpose(w_cat) if PROJ_DGRAD_KC else None   # kept alive by the closure
 
@@ -675,7 +687,7 @@ class MHANewsFn(_GradAwareFn):
                 PROBE.run("proj_wgrad", lambda: wgrad(cus), dw, ur)
         else:
             if ctx.needs_input_grad[0]:
-                dtable = torch.zeros(V, E, device=table.device)
+                dtable = table_grad_buffer(ctx.table_ref, V, E, table.device, zero=True)
                 K.gemm(T, E, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dtable,
                        epilogue=L.EPI_SCATTER, c_rows=K.rows_map(ids, L.ROWS_GATHER), pad_row=pad_row)
                 if TABLE_GRAD_HOOK(ctx.table_ref, dtable):
@@ -747,7 +759,7 @@ class CNNNewsFn(torch.autograd.Function):
                     dw3, dconv_b, T)
         dtable = None
         if ctx.needs_input_grad[0]:
-            dtable = torch.zeros(V, E, device=dev)
+            dtable = table_grad_buffer(ctx.table_ref, V, E, dev, zero=True)
             w3p = w3 if Hp == H else torch.cat([w3, w3.new_zeros(Hp - H, 3 * E)], 0)
             K.gemm(T, 3 * E, Hp, K.operand(dC_full, L.KCONTIG), K.operand(w3p, L.MNCONTIG), dtable,
                    epilogue=L.EPI_SCATTER, c_rows=K.rows_map(ids, L.ROWS_CONV3, seq_len=seq_len, seg=E),
@@ -901,10 +913,10 @@ class CNNNewsRowsFn(_GradAwareFn):
                                                           ctx.prec == L.GEMM_BF16):
                 if ctx.prec == L.GEMM_BF16:
                     epi = L.EPI_SCATTER_STORE
-                dtable = torch.empty(V, E, device=dev)
+                dtable = table_grad_buffer(ctx.table_ref, V, E, dev, zero=False)
                 rflags = _zero_absent_word_rows(ctx.table_ref, dtable, ur, pad_row)
             else:
-                dtable = torch.zeros(V, E, device=dev)
+                dtable = table_grad_buffer(ctx.table_ref, V, E, dev, zero=True)
             if CNN_DGRAD_KC:   # the weights transposed (1.5 MB, by the pack launch) so both operands are k-contiguous
                 w_b = K.operand(w3tt if w3tt is not None else w3t.t().contiguous(), L.KCONTIG)
             else:

@@ -80,7 +80,19 @@ def train_step(model, optimizer, x, grad_sync=None, check_labels=True):
         logits = model(x)[0]
         loss = torch.nn.functional.nll_loss(logits, x["label"].to(logits.device))
     loss.backward()
+    scale = grad_sync() if grad_sync is not None else 1.0
+    if scale != 1.0 and not hasattr(optimizer, "sync_lr"):
+        # a torch optimizer: DDP's mean by hand (FusedAdam folds it into its kernel)
+        with torch.no_grad():
+            for g in optimizer.param_groups:
+                for p in g["params"]:
+                    if p.grad is not None:
+                        p.grad.mul_(scale)
+        scale = 1.0
+    if scale != 1.0:
+        optimizer.step(grad_scale=scale)
+    else:
+        optimizer.step()
     if grad_sync is not None:
-        grad_sync()
-    optimizer.step()
+        grad_sync.after_step()   # sharded tables: gather the updated slabs (no-op otherwise)
     return loss

@@ -52,10 +52,16 @@ class FusedAdam(torch.optim.Optimizer):
                 if p.grad is None:
                     continue
                 st = self.state[p]
+                # a table sharded across ranks (dist.GradSync(shard_tables=True)): this rank updates
+                # rows [row0, row0 + rows) only, with moments for those rows
+                shard = getattr(p, "_nr_shard", None)
+                if shard is not None and shard[1] == 0:
+                    continue
                 if len(st) == 0:
                     st["step"] = (torch.zeros((), dtype=torch.int64, device=p.device) if self.capturable else 0)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    like = p if shard is None else p[shard[0]:shard[0] + shard[1]]
+                    st["exp_avg"] = torch.zeros_like(like, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(like, memory_format=torch.contiguous_format)
                 todo.append((gi, group, p, st))
         # capturable: the device step counts are advanced by the Adam launch itself
         # (nr_adam_multi_step: the bias corrections use count + 1, the last workgroup adds 1)
@@ -68,6 +74,12 @@ class FusedAdam(torch.optim.Optimizer):
             g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
             key = (tuple(group["betas"]), group["eps"], group["weight_decay"])
             lr = self._lr_dev[gi] if self.capturable else group["lr"]
+            shard = getattr(p, "_nr_shard", None)
+            if shard is not None:
+                r0, n = shard
+                batches.setdefault(key, []).append((p.data[r0:r0 + n], g[r0:r0 + n], st["exp_avg"], st["exp_avg_sq"],
+                                                    lr, st["step"]))
+                continue
             ent = (p, g, st["exp_avg"], st["exp_avg_sq"], lr, st["step"])
             # a row-sparse table gradient (functions.LOCAL_ROW_GRAD) carries per-row "touched" flags:
             # the kernel skips reading the rows known to be zero

@@ -358,3 +358,104 @@ def test_bench_dp_check_gloo_world2(diverge):
         assert out["dp_world_size"] == 2
         assert out["dp_in_sync"] is (not diverge)
         assert out["dp_bitwise_equal"] is (not diverge)
+
+
+class TinyWords(torch.nn.Module):
+    """A word table (named like BERT_Embedding's, so GradSync(shard_tables=True) shards it) of 11 rows:
+    world 2 -> slabs of 6 (one pad row), world 3 -> slabs of 4 (the last rank owns 3 rows)."""
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.bert_word_embedding = torch.nn.Embedding(11, 4)
+        self.lin = torch.nn.Linear(4, 3)
+
+
+def _words_loss(model, x):
+    class Gather(torch.autograd.Function):   # the news tower's table gradient handling (MHANewsFn)
+        @staticmethod
+        def forward(ctx, table, idx):
+            ctx.save_for_backward(idx)
+            ctx.table_ref = table
+            return table[idx]
+
+        @staticmethod
+        def backward(ctx, g):
+            (idx,) = ctx.saved_tensors
+            t = ctx.table_ref
+            dt = F.table_grad_buffer(t, t.shape[0], t.shape[1], t.device, zero=True)
+            dt.index_add_(0, idx, g)
+            if F.TABLE_GRAD_HOOK(t, dt):
+                dt = None
+            return dt, None
+    out = model.lin(Gather.apply(model.bert_word_embedding.weight, x))
+    return (out ** 2).sum()
+
+
+def _adam_cpu(entries, beta1, beta2, eps, weight_decay, grad_scale=1.0, advance_steps=False):
+    """K.adam_multi's arithmetic on CPU tensors (torch.optim.Adam's, elementwise) for this host test."""
+    for p, g, m, v, lr, step in (e[:6] for e in entries):
+        gg = g * grad_scale
+        m.mul_(beta1).add_(gg, alpha=1 - beta1)
+        v.mul_(beta2).addcmul_(gg, gg, value=1 - beta2)
+        c1, c2 = 1 - beta1 ** step, 1 - beta2 ** step
+        p.sub_(lr * (m / c1) / ((v / c2).sqrt() + eps))
+
+
+def _shard_worker(rank, world, port, q, deferred):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    D.setup(rank, world, backend="gloo", master_port=str(port))
+    try:
+        from newsrec_amd import optim as O
+        O.K.adam_multi = _adam_cpu
+        res = {}
+        for shard in (False, True):
+            model = TinyWords()
+            sync = D.GradSync(model, bucket_mb=1e-4, inplace_mb=1e-5, shard_tables=shard, deferred=deferred)
+            opt = O.FusedAdam(model.parameters(), lr=1e-2)
+            w = model.bert_word_embedding.weight
+            if shard:
+                S = -(-11 // world)
+                assert w._nr_grad_rows == world * S and w._nr_shard == (rank * S, max(0, min(S, 11 - rank * S)))
+            for step in range(3):
+                opt.zero_grad(set_to_none=True)
+                x = torch.tensor([rank, (rank + 5 * step) % 11, 10, 7])
+                _words_loss(model, x).backward()
+                opt.step(grad_scale=sync())
+                sync.after_step()
+            if shard:   # moments for the rank's own rows only
+                assert opt.state[w]["exp_avg"].shape[0] == w._nr_shard[1]
+            sync.close()
+            res[shard] = {n: p.detach().numpy().copy() for n, p in model.named_parameters()}
+        q.put((rank, None, res))
+    except Exception as e:
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e), None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,deferred", [(2, False), (3, False), (2, True), (3, True)])
+def test_grad_sync_shard_tables_bitwise_gloo(world, deferred):
+    """GradSync(shard_tables=True): the word table's gradient reduce-scattered in place into row slabs,
+    Adam on each rank's slab only (moments for those rows), the slabs all-gathered in place after the
+    step -- three steps, eager (the reduce-scatter issued from inside the backward) and deferred (the
+    graphed step's issue / exchange), world 2 and 3 (a pad row; a short last slab): every parameter
+    BITWISE equal to the dense all-reduce path on every rank."""
+    port = _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_shard_worker, args=(r, world, port, q, deferred)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, err, r in res:
+        assert err is None, err
+        for n in r[False]:
+            assert (r[False][n] == r[True][n]).all(), (rank, n)
+    first = res[0][2][True]
+    for rank, _, r in res[1:]:
+        for n in first:
+            assert (r[True][n] == first[n]).all(), (rank, n)   # replicas identical
