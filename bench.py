@@ -203,13 +203,19 @@ def _one(t):
 def forward_backward(model, opt, x):
     """Manager._train :636-644: zero_grad, forward, NLLLoss, backward (the two-tower models fuse the
     loss into their head: TwoTowerBaseModel.forward_loss)."""
+    from newsrec_amd import functions as F
     opt.zero_grad(set_to_none=True)
     if hasattr(model, "forward_loss"):
         _, loss = model.forward_loss(x)
     else:
         logits, _ = model(x)
         loss = torch.nn.functional.nll_loss(logits, x["label"])
-    loss.backward(_one(loss))
+    F.SIDE.enabled = SIDE_STREAMS
+    try:
+        loss.backward(_one(loss))
+    finally:
+        F.SIDE.join()   # the user tower's weight gradient, forked beside the news-tower backward
+        F.SIDE.enabled = False
     return loss
 
 
@@ -267,6 +273,9 @@ def fast_eval_leg(model, dev, world, rank, n_impr):
 
 
 SHARD_TABLES = False   # --shard-table: the word tables' Adam sharded by rows across ranks (GradSync)
+# the MHA user encoder's weight gradient on a side stream beside the news-tower backward
+# (functions.SIDE; --no-side-streams: everything on the step's one stream)
+SIDE_STREAMS = True
 
 
 def _dp_setup(model, world):
@@ -516,9 +525,12 @@ def main():
     ap.add_argument("--shard-table", action="store_true",
                     help="N > 1: shard the word tables' Adam by rows (reduce-scatter + slab Adam + all-gather) "
                          "instead of the DDP all-reduce + replicated Adam")
+    ap.add_argument("--no-side-streams", action="store_true",
+                    help="run the user tower's weight gradient on the step's stream (no side-stream fork)")
     a = ap.parse_args()
-    global SHARD_TABLES
+    global SHARD_TABLES, SIDE_STREAMS
     SHARD_TABLES = bool(a.shard_table)
+    SIDE_STREAMS = not a.no_side_streams
 
     # one rank per GPU over RCCL; NR_DIST_BACKEND=gloo lets a 1-GPU box rehearse the N > 1 path
     backend = os.environ.get("NR_DIST_BACKEND", "nccl")

@@ -79,16 +79,24 @@ struct TrainArgs {
   int32_t* status;
 };
 
+// History rows per workgroup of form_train_kernel: an impression's 50 history titles go to five
+// workgroups beside the one that samples its candidates, so no workgroup walks more than a short
+// chain of dependent loads (sample index -> impression -> history offsets -> ids -> token rows) and one
+// pass of its token-row gather (one workgroup per impression, every title in it: 15.6 us per B = 32
+// batch, most of it the serial gather loop behind the sampling chain)
+constexpr int FT_HIS_ROWS = 10;
+
 __global__ __launch_bounds__(256) void form_train_kernel(TrainArgs a) {
   extern __shared__ int32_t s_mem[];
   const int C = a.npratio + 1, NH = a.his_size;
-  int32_t* s_ids = s_mem;                 // [C + NH] candidates then history
+  int32_t* s_ids = s_mem;                 // [C] candidates, or this part's history rows
   int32_t* s_pick = s_mem + C + NH;       // [npratio] sampled negative positions
   int32_t* s_perm = s_pick + a.npratio;   // [C] shuffle_pos permutation
   int32_t* s_tmp = s_perm + C;            // [C]
   __shared__ int64_t s_imp;
-  __shared__ int32_t s_neg_num, s_label;
+  __shared__ int32_t s_neg_num, s_label, s_cand0;
   const int64_t b = blockIdx.x;
+  const int part = (int)blockIdx.y;       // 0: candidates (+ user id, label); 1..: history rows
   uint64_t seed = a.seed, off = a.offset;
   if (a.rng) { seed = a.rng[0]; off = a.rng[1]; }
   const uint64_t ctr0 = off + (uint64_t)b * (uint64_t)(4 * C);
@@ -100,79 +108,90 @@ __global__ __launch_bounds__(256) void form_train_kernel(TrainArgs a) {
       sb += (int64_t)((nb > 0 ? a.rng[3] % nb : 0) * (uint64_t)gridDim.x);
     }
     int64_t idx = a.sample_idx[sb];
-    if (idx < 0 || idx >= a.P) { atomicOr(a.status, 1); idx = 0; }
+    if (idx < 0 || idx >= a.P) { if (part == 0) atomicOr(a.status, 1); idx = 0; }
     s_imp = a.imprs[2 * idx];
-    s_ids[0] = a.imprs[2 * idx + 1];
+    s_cand0 = a.imprs[2 * idx + 1];
   }
   __syncthreads();
-  // the negative sampling (thread 0's chain of dependent loads and draws) and the history ids (waves
-  // 1..: his_off -> his_ids) run side by side, not one after the other
-  if (threadIdx.x >= 64) {
-    history_ids(a.his_off, a.his_ids, s_imp, NH, (a.flags & NR_BATCH_REVERSE_HISTORY) != 0, s_ids + C,
-                a.his_mask + b * NH, 64, (int)blockDim.x - 64);
-  } else if (threadIdx.x == 0) {
-    const int64_t imp = s_imp;
-    const int64_t nb = a.neg_off[imp];
-    const int n = (int)(a.neg_off[imp + 1] - nb);
-    const int k = a.npratio;
-    if (k > n) {
-      // newsample: fewer negatives than npratio -> all of them in order, then news 0 (utils.py:95-96)
-      for (int i = 0; i < k; ++i) s_ids[1 + i] = i < n ? a.neg_ids[nb + i] : 0;
-      s_neg_num = n;
-    } else {
-      // random.sample(negs, k): a uniform k-subset (Floyd), in uniform random order (Fisher-Yates)
-      int d = 0;
-      for (int j = n - k, m = 0; j < n; ++j, ++m) {
-        const int t = (int)draw_below(seed, ctr0 + d++, (uint32_t)(j + 1));
-        bool seen = false;
-        for (int q = 0; q < m; ++q) seen |= s_pick[q] == t;
-        s_pick[m] = seen ? j : t;
+  if (part > 0) {
+    // history rows [j0, j1) (utils/MIND.py:327-345)
+    const int j0 = (part - 1) * FT_HIS_ROWS, j1 = j0 + FT_HIS_ROWS < NH ? j0 + FT_HIS_ROWS : NH;
+    if (j0 < j1) {
+      const int64_t imp = s_imp;
+      const int64_t h0 = a.his_off[imp];
+      const int64_t full = a.his_off[imp + 1] - h0;
+      const int hl = full < NH ? (int)full : NH;
+      const bool reverse = (a.flags & NR_BATCH_REVERSE_HISTORY) != 0;
+      for (int j = j0 + (int)threadIdx.x; j < j1; j += blockDim.x) {
+        int32_t id = 0;
+        if (j < hl) id = a.his_ids[h0 + (reverse ? hl - 1 - j : j)];
+        s_ids[j - j0] = id;
+        a.his_mask[b * NH + j] = (j < hl || (hl == 0 && j == 0)) ? 1.0 : 0.0;
+        a.his_id[b * NH + j] = id;
       }
-      for (int i = k - 1; i > 0; --i) {
-        const int r = (int)draw_below(seed, ctr0 + d++, (uint32_t)(i + 1));
-        const int32_t tmp = s_pick[i]; s_pick[i] = s_pick[r]; s_pick[r] = tmp;
-      }
-      for (int i = 0; i < k; ++i) s_ids[1 + i] = a.neg_ids[nb + s_pick[i]];
-      s_neg_num = k;
+      __syncthreads();
+      gather_rows(s_ids, j1 - j0, a.tok, a.attn, a.n_news, a.L, a.his_tok + (b * NH + j0) * a.L,
+                  a.his_attn ? a.his_attn + (b * NH + j0) * a.L : nullptr, a.status);
     }
-    int lab = 0;
-    if (a.flags & NR_BATCH_SHUFFLE_POS) {
-      // np.random.shuffle(arange(C)); cdd_ids = cdd_ids[s]; label = position of the positive
-      // (utils/MIND.py:319-324)
-      for (int i = 0; i < C; ++i) s_perm[i] = i;
-      for (int i = C - 1; i > 0; --i) {
-        const int r = (int)draw_below(seed, ctr0 + 2 * k + (C - 1 - i), (uint32_t)(i + 1));
-        const int32_t tmp = s_perm[i]; s_perm[i] = s_perm[r]; s_perm[r] = tmp;
+  } else {
+    if (threadIdx.x == 0) {
+      s_ids[0] = s_cand0;
+      const int64_t imp = s_imp;
+      const int64_t nb = a.neg_off[imp];
+      const int n = (int)(a.neg_off[imp + 1] - nb);
+      const int k = a.npratio;
+      if (k > n) {
+        // newsample: fewer negatives than npratio -> all of them in order, then news 0 (utils.py:95-96)
+        for (int i = 0; i < k; ++i) s_ids[1 + i] = i < n ? a.neg_ids[nb + i] : 0;
+        s_neg_num = n;
+      } else {
+        // random.sample(negs, k): a uniform k-subset (Floyd), in uniform random order (Fisher-Yates)
+        int d = 0;
+        for (int j = n - k, m = 0; j < n; ++j, ++m) {
+          const int t = (int)draw_below(seed, ctr0 + d++, (uint32_t)(j + 1));
+          bool seen = false;
+          for (int q = 0; q < m; ++q) seen |= s_pick[q] == t;
+          s_pick[m] = seen ? j : t;
+        }
+        for (int i = k - 1; i > 0; --i) {
+          const int r = (int)draw_below(seed, ctr0 + d++, (uint32_t)(i + 1));
+          const int32_t tmp = s_pick[i]; s_pick[i] = s_pick[r]; s_pick[r] = tmp;
+        }
+        for (int i = 0; i < k; ++i) s_ids[1 + i] = a.neg_ids[nb + s_pick[i]];
+        s_neg_num = k;
       }
-      for (int i = 0; i < C; ++i) s_tmp[i] = s_ids[i];
-      for (int i = 0; i < C; ++i) s_ids[i] = s_tmp[s_perm[i]];
-      for (int i = 0; i < C; ++i) if (s_perm[i] == 0) lab = i;
+      int lab = 0;
+      if (a.flags & NR_BATCH_SHUFFLE_POS) {
+        // np.random.shuffle(arange(C)); cdd_ids = cdd_ids[s]; label = position of the positive
+        // (utils/MIND.py:319-324)
+        for (int i = 0; i < C; ++i) s_perm[i] = i;
+        for (int i = C - 1; i > 0; --i) {
+          const int r = (int)draw_below(seed, ctr0 + 2 * k + (C - 1 - i), (uint32_t)(i + 1));
+          const int32_t tmp = s_perm[i]; s_perm[i] = s_perm[r]; s_perm[r] = tmp;
+        }
+        for (int i = 0; i < C; ++i) s_tmp[i] = s_ids[i];
+        for (int i = 0; i < C; ++i) s_ids[i] = s_tmp[s_perm[i]];
+        for (int i = 0; i < C; ++i) if (s_perm[i] == 0) lab = i;
+      }
+      s_label = lab;
+      a.user_id[b] = a.uindex[imp];
     }
-    s_label = lab;
+    __syncthreads();
+    for (int i = threadIdx.x; i < C; i += blockDim.x) {
+      a.cdd_id[b * C + i] = s_ids[i];
+      a.cdd_mask[b * C + i] = i < s_neg_num + 1 ? 1.0 : 0.0;
+    }
+    if (threadIdx.x == 0) a.label[b] = s_label;
+    gather_rows(s_ids, C, a.tok, a.attn, a.n_news, a.L, a.cdd_tok + b * C * a.L,
+                a.cdd_attn ? a.cdd_attn + b * C * a.L : nullptr, a.status);
   }
-  __syncthreads();
-
-  for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    a.cdd_id[b * C + i] = s_ids[i];
-    a.cdd_mask[b * C + i] = i < s_neg_num + 1 ? 1.0 : 0.0;
-  }
-  for (int j = threadIdx.x; j < NH; j += blockDim.x) a.his_id[b * NH + j] = s_ids[C + j];
-  if (threadIdx.x == 0) {
-    a.user_id[b] = a.uindex[s_imp];
-    a.label[b] = s_label;
-  }
-  gather_rows(s_ids, C, a.tok, a.attn, a.n_news, a.L, a.cdd_tok + b * C * a.L,
-              a.cdd_attn ? a.cdd_attn + b * C * a.L : nullptr, a.status);
-  gather_rows(s_ids + C, NH, a.tok, a.attn, a.n_news, a.L, a.his_tok + b * NH * a.L,
-              a.his_attn ? a.his_attn + b * NH * a.L : nullptr, a.status);
   if (a.rng) {
-    // every workgroup has read (rng[0], rng[1]) above; the last one to get here advances the
-    // offset for the next launch and resets the ticket (only thread 0 read the pair for its draws,
-    // and its loads completed before it used them)
+    // every workgroup has read (rng[0], rng[1], rng[3]) above; the last one to get here advances the
+    // offset (and the cursor) for the next launch and resets the ticket
     __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned long long t = atomicAdd(reinterpret_cast<unsigned long long*>(a.rng + 2), 1ull);
-      if (t == (unsigned long long)gridDim.x - 1) {
+      if (t == (unsigned long long)gridDim.x * gridDim.y - 1) {
         atomicAdd(reinterpret_cast<unsigned long long*>(a.rng + 1), (unsigned long long)(4 * C) * gridDim.x);
         if (a.flags & NR_BATCH_CURSOR) atomicAdd(reinterpret_cast<unsigned long long*>(a.rng + 3), 1ull);
         __hip_atomic_store(a.rng + 2, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -373,7 +392,8 @@ extern "C" int nr_form_train_batch(const int64_t* sample_idx, int64_t B, const i
   const int C = npratio + 1;
   const size_t smem = (size_t)(C + his_size + npratio + 2 * C) * sizeof(int32_t);
   if (smem > 60 * 1024) return NR_EINVAL(4);
-  hipLaunchKernelGGL(form_train_kernel, dim3((unsigned)B), dim3(256), smem, stream, a);
+  const unsigned parts = 1u + (unsigned)((his_size + FT_HIS_ROWS - 1) / FT_HIS_ROWS);
+  hipLaunchKernelGGL(form_train_kernel, dim3((unsigned)B, parts), dim3(256), smem, stream, a);
   NR_LAUNCH_CHECK();
   return NR_OK;
 }

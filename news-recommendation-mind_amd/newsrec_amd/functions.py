@@ -355,6 +355,50 @@ FUSED_KEYPOOL = True
 KEYPOOL_SAVE_K = True
 
 
+
+class _SideStreams:
+    """Off-critical-path work of a backward on a per-device side stream.  The MHA user encoder's
+    weight gradient (dW = dYᵀ x, its bias column sum: ~29 µs of small, latency-bound launches for
+    B = 32 users) feeds only the optimizer, while the news tower's backward waits for dx: forked here,
+    it runs beside the news-tower backward instead of before it.  Opt-in (``enabled``, set by the
+    train-step drivers: bench.forward_backward, manager.train_step), because whoever enables it must
+    call ``join()`` after ``loss.backward()`` -- before anything reads the gradients (the optimizer, a
+    test, a copy to the host): ``join()`` makes the current stream wait for the side work, and only then
+    releases the tensors the side work reads.  Graph capture: the fork and the join are both inside
+    the captured region (the side stream joins the capture through the event), as torch requires."""
+
+    def __init__(self):
+        self.enabled = False
+        self._streams = {}
+        self._pending = []   # (device, side stream, tensors kept alive until the join)
+
+    def run(self, dev, fn, *keep):
+        """fn() on dev's side stream after everything queued so far on the current stream; ``keep``:
+        tensors fn reads that must not be freed (and reused) before the join."""
+        if not self.enabled:
+            fn()
+            return
+        side = self._streams.get(dev)
+        if side is None:
+            side = self._streams[dev] = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            fn()
+        self._pending.append((dev, side, keep))
+
+    def join(self):
+        while self._pending:
+            dev, side, _ = self._pending.pop()
+            torch.cuda.current_stream(dev).wait_stream(side)
+
+    @property
+    def pending(self):
+        return len(self._pending)
+
+
+SIDE = _SideStreams()
+
+
 class _TableGradHook:
     """Optional callback ``hook(table_param, dtable) -> bool`` run inside a news-tower backward
     as soon as the dense word-table gradient exists (before the weight-gradient GEMMs).  When it
@@ -1023,7 +1067,8 @@ class MHAFn(_GradAwareFn):
             dx = _grad_out(ctx.dx_dest, rows, D, x)
             K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx)
         dw, db = _backward_zeros(ctx, dev, (NY, D), (NY,))
-        _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows)
+        # off the critical path (only the optimizer reads dw / db): beside the news-tower backward
+        SIDE.run(dev, lambda: _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows), dY, x)
         return dx, None, dw, db, None, None, None, None, None
 
 
