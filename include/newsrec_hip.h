@@ -294,10 +294,15 @@ int nr_mha_attn_fwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v
  *   out[s] = Σ_l XSoftmax(q · O_{s,l} / sqrt(heads*dv), m)_l O_{s,l}.
  * One workgroup per sequence, the attention products on the matrix cores in `prec` (nr_gemm_precision
  * values; bf16x6 = fp32-class).  L <= 64; (dk, dv, heads*dv) in {(32,32,384), (64,32,384), (64,64,768)};
- * y_rows = rows of y (y_rows * ldy * 4 < 2^32); yrows NULL = identity.  No autograd (eval only). */
+ * y_rows = rows of y (y_rows * ldy * 4 < 2^32); yrows NULL = identity.
+ * Training (MHA_User_Encoder's forward under autograd): o (may be NULL) receives the attention output
+ * O [nseq * L, >= heads*dv] (ld_o) and probs (may be NULL) the pooling probabilities [nseq * L] --
+ * what the backward (nr_seq_pool_bwd, nr_mha_attn_bwd) reads -- so the attention core and the pooling
+ * run as one launch in training too. */
 int nr_mha_user_pool_fwd(const float* y, int64_t ldy, int64_t y_rows, const int64_t* yrows, const void* mask,
                          int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, int32_t dk, int32_t dv,
-                         const float* q, float* out, int64_t ldo, int32_t prec, hipStream_t stream);
+                         const float* q, float* out, int64_t ldo, float* o, int64_t ld_o, float* probs,
+                         int32_t prec, hipStream_t stream);
 
 /* Backward of nr_mha_attn_fwd (XSoftmax.backward, Attention.py:77-80, and the two matmuls);
  * recomputes P.  dqk receives the gradient of the shared key projection (both roles). */

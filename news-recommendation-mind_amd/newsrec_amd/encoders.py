@@ -15,10 +15,12 @@ from torch import nn
 from . import _lib as L
 from .attention import MultiheadAttention
 from . import functions as F
+from . import kernels as K_
 from .functions import AttnPoolFn, CNNNewsFn, CNNNewsRowsFn, MHAFn, MHANewsFn, RNNUserFn
 
-# fast eval: the MHA user encoder and its pooling in one launch (nr_mha_user_pool_fwd); False runs the
-# attention core and the pooling as two launches (the form the parity tests compare it with)
+# the MHA user encoder's attention core and its pooling in one launch (nr_mha_user_pool_fwd): fast eval,
+# and training (MHAUserPoolFn, saving O and the pooling probabilities); False runs them as two launches
+# (the form the parity tests compare it with)
 USER_POOL_FUSED = True
 
 
@@ -220,8 +222,12 @@ class MHA_User_Encoder(nn.Module):
         else:
             mask = _his_mask_rows(his_mask, B, N, news_repr.device)
         w, b = self.mha.fused_weight()
-        h = MHAFn.apply(_rows_view(news_repr), mask, w, b, B, N, self.mha.head_num, self.mha.key_dim,
-                        self.mha.value_dim)
+        mha = self.mha
+        if USER_POOL_FUSED and K_.mha_user_pool_supported(N, mha.head_num, mha.key_dim, mha.value_dim):
+            # the attention core + pooling in one launch (training saves O and the pooling probabilities)
+            return F.MHAUserPoolFn.apply(_rows_view(news_repr), mask, w, b, self.query_news, B, N, mha.head_num,
+                                         mha.key_dim, mha.value_dim).unsqueeze(1)
+        h = MHAFn.apply(_rows_view(news_repr), mask, w, b, B, N, mha.head_num, mha.key_dim, mha.value_dim)
         return AttnPoolFn.apply(h, self.query_news, mask, B, N).unsqueeze(1)
 
     @torch.no_grad()

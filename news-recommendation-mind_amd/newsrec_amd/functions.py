@@ -1072,6 +1072,58 @@ class MHAFn(_GradAwareFn):
         return dx, None, dw, db, None, None, None, None, None
 
 
+class MHAUserPoolFn(_GradAwareFn):
+    """MHA_User_Encoder.forward + its Attention_Pooling (MHA.py:58-75 with Pooling.py:12-25) for
+    training: Y = x [Wk; Wv]ᵀ + b (GEMM), then the tied-QK attention core and the learned-query
+    pooling in ONE launch (nr_mha_user_pool_fwd, one workgroup per user, a wave per head, O in LDS),
+    which also stores O and the pooling probabilities for the backward -- instead of the attention
+    launch, O's round trip and the pooling launch.  Backward: the pooling (nr_seq_pool_bwd -> dO), the
+    attention core (nr_mha_attn_bwd -> dY), the input gradient and the weight gradient (the latter on
+    the side stream), as AttnPoolFn + MHAFn.  x: [B*N, D] -> [B, heads*dv]."""
+
+    @staticmethod
+    def forward(ctx, x, mask, w_cat, b_cat, query, B, N, heads, dk, dv):
+        ctx.prec = K.get_gemm_precision()
+        D = x.shape[1]
+        NY = w_cat.shape[0]
+        H = heads * dv
+        rows = B * N
+        Y = _empty(rows, NY, x)
+        K.gemm(rows, NY, D, K.operand(x, L.KCONTIG), K.operand(w_cat, L.KCONTIG), Y, bias=b_cat)
+        O = _empty(rows, H, x)
+        probs = torch.empty(rows, device=x.device)
+        out = _empty(B, H, x)
+        K.mha_user_pool_fwd(Y, None, mask, B, N, heads, dk, dv, query.reshape(-1), out, o=O, probs=probs)
+        ctx.save_for_backward(x, mask, w_cat, Y, O, probs, query)
+        ctx.cfg = (B, N, heads, dk, dv)
+        ctx.dx_dest = GRAD_DEST.take(x)
+        _reserve_zeros(ctx, x.device, (NY, D), (NY,), (H,))
+        return out
+
+    @staticmethod
+    @_gemm_backward
+    def backward(ctx, dout):
+        x, mask, w_cat, Y, O, probs, query = ctx.saved_tensors
+        B, N, heads, dk, dv = ctx.cfg
+        D = x.shape[1]
+        NQ = heads * dk
+        NY = w_cat.shape[0]
+        H = heads * dv
+        rows = B * N
+        dev = x.device
+        dw, db, dq = _backward_zeros(ctx, dev, (NY, D), (NY,), (H,))
+        dO = _empty(rows, H, x)
+        K.seq_pool_bwd(O, query.reshape(-1), mask, B, N, H, probs, dout if dout.stride(-1) == 1 else dout.contiguous(),
+                       dO, dq)
+        dY = _empty(rows, NY, x)
+        K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, B, N, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
+        dx = _grad_out(ctx.dx_dest, rows, D, x)
+        K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx)
+        # off the critical path (only the optimizer reads dw / db): beside the news-tower backward
+        SIDE.run(dev, lambda: _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows), dY, x)
+        return dx, None, dw, db, dq.view_as(query), None, None, None, None, None
+
+
 # ---------------------------------------------------------------------- recurrent user encoders
 
 class RNNUserFn(_GradAwareFn):

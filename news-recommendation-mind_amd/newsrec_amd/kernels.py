@@ -519,22 +519,34 @@ def mha_user_pool_supported(seq_len, heads, dk, dv):
             and mha_user_pool_smem(seq_len, heads * dv) <= MAX_LDS_BYTES)
 
 
-def mha_user_pool_fwd(y, rows, mask, nseq, seq_len, heads, dk, dv, q, out, prec=None):
-    """Eval MHA user encoder + pooling (MHA.py:58-75 with Pooling.py:12-25) in one launch
+def mha_user_pool_fwd(y, rows, mask, nseq, seq_len, heads, dk, dv, q, out, prec=None, o=None, probs=None):
+    """MHA user encoder + pooling (MHA.py:58-75 with Pooling.py:12-25) in one launch
     (nr_mha_user_pool_fwd): y [R, >= heads*(dk+dv)] per-news [key | value] projections, rows int64
-    [nseq*L] (history slot -> y row), mask [nseq, L], q [heads*dv] -> out [nseq, heads*dv]."""
-    _f32(y, q, out)
+    [nseq*L] (history slot -> y row; None: slot t reads row t), mask [nseq, L], q [heads*dv] -> out
+    [nseq, heads*dv].  Training: o [nseq*L, >= heads*dv] receives the attention output and probs
+    [nseq*L] the pooling probabilities (the backward's inputs)."""
+    _f32(y, q, out, o, probs)
     H = heads * dv
     _cols(y, heads * (dk + dv), "y")
     _cols(out, H, "out")
     if out.shape[0] != nseq or q.numel() != H or not q.is_contiguous():
         raise L.HipError("mha_user_pool_fwd: out [nseq, H] and a contiguous q [H] expected")
-    _check_rows(rows, None, "rows")
-    if rows.numel() != nseq * seq_len:
-        raise L.HipError("mha_user_pool_fwd: rows must hold nseq*L entries")
+    if rows is not None:
+        _check_rows(rows, None, "rows")
+        if rows.numel() != nseq * seq_len:
+            raise L.HipError("mha_user_pool_fwd: rows must hold nseq*L entries")
+    elif y.shape[0] < nseq * seq_len:
+        raise L.HipError("mha_user_pool_fwd: y needs nseq*L rows without a row table")
+    if o is not None:
+        _cols(o, H, "o")
+        if o.shape[0] < nseq * seq_len:
+            raise L.HipError("mha_user_pool_fwd: o needs nseq*L rows")
+    if probs is not None and (probs.numel() < nseq * seq_len or not probs.is_contiguous()):
+        raise L.HipError("mha_user_pool_fwd: probs needs nseq*L contiguous floats")
     mp, mdt = mask_arg(mask, nseq * seq_len)
     L.call("nr_mha_user_pool_fwd", L.ptr(y), y.stride(0), y.shape[0], L.ptr(rows), mp, mdt, nseq, seq_len, heads,
-           dk, dv, L.ptr(q), L.ptr(out), out.stride(0), _prec(prec), L.stream_ptr(out))
+           dk, dv, L.ptr(q), L.ptr(out), out.stride(0), L.ptr(o), o.stride(0) if o is not None else 0, L.ptr(probs),
+           _prec(prec), L.stream_ptr(out))
 
 
 def mha_attn_bwd(qk, v, mask, nseq, seq_len, heads, dk, dv, dout, dqk, dvv):

@@ -287,13 +287,16 @@ def test_big_planes_operands_bitwise(prec, N, M):
                prec=prec)
     torch.cuda.synchronize()
     assert torch.equal(Y0[:M - 77], Y1[:M - 77]) and torch.isnan(Y1[M - 77:]).all()
-    # plain x plain: C = X Wᵀ over stored planes of both (the dgrad shape dY Wᵀᵀ when X = dY)
-    X = torch.randn(M, E, generator=g).cuda()
+    # plain x plain: C = X Wᵀ over stored planes of both (the dgrad shape dY Wᵀᵀ when X = dY); 12,800
+    # rows, where the fp32-operand call takes the 256 x 256 kernel too (a smaller M goes to the 128 x 128
+    # kernel, whose product order differs)
+    M2 = 12800
+    X = torch.randn(M2, E, generator=g).cuda()
     xp = K.split_planes(X, nplanes=np_)
-    C0 = torch.empty(M, N, device="cuda")
-    C1 = torch.empty(M, N, device="cuda")
-    K.gemm(M, N, E, K.operand(X, L.KCONTIG), K.operand(W, L.KCONTIG), C0, prec=prec)
-    K.gemm(M, N, E, K.planes_operand(xp, E), K.planes_operand(wp, E), C1, prec=prec)
+    C0 = torch.empty(M2, N, device="cuda")
+    C1 = torch.empty(M2, N, device="cuda")
+    K.gemm(M2, N, E, K.operand(X, L.KCONTIG), K.operand(W, L.KCONTIG), C0, prec=prec)
+    K.gemm(M2, N, E, K.planes_operand(xp, E), K.planes_operand(wp, E), C1, prec=prec)
     torch.cuda.synchronize()
     assert torch.equal(C0, C1)
 
