@@ -274,8 +274,9 @@ def fast_eval_leg(model, dev, world, rank, n_impr):
 
 SHARD_TABLES = False   # --shard-table: the word tables' Adam sharded by rows across ranks (GradSync)
 # the MHA user encoder's weight gradient on a side stream beside the news-tower backward
-# (functions.SIDE; --no-side-streams: everything on the step's one stream)
-SIDE_STREAMS = True
+# (functions.SIDE; --side-streams).  Off: one-box A/B, 1.388-1.390 ms with it against 1.384 ms without
+# (profiles/r06_c_bench_side_ab.json) -- the fork / join costs what the overlap hides
+SIDE_STREAMS = False
 
 
 def _dp_setup(model, world):
@@ -525,12 +526,12 @@ def main():
     ap.add_argument("--shard-table", action="store_true",
                     help="N > 1: shard the word tables' Adam by rows (reduce-scatter + slab Adam + all-gather) "
                          "instead of the DDP all-reduce + replicated Adam")
-    ap.add_argument("--no-side-streams", action="store_true",
-                    help="run the user tower's weight gradient on the step's stream (no side-stream fork)")
+    ap.add_argument("--side-streams", action="store_true",
+                    help="run the user tower's weight gradient on a side stream beside the news-tower backward")
     a = ap.parse_args()
     global SHARD_TABLES, SIDE_STREAMS
     SHARD_TABLES = bool(a.shard_table)
-    SIDE_STREAMS = not a.no_side_streams
+    SIDE_STREAMS = bool(a.side_streams)
 
     # one rank per GPU over RCCL; NR_DIST_BACKEND=gloo lets a 1-GPU box rehearse the N > 1 path
     backend = os.environ.get("NR_DIST_BACKEND", "nccl")

@@ -42,13 +42,7 @@ enum nr_rows_map {
 
 enum nr_layout {
   NR_KCONTIG = 0, /* stored rows are the M (or N) index, k contiguous: A[M][K], B[N][K]   */
-  NR_MNCONTIG = 1, /* stored rows are the k index, M (or N) contiguous: A[K][M], B[K][N]  */
-  NR_KPLANES = 2  /* k contiguous, stored PRE-SPLIT as bf16 planes (nr_split_planes): data is a
-                     uint16 array, term p (0 = hi, 1 = mid, 2 = lo) of element (row, k) at
-                     data + r * ld + p * seg + k (ld, seg in uint16 elements, multiples of 8,
-                     16-B aligned; r = row, or rows[row] for NR_ROWS_GATHER).  bf16x6 reads all
-                     three planes, bf16 only plane 0 (= the RNE rounding it applies itself): the
-                     GEMM does no operand split.  256 x 256-tile kernel only.                 */
+  NR_MNCONTIG = 1 /* stored rows are the k index, M (or N) contiguous: A[K][M], B[K][N]   */
 };
 
 typedef struct nr_operand {
@@ -106,16 +100,6 @@ int nr_gemm_f32(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_o
                 float* C, int64_t ldc, const float* bias, int32_t epilogue,
                 const nr_operand* c_rows, int64_t pad_row, int32_t split_k, int32_t prec,
                 hipStream_t stream);
-
-/* Operand planes for NR_KPLANES: dst[r][p][k] (row r at dst + r * ld_dst, plane p at + p * seg) =
- * term p of src[rows ? rows[r] : r][k] for r < n (nplanes 3: x = h + m + l, h = RNE bf16(x),
- * m = RNE bf16(x - h), l = RNE bf16(x - h - m) -- bitwise the split the bf16x6 GEMM applies to fp32
- * operands in its k-loop; nplanes 1: h only).  K % 4 == 0; src 16-B aligned with ld_src % 4 == 0;
- * dst 8-B aligned, ld_dst and seg multiples of 4.  Produces the split once per step for operands
- * the projection GEMMs would otherwise split in every tile that reads them (BERT.py:39's table rows,
- * Attention.py:107-108's weights). */
-int nr_split_planes(const float* src, int64_t ld_src, const int64_t* rows, int64_t n, int64_t K,
-                    int32_t nplanes, uint16_t* dst, int64_t ld_dst, int64_t seg, hipStream_t stream);
 
 /* nr_gemm_f32 with device-resident extents: M and K are host upper bounds (grid sizing) and
  * the kernel reads the actual values from m_dev / k_dev (either may be NULL), so a row count

@@ -30,7 +30,7 @@ constexpr int BIG_BM = 256;
 // weight gradient 657 -> 387, NRMS table dgrad 208 -> 141, CNN conv weight gradient 144 -> 115;
 // the K-contiguous forward shapes keep 32: BERT FFN-out 152 vs 187 at 16)
 template <int NP, int AM, int BMODE>
-constexpr int big_bk() { return NP == 1 && (is_kc(AM) || is_kp(AM)) && (is_kc(BMODE) || is_kp(BMODE)) ? 32 : 16; }
+constexpr int big_bk() { return NP == 1 && is_kc(AM) && is_kc(BMODE) ? 32 : 16; }
 // bf16 per LDS row: BK k + 8 pad (48 / 80 B: odd multiples of 16 B, conflict-free ds_read_b128)
 template <int BK>
 constexpr int big_sr() { return BK + 8; }
@@ -248,77 +248,8 @@ struct BigMN {
   }
 };
 
-// K-contiguous operand stored PRE-SPLIT as bf16 planes (NR_KPLANES, nr_split_planes): the loader moves
-// the NP planes' 16-B pieces global -> registers -> LDS ([plane][row][SR] as for BigKC) with no split
-// VALU.  Per plane a k-tile row is BK bf16 = QPR pieces; a 64-lane block covers 64 / QPR rows, and
-// each 8-lane ds_write_b128 group spans 32 distinct banks: at BK = 16 (rows of 12 dwords, two pieces
-// each) rows {0, 2, 4, 6} (+ parity) start 0, 24, 16, 8 mod 32; at BK = 32 (20 dwords, four pieces)
-// rows r and r + 4 start 16 banks apart.
-template <int R, int MODE, int BK, int NPL>
-struct BigKP {
-  static constexpr int QPR = BK / 8;                       // 16-B pieces per row and plane
-  static constexpr int PER = R * QPR;                      // pieces per plane and tile
-  static constexpr int NV = PER >= 512 ? PER / 512 : 1;    // pieces per thread and plane
-  static constexpr int ACT = PER >= 512 ? 512 : PER;       // threads that load
-  static constexpr int SR = big_sr<BK>();
-  static_assert(QPR == 2 || QPR == 4, "BigKP: 16- or 32-deep k-tiles");
-  static_assert(PER % 512 == 0 || PER < 512, "BigKP: whole pieces per thread");
-  uint4 v[2][NV][NPL];
-  const uint16_t* rowp[NV];
-  int64_t seg;
-  __device__ __forceinline__ static int row_of(int f) {
-    const int l = f & 63, g8 = l >> 3;
-    return QPR == 2 ? 32 * (f >> 6) + 8 * (g8 >> 1) + (g8 & 1) + 2 * ((l >> 1) & 3)
-                    : 16 * (f >> 6) + (g8 & 3) + 8 * (g8 >> 2) + 4 * ((l >> 2) & 1);
-  }
-  __device__ __forceinline__ static int q_of(int f) { return f & (QPR - 1); }
-  __device__ __forceinline__ void init(const Op& d, int64_t r0, int64_t rlim, int tid) {
-    const uint16_t* base = reinterpret_cast<const uint16_t*>(d.base);
-    seg = d.seg;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int f = tid + 512 * i;
-      int64_t row = r0 + row_of(f);
-      row = row < rlim ? row : rlim - 1;   // clamp: rows >= M are computed and discarded
-      rowp[i] = base + (MODE == KP_GATHER ? d.idx[row] : row) * d.ld + 8 * q_of(f);
-    }
-  }
-  template <int S>
-  __device__ __forceinline__ void prefetch_idx(const Op&, int64_t, int64_t, int) {}
-  template <int S>
-  __device__ __forceinline__ void load(const Op&, int64_t, int64_t, int64_t k0, int tid) {
-    if (ACT < 512 && tid >= ACT) return;
-#pragma unroll
-    for (int i = 0; i < NV; ++i)
-#pragma unroll
-      for (int p = 0; p < NPL; ++p) v[S][i][p] = *reinterpret_cast<const uint4*>(rowp[i] + p * seg + k0);
-  }
-  template <int S, int NP>
-  __device__ __forceinline__ void store_one(uint16_t* lds, int tid, int i) const {
-    static_assert(NP == NPL, "BigKP: loads and LDS planes agree");
-    if (ACT < 512 && tid >= ACT) return;
-    constexpr int PL = R * SR;
-    const int f = tid + 512 * i;
-    uint16_t* q = lds + row_of(f) * SR + 8 * q_of(f);
-#pragma unroll
-    for (int p = 0; p < NPL; ++p) *reinterpret_cast<uint4*>(q + p * PL) = v[S][i][p];
-  }
-  template <int S, int NP>
-  __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) store_one<S, NP>(lds, tid, i);
-  }
-  static constexpr int PIECES = NV;
-  template <int S, int NP>
-  __device__ __forceinline__ void store_piece(uint16_t* lds, int tid, int p) const {
-    store_one<S, NP>(lds, tid, p);
-  }
-};
-
-template <int R, int MODE, int BK, int NP>
-using BigLoader = typename std::conditional<
-    is_kp(MODE), BigKP<R, MODE, BK, NP>,
-    typename std::conditional<is_kc(MODE), BigKC<R, MODE, BK>, BigMN<R, MODE, BK>>::type>::type;
+template <int R, int MODE, int BK>
+using BigLoader = typename std::conditional<is_kc(MODE), BigKC<R, MODE, BK>, BigMN<R, MODE, BK>>::type;
 
 // Tail pieces through a workspace (NR_EPI_SCATTER_ZEROED with Args::slab): header ints {full, rem,
 // pieces, gn} at slab[0..4) (block 0 writes them every launch), then one 256 x 256 partial tile per
@@ -376,8 +307,8 @@ template <int AM, int BMODE, bool TR, int NP, int BN>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(Args g) {
   constexpr int BM = BIG_BM;
   constexpr int BK = big_bk<NP, AM, BMODE>(), SR = big_sr<BK>(), KS = BK / 16;   // KS: 16-deep MFMA steps per k-tile
-  using LA = BigLoader<BM, AM, BK, NP>;
-  using LB = BigLoader<BN, BMODE, BK, NP>;
+  using LA = BigLoader<BM, AM, BK>;
+  using LB = BigLoader<BN, BMODE, BK>;
   constexpr int PA = BM * SR, PB = BN * SR;   // one plane
   __shared__ __attribute__((aligned(16))) uint16_t As[2 * NP * PA];
   __shared__ __attribute__((aligned(16))) uint16_t Bs[2 * NP * PB];
@@ -720,11 +651,6 @@ int launch_big_modes(const Args& g, int am, int bm, int splits, hipStream_t s) {
   NR_BIG(KC_PLAIN, MN_PLAIN, true)     // dgrad (store / scatter-store epilogues)
   NR_BIG(MN_PLAIN, MN_GATHER, false)   // wgrad over gathered rows
   NR_BIG(MN_PLAIN, MN_PLAIN, false)    // wgrad
-  // operands pre-split into bf16 planes (NR_KPLANES): no split in the k-loop
-  if constexpr (BN == 256) {
-    NR_BIG(KP_GATHER, KP_PLAIN, true)  // gathered projection (fwd) over the table's planes
-    NR_BIG(KP_PLAIN, KP_PLAIN, true)   // y = x Wᵀ / the dgrad over Wᵀ's planes
-  }
 #undef NR_BIG
   return -1;
 }

@@ -341,12 +341,9 @@ int gemm_static(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_o
     // bf16: every eligible shape runs on the bf16 kernel (one product per tile is cheap).
     const int64_t small_min = 400;
     const int fb = (prec == NR_GEMM_BF16 || t128 >= small_min) ? 128 : 64;
-    const bool planes = A->layout == NR_KPLANES || B->layout == NR_KPLANES;
-    const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, planes ? 128 : fb,
-                                planes ? 128 : fb, nullptr, nullptr, prec, 0, work, work_elems, colsum, colsum_folded,
-                                stream);
+    const int rc = nr_gemm_fast(M, N, K, A, B, C, ldc, bias, epilogue, c_rows, pad_row, split_k, fb, fb, nullptr,
+                                nullptr, prec, 0, work, work_elems, colsum, colsum_folded, stream);
     if (rc != -1) return rc;
-    if (planes) return NR_EINVAL(18);   // planar operands exist only on the 256 x 256 kernel's path
   }
   // generic kernel: same sums via atomics
   if (epilogue == NR_EPI_SCATTER_STORE || epilogue == NR_EPI_SCATTER_ZEROED) g.epi = NR_EPI_SCATTER;

@@ -152,46 +152,7 @@ __global__ __launch_bounds__(256) void tail_reduce_kernel(float* __restrict__ C,
   }
 }
 
-// NR_KPLANES producer: four k of one row per thread -> the planes (split2: the k-loop's own split)
-__global__ __launch_bounds__(256) void split_planes_kernel(const float* __restrict__ src, int64_t lds,
-                                                           const int64_t* __restrict__ rows, int64_t n, int64_t k4,
-                                                           int nplanes, uint16_t* __restrict__ dst, int64_t ldd,
-                                                           int64_t seg) {
-  const int64_t total = n * k4;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int64_t r = e / k4, k = 4 * (e - r * k4);
-    const float4 x = *reinterpret_cast<const float4*>(src + (rows ? rows[r] : r) * lds + k);
-    uint16_t* d = dst + r * ldd + k;
-    if (nplanes == 1) {
-      *reinterpret_cast<uint2*>(d) = hi4(x.x, x.y, x.z, x.w);
-    } else {
-      uint2 p0, p1, p2;
-      split4(x.x, x.y, x.z, x.w, p0, p1, p2);
-      *reinterpret_cast<uint2*>(d) = p0;
-      *reinterpret_cast<uint2*>(d + seg) = p1;
-      *reinterpret_cast<uint2*>(d + 2 * seg) = p2;
-    }
-  }
-}
-
 }  // namespace nrfast
-
-extern "C" int nr_split_planes(const float* src, int64_t ld_src, const int64_t* rows, int64_t n, int64_t K,
-                               int32_t nplanes, uint16_t* dst, int64_t ld_dst, int64_t seg, hipStream_t stream) {
-  if (n < 0 || K < 0 || (K & 3) || (ld_src & 3) || (ld_dst & 3) || (seg & 3) || ld_src < K) return NR_EINVAL(0);
-  if (nplanes != 1 && nplanes != 3) return NR_EINVAL(1);
-  if (!src || !dst || (reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 7))
-    return NR_EINVAL(2);
-  if (ld_dst < (nplanes == 3 ? 2 * seg + K : K) || (nplanes == 3 && seg < K && seg > -K)) return NR_EINVAL(3);
-  if (n == 0 || K == 0) return NR_OK;
-  const int64_t total = n * (K / 4);
-  int64_t blocks = (total + 255) / 256;
-  blocks = blocks > 8192 ? 8192 : blocks;
-  hipLaunchKernelGGL(nrfast::split_planes_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, src, ld_src, rows, n,
-                     K / 4, (int)nplanes, dst, ld_dst, seg);
-  NR_LAUNCH_CHECK();
-  return NR_OK;
-}
 
 // Elements of nr_gemm_f32_ws' split-K workspace that serve any shape: one round of 256 x 256
 // partial tiles over the device's CUs (the big kernel re-splits a split-K contraction to one unit
@@ -217,32 +178,16 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   auto aligned = [](const nr_operand* o) {
     return (o->ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(o->data) & 15) == 0);
   };
-  const bool planes = A->layout == NR_KPLANES || B->layout == NR_KPLANES;
-  if (planes) {
-    // pre-split bf16 planes: the 256 x 256 kernel over plain / gathered K-contiguous rows, both
-    // operands planar (no mixed loaders), bf16x6 (three planes) or bf16 (plane 0)
-    auto ok = [](const nr_operand* o) {
-      return o->layout == NR_KPLANES && (o->map == NR_ROWS_PLAIN || o->map == NR_ROWS_GATHER) &&
-             o->ld % 8 == 0 && o->seg % 8 == 0 && (reinterpret_cast<uintptr_t>(o->data) & 15) == 0;
-    };
-    if (!ok(A) || !ok(B) || B->map != NR_ROWS_PLAIN || prec == NR_GEMM_F32 || K % 32 || split_k > 1) return -1;
-    if (epilogue == NR_EPI_ATOMIC || epilogue == NR_EPI_SCATTER) return -1;
-  } else if (!aligned(A) || !aligned(B) || (K % 32)) {
-    return -1;
-  }
+  if (!aligned(A) || !aligned(B) || (K % 32)) return -1;
   int am, bmode;
-  if (A->layout == NR_KPLANES) {
-    am = A->map == NR_ROWS_PLAIN ? KP_PLAIN : KP_GATHER;
-  } else if (A->layout == NR_KCONTIG) {
+  if (A->layout == NR_KCONTIG) {
     am = A->map == NR_ROWS_PLAIN ? KC_PLAIN : A->map == NR_ROWS_GATHER ? KC_GATHER : KC_CONV3;
     if (am == KC_CONV3 && (A->seg % 32)) return -1;
   } else {
     if (A->map != NR_ROWS_PLAIN || A->ld < ((M + 3) & ~3LL)) return -1;
     am = MN_PLAIN;
   }
-  if (B->layout == NR_KPLANES) {
-    bmode = KP_PLAIN;
-  } else if (B->layout == NR_KCONTIG) {
+  if (B->layout == NR_KCONTIG) {
     if (B->map != NR_ROWS_PLAIN) return -1;
     bmode = KC_PLAIN;
   } else {
@@ -289,8 +234,7 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
     const int bb = big_bn(M, N, K, splits, resplit, m_dev != nullptr, kmin);
     // the bf16x6 big kernel runs its k-loop two 16-deep k-tiles per iteration with no branch: every
     // unit's k range must be a multiple of 32 (k chunks are; K must be)
-    int BN = prec == NR_GEMM_BF16X6 && K % 32 != 0 ? 0 : (tailed ? 256 : (bb > 0 ? bb : 0));
-    if (planes) BN = 256;   // the planes loader exists for the 256 x 256 tiles only
+    const int BN = prec == NR_GEMM_BF16X6 && K % 32 != 0 ? 0 : (tailed ? 256 : (bb > 0 ? bb : 0));
     if (BN) {
       Args gb = g;
       if (tailed) gb.tail = 16;
@@ -350,7 +294,6 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
       if (rc != -1) return rc;
     }
   }
-  if (planes) return -1;
   if (bm == 128 && bn == 128) return launch_modes<128, 128>(g, am, bmode, splits, prec, stream);
   if (bm == 64 && bn == 64) return launch_modes64(g, am, bmode, splits, stream);
   return -1;

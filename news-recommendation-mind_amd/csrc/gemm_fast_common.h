@@ -50,12 +50,9 @@ constexpr int SROW = 40;          // split LDS image: [plane][row][k] bf16, 32 k
 constexpr int SPL = 128 * SROW;   // one plane of a 128-row operand tile
 
 // operand modes
-// KP_*: K-contiguous rows stored pre-split as bf16 planes (NR_KPLANES; the 256 x 256 kernel only)
-enum { KC_PLAIN = 0, KC_GATHER = 1, KC_CONV3 = 2, MN_PLAIN = 3, MN_GATHER = 4, MN_CONV3 = 5, KP_PLAIN = 6,
-       KP_GATHER = 7 };
+enum { KC_PLAIN = 0, KC_GATHER = 1, KC_CONV3 = 2, MN_PLAIN = 3, MN_GATHER = 4, MN_CONV3 = 5 };
 
 constexpr bool is_kc(int m) { return m <= KC_CONV3; }
-constexpr bool is_kp(int m) { return m == KP_PLAIN || m == KP_GATHER; }
 
 struct Op {
   const float* base;

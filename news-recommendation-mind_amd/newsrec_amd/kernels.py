@@ -416,45 +416,6 @@ def operand(t, layout, rows=None, mapping=L.ROWS_PLAIN, seq_len=1, seg=1, ld=Non
     return op
 
 
-def planes_width(K):
-    """Elements per plane of a NR_KPLANES row: K rounded up to 8 (16-B aligned plane pieces)."""
-    return (K + 7) // 8 * 8
-
-
-def split_planes(src, rows=None, nplanes=3, out=None):
-    """The bf16 terms of src's rows (or of src[rows]) for NR_KPLANES operands (nr_split_planes):
-    -> bf16 [n, nplanes * Kp] (Kp = planes_width(K)): row r = [hi | mid | lo] of src row r, the very
-    split the bf16x6 GEMM applies in its k-loop (nplanes 1: the RNE bf16 rounding only)."""
-    _f32(src)
-    if src.dim() != 2 or src.stride(1) != 1 or src.stride(0) % 4 or src.data_ptr() % 16 or src.shape[1] % 4:
-        raise L.HipError("split_planes: src must be row-major with ld % 4 == 0, K % 4 == 0, 16-B aligned")
-    _check_rows(rows, None, "split_planes")
-    n = rows.numel() if rows is not None else src.shape[0]
-    K = src.shape[1]
-    kp = planes_width(K)
-    if out is None:
-        out = torch.zeros(n, nplanes * kp, device=src.device, dtype=torch.bfloat16)
-    if out.dtype != torch.bfloat16 or out.dim() != 2 or out.shape[0] < n or out.shape[1] < nplanes * kp or \
-            out.stride(1) != 1 or out.stride(0) % 8 or out.data_ptr() % 16:
-        raise L.HipError("split_planes: out must be a row-major bf16 [n, nplanes * Kp] tensor, ld % 8 == 0")
-    L.call("nr_split_planes", L.ptr(src), src.stride(0), L.ptr(rows), n, K, nplanes, L.ptr(out), out.stride(0), kp,
-           L.stream_ptr(src))
-    return out
-
-
-def planes_operand(planes, K, rows=None):
-    """A NR_KPLANES operand over split_planes' output: K-contiguous rows of K elements (gathered by
-    ``rows`` when given), plane p at column p * planes_width(K)."""
-    if planes.dtype != torch.bfloat16 or not planes.is_cuda or planes.dim() != 2 or planes.stride(1) != 1 or \
-            planes.stride(0) % 8 or planes.data_ptr() % 16:
-        raise L.HipError("planes_operand: a row-major bf16 CUDA tensor, ld % 8 == 0, 16-B aligned")
-    _check_rows(rows, None, "planes_operand")
-    op = L.nr_operand(planes.data_ptr(), planes.stride(0), rows.data_ptr() if rows is not None else 0,
-                      L.ROWS_GATHER if rows is not None else L.ROWS_PLAIN, 1, planes_width(K), L.KPLANES)
-    op._keep = (planes, rows)
-    return op
-
-
 def rows_map(rows, mapping, seq_len=1, seg=1):
     """A row map for the SCATTER epilogue (no data)."""
     _check_rows(rows, None, "rows_map")

@@ -245,69 +245,3 @@ def test_big_wgrad_folds_bias_colsum(kd):
                 epilogue=L.EPI_ATOMIC, split_k=2, colsum=small[:64])
     assert not f2 and torch.equal(small.cpu(), db0)
 
-
-def test_split_planes_terms():
-    """nr_split_planes: hi = RNE bf16(x), mid = RNE bf16(x - hi), lo = RNE bf16(x - hi - mid) (the
-    k-loop's split), gathered rows, h + m + l within 2^-24 |x|; one plane = the RNE rounding."""
-    g = torch.Generator().manual_seed(3)
-    src = torch.randn(300, 772, generator=g).cuda()[:, :768]
-    rows = torch.randint(0, 300, (123,), generator=g).cuda()
-    pl = K.split_planes(src, rows=rows)
-    kp = K.planes_width(768)
-    x = src[rows].double()
-    h, m, l = (pl[:, i * kp:i * kp + 768].double() for i in range(3))
-    assert torch.equal(pl[:, :768], src[rows].bfloat16())
-    assert torch.equal(pl[:, kp:kp + 768], (src[rows] - h.float()).bfloat16())
-    assert ((h + m + l - x).abs() <= x.abs() * 2.0 ** -23).all()
-    one = K.split_planes(src, nplanes=1)
-    assert torch.equal(one[:, :768], src.bfloat16())
-
-
-@pytest.mark.parametrize("prec", PRECS)
-@pytest.mark.parametrize("N,M", [(1152, 3000), (768, 1000)])
-def test_big_planes_operands_bitwise(prec, N, M):
-    """NR_KPLANES operands (pre-split bf16 planes, no split in the k-loop) give BITWISE the result of
-    the same GEMM on the fp32 operands: the gathered projection (table planes gathered by ids, W's
-    planes) and the plain form (the dgrad over Wᵀ's planes), device-resident M, bias; bf16 reads the
-    hi plane only (nplanes 1 or 3 in memory)."""
-    g = torch.Generator().manual_seed(N + M)
-    V, E = 5000, 768
-    table = torch.randn(V, E, generator=g).cuda()
-    ids = torch.randint(0, V, (M,), generator=g).cuda()
-    W = (torch.randn(N, E, generator=g) / 16).cuda()
-    bias = torch.randn(N, generator=g).cuda()
-    m_dev = torch.tensor([M - 77], dtype=torch.int32, device="cuda")
-    np_ = 1 if prec == L.GEMM_BF16 and N == 768 else 3
-    tp, wp = K.split_planes(table, nplanes=np_), K.split_planes(W, nplanes=np_)
-    Y0 = torch.full((M, N), float("nan"), device="cuda")
-    Y1 = Y0.clone()
-    K.gemm_dyn(M, N, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(W, L.KCONTIG), Y0,
-               m_dev=m_dev, bias=bias, prec=prec)
-    K.gemm_dyn(M, N, E, K.planes_operand(tp, E, rows=ids), K.planes_operand(wp, E), Y1, m_dev=m_dev, bias=bias,
-               prec=prec)
-    torch.cuda.synchronize()
-    assert torch.equal(Y0[:M - 77], Y1[:M - 77]) and torch.isnan(Y1[M - 77:]).all()
-    # plain x plain: C = X Wᵀ over stored planes of both (the dgrad shape dY Wᵀᵀ when X = dY); 12,800
-    # rows, where the fp32-operand call takes the 256 x 256 kernel too (a smaller M goes to the 128 x 128
-    # kernel, whose product order differs)
-    M2 = 12800
-    X = torch.randn(M2, E, generator=g).cuda()
-    xp = K.split_planes(X, nplanes=np_)
-    C0 = torch.empty(M2, N, device="cuda")
-    C1 = torch.empty(M2, N, device="cuda")
-    K.gemm(M2, N, E, K.operand(X, L.KCONTIG), K.operand(W, L.KCONTIG), C0, prec=prec)
-    K.gemm(M2, N, E, K.planes_operand(xp, E), K.planes_operand(wp, E), C1, prec=prec)
-    torch.cuda.synchronize()
-    assert torch.equal(C0, C1)
-
-
-def test_big_planes_refused_where_unsupported():
-    """Planar operands exist on the 256 x 256 kernel only: f32 arithmetic, a planar operand beside an
-    fp32 one, or split-K raise instead of running a kernel that would misread them."""
-    a = torch.randn(512, 768, device="cuda")
-    ap = K.split_planes(a)
-    C = torch.empty(512, 512, device="cuda")
-    with pytest.raises(L.HipError):
-        K.gemm(512, 512, 768, K.planes_operand(ap, 768), K.planes_operand(ap, 768), C, prec=L.GEMM_F32)
-    with pytest.raises(L.HipError):
-        K.gemm(512, 512, 768, K.planes_operand(ap, 768), K.operand(a, L.KCONTIG), C, prec=L.GEMM_BF16X6)

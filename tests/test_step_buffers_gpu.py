@@ -142,7 +142,7 @@ def test_side_stream_user_wgrad(side):
         try:
             bench.forward_backward(model, FusedAdam(model.parameters()), x)
         finally:
-            bench.SIDE_STREAMS = True
+            bench.SIDE_STREAMS = False
         assert F.SIDE.pending == 0 and not F.SIDE.enabled
         out[s] = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
         _check(g, model)

@@ -1,5 +1,5 @@
 """A/B of the NRMS train step (bench.py's headline, graphed, device-formed batches) under module-level
-switches of newsrec_amd.functions, interleaved in ONE process (rounds x variants), so box-to-box and
+switches (newsrec_amd.functions NAME, or encoders.NAME / bench.NAME), interleaved in ONE process (rounds x variants), so box-to-box and
 clock drift cancel.  python tools/ab_step.py DEDUP_ROWS=1 DEDUP_ROWS=0 [--rounds 3 --steps 20]"""
 import argparse
 import json
@@ -26,11 +26,17 @@ def main():
     dev = torch.device("cuda", 0)
     feed = bench.DeviceFeed(dev, 1, 0)
     steps = {}
+    from newsrec_amd import encoders as EN
+    mods = {"functions": F, "encoders": EN, "bench": bench}
     for v in a.variants:
         for kv in v.split(","):
             k, val = kv.split("=")
-            cur = getattr(F, k)
-            setattr(F, k, bool(int(val)) if isinstance(cur, bool) else int(val))
+            mod = F
+            if "." in k:   # module.NAME (functions, encoders, bench); bare NAME = functions.NAME
+                m, k = k.split(".", 1)
+                mod = mods[m]
+            cur = getattr(mod, k)
+            setattr(mod, k, bool(int(val)) if isinstance(cur, bool) else int(val))
         model = bench.build(dev)
         model.train()
         opt = bench.make_optim(model, capturable=True)

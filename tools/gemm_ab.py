@@ -40,8 +40,6 @@ dYc = torch.randn(52800, 1152, device=dev); WT = W.t().contiguous()
 ux = torch.randn(1600, 384, device=dev); uw = torch.randn(768, 384, device=dev) / 20; ub = torch.randn(768, device=dev)
 uy = torch.empty(1600, 768, device=dev); udy = torch.randn(1600, 768, device=dev); udx = torch.empty(1600, 384, device=dev)
 udw = torch.zeros(768, 384, device=dev); udb = torch.zeros(768, device=dev); uwT = uw.t().contiguous(); m_dev = torch.tensor([24600], dtype=torch.int32, device=dev)
-tplanes = K.split_planes(table); rplanes = K.split_planes(table, rows=ids); Wp = K.split_planes(W)
-dYp = K.split_planes(dYc); WTp = K.split_planes(WT)
 adam_p = [torch.randn(30522, 768, device=dev), torch.randn(1152, 768, device=dev), torch.randn(768, 384, device=dev)]
 adam_s = [(q, torch.randn_like(q), torch.zeros_like(q), torch.zeros_like(q)) for q in adam_p]
 def adam_step(p):
@@ -77,12 +75,7 @@ cases = {
  "cnn_conv_wgrad": (2*U*E*480, lambda p: K.gemm_dyn(480, E, U, K.operand(Pg, L.MNCONTIG), K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), dw3, epilogue=L.EPI_ATOMIC, split_k=F._split_k(480, E, U), prec=p)),
  "cnn_table_dgrad_kc": (2*24600*E*480, lambda p: K.gemm_dyn(U, E, 480, K.operand(Pg, L.KCONTIG), K.operand(w3T, L.KCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
  "cnn_table_dgrad": (2*24600*E*480, lambda p: K.gemm_dyn(U, E, 480, K.operand(Pg, L.KCONTIG), K.operand(w3, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
- "split_table_planes": (0, lambda p: K.split_planes(table, out=tplanes)),
- "split_rows_planes": (0, lambda p: K.split_planes(table, rows=ids, out=rplanes)),
- "nrms_proj_fwd_planes": (2*U*E*1152, lambda p: K.gemm_dyn(U, 1152, E, K.planes_operand(tplanes, E, rows=ids), K.planes_operand(Wp, E), Y, prec=p)),
- "nrms_proj_fwd_rplanes": (2*U*E*1152, lambda p: K.gemm_dyn(U, 1152, E, K.planes_operand(rplanes, E), K.planes_operand(Wp, E), Y, prec=p)),
  "nrms_dgrad_table_kc_ws": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), K.operand(WT, L.KCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p, workspace=True)),
- "nrms_dgrad_table_planes": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.planes_operand(dYp, 1152), K.planes_operand(WTp, 1152), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p, workspace=True)),
  "nrms_proj_wgrad_atomic": (2*U*E*1152, lambda p: L.call("nr_gemm_f32_dyn", 1152, E, U, K.operand(dY, L.MNCONTIG), K.operand(table, L.MNCONTIG, rows=ids, mapping=L.ROWS_GATHER), L.ptr(dW), E, None, L.EPI_ATOMIC, None, -1, F._split_k(1152, E, U), None, None, p, L.stream_ptr(dW))),
 }
 out = {}
