@@ -203,19 +203,13 @@ def _one(t):
 def forward_backward(model, opt, x):
     """Manager._train :636-644: zero_grad, forward, NLLLoss, backward (the two-tower models fuse the
     loss into their head: TwoTowerBaseModel.forward_loss)."""
-    from newsrec_amd import functions as F
     opt.zero_grad(set_to_none=True)
     if hasattr(model, "forward_loss"):
         _, loss = model.forward_loss(x)
     else:
         logits, _ = model(x)
         loss = torch.nn.functional.nll_loss(logits, x["label"])
-    F.SIDE.enabled = SIDE_STREAMS
-    try:
-        loss.backward(_one(loss))
-    finally:
-        F.SIDE.join()   # the user tower's weight gradient, forked beside the news-tower backward
-        F.SIDE.enabled = False
+    loss.backward(_one(loss))
     return loss
 
 
@@ -273,10 +267,6 @@ def fast_eval_leg(model, dev, world, rank, n_impr):
 
 
 SHARD_TABLES = False   # --shard-table: the word tables' Adam sharded by rows across ranks (GradSync)
-# the MHA user encoder's weight gradient on a side stream beside the news-tower backward
-# (functions.SIDE; --side-streams).  Off: one-box A/B, 1.388-1.390 ms with it against 1.384 ms without
-# (profiles/r06_c_bench_side_ab.json) -- the fork / join costs what the overlap hides
-SIDE_STREAMS = False
 
 
 def _dp_setup(model, world):
@@ -526,12 +516,9 @@ def main():
     ap.add_argument("--shard-table", action="store_true",
                     help="N > 1: shard the word tables' Adam by rows (reduce-scatter + slab Adam + all-gather) "
                          "instead of the DDP all-reduce + replicated Adam")
-    ap.add_argument("--side-streams", action="store_true",
-                    help="run the user tower's weight gradient on a side stream beside the news-tower backward")
     a = ap.parse_args()
-    global SHARD_TABLES, SIDE_STREAMS
+    global SHARD_TABLES
     SHARD_TABLES = bool(a.shard_table)
-    SIDE_STREAMS = bool(a.side_streams)
 
     # one rank per GPU over RCCL; NR_DIST_BACKEND=gloo lets a 1-GPU box rehearse the N > 1 path
     backend = os.environ.get("NR_DIST_BACKEND", "nccl")

@@ -296,6 +296,18 @@ int nr_mha_attn_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v
                     int64_t ld_dout, float* dqk, int64_t ld_dqk, float* dv_out, int64_t ld_dv,
                     hipStream_t stream);
 
+/* Backward of MHA_User_Encoder's attention core AND its Attention_Pooling (MHA.py:58-75,
+ * Pooling.py:12-25) in one launch, for histories of 32 < L <= 64 slots: from the pooled gradient dout
+ * [nseq][heads*dv], the forward's saved attention output o and pooling probabilities (nr_mha_user_pool_fwd),
+ * each (sequence, head) workgroup forms dO_l = p_l dout + ds_l q (ds_l = p_l (dout·O_l - Σ p dout·O) /
+ * sqrt(H)) in LDS, adds its head's slice of dq (+= Σ_l ds_l O_l, atomically across sequences), and runs
+ * the tied-QK attention backward of nr_mha_attn_bwd on it -- dO never leaves the chip. */
+int nr_mha_user_pool_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v, const void* mask,
+                         int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, int32_t dk, int32_t dv,
+                         const float* o, int64_t ld_o, const float* probs, const float* dout, int64_t ld_dout,
+                         const float* q, float* dq, float* dqk, int64_t ld_dqk, float* dv_out, int64_t ld_dv,
+                         hipStream_t stream);
+
 /* Fused MHA news-encoder tail, one workgroup per title (L <= 32): for each head the tied-QK
  * attention on the f32 MFMA (S = Kp Kpᵀ / sqrt(dk), XSoftmax with m_i m_j, O = P Vp), then
  * LayerNorm (eps) -> dropout(p, counter RNG) -> learned-query pooling, all in LDS.
@@ -383,7 +395,7 @@ int nr_attn_pool_bwd(const float* x, int64_t ldx, const float* key, int64_t ldk,
  * (rows split over its 8 waves) for D > 256 or fewer than 1024 sequences:
  *   out[s] = Σ_l XSoftmax(scale * q·K_l, mask)_l X_l,  K = key rows, or X when key == NULL.
  * Replaces CNN_Encoder's pooling (CNN.py:46, key = tanh(W c + b)) and Attention_Pooling
- * (Pooling.py:22-24).  D <= 512, L <= 64; the row matrices (x, key, out, dx, dk, dz) 16-B aligned with
+ * (Pooling.py:22-24).  D <= 1024, L <= 64; the row matrices (x, key, out, dx, dk, dz) 16-B aligned with
  * ld % 4 == 0 and ld >= D; q (and each dout row) hold qn <= D valid floats, any alignment, features
  * past qn taken as zero (a zero-padded row width D > qn then pools exact zeros there).  Saves
  * probs [nseq*L]. */

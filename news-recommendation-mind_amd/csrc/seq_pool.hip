@@ -224,7 +224,7 @@ __global__ __launch_bounds__(64 * SP_WAVES) void seq_pool_bwd_kernel(SeqPoolArgs
   }
 }
 
-// ---- workgroup per sequence (L <= 64, D <= 64 * 4 * NF)
+// ---- workgroup per sequence (L <= 64, D <= 64 * 4 * NF; NF = 1, 2, 4: D <= 1024)
 constexpr int WG_WAVES = 8;
 constexpr int WG_RPW = 64 / WG_WAVES;   // rows per wave
 
@@ -386,7 +386,7 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 int64_t r4(int D) { return (D + 3) & ~3; }
 
 bool shape_ok(int L, int D, int qn, int64_t ldx, int64_t ldk, const void* x, const void* key) {
-  return L >= 1 && L <= 64 && D >= 1 && D <= 512 && qn >= 1 && qn <= D && ldx >= r4(D) && (ldx & 3) == 0 && al16(x) &&
+  return L >= 1 && L <= 64 && D >= 1 && D <= 1024 && qn >= 1 && qn <= D && ldx >= r4(D) && (ldx & 3) == 0 && al16(x) &&
          (!key || ((ldk & 3) == 0 && ldk >= r4(D) && al16(key)));
 }
 
@@ -405,8 +405,10 @@ extern "C" int nr_seq_pool_fwd(const float* x, int64_t ldx, const float* key, in
   if (use_wg(nseq, D)) {
     if (D <= 256)
       hipLaunchKernelGGL(seq_pool_wg_fwd_kernel<1>, dim3((unsigned)nseq), dim3(64 * WG_WAVES), 0, stream, g);
-    else
+    else if (D <= 512)
       hipLaunchKernelGGL(seq_pool_wg_fwd_kernel<2>, dim3((unsigned)nseq), dim3(64 * WG_WAVES), 0, stream, g);
+    else   // BERT-width history vectors (the 768-wide MHA user encoder)
+      hipLaunchKernelGGL(seq_pool_wg_fwd_kernel<4>, dim3((unsigned)nseq), dim3(64 * WG_WAVES), 0, stream, g);
     NR_LAUNCH_CHECK();
     return NR_OK;
   }
@@ -438,8 +440,10 @@ extern "C" int nr_seq_pool_bwd(const float* x, int64_t ldx, const float* key, in
   if (use_wg(nseq, D)) {
     if (D <= 256)
       hipLaunchKernelGGL(seq_pool_wg_bwd_kernel<1>, dim3((unsigned)nseq), dim3(64 * WG_WAVES), 0, stream, g);
-    else
+    else if (D <= 512)
       hipLaunchKernelGGL(seq_pool_wg_bwd_kernel<2>, dim3((unsigned)nseq), dim3(64 * WG_WAVES), 0, stream, g);
+    else
+      hipLaunchKernelGGL(seq_pool_wg_bwd_kernel<4>, dim3((unsigned)nseq), dim3(64 * WG_WAVES), 0, stream, g);
     NR_LAUNCH_CHECK();
     return NR_OK;
   }

@@ -18,9 +18,8 @@ from . import functions as F
 from . import kernels as K_
 from .functions import AttnPoolFn, CNNNewsFn, CNNNewsRowsFn, MHAFn, MHANewsFn, RNNUserFn
 
-# the MHA user encoder's attention core and its pooling in one launch (nr_mha_user_pool_fwd): fast eval,
-# and training (MHAUserPoolFn, saving O and the pooling probabilities); False runs them as two launches
-# (the form the parity tests compare it with)
+# fast eval: the MHA user encoder and its pooling in one launch (nr_mha_user_pool_fwd); False runs the
+# attention core and the pooling as two launches (the form the parity tests compare it with)
 USER_POOL_FUSED = True
 
 
@@ -223,8 +222,9 @@ class MHA_User_Encoder(nn.Module):
             mask = _his_mask_rows(his_mask, B, N, news_repr.device)
         w, b = self.mha.fused_weight()
         mha = self.mha
-        if USER_POOL_FUSED and K_.mha_user_pool_supported(N, mha.head_num, mha.key_dim, mha.value_dim):
-            # the attention core + pooling in one launch (training saves O and the pooling probabilities)
+        if K_.mha_user_pool_bwd_supported(N, mha.head_num, mha.key_dim, mha.value_dim) and \
+                K_.seq_pool_supported(mha.head_num * mha.value_dim, N):
+            # the pooling backward inside the attention backward (one launch, dO kept on chip)
             return F.MHAUserPoolFn.apply(_rows_view(news_repr), mask, w, b, self.query_news, B, N, mha.head_num,
                                          mha.key_dim, mha.value_dim).unsqueeze(1)
         h = MHAFn.apply(_rows_view(news_repr), mask, w, b, B, N, mha.head_num, mha.key_dim, mha.value_dim)

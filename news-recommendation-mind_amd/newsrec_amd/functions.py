@@ -356,47 +356,6 @@ KEYPOOL_SAVE_K = True
 
 
 
-class _SideStreams:
-    """Off-critical-path work of a backward on a per-device side stream.  The MHA user encoder's
-    weight gradient (dW = dYᵀ x, its bias column sum: ~29 µs of small, latency-bound launches for
-    B = 32 users) feeds only the optimizer, while the news tower's backward waits for dx: forked here,
-    it runs beside the news-tower backward instead of before it.  Opt-in (``enabled``, set by the
-    train-step drivers: bench.forward_backward, manager.train_step), because whoever enables it must
-    call ``join()`` after ``loss.backward()`` -- before anything reads the gradients (the optimizer, a
-    test, a copy to the host): ``join()`` makes the current stream wait for the side work, and only then
-    releases the tensors the side work reads.  Graph capture: the fork and the join are both inside
-    the captured region (the side stream joins the capture through the event), as torch requires."""
-
-    def __init__(self):
-        self.enabled = False
-        self._streams = {}
-        self._pending = []   # (device, side stream, tensors kept alive until the join)
-
-    def run(self, dev, fn, *keep):
-        """fn() on dev's side stream after everything queued so far on the current stream; ``keep``:
-        tensors fn reads that must not be freed (and reused) before the join."""
-        if not self.enabled:
-            fn()
-            return
-        side = self._streams.get(dev)
-        if side is None:
-            side = self._streams[dev] = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            fn()
-        self._pending.append((dev, side, keep))
-
-    def join(self):
-        while self._pending:
-            dev, side, _ = self._pending.pop()
-            torch.cuda.current_stream(dev).wait_stream(side)
-
-    @property
-    def pending(self):
-        return len(self._pending)
-
-
-SIDE = _SideStreams()
 
 
 class _TableGradHook:
@@ -1067,33 +1026,36 @@ class MHAFn(_GradAwareFn):
             dx = _grad_out(ctx.dx_dest, rows, D, x)
             K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx)
         dw, db = _backward_zeros(ctx, dev, (NY, D), (NY,))
-        # off the critical path (only the optimizer reads dw / db): beside the news-tower backward
-        SIDE.run(dev, lambda: _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows), dY, x)
+        _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows)
         return dx, None, dw, db, None, None, None, None, None
 
 
 class MHAUserPoolFn(_GradAwareFn):
-    """MHA_User_Encoder.forward + its Attention_Pooling (MHA.py:58-75 with Pooling.py:12-25) for
-    training: Y = x [Wk; Wv]ᵀ + b (GEMM), then the tied-QK attention core and the learned-query
-    pooling in ONE launch (nr_mha_user_pool_fwd, one workgroup per user, a wave per head, O in LDS),
-    which also stores O and the pooling probabilities for the backward -- instead of the attention
-    launch, O's round trip and the pooling launch.  Backward: the pooling (nr_seq_pool_bwd -> dO), the
-    attention core (nr_mha_attn_bwd -> dY), the input gradient and the weight gradient (the latter on
-    the side stream), as AttnPoolFn + MHAFn.  x: [B*N, D] -> [B, heads*dv]."""
+    """MHA_User_Encoder.forward + its Attention_Pooling (MHA.py:58-75 with Pooling.py:12-25) in
+    training, for histories of 32 < N <= 64: the forward is MHAFn's and AttnPoolFn's (Y = x [Wk; Wv]ᵀ +
+    b, the tied-QK attention core, the learned-query pooling, O and the pooling probabilities saved);
+    the backward runs the pooling backward INSIDE the attention backward (nr_mha_user_pool_bwd: dO
+    formed in LDS per (user, head) instead of written to and re-read from HBM, one launch instead of
+    two), then the input gradient and the weight gradient as MHAFn.  (The forward's attention + pooling
+    as one launch per user, nr_mha_user_pool_fwd, the fast eval's kernel, measured slower here: 32
+    workgroups of 12 waves against 384 of the split attention kernel -- NRMS step 1.3192 vs 1.3078 ms,
+    profiles/r06_d_ab_step.json.)  x: [B*N, D] -> [B, heads*dv]."""
 
     @staticmethod
     def forward(ctx, x, mask, w_cat, b_cat, query, B, N, heads, dk, dv):
         ctx.prec = K.get_gemm_precision()
         D = x.shape[1]
+        NQ = heads * dk
         NY = w_cat.shape[0]
         H = heads * dv
         rows = B * N
         Y = _empty(rows, NY, x)
         K.gemm(rows, NY, D, K.operand(x, L.KCONTIG), K.operand(w_cat, L.KCONTIG), Y, bias=b_cat)
         O = _empty(rows, H, x)
+        K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:NY], mask, B, N, heads, dk, dv, O)
         probs = torch.empty(rows, device=x.device)
         out = _empty(B, H, x)
-        K.mha_user_pool_fwd(Y, None, mask, B, N, heads, dk, dv, query.reshape(-1), out, o=O, probs=probs)
+        K.seq_pool_fwd(O, query.reshape(-1), mask, B, N, H, out, probs)
         ctx.save_for_backward(x, mask, w_cat, Y, O, probs, query)
         ctx.cfg = (B, N, heads, dk, dv)
         ctx.dx_dest = GRAD_DEST.take(x)
@@ -1112,16 +1074,25 @@ class MHAUserPoolFn(_GradAwareFn):
         rows = B * N
         dev = x.device
         dw, db, dq = _backward_zeros(ctx, dev, (NY, D), (NY,), (H,))
-        dO = _empty(rows, H, x)
-        K.seq_pool_bwd(O, query.reshape(-1), mask, B, N, H, probs, dout if dout.stride(-1) == 1 else dout.contiguous(),
-                       dO, dq)
+        dout = dout if dout.stride(-1) == 1 else dout.contiguous()
         dY = _empty(rows, NY, x)
-        K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, B, N, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
+        if USER_POOL_BWD_FUSED:
+            # the pooling backward inside the attention backward: dO formed in LDS per (user, head)
+            K.mha_user_pool_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, B, N, heads, dk, dv, O, probs, dout,
+                                query.reshape(-1), dq, dY[:, :NQ], dY[:, NQ:NY])
+        else:
+            dO = _empty(rows, H, x)
+            K.seq_pool_bwd(O, query.reshape(-1), mask, B, N, H, probs, dout, dO, dq)
+            K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, B, N, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
         dx = _grad_out(ctx.dx_dest, rows, D, x)
         K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx)
-        # off the critical path (only the optimizer reads dw / db): beside the news-tower backward
-        SIDE.run(dev, lambda: _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows), dY, x)
+        _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows)
         return dx, None, dw, db, dq.view_as(query), None, None, None, None, None
+
+
+# MHAUserPoolFn's backward: the pooling backward fused into the attention backward (nr_mha_user_pool_bwd,
+# 32 < N <= 64); False: nr_seq_pool_bwd (dO through HBM) then nr_mha_attn_bwd
+USER_POOL_BWD_FUSED = True
 
 
 # ---------------------------------------------------------------------- recurrent user encoders

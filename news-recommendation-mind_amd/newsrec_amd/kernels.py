@@ -510,6 +510,32 @@ def mha_user_pool_fwd(y, rows, mask, nseq, seq_len, heads, dk, dv, q, out, prec=
            _prec(prec), L.stream_ptr(out))
 
 
+def mha_user_pool_bwd_supported(seq_len, heads, dk, dv):
+    return 32 < seq_len <= 64 and (dk, dv) in ((32, 32), (64, 32), (64, 64)) and heads * dv % 64 == 0 and \
+        heads * dv <= 512
+
+
+def mha_user_pool_bwd(qk, v, mask, nseq, seq_len, heads, dk, dv, o, probs, dout, q, dq, dqk, dvv):
+    """nr_mha_user_pool_bwd: the pooling backward (from dout [nseq, H], the saved O and probabilities)
+    and the tied-QK attention backward in one launch -> dqk, dvv ([nseq*L] rows) and dq += (atomic)."""
+    _f32(qk, v, o, probs, dout, q, dq, dqk, dvv)
+    H = heads * dv
+    for t, need, n in ((qk, heads * dk, "qk"), (v, heads * dv, "v"), (dqk, heads * dk, "dqk"), (dvv, heads * dv, "dv"),
+                       (o, H, "o")):
+        _cols(t, need, n)
+        if t.shape[0] != nseq * seq_len:
+            raise L.HipError("%s has %d rows, expected %d" % (n, t.shape[0], nseq * seq_len))
+    if dout.dim() != 2 or dout.stride(1) != 1 or dout.shape[0] != nseq or dout.shape[1] < H:
+        raise L.HipError("mha_user_pool_bwd: dout must be a row-major [nseq, H] matrix")
+    for t, n in ((probs, nseq * seq_len), (q, H), (dq, H)):
+        if not t.is_contiguous() or t.numel() < n:
+            raise L.HipError("mha_user_pool_bwd: a contiguous vector of %d floats expected" % n)
+    mp, mdt = mask_arg(mask, nseq * seq_len)
+    L.call("nr_mha_user_pool_bwd", L.ptr(qk), qk.stride(0), L.ptr(v), v.stride(0), mp, mdt, nseq, seq_len, heads, dk,
+           dv, L.ptr(o), o.stride(0), L.ptr(probs), L.ptr(dout), dout.stride(0), L.ptr(q), L.ptr(dq), L.ptr(dqk),
+           dqk.stride(0), L.ptr(dvv), dvv.stride(0), L.stream_ptr(dqk))
+
+
 def mha_attn_bwd(qk, v, mask, nseq, seq_len, heads, dk, dv, dout, dqk, dvv):
     _f32(qk, v, dout, dqk, dvv)
     for t, need, n in ((qk, heads * dk, "qk"), (v, heads * dv, "v"), (dout, heads * dv, "dout"),
@@ -584,7 +610,7 @@ def attn_pool_bwd(x, q, mask, nseq, seq_len, probs, dout, dx, dq, key=None, dk=N
 
 
 def seq_pool_supported(D, L):
-    return 1 <= D <= 512 and 1 <= L <= 64
+    return 1 <= D <= 1024 and 1 <= L <= 64
 
 
 def _sp_rows(t, rows, D, name):
@@ -605,7 +631,7 @@ def seq_pool_fwd(x, q, mask, nseq, seq_len, D, out, probs, key=None, scale=None,
     _f32(x, q, out, probs, key)
     qn = D if qn is None else qn
     if not seq_pool_supported(D, seq_len):
-        raise L.HipError("seq_pool: D <= 512, L <= 64 required (D=%d, L=%d)" % (D, seq_len))
+        raise L.HipError("seq_pool: D <= 1024, L <= 64 required (D=%d, L=%d)" % (D, seq_len))
     _sp_rows(x, nseq * seq_len, D, "seq_pool x")
     _sp_rows(key, nseq * seq_len, D, "seq_pool key")
     _sp_rows(out, nseq, D, "seq_pool out")
@@ -624,7 +650,7 @@ def seq_pool_bwd(x, q, mask, nseq, seq_len, D, probs, dout, dx, dq, key=None, dk
     _f32(x, q, probs, dout, dx, dq, key, dk, dz)
     qn = D if qn is None else qn
     if not seq_pool_supported(D, seq_len):
-        raise L.HipError("seq_pool: D <= 512, L <= 64 required (D=%d, L=%d)" % (D, seq_len))
+        raise L.HipError("seq_pool: D <= 1024, L <= 64 required (D=%d, L=%d)" % (D, seq_len))
     for t, r, n in ((x, nseq * seq_len, "x"), (key, nseq * seq_len, "key"), (dk, nseq * seq_len, "dk"),
                     (dx, nseq * seq_len, "dx"), (dz, nseq * seq_len, "dz")):
         _sp_rows(t, r, D, "seq_pool_bwd " + n)

@@ -79,13 +79,7 @@ def train_step(model, optimizer, x, grad_sync=None, check_labels=True):
     else:
         logits = model(x)[0]
         loss = torch.nn.functional.nll_loss(logits, x["label"].to(logits.device))
-    from . import functions as F
-    F.SIDE.enabled = True
-    try:
-        loss.backward()
-    finally:
-        F.SIDE.join()    # side-stream weight gradients (functions.SIDE) done before anything reads them
-        F.SIDE.enabled = False
+    loss.backward()
     scale = grad_sync() if grad_sync is not None else 1.0
     if scale != 1.0 and not hasattr(optimizer, "sync_lr"):
         # a torch optimizer: DDP's mean by hand (FusedAdam folds it into its kernel)

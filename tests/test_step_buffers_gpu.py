@@ -125,26 +125,3 @@ def test_probe_replays_with_a_hook_owned_table_gradient():
     assert all(res[k] > 0 for k in ("proj_fwd_ms", "proj_dgrad_ms", "proj_wgrad_ms"))
     assert torch.equal(taken["g"], before)
 
-
-@pytest.mark.parametrize("side", [False, True])
-def test_side_stream_user_wgrad(side):
-    """bench.forward_backward with the MHA user encoder's weight gradient forked onto a side stream
-    (functions.SIDE, joined after the backward) against the golden gradients, and BITWISE the
-    one-stream backward: the same kernels on other streams; nothing left pending after the join."""
-    import bench
-    from newsrec_amd import functions as F
-    from newsrec_amd.optim import FusedAdam
-    out = {}
-    for s in (False, side):
-        g, model, x = _setup("nrms")
-        model.train()
-        bench.SIDE_STREAMS = s
-        try:
-            bench.forward_backward(model, FusedAdam(model.parameters()), x)
-        finally:
-            bench.SIDE_STREAMS = False
-        assert F.SIDE.pending == 0 and not F.SIDE.enabled
-        out[s] = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
-        _check(g, model)
-    for n in out[False]:
-        assert torch.equal(out[False][n], out[side][n]), n
