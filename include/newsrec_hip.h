@@ -278,15 +278,10 @@ int nr_mha_attn_fwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v
  *   out[s] = Σ_l XSoftmax(q · O_{s,l} / sqrt(heads*dv), m)_l O_{s,l}.
  * One workgroup per sequence, the attention products on the matrix cores in `prec` (nr_gemm_precision
  * values; bf16x6 = fp32-class).  L <= 64; (dk, dv, heads*dv) in {(32,32,384), (64,32,384), (64,64,768)};
- * y_rows = rows of y (y_rows * ldy * 4 < 2^32); yrows NULL = identity.
- * Training (MHA_User_Encoder's forward under autograd): o (may be NULL) receives the attention output
- * O [nseq * L, >= heads*dv] (ld_o) and probs (may be NULL) the pooling probabilities [nseq * L] --
- * what the backward (nr_seq_pool_bwd, nr_mha_attn_bwd) reads -- so the attention core and the pooling
- * run as one launch in training too. */
+ * y_rows = rows of y (y_rows * ldy * 4 < 2^32); yrows NULL = identity.  No autograd (eval only). */
 int nr_mha_user_pool_fwd(const float* y, int64_t ldy, int64_t y_rows, const int64_t* yrows, const void* mask,
                          int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, int32_t dk, int32_t dv,
-                         const float* q, float* out, int64_t ldo, float* o, int64_t ld_o, float* probs,
-                         int32_t prec, hipStream_t stream);
+                         const float* q, float* out, int64_t ldo, int32_t prec, hipStream_t stream);
 
 /* Backward of nr_mha_attn_fwd (XSoftmax.backward, Attention.py:77-80, and the two matmuls);
  * recomputes P.  dqk receives the gradient of the shared key projection (both roles). */
@@ -295,18 +290,6 @@ int nr_mha_attn_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v
                     int32_t heads, int32_t dk, int32_t dv, float scale, const float* dout,
                     int64_t ld_dout, float* dqk, int64_t ld_dqk, float* dv_out, int64_t ld_dv,
                     hipStream_t stream);
-
-/* Backward of MHA_User_Encoder's attention core AND its Attention_Pooling (MHA.py:58-75,
- * Pooling.py:12-25) in one launch, for histories of 32 < L <= 64 slots: from the pooled gradient dout
- * [nseq][heads*dv], the forward's saved attention output o and pooling probabilities (nr_mha_user_pool_fwd),
- * each (sequence, head) workgroup forms dO_l = p_l dout + ds_l q (ds_l = p_l (dout·O_l - Σ p dout·O) /
- * sqrt(H)) in LDS, adds its head's slice of dq (+= Σ_l ds_l O_l, atomically across sequences), and runs
- * the tied-QK attention backward of nr_mha_attn_bwd on it -- dO never leaves the chip. */
-int nr_mha_user_pool_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v, const void* mask,
-                         int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, int32_t dk, int32_t dv,
-                         const float* o, int64_t ld_o, const float* probs, const float* dout, int64_t ld_dout,
-                         const float* q, float* dq, float* dqk, int64_t ld_dqk, float* dv_out, int64_t ld_dv,
-                         hipStream_t stream);
 
 /* Fused MHA news-encoder tail, one workgroup per title (L <= 32): for each head the tied-QK
  * attention on the f32 MFMA (S = Kp Kpᵀ / sqrt(dk), XSoftmax with m_i m_j, O = P Vp), then

@@ -26,15 +26,6 @@ struct AttnArgs {
   float* out; int64_t ld_out;           // fwd: O         bwd: dKp
   float* dv; int64_t ld_dv;             // bwd: dVp
   const int64_t* rows;                  // fwd: physical qk / v row of token (seq*L + j), or null
-  // nr_mha_user_pool_bwd: the attention output's pooling backward runs in the attention backward
-  // (dO formed in LDS from the pooled gradient instead of read from dout)
-  const float* po = nullptr; int64_t ld_po = 0;   // saved attention output O [nseq * L][H]
-  const float* pprobs = nullptr;                  // pooling probabilities [nseq * L]
-  const float* pdout = nullptr; int64_t ld_pdout = 0;   // d(user) [nseq][H]
-  const float* pq = nullptr;                      // pooling query [H]
-  float pscale = 0.f;                             // 1 / sqrt(H)
-  float* pdq = nullptr;                           // d(query) [H], accumulated
-  int ph = 0;                                     // H = heads * dv
 };
 
 template <int LMAX, int DK, int DV>
@@ -371,68 +362,7 @@ __global__ __launch_bounds__(64 * SPLIT_NW) void mha_attn_fwd_split_kernel(AttnA
   }
 }
 
-// POOL (nr_mha_user_pool_bwd, Attention_Pooling's backward, Pooling.py:12-25, ahead of the attention
-// core's): user = Σ_l p_l O_l with p = XSoftmax(q·O_l / sqrt(H)), so dO_l = p_l du + ds_l q with
-// ds_l = p_l (du·O_l - Σ_j p_j du·O_j) / sqrt(H), and dq += Σ_l ds_l O_l.  Every (sequence, head)
-// workgroup forms the scores' gradient over the whole H (50 dot products of H) and its head's dO slice
-// in LDS -- dO never goes to HBM -- and adds its head's slice of dq.
 template <int DK, int DV>
-__device__ __forceinline__ void pool_bwd_slice(const AttnArgs& g, int64_t seq, int head, float (*d)[DV], float* dps,
-                                               float (*red)[DV]) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int nf = g.ph / 64;   // H = 64 nf, nf <= 8
-  float du[8];
-#pragma unroll
-  for (int f = 0; f < 8; ++f) du[f] = f < nf ? g.pdout[seq * g.ld_pdout + 64 * f + lane] : 0.f;
-  // dp_l = du · O_l: wave w takes rows w, w + 4, ...; all its row loads in flight together
-  for (int l0 = w; l0 < g.L; l0 += 4 * 4) {
-    float acc[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int l = l0 + 4 * r;
-      const float* orow = g.po + (seq * g.L + (l < g.L ? l : 0)) * g.ld_po;
-      float a = 0.f;
-#pragma unroll
-      for (int f = 0; f < 8; ++f)
-        if (f < nf) a = fmaf(du[f], orow[64 * f + lane], a);
-      acc[r] = a;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float t = nr_wave_sum(acc[r]);
-      if (lane == 0 && l0 + 4 * r < g.L) dps[l0 + 4 * r] = t;
-    }
-  }
-  __syncthreads();
-  const float pme = lane < g.L ? g.pprobs[seq * g.L + lane] : 0.f;
-  const float dpme = lane < g.L ? dps[lane] : 0.f;
-  const float rsum = nr_wave_sum(pme * dpme);
-  const float dsme = pme * (dpme - rsum) * g.pscale;   // lane l: ds_l (0 past L and where masked: p = 0)
-  // dO rows of this head (rows >= L zero, as load_rows_split leaves k / v), and dq's head slice
-  const int c = tid % DV, grp = tid / DV;
-  constexpr int NG = 64 * SPLIT_NW / DV;
-  const float duc = g.pdout[seq * g.ld_pdout + head * DV + c], qc = g.pq[head * DV + c];
-  float dqa = 0.f;
-  for (int l = grp; l < 64; l += NG) {
-    const float pl = __shfl(pme, l, 64), dsl = __shfl(dsme, l, 64);
-    float val = 0.f;
-    if (l < g.L) {
-      val = fmaf(pl, duc, dsl * qc);
-      dqa = fmaf(dsl, g.po[(seq * g.L + l) * g.ld_po + head * DV + c], dqa);
-    }
-    d[l][c] = val;
-  }
-  red[grp][c] = dqa;
-  __syncthreads();
-  if (tid < DV) {
-    float a = 0.f;
-#pragma unroll
-    for (int r = 0; r < NG; ++r) a += red[r][tid];
-    atomicAdd(g.pdq + head * DV + tid, a);
-  }
-}
-
-template <int DK, int DV, bool POOL = false>
 __global__ __launch_bounds__(64 * SPLIT_NW) void mha_attn_bwd_split_kernel(AttnArgs g) {
   constexpr int JW = 64 / SPLIT_NW, CK = DK / SPLIT_NW, CV = DV / SPLIT_NW;
   __shared__ __attribute__((aligned(16))) float k[64][DK];
@@ -445,11 +375,7 @@ __global__ __launch_bounds__(64 * SPLIT_NW) void mha_attn_bwd_split_kernel(AttnA
   const int head = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane;
   const uint64_t bits = seq_mask_bits(g, seq);
-  load_rows_split<!POOL, DK, DV>(g, seq, head, k, v, d);
-  if constexpr (POOL) {
-    // pm / ds are free until (1): the pooling backward's scratch
-    pool_bwd_slice<DK, DV>(g, seq, head, d, &pm[0][0], reinterpret_cast<float (*)[DV]>(&ds[0][0]));
-  }
+  load_rows_split<true, DK, DV>(g, seq, head, k, v, d);
   __syncthreads();
   const bool row_ok = (bits >> i) & 1ull;
   // (1) scores over the wave's keys, row max / sum merged through LDS -> P
@@ -575,34 +501,6 @@ int dispatch(const AttnArgs& g, int dk, int dv, bool bwd, hipStream_t s) {
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
-
-extern "C" int nr_mha_user_pool_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v, const void* mask,
-                                    int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads, int32_t dk, int32_t dv,
-                                    const float* o, int64_t ld_o, const float* probs, const float* dout,
-                                    int64_t ld_dout, const float* q, float* dq, float* dqk, int64_t ld_dqk,
-                                    float* dvout, int64_t ld_dv, hipStream_t stream) {
-  if (L <= 32 || L > 64 || heads < 1) return NR_EINVAL(0);   // the split (four-wave) backward's range
-  if (!qk || !v || !mask || !o || !probs || !dout || !q || !dq || !dqk || !dvout) return NR_EINVAL(1);
-  if ((ld_qk | ld_v | ld_dqk | ld_dv) & 3 || !aligned16(qk) || !aligned16(v) || !aligned16(dqk) || !aligned16(dvout))
-    return NR_EINVAL(2);
-  const int H = heads * dv;
-  if (H % 64 || H > 512 || ld_o < H || ld_dout < H) return NR_EINVAL(3);
-  if (nseq == 0) return NR_OK;
-  AttnArgs g{qk, ld_qk, v, ld_v, mask, mask_dtype, nseq, L, heads, 1.0f / sqrtf((float)dk),
-             nullptr, 0, dqk, ld_dqk, dvout, ld_dv, nullptr};
-  g.po = o; g.ld_po = ld_o; g.pprobs = probs; g.pdout = dout; g.ld_pdout = ld_dout; g.pq = q;
-  g.pscale = 1.0f / sqrtf((float)H); g.pdq = dq; g.ph = H;
-  const dim3 grid((unsigned)nseq, (unsigned)heads);
-#define NR_UPB(K, V)                                                                                  \
-  if (dk == K && dv == V) {                                                                          \
-    hipLaunchKernelGGL((mha_attn_bwd_split_kernel<K, V, true>), grid, dim3(64 * SPLIT_NW), 0, stream, g); \
-    NR_LAUNCH_CHECK();                                                                                \
-    return NR_OK;                                                                                     \
-  }
-  NR_UPB(32, 32) NR_UPB(64, 32) NR_UPB(64, 64)
-#undef NR_UPB
-  return NR_EINVAL(8);
-}
 
 extern "C" int nr_mha_attn_fwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v,
                                const int64_t* rows, const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L,

@@ -1032,12 +1032,6 @@ __global__ __launch_bounds__(768) void mha_user_pool_fwd_kernel(MPArgs g) {
     user_rows<DK, DV, NP>(g, bits, head, ka0, ka1, ka1, 1, rw, os, SO);
   }
   __syncthreads();
-  if (g.o) {   // training: the attention output rows for the backward (coalesced from LDS)
-    for (int e = tid; e < g.L * H; e += nt) {
-      const int l = e / H, d = e - l * H;
-      g.o[(seq * g.L + l) * g.ldo + d] = os[l * SO + d];
-    }
-  }
   // pooling: s_l = q · O_l / sqrt(H), one wave per slot
   float qv[NH64];
 #pragma unroll
@@ -1056,9 +1050,7 @@ __global__ __launch_bounds__(768) void mha_user_pool_fwd_kernel(MPArgs g) {
     const float mx = nr_wave_max(v);
     const float e = keep ? __expf(v - mx) : 0.f;
     const float sum = nr_wave_sum(e);
-    const float pr = sum > 0.f ? e / sum : 0.f;
-    sc[lane] = pr;
-    if (g.probs && lane < g.L) g.probs[seq * g.L + lane] = pr;   // training: the pooling backward's input
+    sc[lane] = sum > 0.f ? e / sum : 0.f;
   }
   __syncthreads();
   for (int d = tid; d < H; d += nt) {
@@ -1187,8 +1179,8 @@ extern "C" int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows
 
 extern "C" int nr_mha_user_pool_fwd(const float* y, int64_t ldy, int64_t y_rows, const int64_t* yrows,
                                     const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L, int32_t heads,
-                                    int32_t dk, int32_t dv, const float* q, float* out, int64_t ldo, float* o,
-                                    int64_t ld_o, float* probs, int32_t prec, hipStream_t stream) {
+                                    int32_t dk, int32_t dv, const float* q, float* out, int64_t ldo, int32_t prec,
+                                    hipStream_t stream) {
   if (L < 1 || L > 64 || heads < 1 || heads > 12) return NR_EINVAL(0);
   if (y_rows < 1 || y_rows * ldy * 4 >= ((int64_t)1 << 32)) return NR_EINVAL(5);   // 32-bit row byte offsets
   if (prec != NR_GEMM_F32 && prec != NR_GEMM_BF16X6 && prec != NR_GEMM_BF16) return NR_EINVAL(4);
@@ -1200,8 +1192,6 @@ extern "C" int nr_mha_user_pool_fwd(const float* y, int64_t ldy, int64_t y_rows,
   g.y = y; g.ldy = ldy; g.yrows = yrows; g.mask = mask; g.mask_dt = mask_dtype; g.nseq = nseq; g.L = L;
   g.heads = heads; g.scale_attn = 1.0f / sqrtf((float)dk); g.scale_pool = 1.0f / sqrtf((float)(heads * dv));
   g.q = q; g.news = out; g.ldn = ldo;
-  if (o && ld_o < (int64_t)heads * dv) return NR_EINVAL(11);
-  g.o = o; g.ldo = ld_o; g.probs = probs;
   g.np = prec == NR_GEMM_BF16X6 ? 3 : prec == NR_GEMM_BF16 ? 1 : 0;
   const int nh64 = heads * dv / 64;
   if ((heads * dv) % 64) return NR_EINVAL(9);

@@ -15,7 +15,6 @@ from torch import nn
 from . import _lib as L
 from .attention import MultiheadAttention
 from . import functions as F
-from . import kernels as K_
 from .functions import AttnPoolFn, CNNNewsFn, CNNNewsRowsFn, MHAFn, MHANewsFn, RNNUserFn
 
 # fast eval: the MHA user encoder and its pooling in one launch (nr_mha_user_pool_fwd); False runs the
@@ -221,13 +220,8 @@ class MHA_User_Encoder(nn.Module):
         else:
             mask = _his_mask_rows(his_mask, B, N, news_repr.device)
         w, b = self.mha.fused_weight()
-        mha = self.mha
-        if K_.mha_user_pool_bwd_supported(N, mha.head_num, mha.key_dim, mha.value_dim) and \
-                K_.seq_pool_supported(mha.head_num * mha.value_dim, N):
-            # the pooling backward inside the attention backward (one launch, dO kept on chip)
-            return F.MHAUserPoolFn.apply(_rows_view(news_repr), mask, w, b, self.query_news, B, N, mha.head_num,
-                                         mha.key_dim, mha.value_dim).unsqueeze(1)
-        h = MHAFn.apply(_rows_view(news_repr), mask, w, b, B, N, mha.head_num, mha.key_dim, mha.value_dim)
+        h = MHAFn.apply(_rows_view(news_repr), mask, w, b, B, N, self.mha.head_num, self.mha.key_dim,
+                        self.mha.value_dim)
         return AttnPoolFn.apply(h, self.query_news, mask, B, N).unsqueeze(1)
 
     @torch.no_grad()

@@ -1030,71 +1030,6 @@ class MHAFn(_GradAwareFn):
         return dx, None, dw, db, None, None, None, None, None
 
 
-class MHAUserPoolFn(_GradAwareFn):
-    """MHA_User_Encoder.forward + its Attention_Pooling (MHA.py:58-75 with Pooling.py:12-25) in
-    training, for histories of 32 < N <= 64: the forward is MHAFn's and AttnPoolFn's (Y = x [Wk; Wv]ᵀ +
-    b, the tied-QK attention core, the learned-query pooling, O and the pooling probabilities saved);
-    the backward runs the pooling backward INSIDE the attention backward (nr_mha_user_pool_bwd: dO
-    formed in LDS per (user, head) instead of written to and re-read from HBM, one launch instead of
-    two), then the input gradient and the weight gradient as MHAFn.  (The forward's attention + pooling
-    as one launch per user, nr_mha_user_pool_fwd, the fast eval's kernel, measured slower here: 32
-    workgroups of 12 waves against 384 of the split attention kernel -- NRMS step 1.3192 vs 1.3078 ms,
-    profiles/r06_d_ab_step.json.)  x: [B*N, D] -> [B, heads*dv]."""
-
-    @staticmethod
-    def forward(ctx, x, mask, w_cat, b_cat, query, B, N, heads, dk, dv):
-        ctx.prec = K.get_gemm_precision()
-        D = x.shape[1]
-        NQ = heads * dk
-        NY = w_cat.shape[0]
-        H = heads * dv
-        rows = B * N
-        Y = _empty(rows, NY, x)
-        K.gemm(rows, NY, D, K.operand(x, L.KCONTIG), K.operand(w_cat, L.KCONTIG), Y, bias=b_cat)
-        O = _empty(rows, H, x)
-        K.mha_attn_fwd(Y[:, :NQ], Y[:, NQ:NY], mask, B, N, heads, dk, dv, O)
-        probs = torch.empty(rows, device=x.device)
-        out = _empty(B, H, x)
-        K.seq_pool_fwd(O, query.reshape(-1), mask, B, N, H, out, probs)
-        ctx.save_for_backward(x, mask, w_cat, Y, O, probs, query)
-        ctx.cfg = (B, N, heads, dk, dv)
-        ctx.dx_dest = GRAD_DEST.take(x)
-        _reserve_zeros(ctx, x.device, (NY, D), (NY,), (H,))
-        return out
-
-    @staticmethod
-    @_gemm_backward
-    def backward(ctx, dout):
-        x, mask, w_cat, Y, O, probs, query = ctx.saved_tensors
-        B, N, heads, dk, dv = ctx.cfg
-        D = x.shape[1]
-        NQ = heads * dk
-        NY = w_cat.shape[0]
-        H = heads * dv
-        rows = B * N
-        dev = x.device
-        dw, db, dq = _backward_zeros(ctx, dev, (NY, D), (NY,), (H,))
-        dout = dout if dout.stride(-1) == 1 else dout.contiguous()
-        dY = _empty(rows, NY, x)
-        if USER_POOL_BWD_FUSED:
-            # the pooling backward inside the attention backward: dO formed in LDS per (user, head)
-            K.mha_user_pool_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, B, N, heads, dk, dv, O, probs, dout,
-                                query.reshape(-1), dq, dY[:, :NQ], dY[:, NQ:NY])
-        else:
-            dO = _empty(rows, H, x)
-            K.seq_pool_bwd(O, query.reshape(-1), mask, B, N, H, probs, dout, dO, dq)
-            K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, B, N, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
-        dx = _grad_out(ctx.dx_dest, rows, D, x)
-        K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx)
-        _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows)
-        return dx, None, dw, db, dq.view_as(query), None, None, None, None, None
-
-
-# MHAUserPoolFn's backward: the pooling backward fused into the attention backward (nr_mha_user_pool_bwd,
-# 32 < N <= 64); False: nr_seq_pool_bwd (dO through HBM) then nr_mha_attn_bwd
-USER_POOL_BWD_FUSED = True
-
-
 # ---------------------------------------------------------------------- recurrent user encoders
 
 class RNNUserFn(_GradAwareFn):

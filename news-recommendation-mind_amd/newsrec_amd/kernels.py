@@ -480,60 +480,22 @@ def mha_user_pool_supported(seq_len, heads, dk, dv):
             and mha_user_pool_smem(seq_len, heads * dv) <= MAX_LDS_BYTES)
 
 
-def mha_user_pool_fwd(y, rows, mask, nseq, seq_len, heads, dk, dv, q, out, prec=None, o=None, probs=None):
-    """MHA user encoder + pooling (MHA.py:58-75 with Pooling.py:12-25) in one launch
+def mha_user_pool_fwd(y, rows, mask, nseq, seq_len, heads, dk, dv, q, out, prec=None):
+    """Eval MHA user encoder + pooling (MHA.py:58-75 with Pooling.py:12-25) in one launch
     (nr_mha_user_pool_fwd): y [R, >= heads*(dk+dv)] per-news [key | value] projections, rows int64
-    [nseq*L] (history slot -> y row; None: slot t reads row t), mask [nseq, L], q [heads*dv] -> out
-    [nseq, heads*dv].  Training: o [nseq*L, >= heads*dv] receives the attention output and probs
-    [nseq*L] the pooling probabilities (the backward's inputs)."""
-    _f32(y, q, out, o, probs)
+    [nseq*L] (history slot -> y row), mask [nseq, L], q [heads*dv] -> out [nseq, heads*dv]."""
+    _f32(y, q, out)
     H = heads * dv
     _cols(y, heads * (dk + dv), "y")
     _cols(out, H, "out")
     if out.shape[0] != nseq or q.numel() != H or not q.is_contiguous():
         raise L.HipError("mha_user_pool_fwd: out [nseq, H] and a contiguous q [H] expected")
-    if rows is not None:
-        _check_rows(rows, None, "rows")
-        if rows.numel() != nseq * seq_len:
-            raise L.HipError("mha_user_pool_fwd: rows must hold nseq*L entries")
-    elif y.shape[0] < nseq * seq_len:
-        raise L.HipError("mha_user_pool_fwd: y needs nseq*L rows without a row table")
-    if o is not None:
-        _cols(o, H, "o")
-        if o.shape[0] < nseq * seq_len:
-            raise L.HipError("mha_user_pool_fwd: o needs nseq*L rows")
-    if probs is not None and (probs.numel() < nseq * seq_len or not probs.is_contiguous()):
-        raise L.HipError("mha_user_pool_fwd: probs needs nseq*L contiguous floats")
+    _check_rows(rows, None, "rows")
+    if rows.numel() != nseq * seq_len:
+        raise L.HipError("mha_user_pool_fwd: rows must hold nseq*L entries")
     mp, mdt = mask_arg(mask, nseq * seq_len)
     L.call("nr_mha_user_pool_fwd", L.ptr(y), y.stride(0), y.shape[0], L.ptr(rows), mp, mdt, nseq, seq_len, heads,
-           dk, dv, L.ptr(q), L.ptr(out), out.stride(0), L.ptr(o), o.stride(0) if o is not None else 0, L.ptr(probs),
-           _prec(prec), L.stream_ptr(out))
-
-
-def mha_user_pool_bwd_supported(seq_len, heads, dk, dv):
-    return 32 < seq_len <= 64 and (dk, dv) in ((32, 32), (64, 32), (64, 64)) and heads * dv % 64 == 0 and \
-        heads * dv <= 512
-
-
-def mha_user_pool_bwd(qk, v, mask, nseq, seq_len, heads, dk, dv, o, probs, dout, q, dq, dqk, dvv):
-    """nr_mha_user_pool_bwd: the pooling backward (from dout [nseq, H], the saved O and probabilities)
-    and the tied-QK attention backward in one launch -> dqk, dvv ([nseq*L] rows) and dq += (atomic)."""
-    _f32(qk, v, o, probs, dout, q, dq, dqk, dvv)
-    H = heads * dv
-    for t, need, n in ((qk, heads * dk, "qk"), (v, heads * dv, "v"), (dqk, heads * dk, "dqk"), (dvv, heads * dv, "dv"),
-                       (o, H, "o")):
-        _cols(t, need, n)
-        if t.shape[0] != nseq * seq_len:
-            raise L.HipError("%s has %d rows, expected %d" % (n, t.shape[0], nseq * seq_len))
-    if dout.dim() != 2 or dout.stride(1) != 1 or dout.shape[0] != nseq or dout.shape[1] < H:
-        raise L.HipError("mha_user_pool_bwd: dout must be a row-major [nseq, H] matrix")
-    for t, n in ((probs, nseq * seq_len), (q, H), (dq, H)):
-        if not t.is_contiguous() or t.numel() < n:
-            raise L.HipError("mha_user_pool_bwd: a contiguous vector of %d floats expected" % n)
-    mp, mdt = mask_arg(mask, nseq * seq_len)
-    L.call("nr_mha_user_pool_bwd", L.ptr(qk), qk.stride(0), L.ptr(v), v.stride(0), mp, mdt, nseq, seq_len, heads, dk,
-           dv, L.ptr(o), o.stride(0), L.ptr(probs), L.ptr(dout), dout.stride(0), L.ptr(q), L.ptr(dq), L.ptr(dqk),
-           dqk.stride(0), L.ptr(dvv), dvv.stride(0), L.stream_ptr(dqk))
+           dk, dv, L.ptr(q), L.ptr(out), out.stride(0), _prec(prec), L.stream_ptr(out))
 
 
 def mha_attn_bwd(qk, v, mask, nseq, seq_len, heads, dk, dv, dout, dqk, dvv):

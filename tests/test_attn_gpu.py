@@ -180,37 +180,3 @@ def test_mha_user_pool_lds_cap_falls_back():
     got = enc.forward_rows(y.float().cuda(), rows.view(n, L).cuda(), mask.view(n, L, 1).cuda(), n, L)
     err = (got.view(n, H).double().cpu() - want).abs().max().item()
     assert err <= 2e-5 * want.abs().max().item()
-
-
-@pytest.mark.parametrize("L,empty", [(50, True), (33, False)])
-def test_mha_user_encoder_fused_training(L, empty, monkeypatch):
-    """MHA_User_Encoder's training forward / backward through MHAUserPoolFn (the attention core and the
-    pooling in one launch, O and the pooling probabilities saved) against the unfused MHAFn +
-    AttnPoolFn path: user vectors and every gradient (x, [Wk; Wv], biases, query) to fp32 rounding,
-    ragged histories and (empty=True) one empty history."""
-    from newsrec_amd import encoders as EN
-    H, heads, B = 384, 12, 9
-
-    class _M:
-        hidden_dim, head_num, dropout_p = H, heads, 0.2
-    torch.manual_seed(L)
-    enc = EN.MHA_User_Encoder(_M()).cuda()
-    x0 = torch.randn(B, L, H, device="cuda")
-    lens = torch.randint(1, L + 1, (B,))
-    if empty:
-        lens[0] = 0
-    lens[1] = L
-    his = (torch.arange(L)[None] < lens[:, None]).double().unsqueeze(-1)
-    dout = torch.randn(B, 1, H, device="cuda")
-    res = {}
-    for fused in (False, True):
-        monkeypatch.setattr(EN, "USER_POOL_FUSED", fused)
-        enc.zero_grad(set_to_none=True)
-        x = x0.clone().requires_grad_(True)
-        y = enc(x, his_mask=his)
-        y.backward(dout)
-        torch.cuda.synchronize()
-        res[fused] = [y.detach()] + [x.grad] + [p.grad.clone() for p in enc.parameters()]
-    for a, b in zip(res[False], res[True]):
-        scale = a.abs().max().item()
-        assert (a - b).abs().max().item() <= 2e-5 * max(scale, 1e-6) + 1e-7

@@ -85,3 +85,33 @@ def test_seq_pool_matches_float64(nseq, L, D, qn, tied):
     if dk is not None:
         close(dk.view(nseq, L, D), dk_want, 1e-5, "dk")
     assert out[0].abs().max().item() == 0.0                  # fully masked: exact zeros
+
+
+@pytest.mark.parametrize("L", [50, 64])
+def test_seq_pool_768_wide(L):
+    """nr_seq_pool_fwd / bwd at BERT width (D = 768, the workgroup form's NF = 4 instantiation: the
+    768-wide MHA user encoder's pooling, Pooling.py:12-25) against float64 autograd."""
+    from newsrec_amd import kernels as K
+    from oracle import restatement as R
+    g = torch.Generator().manual_seed(L)
+    n, D = 7, 768
+    x = torch.randn(n * L, D, generator=g, dtype=torch.float64)
+    q = torch.randn(D, generator=g, dtype=torch.float64)
+    lens = torch.randint(1, L + 1, (n,), generator=g)
+    lens[0] = L
+    mask = (torch.arange(L)[None] < lens[:, None]).to(torch.float64)
+    xr, qr = x.clone().requires_grad_(True), q.clone().requires_grad_(True)
+    want = R.scaled_dp_attention(qr.view(1, 1, D).expand(n, 1, D), xr.view(n, L, D), xr.view(n, L, D),
+                                 mask.view(n, 1, L)).view(n, D)
+    dout = torch.randn(n, D, generator=g, dtype=torch.float64)
+    want.backward(dout)
+    xd, qd, md = x.float().cuda(), q.float().cuda(), mask.cuda()
+    out = torch.empty(n, D, device="cuda")
+    probs = torch.empty(n * L, device="cuda")
+    K.seq_pool_fwd(xd, qd, md, n, L, D, out, probs)
+    dx = torch.empty(n * L, D, device="cuda")
+    dq = torch.zeros(D, device="cuda")
+    K.seq_pool_bwd(xd, qd, md, n, L, D, probs, dout.float().cuda(), dx, dq)
+    for got, ref in ((out, want), (dx, xr.grad), (dq, qr.grad)):
+        err = (got.double().cpu().view_as(ref) - ref.detach()).abs().max().item()
+        assert err <= 2e-5 * max(ref.abs().max().item(), 1e-6)
