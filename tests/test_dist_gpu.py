@@ -273,100 +273,3 @@ def test_data_parallel_shard_tables_world2(case, mode):
             assert dmax <= 4 * 2 * lr + 1e-6, (rank, n, dmax)
             if not n.endswith("attention.self.key.bias"):
                 assert n_off <= max(4, 1e-3 * n_all), (rank, n, n_off, n_all)
-
-
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("shard", [False, True])
-def test_bench_gpus2_spawns_two_ranks(shard):
-    """`bench.py --gpus 2` (no WORLD_SIZE) must launch two ranks itself (twotower.py:62-73) and
-    report the live world size, with the 8-GPU configurations of BASELINE.json measured on those
-    ranks too: configs[3] LSTUR (the row-sparse user-table exchange) and configs[4] XFormer, each
-    with its replicas bitwise identical after the timed steps; gloo on the one leased GPU stands in
-    for RCCL here."""
-    import json
-    import subprocess
-    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
-    env["NR_DIST_BACKEND"] = "gloo"
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
-           "--eval-impr", "0", "--legs", "cnn_lstur", "--xformer-steps", "2", "--no-cpu-baseline"] + \
-        (["--shard-table"] if shard else [])
-    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=580)
-    assert r.returncode == 0, r.stderr[-4000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout[-4000:]
-    out = json.loads(lines[0])
-    assert out["n_gpus"] == 2
-    assert out["config"]["parallelism"] == "dp2"
-    assert out["config"]["global_batch"] == 64
-    assert out["value"] > 0
-    assert out["dp_bitwise_equal"] is True and out["dp_world_size"] == 2
-    assert out["dp_shard_tables"] is shard
-    for leg in (out["other_configs"]["cnn_lstur"], out["xformer"]):
-        assert leg["n_gpus"] == 2 and leg["impressions_per_s"] > 0, leg
-        assert leg["dp_world_size"] == 2 and leg["dp_in_sync"] is True, leg
-        assert leg["dp_bitwise_equal"] is True, leg
-
-
-def _shard_worker(rank, world, port, case, mode, q):
-    """Dense all-reduce vs GradSync(shard_tables=True) on the same half batches: every parameter after
-    the steps must be bitwise equal (the word table's Adam on this rank's slab + the all-gather)."""
-    try:
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        sys.path.insert(0, os.path.join(ROOT, "news-recommendation-mind_amd"))
-        sys.path.insert(0, ROOT)
-        import torch.distributed as dist
-        import bench
-        from newsrec_amd.dist import GradSync
-        from newsrec_amd.manager import get_optim
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        dev = torch.device("cuda", 0)
-        torch.cuda.set_device(dev)
-        steps = 4
-        halves = [_half(_batch(100 + i, dev), rank, world) for i in range(steps)]
-        out = {}
-        for shard in (False, True):
-            m = _model(case, dev)
-            m.train()
-            sync = GradSync(m, bucket_mb=0.5, shard_tables=shard)
-            if mode == "eager":
-                opt = get_optim(m)
-                for x in halves:
-                    bench.train_step(m, opt, x, sync)
-            else:
-                opt = get_optim(m, capturable=True)
-                g = bench.GraphedStep(m, opt, bench.ResidentFeed(halves), sync, 2)
-                for i in range(2, steps):
-                    g(i)
-            torch.cuda.synchronize()
-            if shard:
-                sh = [p for p in m.parameters() if getattr(p, "_nr_shard", None) is not None]
-                assert len(sh) == 1 and opt.state[sh[0]]["exp_avg"].shape[0] == sh[0]._nr_shard[1]
-            sync.close()
-            out[shard] = {n: p.detach().clone() for n, p in m.named_parameters()}
-        bad = [n for n in out[False] if not torch.equal(out[False][n], out[True][n])]
-        q.put((rank, None, bad))
-        dist.barrier()
-        dist.destroy_process_group()
-    except Exception as e:
-        import traceback
-        q.put((rank, traceback.format_exc() + repr(e), None))
-
-
-@pytest.mark.parametrize("mode", ["eager", "graphs"])
-@pytest.mark.parametrize("case", ["nrms", "xformer"])
-def test_data_parallel_shard_tables_bitwise_world2(case, mode):
-    """GradSync(shard_tables=True) on the real models at world 2 (gloo on device tensors): the word
-    table's gradient reduce-scattered in place, FusedAdam on the rank's row slab, the slabs all-gathered
-    -- bitwise the dense all-reduce path's parameters, eager and through the three-graph step."""
-    world, port = 2, _port()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    ps = [ctx.Process(target=_shard_worker, args=(r, world, port, case, mode, q)) for r in range(world)]
-    for p in ps:
-        p.start()
-    res = [q.get(timeout=300) for _ in range(world)]
-    for p in ps:
-        p.join(timeout=60)
-    for rank, err, bad in res:
-        assert err is None, err
-        assert bad == [], (rank, bad)
