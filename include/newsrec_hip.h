@@ -317,8 +317,10 @@ int nr_mha_pool_fwd(const float* y, int64_t ldy, const int64_t* yrows, const voi
 /* Backward of nr_mha_pool_fwd: writes dy [T][heads*(dk+dv)] and ATOMICALLY ACCUMULATES dbias
  * (= column sums of dy), dq, dgamma, dbeta (caller zeroes).  dy stays per token (row t) when
  * yrows is given; rows of masked tokens are exactly zero.  With o (the forward's oout) and dob the
- * backward runs split: a per-title pooling/LN pass writes dO into dob [T][heads*dv] (caller's
- * workspace), then a per-(title, head) attention pass at high occupancy; with o and dob NULL one
+ * backward runs split: a per-title pooling/LN pass writes each token's LayerNorm-backward row terms
+ * into dob [T][lddob >= 8] (caller's workspace, 16-B aligned, lddob % 4 == 0), then a per-(title, head)
+ * attention pass at high occupancy rebuilds its head's slice of dO from o and those terms (dO never
+ * goes through HBM); with o and dob NULL one
  * fused kernel per title loads the saved O, keeps dO in LDS and runs every head's attention
  * backward; without o the fused kernel recomputes the attention.
  * ws (optional, forms with o only): ws_copies x ceil4(3*heads*dv + heads*(dk+dv)) floats, ZERO on entry

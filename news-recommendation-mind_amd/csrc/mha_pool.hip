@@ -681,8 +681,19 @@ __global__ __launch_bounds__(384) void mha_pool_bwd_kernel(MPArgs g) {
   }
 }
 
+// One element of the LayerNorm / dropout / pooling backward, dO = rstd (dyv γ - sg - x̂ sgx) with
+// x̂ = (O - mean) rstd and dyv = (p_l dnews + ds_l q (+ dz)) · keep / (1 - p): the split backward's LN
+// pass (mha_ln_bwd_kernel) forms the row terms, the head pass (mha_head_bwd_kernel) the elements of its
+// head's columns, both through this function (the same operations in the same order).
+__device__ __forceinline__ float ln_row_dO(float xh, float rstd, float sg, float sgx, float pl, float dsl, float dn,
+                                           float qd, float gm, float dzv, float sk) {
+  const float dyv = (fmaf(pl, dn, dsl * qd) + dzv) * sk;
+  return rstd * fmaf(-xh, sgx, fmaf(dyv, gm, -sg));
+}
+
 // Split backward, kernel 1 (forward saved O): pooling/LN backward per title from the saved O
-// rows; dO rows to global.  Register-resident: wave w owns rows w, w + 4, ... of the title and keeps
+// rows; the per-row terms of dO to global ([T][8]: mean, rstd, sg, sgx, ds_l, p_l).  Register-resident:
+// wave w owns rows w, w + 4, ... of the title and keeps
 // them (and their dropout keep-bits) in registers through both passes; only the 32 pooling scores
 // and the cross-wave dgamma / dbeta / dq partials go through LDS (~19 KB instead of ~68 KB staging
 // the whole O tile, so several titles share a CU and their loads overlap).
@@ -767,9 +778,8 @@ __global__ __launch_bounds__(256) void mha_ln_bwd_kernel(MPArgs g) {
       const int d = lane + 64 * k;
       const float sk = ((kbit[i] >> k) & 1u) ? dsc : 0.f;
       dqp[k] = fmaf(dsl, (x[i][k] * gam[k] + bet[k]) * sk, dqp[k]);
-      float dz = fmaf(pl, dnv[k], dsl * qv[k]);
-      if (g.dz) dz += g.dz[row * g.lddz + d];
-      dyv[k] = dz * sk;
+      // dyv exactly as ln_row_dO forms it in the head pass
+      dyv[k] = (fmaf(pl, dnv[k], dsl * qv[k]) + (g.dz ? g.dz[row * g.lddz + d] : 0.f)) * sk;
       const float gg = dyv[k] * gam[k];
       sg += gg;
       sgx = fmaf(gg, x[i][k], sgx);
@@ -778,9 +788,13 @@ __global__ __launch_bounds__(256) void mha_ln_bwd_kernel(MPArgs g) {
     }
     sg = nr_wave_sum(sg) * (1.f / H);
     sgx = nr_wave_sum(sgx) * (1.f / H);
-    float* drow = g.dob + row * g.lddob;
-#pragma unroll
-    for (int k = 0; k < NH64; ++k) drow[lane + 64 * k] = rstd * (dyv[k] * gam[k] - sg - x[i][k] * sgx);
+    // the row's terms of dO = rstd (dyv γ - sg - x̂ sgx): the head pass rebuilds its slice of dO from
+    // the saved O with them (ln_row_dO), so the [T, H] dO never goes through HBM
+    if (lane == 0) {
+      float4* rc = reinterpret_cast<float4*>(g.dob + row * g.lddob);
+      rc[0] = make_float4(g.stats[2 * row], rstd, sg, sgx);
+      rc[1] = make_float4(dsl, pl, 0.f, 0.f);
+    }
   }
 #pragma unroll
   for (int k = 0; k < NH64; ++k) {
@@ -807,6 +821,7 @@ constexpr int HB_TITLES = 1;
 
 template <int DK, int DV, int NP>
 __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
+  if (g.rng) g.dkey = nr_dropout_key(g.rng[0], g.rng[1] + g.offset);   // graph-replay RNG (dO's dropout)
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int head = blockIdx.y * nw + w;
@@ -828,15 +843,51 @@ __global__ __launch_bounds__(256, 4) void mha_head_bwd_kernel(MPArgs g) {
     if (lane < g.L) doff = g.dsto ? g.dsto[seq * g.L + lane] : (uint32_t)((seq * g.L + lane) * g.lddy * 4);
     constexpr int F4 = DV / 4;                 // float4 per dO row
     constexpr int PER = 32 * F4 / 64;          // per lane
-    float4 v[PER];
+    static_assert(64 % F4 == 0, "a lane keeps its four columns in every row it loads");
+    // this head's slice of dO, rebuilt from the saved attention output O and the LN pass's row terms
+    // (ln_row_dO: the dO rows never go through HBM); lane: rows e / F4 of e = lane + 64 i, columns
+    // 4 (lane % F4) .. + 3 of the head
+    float4 v[PER], ra[PER], rb[PER];
+    const int col0 = head * DV + 4 * (lane % F4);
     {
-      const float* src = g.dob + (seq * g.L) * g.lddob + head * DV;
+      const float* src = g.o + (seq * g.L) * g.ldo + head * DV;
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int e = lane + 64 * i, r = e / F4, c4 = e % F4;
+        const int rr = r < g.L ? r : 0;
         v[i] = *reinterpret_cast<const float4*>(
-            reinterpret_cast<const char*>(src) + 4u * (uint32_t)((r < g.L ? r : 0) * (int)g.lddob + 4 * c4));
-        if (r >= g.L) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            reinterpret_cast<const char*>(src) + 4u * (uint32_t)(rr * (int)g.ldo + 4 * c4));
+        const float4* rc = reinterpret_cast<const float4*>(g.dob + (seq * g.L + rr) * g.lddob);
+        ra[i] = rc[0];   // mean, rstd, sg, sgx
+        rb[i] = rc[1];   // ds_l, p_l
+      }
+    }
+    float gm[4], qd[4], dn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      gm[j] = g.gamma[col0 + j];
+      qd[j] = g.q[col0 + j];
+      dn[j] = g.news[seq * g.ldn + col0 + j];
+    }
+    {
+      const bool drop = g.p_drop > 0.f;
+      const float dsc = drop ? 1.f / (1.f - g.p_drop) : 1.f;
+      const uint32_t Hc = (uint32_t)(g.heads * DV);
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int r = (lane + 64 * i) / F4;
+        const int64_t row = seq * g.L + (r < g.L ? r : 0);
+        float o[4] = {v[i].x, v[i].y, v[i].z, v[i].w}, d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t col = (uint32_t)(col0 + j);
+          const bool keep = !drop || nr_dropout_keep(g.dkey, (uint32_t)row * Hc + col, g.dthresh);
+          const float dzv = g.dz ? g.dz[row * g.lddz + col] : 0.f;
+          const float xh = (o[j] - ra[i].x) * ra[i].y;
+          d[j] = ln_row_dO(xh, ra[i].y, ra[i].z, ra[i].w, rb[i].y, rb[i].x, dn[j], qd[j], gm[j], dzv,
+                           keep ? dsc : 0.f);
+        }
+        v[i] = r < g.L ? make_float4(d[0], d[1], d[2], d[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
     if (lane < 32) {
@@ -1233,8 +1284,9 @@ extern "C" int nr_mha_pool_bwd(const float* y, int64_t ldy, const int64_t* yrows
   g.dq = dq; g.dgamma = dgamma; g.dbeta = dbeta;
   g.o = const_cast<float*>(o); g.ldo = ldo; g.dob = dob; g.lddob = lddob;
   g.seg_off = seg_off; g.dyu_row0 = dyu_row0; g.dsto = seg_off ? dsto : nullptr;
-  // o with dob: the split backward (dO through dob); o without dob: the fused backward on the saved O
-  if (o && ((dob && lddob < (int64_t)heads * dv) || ldo < (int64_t)heads * dv || (ldo & 3) || !al16(o)))
+  // o with dob: the split backward (dob: the LN pass's per-token row terms, [T][>= 8] floats); o without
+  // dob: the fused backward on the saved O
+  if (o && ((dob && (lddob < 8 || (lddob & 3) || !al16(dob))) || ldo < (int64_t)heads * dv || (ldo & 3) || !al16(o)))
     return NR_EINVAL(3);
   // backward: the six-product form measured slower than exact f32 MFMA products here (the split
   // VALU work lands on a latency-bound kernel: head pass 170 -> 189 us), so bf16x6 callers get the

@@ -633,7 +633,8 @@ class MHANewsFn(_GradAwareFn):
         dYall = _empty(T + (ur.cap if ur is not None else 0), NY, table)
         dY = dYall[:T]
         if fused:
-            dob = _empty(T, H, table) if O is not None and not FUSED_SAVED_BWD else None
+            # split form: the LN pass's per-token row terms (the head pass rebuilds dO from O with them)
+            dob = torch.empty(T, 8, device=table.device) if O is not None and not FUSED_SAVED_BWD else None
             ws = _grad_copies(table.device, 3 * H + NY) if O is not None else None
             K.mha_pool_bwd(Y, mask, n, seq_len, heads, dk, dv, gamma, beta, query, stats, probs, dnews,
                            dYall if direct else dY, db, dq,

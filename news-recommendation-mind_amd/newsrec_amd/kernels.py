@@ -915,8 +915,9 @@ def mha_pool_fwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, news, st
 def mha_pool_bwd(y, mask, nseq, seq_len, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, dbias, dq,
                  dgamma, dbeta, p_drop=0.0, seed=0, offset=0, dz=None, yrows=None, rng=None, o=None, dob=None,
                  prec=None, ws=None, ws_copies=0, seg=None, dyu_row0=0):
-    """``o`` (the forward's ``oout``) with ``dob`` [T, heads*dv] (its dO workspace) selects the split
-    backward, ``o`` without ``dob`` the fused backward on the saved O (dO kept in LDS); ``ws`` (forms
+    """``o`` (the forward's ``oout``) with ``dob`` [T, >= 8] (the LN pass's per-token row terms, from
+    which the head pass rebuilds dO) selects the split backward, ``o`` without ``dob`` the fused
+    backward on the saved O (dO kept in LDS); ``ws`` (forms
     with ``o``) a zeroed [ws_copies, >= 3*heads*dv + heads*(dk+dv)] buffer that spreads the
     parameter-gradient atomics (left zero).  ``seg`` (a UniqueRows built with the token mask, with
     ``yrows`` = its inv): tokens alone in their distinct row's segment write their gradient row to dy

@@ -290,7 +290,7 @@ def test_mha_pool_bwd_single_rows_direct(form):
     outs = []
     for direct in (False, True):
         dyall = torch.full((T + ur.cap, NY), float("nan"), device="cuda")
-        dob = torch.empty(T, H, device="cuda") if form == "split" else None
+        dob = torch.empty(T, 8, device="cuda") if form == "split" else None
         db, dq, dg, dbt = (torch.zeros(NY, device="cuda"), torch.zeros(H, device="cuda"),
                            torch.zeros(H, device="cuda"), torch.zeros(H, device="cuda"))
         K.mha_pool_bwd(Yu, mask, n, Lq, heads, dk, dv, gamma, beta, q, stats, probs, dnews,

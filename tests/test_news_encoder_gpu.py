@@ -87,12 +87,14 @@ def _fused_mha_news_encoder(p_drop):
                                    msg=k)
 
 
+@pytest.mark.parametrize("with_dz", [False, True])
 @pytest.mark.parametrize("mode", ["split", "fused_saved", "fused_saved_ws"])
 @pytest.mark.parametrize("p_drop", [0.0, 0.2])
-def test_mha_pool_split_backward_matches_fused(p_drop, mode):
-    """The backward forms with the saved attention output O -- split (pooling/LN pass, dO through
-    HBM, per-head attention pass) and fused on the saved O (dO kept in LDS; with and without the
-    parameter-gradient copies) -- against the fused one that recomputes the attention."""
+def test_mha_pool_split_backward_matches_fused(p_drop, mode, with_dz):
+    """The backward forms with the saved attention output O -- split (pooling/LN pass writing each
+    token's row terms, per-head attention pass rebuilding its slice of dO from O) and fused on the saved
+    O (dO kept in LDS; with and without the parameter-gradient copies) -- against the fused one that
+    recomputes the attention; with_dz: a gradient of the token outputs Z too (MHANewsFn's dtok)."""
     from newsrec_amd import kernels as K
     torch.manual_seed(11)
     n, Lq, heads, dk, dv = 97, 30, 12, 64, 32
@@ -105,6 +107,7 @@ def test_mha_pool_split_backward_matches_fused(p_drop, mode):
     beta = 0.1 * torch.randn(H, device="cuda")
     q = torch.randn(H, device="cuda")
     dnews = torch.randn(n, H, device="cuda")
+    dz = torch.randn(T, H, device="cuda") if with_dz else None
     outs = []
     for form in ("recompute", mode):
         saved = form != "recompute"
@@ -117,10 +120,11 @@ def test_mha_pool_split_backward_matches_fused(p_drop, mode):
         dy = torch.zeros(T, NY, device="cuda")
         db, dq, dg, dbt = (torch.zeros(NY, device="cuda"), torch.zeros(H, device="cuda"),
                            torch.zeros(H, device="cuda"), torch.zeros(H, device="cuda"))
-        dob = torch.empty(T, H, device="cuda") if form == "split" else None
+        dob = torch.empty(T, 8, device="cuda") if form == "split" else None
         ws = torch.zeros(32, (3 * H + NY + 3) // 4 * 4, device="cuda") if form == "fused_saved_ws" else None
         K.mha_pool_bwd(y, mask, n, Lq, heads, dk, dv, gamma, beta, q, stats, probs, dnews, dy, db, dq, dg, dbt,
-                       p_drop=p_drop, seed=9, offset=3, o=O, dob=dob, ws=ws, ws_copies=32 if ws is not None else 0)
+                       p_drop=p_drop, seed=9, offset=3, dz=dz, o=O, dob=dob, ws=ws,
+                       ws_copies=32 if ws is not None else 0)
         if ws is not None:
             torch.cuda.synchronize()
             assert not bool(ws.any().item())   # the copies are left zero

@@ -49,7 +49,7 @@ def main():
     t_fwd = timed(fwd, a.reps)
     dnews = torch.randn(n, H, device=dev)
     dY = torch.empty(T, NY, device=dev)
-    dob = torch.empty(T, H, device=dev)
+    dob = torch.empty(T, 8, device=dev)
     db, dq, dg, dbt = (torch.zeros(NY, device=dev), torch.zeros(H, device=dev), torch.zeros(H, device=dev),
                        torch.zeros(H, device=dev))
     from newsrec_amd.functions import GRAD_COPIES, _grad_copies
