@@ -71,10 +71,13 @@ def synth_batch(gen, device, b=B, c=C, nh=NH, l=L, full=True):
     return {k: v.to(device) for k, v in x.items()}
 
 
+DROPOUT_P = 0.2   # the headline's dropout (tools/ab_step.py may set bench.DROPOUT_P for an A/B)
+
+
 def build(device):
     from newsrec_amd.manager import build_model
     torch.manual_seed(42)
-    return build_model("mha", "mha", H, vocab=V, device=device, user_num=USERS_LARGE, dropout_p=0.2)
+    return build_model("mha", "mha", H, vocab=V, device=device, user_num=USERS_LARGE, dropout_p=DROPOUT_P)
 
 
 def make_optim(model, capturable=False):

@@ -36,7 +36,7 @@ def main():
                 m, k = k.split(".", 1)
                 mod = mods[m]
             cur = getattr(mod, k)
-            setattr(mod, k, bool(int(val)) if isinstance(cur, bool) else int(val))
+            setattr(mod, k, bool(int(val)) if isinstance(cur, bool) else float(val) if isinstance(cur, float) else int(val))
         model = bench.build(dev)
         model.train()
         opt = bench.make_optim(model, capturable=True)
