@@ -132,4 +132,6 @@ def test_mha_pool_split_backward_matches_fused(p_drop, mode, with_dz):
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0])
     for a, b in zip(outs[0][1:], outs[1][1:]):
-        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-4)   # dbias: atomic order
+        # dbias / dq / dgamma / dbeta are sums over the ~3k tokens in atomic order: the bar scales with
+        # their magnitude (a random token-output gradient dz makes them O(10))
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-4 * max(1.0, a.abs().max().item()))
