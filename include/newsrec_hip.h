@@ -284,12 +284,15 @@ int nr_mha_user_pool_fwd(const float* y, int64_t ldy, int64_t y_rows, const int6
                          const float* q, float* out, int64_t ldo, int32_t prec, hipStream_t stream);
 
 /* Backward of nr_mha_attn_fwd (XSoftmax.backward, Attention.py:77-80, and the two matmuls);
- * recomputes P.  dqk receives the gradient of the shared key projection (both roles). */
+ * recomputes P.  dqk receives the gradient of the shared key projection (both roles).
+ * dbias_k [heads*dk] / dbias_v [heads*dv] (both or neither; device): the projection bias gradient
+ * (keyProject / valueProject bias, Attention.py:107-108) ATOMICALLY ACCUMULATED as the column sums of
+ * dqk / dv_out over the nseq*L rows (caller zeroes) -- the separate column-sum pass folded in. */
 int nr_mha_attn_bwd(const float* qk, int64_t ld_qk, const float* v, int64_t ld_v,
                     const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L,
                     int32_t heads, int32_t dk, int32_t dv, float scale, const float* dout,
                     int64_t ld_dout, float* dqk, int64_t ld_dqk, float* dv_out, int64_t ld_dv,
-                    hipStream_t stream);
+                    float* dbias_k, float* dbias_v, hipStream_t stream);
 
 /* Fused MHA news-encoder tail, one workgroup per title (L <= 32): for each head the tied-QK
  * attention on the f32 MFMA (S = Kp Kpᵀ / sqrt(dk), XSoftmax with m_i m_j, O = P Vp), then

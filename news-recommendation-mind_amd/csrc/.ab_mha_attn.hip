@@ -26,48 +26,7 @@ struct AttnArgs {
   float* out; int64_t ld_out;           // fwd: O         bwd: dKp
   float* dv; int64_t ld_dv;             // bwd: dVp
   const int64_t* rows;                  // fwd: physical qk / v row of token (seq*L + j), or null
-  // bwd, optional: the projection bias gradient, += column sums of dKp / dVp (atomic, caller zeroes)
-  float* dbk; float* dbv;
 };
-
-// Column sum over the W (32 or 64) consecutive lanes of a group (the tokens of one sequence), in every
-// lane: DPP row sums and permlane swaps (nr_wave_sum's steps; no LDS round trips, which made sixteen
-// __shfl_xor reductions per wave double the kernel)
-template <int W>
-__device__ __forceinline__ float group_sum(float v) {
-  static_assert(W == 32 || W == 64, "group_sum: half or whole waves");
-  if constexpr (W == 64) {
-    return nr_wave_sum(v);
-  } else {
-    v += nr_dpp(v, 0);
-    v += nr_dpp(v, 1);
-    v += nr_dpp(v, 2);
-    v += nr_dpp(v, 3);
-    const unsigned x = __builtin_bit_cast(unsigned, v);
-    auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
-  }
-}
-
-// dst[c] += Σ over the group's lanes of acc[c] (lanes with live == false add nothing); lane gi of the
-// group (gi = its index in the group) adds columns gi, gi + W, ...: the N column sums leave in
-// ceil(N / W) wave-wide atomic instructions, not N single-lane ones (device-scope atomics are
-// serviced per instruction past the L2: sixteen single-lane adds per wave doubled this kernel)
-template <int N, int W>
-__device__ __forceinline__ void flush_colsum(const float (&acc)[N], bool live, int gi, float* dst) {
-  constexpr int PER = (N + W - 1) / W;
-  float mine[PER];
-#pragma unroll
-  for (int k = 0; k < PER; ++k) mine[k] = 0.f;
-#pragma unroll
-  for (int c = 0; c < N; ++c) {
-    const float s = group_sum<W>(live ? acc[c] : 0.f);
-    mine[c / W] = gi == c % W ? s : mine[c / W];
-  }
-#pragma unroll
-  for (int k = 0; k < PER; ++k)
-    if (k * W + gi < N) atomicAdd(dst + k * W + gi, mine[k]);
-}
 
 template <int LMAX, int DK, int DV>
 struct Smem {
@@ -252,14 +211,13 @@ __global__ __launch_bounds__(64) void mha_attn_bwd_kernel(AttnArgs g) {
       for (int c = 0; c < DV; c += 4)
         *reinterpret_cast<float4*>(dst + c) = make_float4(acc[c], acc[c + 1], acc[c + 2], acc[c + 3]);
     }
-    if (g.dbv && head < g.heads) flush_colsum<DV, LMAX>(acc, active, i, g.dbv + head * DV);
   }
   __syncthreads();
   // dS row (scaled) overwrites P in LDS
 #pragma unroll
   for (int j = 0; j < LMAX; ++j) sm.p[hh][i][j] = p[j] * (dp[j] - rs) * g.scale;
   __syncthreads();
-  if (!active && !g.dbk) return;
+  if (!active) return;
   float acc[DK];
 #pragma unroll
   for (int c = 0; c < DK; ++c) acc[c] = 0.f;
@@ -273,13 +231,10 @@ __global__ __launch_bounds__(64) void mha_attn_bwd_kernel(AttnArgs g) {
       acc[c + 2] = fmaf(w, kj.z, acc[c + 2]); acc[c + 3] = fmaf(w, kj.w, acc[c + 3]);
     }
   }
-  if (active) {
-    float* dst = g.out + (seq * g.L + i) * g.ld_out + head * DK;
+  float* dst = g.out + (seq * g.L + i) * g.ld_out + head * DK;
 #pragma unroll
-    for (int c = 0; c < DK; c += 4)
-      *reinterpret_cast<float4*>(dst + c) = make_float4(acc[c], acc[c + 1], acc[c + 2], acc[c + 3]);
-  }
-  if (g.dbk && head < g.heads) flush_colsum<DK, LMAX>(acc, active, i, g.dbk + head * DK);
+  for (int c = 0; c < DK; c += 4)
+    *reinterpret_cast<float4*>(dst + c) = make_float4(acc[c], acc[c + 1], acc[c + 2], acc[c + 3]);
 }
 
 // ---- L in (32, 64] (the user encoder's 50-click histories: few sequences): FOUR waves per
@@ -470,7 +425,7 @@ __global__ __launch_bounds__(64 * SPLIT_NW) void mha_attn_bwd_split_kernel(AttnA
 #pragma unroll
   for (int jj = 0; jj < JW; ++jj) ds[i][w * JW + jj] = p[jj] * (dp[jj] - R) * g.scale;
   __syncthreads();
-  const bool live = i < g.L;   // lanes past L compute on zero rows: no stores, nothing in the column sums
+  if (i >= g.L) return;
   // (3) dV_j (lane = key j) = Σ_r P_rj dO_r over this wave's CV columns
   {
     float acc[CV];
@@ -486,13 +441,9 @@ __global__ __launch_bounds__(64 * SPLIT_NW) void mha_attn_bwd_split_kernel(AttnA
         acc[c + 2] = fmaf(pr, d4.z, acc[c + 2]); acc[c + 3] = fmaf(pr, d4.w, acc[c + 3]);
       }
     }
-    if (live) {
-      float* dst = g.dv + (seq * g.L + i) * g.ld_dv + head * DV + w * CV;
+    float* dst = g.dv + (seq * g.L + i) * g.ld_dv + head * DV + w * CV;
 #pragma unroll
-      for (int c = 0; c < CV; c += 4)
-        *reinterpret_cast<float4*>(dst + c) = make_float4(acc[c], acc[c + 1], acc[c + 2], acc[c + 3]);
-    }
-    if (g.dbv) flush_colsum<CV, 64>(acc, live, lane, g.dbv + head * DV + w * CV);
+    for (int c = 0; c < CV; c += 4) *reinterpret_cast<float4*>(dst + c) = make_float4(acc[c], acc[c + 1], acc[c + 2], acc[c + 3]);
   }
   // (4) dKp_i = Σ_j (dS_ij + dS_ji) Kp_j over this wave's CK columns
   {
@@ -509,13 +460,9 @@ __global__ __launch_bounds__(64 * SPLIT_NW) void mha_attn_bwd_split_kernel(AttnA
         acc[c + 2] = fmaf(wgt, kj.z, acc[c + 2]); acc[c + 3] = fmaf(wgt, kj.w, acc[c + 3]);
       }
     }
-    if (live) {
-      float* dst = g.out + (seq * g.L + i) * g.ld_out + head * DK + w * CK;
+    float* dst = g.out + (seq * g.L + i) * g.ld_out + head * DK + w * CK;
 #pragma unroll
-      for (int c = 0; c < CK; c += 4)
-        *reinterpret_cast<float4*>(dst + c) = make_float4(acc[c], acc[c + 1], acc[c + 2], acc[c + 3]);
-    }
-    if (g.dbk) flush_colsum<CK, 64>(acc, live, lane, g.dbk + head * DK + w * CK);
+    for (int c = 0; c < CK; c += 4) *reinterpret_cast<float4*>(dst + c) = make_float4(acc[c], acc[c + 1], acc[c + 2], acc[c + 3]);
   }
 }
 
@@ -572,16 +519,14 @@ extern "C" int nr_mha_attn_bwd(const float* qk, int64_t ld_qk, const float* v, i
                                const void* mask, int32_t mask_dtype, int64_t nseq, int32_t L,
                                int32_t heads, int32_t dk, int32_t dv, float scale,
                                const float* dout, int64_t ld_dout, float* dqk, int64_t ld_dqk,
-                               float* dvout, int64_t ld_dv, float* dbias_k, float* dbias_v,
-                               hipStream_t stream) {
+                               float* dvout, int64_t ld_dv, hipStream_t stream) {
   if (L < 1 || L > 64 || heads < 1) return NR_EINVAL(0);
   if (!qk || !v || !mask || !dout || !dqk || !dvout) return NR_EINVAL(1);
   if ((ld_qk | ld_v | ld_dout | ld_dqk | ld_dv) & 3 || !aligned16(qk) || !aligned16(v) ||
       !aligned16(dout) || !aligned16(dqk) || !aligned16(dvout))
     return NR_EINVAL(2);
   if (nseq == 0) return NR_OK;
-  if ((dbias_k == nullptr) != (dbias_v == nullptr)) return NR_EINVAL(3);
   AttnArgs g{qk, ld_qk, v, ld_v, mask, mask_dtype, nseq, L, heads, scale,
-             dout, ld_dout, dqk, ld_dqk, dvout, ld_dv, nullptr, dbias_k, dbias_v};
+             dout, ld_dout, dqk, ld_dqk, dvout, ld_dv, nullptr};
   return dispatch(g, dk, dv, true, stream);
 }

@@ -646,8 +646,8 @@ class MHANewsFn(_GradAwareFn):
             K.attn_pool_bwd(O, query, mask, n, seq_len, probs, dnews, dO, dq, gamma=gamma, beta=beta, stats=stats,
                             dgamma=dgamma, dbeta=dbeta, p_drop=p_drop, seed=seed,
                             offset=0 if ctx.rng is not None else offset, dz=dz, rng=ctx.rng)
-            K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
-            K.colsum(dY, T, NY, db)
+            K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, n, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY],
+                           dbias=db)
         dtable = None
         if ur is not None:
             # per-distinct-row gradient, then the two GEMMs over U rows instead of T tokens
@@ -1015,7 +1015,10 @@ class MHAFn(_GradAwareFn):
         if dO.stride(-1) != 1 or dO.stride(0) % 4 or dO.data_ptr() % 16:
             dO = dO.contiguous()
         dY = _empty(rows, NY, x)
-        K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, nseq, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY])
+        dw, db = _backward_zeros(ctx, dev, (NY, D), (NY,))
+        # the projection bias gradient (column sums of dY) accumulates inside the attention backward
+        K.mha_attn_bwd(Y[:, :NQ], Y[:, NQ:NY], mask, nseq, seq_len, heads, dk, dv, dO, dY[:, :NQ], dY[:, NQ:NY],
+                       dbias=db)
         split = USER_DGRAD_SPLIT if NY >= 512 * USER_DGRAD_SPLIT else 1
         if split > 1:
             # few output tiles (1600 x 384 for the NRMS user encoder) over a long contraction (1152): split
@@ -1026,8 +1029,7 @@ class MHAFn(_GradAwareFn):
         else:
             dx = _grad_out(ctx.dx_dest, rows, D, x)
             K.gemm(rows, D, NY, K.operand(dY, L.KCONTIG), K.operand(w_cat, L.MNCONTIG), dx)
-        dw, db = _backward_zeros(ctx, dev, (NY, D), (NY,))
-        _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, db, rows)
+        _proj_wgrad(dY, K.operand(x, L.MNCONTIG), dw, None, rows)
         return dx, None, dw, db, None, None, None, None, None
 
 

@@ -498,8 +498,12 @@ def mha_user_pool_fwd(y, rows, mask, nseq, seq_len, heads, dk, dv, q, out, prec=
            dk, dv, L.ptr(q), L.ptr(out), out.stride(0), _prec(prec), L.stream_ptr(out))
 
 
-def mha_attn_bwd(qk, v, mask, nseq, seq_len, heads, dk, dv, dout, dqk, dvv):
-    _f32(qk, v, dout, dqk, dvv)
+def mha_attn_bwd(qk, v, mask, nseq, seq_len, heads, dk, dv, dout, dqk, dvv, dbias=None):
+    """``dbias`` [heads*(dk+dv)] (optional): += the column sums of [dqk | dvv] (the projection bias
+    gradient, accumulated atomically inside the kernel)."""
+    _f32(qk, v, dout, dqk, dvv, dbias)
+    if dbias is not None and (dbias.numel() < heads * (dk + dv) or not dbias.is_contiguous()):
+        raise L.HipError("mha_attn_bwd: dbias needs heads*(dk+dv) contiguous floats")
     for t, need, n in ((qk, heads * dk, "qk"), (v, heads * dv, "v"), (dout, heads * dv, "dout"),
                        (dqk, heads * dk, "dqk"), (dvv, heads * dv, "dv")):
         _cols(t, need, n)
@@ -508,7 +512,8 @@ def mha_attn_bwd(qk, v, mask, nseq, seq_len, heads, dk, dv, dout, dqk, dvv):
     mp, mdt = mask_arg(mask, nseq * seq_len)
     L.call("nr_mha_attn_bwd", L.ptr(qk), qk.stride(0), L.ptr(v), v.stride(0), mp, mdt, nseq, seq_len,
            heads, dk, dv, 1.0 / float(dk) ** 0.5, L.ptr(dout), dout.stride(0), L.ptr(dqk), dqk.stride(0),
-           L.ptr(dvv), dvv.stride(0), L.stream_ptr(dout))
+           L.ptr(dvv), dvv.stride(0), L.ptr(dbias[:heads * dk]) if dbias is not None else None,
+           L.ptr(dbias[heads * dk:]) if dbias is not None else None, L.stream_ptr(dout))
 
 
 def aux_operand(t):

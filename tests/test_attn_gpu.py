@@ -51,10 +51,19 @@ def test_mha_attn(L, heads, dk, dv, mdt):
 
     dqk = torch.zeros(n * L, heads * dk, device="cuda")
     dvv = torch.zeros(n * L, heads * dv, device="cuda")
+    db = torch.zeros(heads * (dk + dv), device="cuda")
     K.mha_attn_bwd(qkd[:, :heads * dk], vd[:, :heads * dv], md, n, L, heads, dk, dv,
-                   dout.reshape(n * L, -1).float().cuda(), dqk, dvv)
+                   dout.reshape(n * L, -1).float().cuda(), dqk, dvv, dbias=db)
     torch.testing.assert_close(dqk.cpu().double().view(n, L, -1), qk.grad, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dvv.cpu().double().view(n, L, -1), v.grad, rtol=1e-4, atol=1e-4)
+    # the projection bias gradient folded into the kernel: the column sums of [dqk | dv]
+    want_db = torch.cat([qk.grad.sum((0, 1)), v.grad.sum((0, 1))])
+    torch.testing.assert_close(db.cpu().double(), want_db, rtol=1e-4, atol=1e-3)
+    # without dbias the gradients are the same, bit for bit
+    dqk2, dvv2 = torch.zeros_like(dqk), torch.zeros_like(dvv)
+    K.mha_attn_bwd(qkd[:, :heads * dk], vd[:, :heads * dv], md, n, L, heads, dk, dv,
+                   dout.reshape(n * L, -1).float().cuda(), dqk2, dvv2)
+    assert torch.equal(dqk, dqk2) and torch.equal(dvv, dvv2)
 
 
 @pytest.mark.parametrize("shape,mshape", [((4, 3, 30), (4, 1, 30)), ((2, 12, 30, 30), (2, 1, 30, 30)), ((5, 50), (5, 50))])
