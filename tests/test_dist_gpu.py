@@ -217,10 +217,12 @@ def _shard_worker(rank, world, port, case, mode, q):
         steps = 4
         halves = [_half(_batch(100 + i, dev), rank, world) for i in range(steps)]
         out = {}
-        for shard in (False, True):
+        # dense twice (the run-to-run spread of this build's gradients, which Adam amplifies into moves
+        # of up to 2 lr), then sharded
+        for shard in ("dense", "dense2", True):
             m = _model(case, dev)
             m.train()
-            sync = GradSync(m, bucket_mb=0.5, shard_tables=shard)
+            sync = GradSync(m, bucket_mb=0.5, shard_tables=shard is True)
             if mode == "eager":
                 opt = get_optim(m)
                 for x in halves:
@@ -231,7 +233,7 @@ def _shard_worker(rank, world, port, case, mode, q):
                 for i in range(2, steps):
                     g(i)
             torch.cuda.synchronize()
-            if shard:
+            if shard is True:
                 sh = [p for p in m.parameters() if getattr(p, "_nr_shard", None) is not None]
                 assert len(sh) == 1 and opt.state[sh[0]]["exp_avg"].shape[0] == sh[0]._nr_shard[1]
                 chk = bench.dp_check(m, opt, world, dev)
@@ -239,9 +241,10 @@ def _shard_worker(rank, world, port, case, mode, q):
             sync.close()
             out[shard] = {n: p.detach().clone() for n, p in m.named_parameters()}
         diffs = {}
-        for n in out[False]:
-            d = (out[True][n] - out[False][n]).abs()
-            diffs[n] = (d.max().item(), int((d > 1e-7).sum().item()), d.numel())
+        for n in out["dense"]:
+            d = (out[True][n] - out["dense"][n]).abs()
+            noise = int(((out["dense2"][n] - out["dense"][n]).abs() > 1e-7).sum().item())
+            diffs[n] = (d.max().item(), int((d > 1e-7).sum().item()), d.numel(), noise)
         q.put((rank, None, diffs))
         dist.barrier()
         dist.destroy_process_group()
@@ -255,7 +258,10 @@ def _shard_worker(rank, world, port, case, mode, q):
 def test_data_parallel_shard_tables_world2(case, mode):
     """GradSync(shard_tables=True) on the real models at world 2 (gloo on device tensors): the word
     table's gradient reduce-scattered in place, FusedAdam on the rank's row slab, the slabs all-gathered
-    -- replicas bitwise identical (bench.dp_check), every parameter within the dense path's spread."""
+    -- replicas bitwise identical (bench.dp_check), every parameter within the dense path's spread: the
+    largest difference within Adam's 2 lr per step, and no more elements off than a second dense run
+    differs from the first (plus a small slack) -- a slab Adam skipped or an all-gather that missed rows
+    would move every row of it."""
     world, port = 2, _port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -267,9 +273,8 @@ def test_data_parallel_shard_tables_world2(case, mode):
         p.join(timeout=60)
     for rank, err, diffs in res:
         assert err is None, err
-        for n, (dmax, n_off, n_all) in diffs.items():
+        for n, (dmax, n_off, n_all, noise) in diffs.items():
             # the bounds of test_data_parallel_real_model_world2 (4 Adam steps, rounding-level gradients)
             lr = 6e-6 if "bert" in n else 1e-4
             assert dmax <= 4 * 2 * lr + 1e-6, (rank, n, dmax)
-            if not n.endswith("attention.self.key.bias"):
-                assert n_off <= max(4, 1e-3 * n_all), (rank, n, n_off, n_all)
+            assert n_off <= 2 * noise + max(4, 1e-3 * n_all), (rank, n, n_off, noise, n_all)
