@@ -457,6 +457,11 @@ class GradSync:
             return self.scale
         hooked = {id(t) for t, _, _ in self.pending} | {id(t) for t, *_ in self.sparse}
         flights = []
+        # a sharded table whose backward did not hand its gradient to TABLE_GRAD_HOOK (the BERT tower's
+        # word embeddings: BertFn returns it to autograd): reduce-scattered in place here
+        for p, _, _, _ in self.shards.values():
+            if id(p) not in hooked and p.grad is not None:
+                flights.append(([p], p.grad, True, self._reduce_scatter(p, p.grad)))
         for bucket, inplace in self._buckets(self._dense_params(hooked)):
             flat = bucket[0].grad.view(-1) if inplace else torch.cat([p.grad.reshape(-1) for p in bucket])
             flights.append((bucket, flat, inplace, dist.all_reduce(flat, group=self.group, async_op=True)))

@@ -370,8 +370,10 @@ class TinyWords(torch.nn.Module):
         self.lin = torch.nn.Linear(4, 3)
 
 
-def _words_loss(model, x):
-    class Gather(torch.autograd.Function):   # the news tower's table gradient handling (MHANewsFn)
+def _words_loss(model, x, hook=True):
+    """hook: the news tower's table gradient handling (MHANewsFn hands it to TABLE_GRAD_HOOK); without,
+    the BERT tower's (BertFn returns it to autograd)."""
+    class Gather(torch.autograd.Function):
         @staticmethod
         def forward(ctx, table, idx):
             ctx.save_for_backward(idx)
@@ -384,7 +386,7 @@ def _words_loss(model, x):
             t = ctx.table_ref
             dt = F.table_grad_buffer(t, t.shape[0], t.shape[1], t.device, zero=True)
             dt.index_add_(0, idx, g)
-            if F.TABLE_GRAD_HOOK(t, dt):
+            if hook and F.TABLE_GRAD_HOOK(t, dt):
                 dt = None
             return dt, None
     out = model.lin(Gather.apply(model.bert_word_embedding.weight, x))
@@ -401,7 +403,7 @@ def _adam_cpu(entries, beta1, beta2, eps, weight_decay, grad_scale=1.0, advance_
         p.sub_(lr * (m / c1) / ((v / c2).sqrt() + eps))
 
 
-def _shard_worker(rank, world, port, q, deferred):
+def _shard_worker(rank, world, port, q, deferred, hook=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     D.setup(rank, world, backend="gloo", master_port=str(port))
@@ -420,7 +422,7 @@ def _shard_worker(rank, world, port, q, deferred):
             for step in range(3):
                 opt.zero_grad(set_to_none=True)
                 x = torch.tensor([rank, (rank + 5 * step) % 11, 10, 7])
-                _words_loss(model, x).backward()
+                _words_loss(model, x, hook).backward()
                 opt.step(grad_scale=sync())
                 sync.after_step()
             if shard:   # moments for the rank's own rows only
@@ -435,17 +437,20 @@ def _shard_worker(rank, world, port, q, deferred):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("hook", [True, False])
 @pytest.mark.parametrize("world,deferred", [(2, False), (3, False), (2, True), (3, True)])
-def test_grad_sync_shard_tables_bitwise_gloo(world, deferred):
+def test_grad_sync_shard_tables_bitwise_gloo(world, deferred, hook):
     """GradSync(shard_tables=True): the word table's gradient reduce-scattered in place into row slabs,
     Adam on each rank's slab only (moments for those rows), the slabs all-gathered in place after the
     step -- three steps, eager (the reduce-scatter issued from inside the backward) and deferred (the
-    graphed step's issue / exchange), world 2 and 3 (a pad row; a short last slab): every parameter
-    BITWISE equal to the dense all-reduce path on every rank."""
+    graphed step's issue / exchange), world 2 and 3 (a pad row; a short last slab), the table's
+    gradient handed to TABLE_GRAD_HOOK (the news towers) or returned to autograd (the BERT tower: the
+    eager exchange reduce-scatters it then -- it once skipped it): every parameter BITWISE equal to the
+    dense all-reduce path on every rank."""
     port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_shard_worker, args=(r, world, port, q, deferred)) for r in range(world)]
+    ps = [ctx.Process(target=_shard_worker, args=(r, world, port, q, deferred, hook)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=180) for _ in range(world)]
