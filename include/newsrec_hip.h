@@ -42,11 +42,7 @@ enum nr_rows_map {
 
 enum nr_layout {
   NR_KCONTIG = 0, /* stored rows are the M (or N) index, k contiguous: A[M][K], B[N][K]   */
-  NR_MNCONTIG = 1, /* stored rows are the k index, M (or N) contiguous: A[K][M], B[K][N]  */
-  NR_KCONTIG_BF16 = 2 /* as NR_KCONTIG with bf16 elements (data points to uint16 bf16 values, ld in
-                          elements, 16-B aligned, ld % 8 == 0): the operand the bf16 arithmetic
-                          (NR_GEMM_BF16) would round to, stored rounded -- a table's bf16 shadow.
-                          Plain or gathered rows, both operands of one call; K % 64 == 0 */
+  NR_MNCONTIG = 1 /* stored rows are the k index, M (or N) contiguous: A[K][M], B[K][N]   */
 };
 
 typedef struct nr_operand {

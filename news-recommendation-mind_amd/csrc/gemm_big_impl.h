@@ -29,12 +29,8 @@ constexpr int BIG_BM = 256;
 // stores at 32 cost more than the extra MFMAs per barrier buy (one-box A/B, bf16, µs: BERT FFN-in
 // weight gradient 657 -> 387, NRMS table dgrad 208 -> 141, CNN conv weight gradient 144 -> 115;
 // the K-contiguous forward shapes keep 32: BERT FFN-out 152 vs 187 at 16)
-// bf16 operands stored rounded (NR_KCONTIG_BF16, both K-contiguous): 64 -- a 16-B load carries 8 k, so a
-// 64-deep tile moves the bytes of a 32-deep fp32 one and gives every barrier twice the MFMAs
 template <int NP, int AM, int BMODE>
-constexpr int big_bk() {
-  return NP == 1 && is_kh(AM) && is_kh(BMODE) ? 64 : NP == 1 && is_kc(AM) && is_kc(BMODE) ? 32 : 16;
-}
+constexpr int big_bk() { return NP == 1 && is_kc(AM) && is_kc(BMODE) ? 32 : 16; }
 // bf16 per LDS row: BK k + 8 pad (48 / 80 B: odd multiples of 16 B, conflict-free ds_read_b128)
 template <int BK>
 constexpr int big_sr() { return BK + 8; }
@@ -252,68 +248,8 @@ struct BigMN {
   }
 };
 
-// K-contiguous bf16 operand (NR_KCONTIG_BF16: the values the bf16 arithmetic rounds to, stored rounded),
-// R rows x 64 k: 512 threads x (R / 64) 16-B chunks of 8 k, in BigKC's QPR = 8 row / chunk order (a
-// 16-lane group of ds_write_b128 covers two rows 4 apart: 64 dwords on 2 x 32 banks); no conversion on
-// the way to LDS.
 template <int R, int MODE, int BK>
-struct BigKH {
-  static constexpr int CPR = BK / 8;   // 16-B chunks per row
-  static constexpr int NV = R * CPR / 512;
-  static constexpr int SR = big_sr<BK>();
-  static_assert(CPR == 8, "BigKH: 64-deep k-tiles");
-  // 8 bf16 each, as a native 4 x u32 vector (HIP's float4 / uint4 structs are copied as aggregates
-  // here, which kept both register sets in scratch: 272 B per lane)
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 v[2][NV];
-  const uint16_t* rowp[NV];
-  __device__ __forceinline__ static int row_of(int f) {
-    const int l = f & 63, g = l >> 4;
-    return 8 * (f >> 6) + g + 4 * ((l >> 3) & 1);
-  }
-  __device__ __forceinline__ static int chunk_of(int f) { return f & 7; }
-  __device__ __forceinline__ void init(const Op& d, int64_t r0, int64_t rlim, int tid) {
-    const uint16_t* base = reinterpret_cast<const uint16_t*>(d.base);
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int f = tid + 512 * i;
-      int64_t row = r0 + row_of(f);
-      row = row < rlim ? row : rlim - 1;   // clamp: rows >= M are computed and discarded
-      rowp[i] = MODE == KH_GATHER ? base + d.idx[row] * d.ld : base + row * d.ld;
-    }
-  }
-  template <int S>
-  __device__ __forceinline__ void prefetch_idx(const Op&, int64_t, int64_t, int) {}
-  template <int S>
-  __device__ __forceinline__ void load(const Op&, int64_t, int64_t, int64_t k0, int tid) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int f = tid + 512 * i;
-      v[S][i] = *reinterpret_cast<const u32x4*>(rowp[i] + k0 + 8 * chunk_of(f));
-    }
-  }
-  template <int S, int NP>
-  __device__ __forceinline__ void store_one(uint16_t* lds, int tid, int i) const {
-    static_assert(NP == 1, "bf16 operands: one plane");
-    const int f = tid + 512 * i;
-    *reinterpret_cast<u32x4*>(lds + row_of(f) * SR + 8 * chunk_of(f)) = v[S][i];
-  }
-  template <int S, int NP>
-  __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) store_one<S, NP>(lds, tid, i);
-  }
-  static constexpr int PIECES = NV;
-  template <int S, int NP>
-  __device__ __forceinline__ void store_piece(uint16_t* lds, int tid, int p) const {
-    store_one<S, NP>(lds, tid, p);
-  }
-};
-
-template <int R, int MODE, int BK>
-using BigLoader = typename std::conditional<
-    is_kh(MODE), BigKH<R, MODE, BK>,
-    typename std::conditional<is_kc(MODE), BigKC<R, MODE, BK>, BigMN<R, MODE, BK>>::type>::type;
+using BigLoader = typename std::conditional<is_kc(MODE), BigKC<R, MODE, BK>, BigMN<R, MODE, BK>>::type;
 
 // Tail pieces through a workspace (NR_EPI_SCATTER_ZEROED with Args::slab): header ints {full, rem,
 // pieces, gn} at slab[0..4) (block 0 writes them every launch), then one 256 x 256 partial tile per
@@ -715,10 +651,6 @@ int launch_big_modes(const Args& g, int am, int bm, int splits, hipStream_t s) {
   NR_BIG(KC_PLAIN, MN_PLAIN, true)     // dgrad (store / scatter-store epilogues)
   NR_BIG(MN_PLAIN, MN_GATHER, false)   // wgrad over gathered rows
   NR_BIG(MN_PLAIN, MN_PLAIN, false)    // wgrad
-  if constexpr (NP == 1) {
-    NR_BIG(KH_GATHER, KH_PLAIN, true)  // bf16-stored operands: gathered rows x Wᵀ (the CNN tap projection)
-    NR_BIG(KH_PLAIN, KH_PLAIN, true)   // bf16-stored operands: dgrad over k-contiguous weights
-  }
 #undef NR_BIG
   return -1;
 }

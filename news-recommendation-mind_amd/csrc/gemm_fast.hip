@@ -178,27 +178,16 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
   auto aligned = [](const nr_operand* o) {
     return (o->ld % 4 == 0) && ((reinterpret_cast<uintptr_t>(o->data) & 15) == 0);
   };
-  const bool kh = A->layout == NR_KCONTIG_BF16 || B->layout == NR_KCONTIG_BF16;
-  if (!aligned(A) || !aligned(B) || (K % 32)) return kh ? NR_EINVAL(9) : -1;   // (no generic bf16 path)
+  if (!aligned(A) || !aligned(B) || (K % 32)) return -1;
   int am, bmode;
-  if (kh) {
-    // bf16-stored operands: both K-contiguous bf16, the bf16 arithmetic, the big kernel's 64-deep tiles
-    if (A->layout != NR_KCONTIG_BF16 || B->layout != NR_KCONTIG_BF16 || prec != NR_GEMM_BF16 || (K % 64) ||
-        (A->ld % 8) || (B->ld % 8) || A->map == NR_ROWS_CONV3 || B->map != NR_ROWS_PLAIN || bm != 128 ||
-        bn != 128 || N < 128)
-      return NR_EINVAL(9);
-    if (epilogue == NR_EPI_ATOMIC || epilogue == NR_EPI_SCATTER || zeroed) return NR_EINVAL(9);
-    am = A->map == NR_ROWS_GATHER ? KH_GATHER : KH_PLAIN;
-    bmode = KH_PLAIN;
-  } else if (A->layout == NR_KCONTIG) {
+  if (A->layout == NR_KCONTIG) {
     am = A->map == NR_ROWS_PLAIN ? KC_PLAIN : A->map == NR_ROWS_GATHER ? KC_GATHER : KC_CONV3;
     if (am == KC_CONV3 && (A->seg % 32)) return -1;
   } else {
     if (A->map != NR_ROWS_PLAIN || A->ld < ((M + 3) & ~3LL)) return -1;
     am = MN_PLAIN;
   }
-  if (kh) {
-  } else if (B->layout == NR_KCONTIG) {
+  if (B->layout == NR_KCONTIG) {
     if (B->map != NR_ROWS_PLAIN) return -1;
     bmode = KC_PLAIN;
   } else {
@@ -245,8 +234,7 @@ int nr_gemm_fast(int64_t M, int64_t N, int64_t K, const nr_operand* A, const nr_
     const int bb = big_bn(M, N, K, splits, resplit, m_dev != nullptr, kmin);
     // the bf16x6 big kernel runs its k-loop two 16-deep k-tiles per iteration with no branch: every
     // unit's k range must be a multiple of 32 (k chunks are; K must be)
-    int BN = prec == NR_GEMM_BF16X6 && K % 32 != 0 ? 0 : (tailed ? 256 : (bb > 0 ? bb : 0));
-    if (kh && BN == 0) BN = N >= 256 ? 256 : 128;   // bf16-stored operands: the big kernel only
+    const int BN = prec == NR_GEMM_BF16X6 && K % 32 != 0 ? 0 : (tailed ? 256 : (bb > 0 ? bb : 0));
     if (BN) {
       Args gb = g;
       if (tailed) gb.tail = 16;

@@ -50,11 +50,9 @@ constexpr int SROW = 40;          // split LDS image: [plane][row][k] bf16, 32 k
 constexpr int SPL = 128 * SROW;   // one plane of a 128-row operand tile
 
 // operand modes
-enum { KC_PLAIN = 0, KC_GATHER = 1, KC_CONV3 = 2, MN_PLAIN = 3, MN_GATHER = 4, MN_CONV3 = 5,
-       KH_PLAIN = 6, KH_GATHER = 7 };   // KH: K-contiguous bf16 (NR_KCONTIG_BF16), big kernel only
+enum { KC_PLAIN = 0, KC_GATHER = 1, KC_CONV3 = 2, MN_PLAIN = 3, MN_GATHER = 4, MN_CONV3 = 5 };
 
 constexpr bool is_kc(int m) { return m <= KC_CONV3; }
-constexpr bool is_kh(int m) { return m == KH_PLAIN || m == KH_GATHER; }
 
 struct Op {
   const float* base;

@@ -22,7 +22,7 @@ c_ptr = ctypes.c_void_p
 
 # enum nr_rows_map / nr_layout / nr_epilogue / nr_mask_dtype
 ROWS_PLAIN, ROWS_GATHER, ROWS_CONV3 = 0, 1, 2
-KCONTIG, MNCONTIG, KCONTIG_BF16 = 0, 1, 2
+KCONTIG, MNCONTIG = 0, 1
 EPI_STORE, EPI_STORE_RELU, EPI_ATOMIC, EPI_SCATTER = 0, 1, 2, 3
 MASK_U8, MASK_I64, MASK_F64, MASK_F32 = 0, 1, 2, 3
 EPI_STORE_TANH, EPI_ACCUM_GATE, EPI_ACCUM, EPI_SCATTER_STORE = 4, 5, 6, 7

@@ -400,16 +400,8 @@ def cnn_keypool_bwd(C, wq, bq, query, nseq, seq_len, H, probs, dnews, dc, dwq, d
 
 
 def operand(t, layout, rows=None, mapping=L.ROWS_PLAIN, seq_len=1, seg=1, ld=None):
-    """Describe a stored matrix ``t`` (2-D, row-major, ld % 4 == 0, 16-B aligned).  ``layout``
-    L.KCONTIG_BF16: ``t`` is a torch.bfloat16 K-contiguous matrix (ld % 8 == 0), the operand the bf16
-    arithmetic rounds to, stored rounded (a table's bf16 shadow)."""
-    if layout == L.KCONTIG_BF16:
-        if t.dtype != torch.bfloat16 or not t.is_cuda:
-            raise L.HipError("a KCONTIG_BF16 operand must be a CUDA torch.bfloat16 tensor")
-        if t.dim() != 2 or t.stride(1) != 1 or t.stride(0) % 8 or t.data_ptr() % 16:
-            raise L.HipError("a KCONTIG_BF16 operand needs 2-D rows, ld % 8 == 0, 16-B alignment")
-    else:
-        _f32(t)
+    """Describe a stored matrix ``t`` (2-D, row-major, ld % 4 == 0, 16-B aligned)."""
+    _f32(t)
     if t.dim() != 2 or t.stride(1) != 1:
         raise L.HipError("operand must be a 2-D row-major tensor")
     ld = t.stride(0) if ld is None else ld

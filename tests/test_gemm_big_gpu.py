@@ -245,57 +245,3 @@ def test_big_wgrad_folds_bias_colsum(kd):
                 epilogue=L.EPI_ATOMIC, split_k=2, colsum=small[:64])
     assert not f2 and torch.equal(small.cpu(), db0)
 
-
-
-@pytest.mark.parametrize("N,M,m_dev", [(480, 24600, 24000), (1152, 3000, None), (160, 700, None)])
-def test_big_bf16_stored_operands_gather(N, M, m_dev):
-    """NR_KCONTIG_BF16 operands (the values the bf16 arithmetic rounds to, stored rounded: a table's bf16
-    shadow and bf16 weights) through the 64-deep k-tile path: BITWISE the bf16 arithmetic over the fp32
-    operands (same products, same 16-deep k order), gathered rows (the CNN tap projection), ragged M,
-    a device-resident M, both tile widths."""
-    g = torch.Generator().manual_seed(N + M)
-    V, E = 30522, 768
-    table = torch.randn(V, E, generator=g).cuda()
-    ids = torch.randint(0, V, (M,), generator=g).cuda()
-    W = (torch.randn(N, E, generator=g) / 16).cuda()
-    md = torch.tensor([m_dev], dtype=torch.int32, device="cuda") if m_dev else None
-    Y32 = torch.full((M, N), float("nan"), device="cuda")
-    Y16 = torch.full((M, N), float("nan"), device="cuda")
-    run = (lambda *a, **k: K.gemm_dyn(*a, m_dev=md, **k)) if md is not None else K.gemm
-    run(M, N, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(W, L.KCONTIG), Y32,
-        prec=L.GEMM_BF16)
-    run(M, N, E, K.operand(table.bfloat16(), L.KCONTIG_BF16, rows=ids, mapping=L.ROWS_GATHER),
-        K.operand(W.bfloat16(), L.KCONTIG_BF16), Y16, prec=L.GEMM_BF16)
-    torch.cuda.synchronize()
-    m = m_dev or M
-    assert torch.equal(Y16[:m], Y32[:m])
-    if md is not None:
-        assert torch.isnan(Y16[m_dev:]).all()   # rows past the device M untouched
-
-
-def test_big_bf16_stored_operands_scatter_store():
-    """bf16-stored plain operands with the distinct-row scatter-store epilogue (the CNN table dgrad over
-    k-contiguous conv weights): bitwise the bf16 arithmetic over the fp32 operands; the rejected forms
-    (a bf16 operand beside an fp32 one, the bf16x6 arithmetic, K % 64) raise."""
-    g = torch.Generator().manual_seed(5)
-    U, N, Kd, V = 2800, 768, 512, 40000
-    dC = torch.randn(U, Kd, generator=g).cuda()
-    Wt = (torch.randn(N, Kd, generator=g) / 30).cuda()
-    rows = (torch.randperm(V - 1, generator=g)[:U] + 1).cuda()
-    out = []
-    for a, b, lay in ((dC, Wt, L.KCONTIG), (dC.bfloat16(), Wt.bfloat16(), L.KCONTIG_BF16)):
-        dt = torch.zeros(V, N, device="cuda")
-        K.gemm(U, N, Kd, K.operand(a, lay), K.operand(b, lay), dt, epilogue=L.EPI_SCATTER_STORE,
-               c_rows=K.rows_map(rows, L.ROWS_GATHER), pad_row=0, prec=L.GEMM_BF16)
-        out.append(dt)
-    torch.cuda.synchronize()
-    assert torch.equal(out[0], out[1])
-    with pytest.raises(L.HipError):
-        K.gemm(U, N, Kd, K.operand(dC.bfloat16(), L.KCONTIG_BF16), K.operand(Wt, L.KCONTIG), out[0],
-               prec=L.GEMM_BF16)
-    with pytest.raises(L.HipError):
-        K.gemm(U, N, Kd, K.operand(dC.bfloat16(), L.KCONTIG_BF16), K.operand(Wt.bfloat16(), L.KCONTIG_BF16),
-               out[0], prec=L.GEMM_BF16X6)
-    with pytest.raises(L.HipError):
-        K.gemm(U, N, 480, K.operand(dC[:, :480].bfloat16().contiguous(), L.KCONTIG_BF16),
-               K.operand(Wt[:, :480].bfloat16().contiguous(), L.KCONTIG_BF16), out[0], prec=L.GEMM_BF16)

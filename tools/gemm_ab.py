@@ -44,16 +44,8 @@ adam_p = [torch.randn(30522, 768, device=dev), torch.randn(1152, 768, device=dev
 adam_s = [(q, torch.randn_like(q), torch.zeros_like(q), torch.zeros_like(q)) for q in adam_p]
 def adam_step(p):
     K.adam_multi([(q, g, m, v, 1e-4, 1) for q, g, m, v in adam_s], 0.9, 0.999, 1e-8, 0.0)
-# bf16-stored operands (NR_KCONTIG_BF16; the bf16 arithmetic only): the table's bf16 shadow, the conv
-# weights, and the per-distinct-row sums with K padded to a multiple of 64 by zero columns
-table_h = table.bfloat16(); w3_h = w3.bfloat16()
-Pg_h = torch.zeros(Pg.shape[0], 512, dtype=torch.bfloat16, device=dev); Pg_h[:, :480] = Pg.bfloat16()
-w3T_h = torch.zeros(w3T.shape[0], 512, dtype=torch.bfloat16, device=dev); w3T_h[:, :480] = w3T.bfloat16()
 cases = {
  "adam_nrms": (0, adam_step),
- "cnn_tap_proj_h": (2*U*E*480, lambda p: K.gemm_dyn(U, 480, E, K.operand(table_h, L.KCONTIG_BF16, rows=ids, mapping=L.ROWS_GATHER), K.operand(w3_h, L.KCONTIG_BF16), P, prec=p)),
- "cnn_table_dgrad_store": (2*24600*E*480, lambda p: K.gemm_dyn(U, E, 480, K.operand(Pg, L.KCONTIG), K.operand(w3T, L.KCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_STORE, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
- "cnn_table_dgrad_store_h": (2*24600*E*480, lambda p: K.gemm_dyn(U, E, 512, K.operand(Pg_h, L.KCONTIG_BF16), K.operand(w3T_h, L.KCONTIG_BF16), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_STORE, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
  "nrms_proj_fwd": (2*U*E*1152, lambda p: K.gemm_dyn(U, 1152, E, K.operand(table, L.KCONTIG, rows=ids, mapping=L.ROWS_GATHER), K.operand(W, L.KCONTIG), Y, prec=p)),
  "nrms_proj_dgrad": (2*U*E*1152, lambda p: K.gemm_dyn(U, E, 1152, K.operand(dY, L.KCONTIG), K.operand(W, L.MNCONTIG), dX, prec=p)),
  "nrms_dgrad_table": (2*24600*E*1152, lambda p: K.gemm_dyn(52800, E, 1152, K.operand(dYc, L.KCONTIG), K.operand(W, L.MNCONTIG), dT, m_dev=m_dev, epilogue=L.EPI_SCATTER_ZEROED, c_rows=K.rows_map(uids, L.ROWS_GATHER), pad_row=0, prec=p)),
@@ -92,8 +84,6 @@ only = os.environ.get("NR_AB_CASES")
 for pn, p in (("bf16x6", L.GEMM_BF16X6), ("bf16", L.GEMM_BF16)):
     for k, (fl, fn) in cases.items():
         if only and k not in only.split(","):
-            continue
-        if k.endswith("_h") and p != L.GEMM_BF16:   # bf16-stored operands: the bf16 arithmetic only
             continue
         ms = bench(lambda: fn(p))
         out.setdefault(k, {})[pn] = {"us": round(ms * 1e3, 1), "tflops": round(fl / ms / 1e9, 1)}
