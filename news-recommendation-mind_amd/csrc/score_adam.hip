@@ -308,17 +308,27 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
   while (t + 1 < a.count && b >= a.blk_off[t + 1]) ++t;
   const AdamEntry& e = a.e[t];
   float step = e.step_size, bc2_sqrt = e.bc2_sqrt;
-  if (e.step_dev || e.lr_dev) {
-    // with a ticket the device count is the one before this step: this step is count + 1
-    const double st = e.step_dev ? (double)*e.step_dev + (a.ticket ? 1.0 : 0.0) : (double)e.step;
-    const double lr = e.lr_dev ? (double)*e.lr_dev : (double)e.lr;
-    step = (float)(lr / (1.0 - pow((double)a.b1, st)));
-    bc2_sqrt = (float)sqrt(1.0 - pow((double)a.b2, st));
-  }
+  // device step count / learning rate: the bias corrections in double precision, by ONE lane of the
+  // workgroup (the other 255 would repeat two pow() calls each), after the thread's loads are issued
+  const bool dev_sched = e.step_dev || e.lr_dev;
+  __shared__ float s_sched[2];
+  auto dev_schedule = [&]() {
+    if (threadIdx.x == 0) {
+      // with a ticket the device count is the one before this step: this step is count + 1
+      const double st = e.step_dev ? (double)*e.step_dev + (a.ticket ? 1.0 : 0.0) : (double)e.step;
+      const double lr = e.lr_dev ? (double)*e.lr_dev : (double)e.lr;
+      s_sched[0] = (float)(lr / (1.0 - pow((double)a.b1, st)));
+      s_sched[1] = (float)sqrt(1.0 - pow((double)a.b2, st));
+    }
+    __syncthreads();
+    step = s_sched[0];
+    bc2_sqrt = s_sched[1];
+  };
   const int64_t base = (int64_t)(b - a.blk_off[t]) * kAdamChunk;
   const int64_t end = base + kAdamChunk < e.n ? base + kAdamChunk : e.n;
   const bool vec = ((reinterpret_cast<uintptr_t>(e.p) | reinterpret_cast<uintptr_t>(e.g) |
                      reinterpret_cast<uintptr_t>(e.m) | reinterpret_cast<uintptr_t>(e.v)) & 15) == 0;
+  if (!(vec && end - base == kAdamChunk) && dev_sched) dev_schedule();   // (workgroup-uniform branch)
   if (vec && end - base == kAdamChunk) {
     // all sixteen float4 loads of the thread in flight before the first store (the four tensors
     // are distinct allocations; without the explicit order the stores of one float4 would have
@@ -362,6 +372,7 @@ __global__ __launch_bounds__(256) void adam_multi_kernel(AdamMulti a) {
         vv[u] = adam_ld(e.v, i);
       }
     }
+    if (dev_sched) dev_schedule();   // while the loads are in flight
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t i = base / 4 + u * 256 + threadIdx.x;

@@ -4,6 +4,7 @@
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=$GRAFT_REPO_ROOT/gpurun_out/${1:-ab}; mkdir -p $O
 VARS=$2; T=$3; R=${4:-3}
+echo tests base; timeout -k 10 600 python -u -m pytest $T -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests_base.log 2>&1 || exit 1
 for v in $VARS; do
   echo tests $v; NR_LIB_PATH=$GRAFT_REPO_ROOT/ab/$v/libnewsrec_hip.so timeout -k 10 600 python -u -m pytest $T -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests_$v.log 2>&1 || exit 1
 done
