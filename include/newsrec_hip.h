@@ -690,7 +690,9 @@ int nr_bert_attn_fwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, 
  * BertSelfAttention, models/XFormer.py:68,94).  NULL: the backward re-hashes (same masks). */
 int64_t nr_bert_attn_keep_words(int64_t nseq, int32_t L, int32_t heads);
 
-/* Bytes of `work` nr_bert_attn_bwd needs. */
+/* Bytes of `work` nr_bert_attn_bwd needs (16-B aligned): D = rowsum(dctx * ctx) per (query, head),
+ * and for L > 96 (four-wave launches) the dS tiles the dK/dV kernel stores and the dQ kernel reads
+ * (4096 * nseq * heads * ceil(L / 32)^2 bytes; unused by prec = NR_GEMM_F32). */
 int64_t nr_bert_attn_bwd_workspace(int64_t nseq, int32_t L, int32_t heads);
 
 /* Backward of nr_bert_attn_fwd: writes dQ, dK, dV into dqkv at the columns of qkv (every column

@@ -279,6 +279,11 @@ struct AttnArgs {
   // of key tile kb, bit r + 16 h = key kb * 32 + crow(r, h) (the forward lane's own 16 bits per half);
   // the bf16-MFMA forward stores them, both backward kernels read them instead of re-hashing
   uint32_t* keep; int nkb;
+  // bwd, four-wave launches (L > 96): dS = P (dP' - D) as attn_bwd_kv_mp_kernel forms it, row
+  // ((seq * heads + head) * nkb + kb) * 32 nkb + q holding query q's 32 keys of key tile kb (128 B;
+  // queries padded to 32 nkb so the stores need no bound);
+  // attn_bwd_q_ds_kernel reads it back instead of recomputing S, P and dP
+  float* dsb;
 };
 
 __device__ __forceinline__ int64_t keep_word(const AttnArgs& g, int64_t seq, int head, int q, int kb) {
@@ -989,7 +994,7 @@ __global__ void __launch_bounds__(256) attn_fwd_mp_kernel(AttnArgs g) {
 // Two waves per SIMD, as attn_bwd_q_mp_kernel: with the own K / V rows held as split planes (96
 // VGPRs) the bound spilled 36 and ran slower (profiles/r04_o_xf_ab.json); held as fp32 and split per
 // query tile it spills 9 and the XFormer step gains 68.15 -> 67.86 ms (profiles/r04_q_xf_ab.json).
-template <int NP, bool DROP, bool PF, bool KB = false>
+template <int NP, bool DROP, bool PF, bool KB = false, bool DS = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) attn_bwd_kv_mp_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t Qp[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Op[NP][32][kKR];
@@ -1128,6 +1133,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) a
       pd[r] = pdr;
       ds[r] = pr * (d - qd[qr]);
     }
+    if constexpr (DS) {   // one 128 B row (query) per half-wave and r, unconditional: keys past L
+      // and the padding queries L .. 32 nkb - 1 store 0 (p = 0 there)
+      float* dsp = g.dsb + (((seq * g.heads + head) * (int64_t)g.nkb + kbt) * g.nkb + qb) * 1024 + c;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dsp[crow(r, hh) * 32] = ds[r];
+    }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const Planes<NP> pp = planes8<NP>(pd + 8 * t), sp = planes8<NP>(ds + 8 * t);
@@ -1249,6 +1260,73 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) a
       }
       ds[r] = pr * (d - dq);
     }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const Planes<NP> sp = planes8<NP>(ds + 8 * t);
+      mfma_x<NP>(a0, colfrag<NP>(Kt, c, hh, t), sp);
+      mfma_x<NP>(a1, colfrag<NP>(Kt, 32 + c, hh, t), sp);
+    }
+  }
+  if (!own) return;
+  float* op = g.dqkv + (row0 + q) * g.lddq + head * kHD;
+#pragma unroll
+  for (int gq = 0; gq < 4; ++gq) {
+    const int d = 8 * gq + 4 * hh;
+    st4(op + d, make_float4(a0[4 * gq] * 0.125f, a0[4 * gq + 1] * 0.125f, a0[4 * gq + 2] * 0.125f,
+                            a0[4 * gq + 3] * 0.125f));
+    st4(op + 32 + d, make_float4(a1[4 * gq] * 0.125f, a1[4 * gq + 1] * 0.125f, a1[4 * gq + 2] * 0.125f,
+                                 a1[4 * gq + 3] * 0.125f));
+  }
+}
+
+// dQ = dS K from the dS tiles attn_bwd_kv_mp_kernel<..., DS = true> stored (four-wave launches, the
+// 501-token user sequence): a wave owns 32 queries; per key tile only K is staged (transposed) and
+// lane (c, h) loads its query's 16 dS values of the tile (four float4, a tile ahead) -- no S, P, dP
+// recompute, no dropout hash, no Q / dctx planes in registers.
+template <int NP>
+__global__ void __launch_bounds__(256) attn_bwd_q_ds_kernel(AttnArgs g) {
+  __shared__ __attribute__((aligned(16))) uint16_t Kt[NP][kHD][kVR];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, hh = lane >> 5;
+  int64_t bid = blockIdx.x;
+  const int qc = (int)(bid % g.chunks);
+  bid /= g.chunks;
+  const int head = (int)(bid % g.heads);
+  const int64_t seq = bid / g.heads;
+  const int L = g.L;
+  const int64_t row0 = seq * L;
+  const int q0 = (qc * 4 + wave) * 32;
+  const bool active = q0 < L;
+  const int q = q0 + c;
+  const bool own = active && q < L;
+  const int nkb = (L + 31) / 32;
+  // slot r = 4 j + u of key tile kb: key kb * 32 + crow(r, h) = 8 j + 4 h + u
+  const float* dsp = g.dsb + ((seq * g.heads + head) * (int64_t)g.nkb * g.nkb * 32 + q) * 32 + 4 * hh;
+  auto load = [&](int kb, float (&d)[16]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 x = own ? ld4(dsp + (int64_t)kb * g.nkb * 1024 + 8 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+      d[4 * j] = x.x; d[4 * j + 1] = x.y; d[4 * j + 2] = x.z; d[4 * j + 3] = x.w;
+    }
+  };
+  f32x16 a0, a1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) a0[r] = a1[r] = 0.f;
+  TileFetch<NP> fk;
+  fk.fetch(g.qkv, g.ldq, row0, 0, L, g.koff + head * kHD);
+  float dn[16];
+  load(0, dn);
+  for (int kb = 0; kb < nkb; ++kb) {
+    float ds[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ds[r] = dn[r];
+    __syncthreads();
+    fk.store(nullptr, Kt);
+    if (kb + 1 < nkb) {
+      fk.fetch(g.qkv, g.ldq, row0, (kb + 1) * 32, L, g.koff + head * kHD);
+      load(kb + 1, dn);
+    }
+    __syncthreads();
+    if (!active) continue;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const Planes<NP> sp = planes8<NP>(ds + 8 * t);
@@ -1416,8 +1494,17 @@ extern "C" int nr_bert_attn_fwd(const float* qkv, int64_t ldq, int64_t koff, int
   return NR_OK;
 }
 
+namespace {
+// floats of the workspace ahead of the dS tiles: D, rounded up to 16 B
+int64_t attn_dq_floats(int64_t nseq, int32_t L, int32_t heads) { return (nseq * (int64_t)L * heads + 3) & ~(int64_t)3; }
+}  // namespace
+
 extern "C" int64_t nr_bert_attn_bwd_workspace(int64_t nseq, int32_t L, int32_t heads) {
-  return nseq * (int64_t)L * heads * (int64_t)sizeof(float);
+  if (nseq < 0 || L <= 0 || heads <= 0) return 0;
+  int64_t f = attn_dq_floats(nseq, L, heads);
+  const int64_t nkb = (L + 31) / 32;
+  if (attn_waves(L) == 4) f += nseq * heads * nkb * nkb * 1024;   // dS tiles
+  return f * (int64_t)sizeof(float);
 }
 
 extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int64_t voff, const void* mask,
@@ -1430,10 +1517,11 @@ extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int
                       const_cast<float*>(ml));
   if (rc) return rc;
   if (!ctx || !dctx || !work || !dqkv) return NR_EINVAL(4);
-  if (!al16(ctx) || !al16(dctx) || !al16(dqkv) || ((ldc | ldd | lddq) & 3)) return NR_EINVAL(5);
+  if (!al16(ctx) || !al16(dctx) || !al16(dqkv) || !al16(work) || ((ldc | ldd | lddq) & 3)) return NR_EINVAL(5);
   if (!prec_ok(prec)) return NR_EINVAL(6);
   if (nseq == 0) return NR_OK;
   const int64_t T = nseq * L;
+  g.dsb = work + attn_dq_floats(nseq, L, heads);
   hipLaunchKernelGGL(attn_dsum_kernel, dim3((unsigned)((T * heads * (kHD / 4) + 255) / 256)), dim3(256), 0, stream, dctx,
                      ldd, ctx, ldc, T, heads, work);
   NR_LAUNCH_CHECK();
@@ -1455,18 +1543,18 @@ extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int
     if (drop) NR_BWD(attn_bwd_kv_kernel<true>, attn_bwd_q_kernel<true>);
     else NR_BWD(attn_bwd_kv_kernel<false>, attn_bwd_q_kernel<false>);
   } else if (kb && nw == 4) {   // the forward's keep bits instead of the per-element hash
-    if (prec == NR_GEMM_BF16) NR_BWD((attn_bwd_kv_mp_kernel<1, true, true, true>), (attn_bwd_q_mp_kernel<1, true, true, true>));
-    else NR_BWD((attn_bwd_kv_mp_kernel<3, true, true, true>), (attn_bwd_q_mp_kernel<3, true, true, true>));
+    if (prec == NR_GEMM_BF16) NR_BWD((attn_bwd_kv_mp_kernel<1, true, true, true, true>), attn_bwd_q_ds_kernel<1>);
+    else NR_BWD((attn_bwd_kv_mp_kernel<3, true, true, true, true>), attn_bwd_q_ds_kernel<3>);
   } else if (kb) {
     if (prec == NR_GEMM_BF16) NR_BWD((attn_bwd_kv_mp_kernel<1, true, false, true>), (attn_bwd_q_mp_kernel<1, true, false, true>));
     else NR_BWD((attn_bwd_kv_mp_kernel<3, true, false, true>), (attn_bwd_q_mp_kernel<3, true, false, true>));
   } else if (nw == 4) {
     if (prec == NR_GEMM_BF16) {
-      if (drop) NR_BWD((attn_bwd_kv_mp_kernel<1, true, true>), (attn_bwd_q_mp_kernel<1, true, true>));
-      else NR_BWD((attn_bwd_kv_mp_kernel<1, false, true>), (attn_bwd_q_mp_kernel<1, false, true>));
+      if (drop) NR_BWD((attn_bwd_kv_mp_kernel<1, true, true, false, true>), attn_bwd_q_ds_kernel<1>);
+      else NR_BWD((attn_bwd_kv_mp_kernel<1, false, true, false, true>), attn_bwd_q_ds_kernel<1>);
     } else {
-      if (drop) NR_BWD((attn_bwd_kv_mp_kernel<3, true, true>), (attn_bwd_q_mp_kernel<3, true, true>));
-      else NR_BWD((attn_bwd_kv_mp_kernel<3, false, true>), (attn_bwd_q_mp_kernel<3, false, true>));
+      if (drop) NR_BWD((attn_bwd_kv_mp_kernel<3, true, true, false, true>), attn_bwd_q_ds_kernel<3>);
+      else NR_BWD((attn_bwd_kv_mp_kernel<3, false, true, false, true>), attn_bwd_q_ds_kernel<3>);
     }
   } else if (prec == NR_GEMM_BF16) {
     if (drop) NR_BWD((attn_bwd_kv_mp_kernel<1, true, false>), (attn_bwd_q_mp_kernel<1, true, false>));

@@ -34,7 +34,7 @@ ATTN_PRECS = {"f32": (2e-5, 1e-4), "bf16x6": (2e-5, 1e-4), "bf16": (3e-2, 3e-2)}
 
 
 @pytest.mark.parametrize("prec", list(ATTN_PRECS))
-@pytest.mark.parametrize("nseq,L,heads", [(7, 30, 2), (3, 77, 12), (2, 501, 12), (5, 1, 1), (4, 33, 2)])
+@pytest.mark.parametrize("nseq,L,heads", [(7, 30, 2), (3, 77, 12), (2, 501, 12), (5, 1, 1), (4, 33, 2), (2, 140, 3)])
 def test_attention_fwd_bwd(nseq, L, heads, prec):
     from newsrec_amd import _lib as Lb, kernels as K
     mode = {"f32": Lb.GEMM_F32, "bf16x6": Lb.GEMM_BF16X6, "bf16": Lb.GEMM_BF16}[prec]
@@ -62,8 +62,9 @@ def test_attention_fwd_bwd(nseq, L, heads, prec):
     np.testing.assert_allclose(dqkv.cpu().numpy(), g, rtol=0, atol=ba * max(1.0, np.abs(g).max()))
 
 
+@pytest.mark.parametrize("L", [45, 140])   # 140: four-wave launches (the dS-tile backward), two chunks
 @pytest.mark.parametrize("prec", ["f32", "bf16x6"])
-def test_attention_dropout_consistent(prec, request):
+def test_attention_dropout_consistent(prec, L, request):
     """Dropout on the probabilities: the backward regenerates the forward's mask (directional
     derivative of <ctx, d> matches finite differences under the same seed); about p of the
     mass is dropped."""
@@ -71,7 +72,7 @@ def test_attention_dropout_consistent(prec, request):
     torch.manual_seed(3)
     old = K.set_gemm_precision(Lb.GEMM_F32 if prec == "f32" else Lb.GEMM_BF16X6)
     request.addfinalizer(lambda: K.set_gemm_precision(old))
-    nseq, L, heads, p = 3, 45, 2, 0.3
+    nseq, heads, p = 3, 2, 0.3
     H, T = heads * 64, nseq * L
     qkv = torch.randn(T, 3 * H, device="cuda")
     mask = torch.ones(T, dtype=torch.long, device="cuda")
