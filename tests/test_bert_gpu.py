@@ -34,7 +34,7 @@ ATTN_PRECS = {"f32": (2e-5, 1e-4), "bf16x6": (2e-5, 1e-4), "bf16": (3e-2, 3e-2)}
 
 
 @pytest.mark.parametrize("prec", list(ATTN_PRECS))
-@pytest.mark.parametrize("nseq,L,heads", [(7, 30, 2), (3, 77, 12), (2, 501, 12), (5, 1, 1), (4, 33, 2), (2, 140, 3)])
+@pytest.mark.parametrize("nseq,L,heads", [(7, 30, 2), (3, 77, 12), (2, 501, 12), (5, 1, 1), (4, 33, 2), (2, 140, 3), (3, 97, 2)])
 def test_attention_fwd_bwd(nseq, L, heads, prec):
     from newsrec_amd import _lib as Lb, kernels as K
     mode = {"f32": Lb.GEMM_F32, "bf16x6": Lb.GEMM_BF16X6, "bf16": Lb.GEMM_BF16}[prec]
@@ -100,7 +100,7 @@ def test_attention_dropout_consistent(prec, L, request):
 
 
 @pytest.mark.parametrize("prec", ["bf16x6", "bf16"])
-@pytest.mark.parametrize("nseq,L,heads", [(3, 45, 2), (2, 501, 12), (4, 30, 12), (2, 33, 1)])
+@pytest.mark.parametrize("nseq,L,heads", [(3, 45, 2), (2, 501, 12), (4, 30, 12), (2, 33, 1), (3, 97, 2)])
 def test_attention_dropout_keep_bits(nseq, L, heads, prec):
     """The bf16-MFMA forward's stored keep bits (nr_bert_attn_keep_words): the backward reading them
     is BITWISE the backward that re-hashes every probability's counter (the same masks, the same
