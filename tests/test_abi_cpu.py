@@ -72,3 +72,25 @@ def test_library_built_from_this_tree():
     lib = ctypes.CDLL(_lib.LIB_PATH)
     lib.nr_build_hash.restype = ctypes.c_char_p
     assert lib.nr_build_hash().decode() == b.source_hash()
+
+
+def test_bert_attn_bwd_workspace_sizes():
+    """Host-side size query (no device call): D per (query, head) rounded to 16 B, plus for four-wave
+    launches (L > 96) the padded dS tiles of the stored-dS backward (4 KB per (sequence, head, key
+    tile, query tile))."""
+    from newsrec_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    f = lib.nr_bert_attn_bwd_workspace
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]
+
+    def want(nseq, L, heads):
+        d = (nseq * L * heads + 3) // 4 * 4
+        nkb = (L + 31) // 32
+        return 4 * (d + (nseq * heads * nkb * nkb * 1024 if L > 96 else 0))
+    for nseq, L, heads in [(7, 30, 2), (5, 1, 1), (3, 96, 2), (3, 97, 2), (2, 140, 3), (32, 501, 12)]:
+        assert f(nseq, L, heads) == want(nseq, L, heads), (nseq, L, heads)
+    assert f(32, 501, 12) - 4 * 32 * 501 * 12 == 402_653_184   # the XFormer user sequence's dS tiles
+    assert f(-1, 30, 2) == 0 and f(2, 0, 2) == 0 and f(2, 30, 0) == 0
