@@ -874,8 +874,10 @@ __device__ __forceinline__ float key_add(const AttnArgs& g, int64_t row0, int j,
 
 // (232 VGPRs: two waves per SIMD.  Bounded to three, 13 spilled and the XFormer step did not move,
 // 69.0 vs 69.1 ms, profiles/r04_p_xf_ab.json.)
-template <int NP, bool DROP, bool PF>
-__global__ void __launch_bounds__(256) attn_fwd_mp_kernel(AttnArgs g) {
+// W8 (the 501-token user sequence): eight-wave workgroups, threads 0..255 stage K and 256..511 V, so
+// each K / V tile is split once per 256 queries instead of per 128 and each thread splits one tensor.
+template <int NP, bool DROP, bool PF, bool W8 = false>
+__global__ void __launch_bounds__(W8 ? 512 : 256) attn_fwd_mp_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t Kp[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Vt[NP][kHD][kVR];
   __shared__ float kadd[32];
@@ -902,20 +904,35 @@ __global__ void __launch_bounds__(256) attn_fwd_mp_kernel(AttnArgs g) {
   const int nkb = (L + 31) / 32;
   TileFetch<NP> fk, fv;
   float kadd_n = 0.f;
+  const bool kside = threadIdx.x < 256;   // W8: this thread stages K (else V)
+  const int64_t wcol = (kside ? g.koff : g.voff) + head * kHD;
   if constexpr (PF) {
-    fk.fetch(g.qkv, g.ldq, row0, 0, L, g.koff + head * kHD);
-    fv.fetch(g.qkv, g.ldq, row0, 0, L, g.voff + head * kHD);
+    if constexpr (W8) {
+      fk.fetch(g.qkv, g.ldq, row0, 0, L, wcol);
+    } else {
+      fk.fetch(g.qkv, g.ldq, row0, 0, L, g.koff + head * kHD);
+      fv.fetch(g.qkv, g.ldq, row0, 0, L, g.voff + head * kHD);
+    }
     if (threadIdx.x < 32) kadd_n = key_add(g, row0, threadIdx.x, L);
   }
   for (int kb = 0; kb < nkb; ++kb) {
     __syncthreads();
     if constexpr (PF) {
-      fk.store(Kp, nullptr);
-      fv.store(nullptr, Vt);
+      if constexpr (W8) {
+        if (kside) fk.store(Kp, nullptr);
+        else fk.store(nullptr, Vt);
+      } else {
+        fk.store(Kp, nullptr);
+        fv.store(nullptr, Vt);
+      }
       if (threadIdx.x < 32) kadd[threadIdx.x] = kadd_n;
       if (kb + 1 < nkb) {
-        fk.fetch(g.qkv, g.ldq, row0, (kb + 1) * 32, L, g.koff + head * kHD);
-        fv.fetch(g.qkv, g.ldq, row0, (kb + 1) * 32, L, g.voff + head * kHD);
+        if constexpr (W8) {
+          fk.fetch(g.qkv, g.ldq, row0, (kb + 1) * 32, L, wcol);
+        } else {
+          fk.fetch(g.qkv, g.ldq, row0, (kb + 1) * 32, L, g.koff + head * kHD);
+          fv.fetch(g.qkv, g.ldq, row0, (kb + 1) * 32, L, g.voff + head * kHD);
+        }
         if (threadIdx.x < 32) kadd_n = key_add(g, row0, (kb + 1) * 32 + threadIdx.x, L);
       }
     } else {
@@ -1466,7 +1483,8 @@ extern "C" int nr_bert_attn_fwd(const float* qkv, int64_t ldq, int64_t koff, int
   if (nseq == 0) return NR_OK;
   g.ctx = ctx; g.ldc = ldc;
   g.keep = p_drop > 0.f ? keep : nullptr; g.nkb = (L + 31) / 32;
-  const int nw = attn_waves(L);
+  // four-wave sequences (L > 96) with the MFMA arithmetic run as eight-wave workgroups (W8)
+  const int nw = attn_waves(L) == 4 && prec != NR_GEMM_F32 ? 8 : attn_waves(L);
   g.chunks = (L + 32 * nw - 1) / (32 * nw);
   const dim3 grid((unsigned)(nseq * heads * g.chunks)), block(64 * nw);
   const bool drop = p_drop > 0.f;
@@ -1474,13 +1492,13 @@ extern "C" int nr_bert_attn_fwd(const float* qkv, int64_t ldq, int64_t koff, int
   if (prec == NR_GEMM_F32) {
     if (drop) NR_FWD(attn_fwd_kernel<true>);
     else NR_FWD(attn_fwd_kernel<false>);
-  } else if (nw == 4) {
+  } else if (nw == 8) {
     if (prec == NR_GEMM_BF16) {
-      if (drop) NR_FWD((attn_fwd_mp_kernel<1, true, true>));
-      else NR_FWD((attn_fwd_mp_kernel<1, false, true>));
+      if (drop) NR_FWD((attn_fwd_mp_kernel<1, true, true, true>));
+      else NR_FWD((attn_fwd_mp_kernel<1, false, true, true>));
     } else {
-      if (drop) NR_FWD((attn_fwd_mp_kernel<3, true, true>));
-      else NR_FWD((attn_fwd_mp_kernel<3, false, true>));
+      if (drop) NR_FWD((attn_fwd_mp_kernel<3, true, true, true>));
+      else NR_FWD((attn_fwd_mp_kernel<3, false, true, true>));
     }
   } else if (prec == NR_GEMM_BF16) {
     if (drop) NR_FWD((attn_fwd_mp_kernel<1, true, false>));
