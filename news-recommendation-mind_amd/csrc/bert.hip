@@ -152,6 +152,9 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(LnArgs g) {
   }
 }
 
+// The add-LN backward (!EMBED) loads the NEXT row's x, res, dout and stats into registers before the
+// current row's arithmetic: a wave walks ~4 rows of the 16 k-token user sequence one after another,
+// and without it each row paid its loads' full latency.
 template <bool EMBED, int NV>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(LnArgs g) {
   __shared__ float red[4][2][256 * NV];
@@ -161,11 +164,8 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnArgs g) {
 #pragma unroll
   for (int j = 0; j < NV; ++j) ag[j] = ab[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   const float invH = 1.f / (float)g.H;
-  for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < g.T; t += (int64_t)gridDim.x * 4) {
-    float4 v[NV];
-    load_s<EMBED, NV>(g, t, lane, v, key);
-    const float mean = g.stats[2 * t], rstd = g.stats[2 * t + 1];
-    const float* drow = g.dout + t * g.ldd;
+  // one row: v = the LN input (dropout and residual applied), d = dL/d(out) as loaded
+  auto row = [&](int64_t t, const float4 (&v)[NV], const float4 (&dl)[NV], float mean, float rstd) {
     const uint32_t e0 = (uint32_t)(t * g.H);
     float4 dy[NV], xh[NV];
     float s1 = 0.f, s2 = 0.f;
@@ -176,7 +176,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnArgs g) {
         dy[j] = xh[j] = make_float4(0.f, 0.f, 0.f, 0.f);
         continue;
       }
-      float4 d = ld4(drow + c);
+      float4 d = dl[j];
       if (EMBED && g.p > 0.f) {
         d.x = nr_dropout_keep(key, e0 + c, g.thresh) ? d.x * g.pscale : 0.f;
         d.y = nr_dropout_keep(key, e0 + c + 1, g.thresh) ? d.y * g.pscale : 0.f;
@@ -217,6 +217,61 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnArgs g) {
         st4(xrow + c, dx);
       }
     }
+  };
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  if constexpr (EMBED) {
+    for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < g.T; t += stride) {
+      float4 v[NV], dl[NV];
+      load_s<EMBED, NV>(g, t, lane, v, key);
+      const float* drow = g.dout + t * g.ldd;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int c = 4 * (lane + 64 * j);
+        dl[j] = c < g.H ? ld4(drow + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      row(t, v, dl, g.stats[2 * t], g.stats[2 * t + 1]);
+    }
+  } else {
+    float4 xn[NV], rn[NV], dn[NV];
+    float mn = 0.f, sn = 0.f;
+    auto fetch = [&](int64_t t) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int c = 4 * (lane + 64 * j);
+        if (c < g.H) {
+          xn[j] = ld4(g.x + t * g.ldx + c);
+          rn[j] = ld4(g.res + t * g.ldr + c);
+          dn[j] = ld4(g.dout + t * g.ldd + c);
+        } else {
+          xn[j] = rn[j] = dn[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+      mn = g.stats[2 * t];
+      sn = g.stats[2 * t + 1];
+    };
+    int64_t t = (int64_t)blockIdx.x * 4 + wave;
+    if (t < g.T) fetch(t);
+    for (; t < g.T; t += stride) {
+      float4 v[NV], dl[NV];
+      const uint32_t e0 = (uint32_t)(t * g.H);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {   // load_s's arithmetic on the prefetched row
+        const int c = 4 * (lane + 64 * j);
+        float4 a = xn[j];
+        const float4 b = rn[j];
+        if (c < g.H && g.p > 0.f) {
+          a.x = nr_dropout_keep(key, e0 + c, g.thresh) ? a.x * g.pscale : 0.f;
+          a.y = nr_dropout_keep(key, e0 + c + 1, g.thresh) ? a.y * g.pscale : 0.f;
+          a.z = nr_dropout_keep(key, e0 + c + 2, g.thresh) ? a.z * g.pscale : 0.f;
+          a.w = nr_dropout_keep(key, e0 + c + 3, g.thresh) ? a.w * g.pscale : 0.f;
+        }
+        v[j] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+        dl[j] = dn[j];
+      }
+      const float mean = mn, rstd = sn;
+      if (t + stride < g.T) fetch(t + stride);
+      row(t, v, dl, mean, rstd);
+    }
   }
   // dgamma / dbeta: per-wave partials -> LDS -> one atomic per column per workgroup
 #pragma unroll
@@ -232,20 +287,33 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(LnArgs g) {
   }
 }
 
+// the backward's grid-stride launch: at most one round of resident workgroups (CUs x occupancy of this
+// instantiation, cached per device), at most 1024 -- each workgroup ends in one dgamma / dbeta atomic per
+// column, and a second round would run the last rows' workgroups on an otherwise idle chip
+template <bool EMBED, int NV>
+unsigned ln_bwd_grid(int64_t T) {
+  static int cap[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  if (cap[dev] == 0) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ln_bwd_kernel<EMBED, NV>, 256, 0) != hipSuccess || per < 1)
+      per = 1;
+    cap[dev] = cus * per < 1024 ? cus * per : 1024;
+  }
+  const int64_t nb = (T + 3) / 4;
+  return (unsigned)(nb < cap[dev] ? nb : cap[dev]);
+}
+
 template <bool EMBED, bool BWD>
 int launch_ln(const LnArgs& g, hipStream_t s) {
   if (g.T == 0) return NR_OK;
   const int nv = (g.H + 255) / 256;
-  dim3 grid;
-  if (BWD) {
-    int64_t nb = (g.T + 3) / 4;
-    grid = dim3((unsigned)(nb < 1024 ? nb : 1024));
-  } else {
-    grid = dim3((unsigned)((g.T + 3) / 4));
-  }
+  const dim3 grid((unsigned)((g.T + 3) / 4));
 #define NR_LN(NV)                                                                                    \
   if (nv == NV) {                                                                                    \
-    if (BWD) hipLaunchKernelGGL((ln_bwd_kernel<EMBED, NV>), grid, dim3(256), 0, s, g);               \
+    if (BWD) hipLaunchKernelGGL((ln_bwd_kernel<EMBED, NV>), dim3(ln_bwd_grid<EMBED, NV>(g.T)), dim3(256), 0, s, g); \
     else hipLaunchKernelGGL((ln_fwd_kernel<EMBED, NV>), grid, dim3(256), 0, s, g);                   \
   }
   NR_LN(1) else NR_LN(2) else NR_LN(3) else NR_LN(4) else return NR_EINVAL(9);
@@ -681,6 +749,11 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(AttnArgs g) {
 //     holds belongs to -- so the tile is staged TRANSPOSED (dims x rows) and read as two 4-row runs
 //     per plane (colfrag).
 // Every staged element is split once per tile by the staging threads, not once per wave.
+// compile-time A/B knob (tools/build_ab.sh): the dK/dV pass of four-wave sequences as eight-wave workgroups
+#ifndef NR_ATTN_BWD_W8
+#define NR_ATTN_BWD_W8 1
+#endif
+constexpr bool kNrAttnBwdW8 = NR_ATTN_BWD_W8;
 constexpr int kKR = kHD + 8;   // row-major plane row: 64 dims + 8 pad (144 B: ds_read_b128 conflict-free)
 constexpr int kVR = 36;        // transposed plane row: 32 rows + 4 pad (72 B: ds_read_b64 conflict-free)
 
@@ -1011,14 +1084,16 @@ __global__ void __launch_bounds__(W8 ? 512 : 256) attn_fwd_mp_kernel(AttnArgs g)
 // Two waves per SIMD, as attn_bwd_q_mp_kernel: with the own K / V rows held as split planes (96
 // VGPRs) the bound spilled 36 and ran slower (profiles/r04_o_xf_ab.json); held as fp32 and split per
 // query tile it spills 9 and the XFormer step gains 68.15 -> 67.86 ms (profiles/r04_q_xf_ab.json).
-template <int NP, bool DROP, bool PF, bool KB = false, bool DS = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) attn_bwd_kv_mp_kernel(AttnArgs g) {
+// W8 (the 501-token user sequence): eight-wave workgroups, threads 0..255 stage the Q tile and 256..511
+// the dctx tile, so each query tile is split once per 256 keys instead of per 128 (as the forward's W8).
+template <int NP, bool DROP, bool PF, bool KB = false, bool DS = false, bool W8 = false>
+__global__ void __launch_bounds__(W8 ? 512 : 256) __attribute__((amdgpu_waves_per_eu(2))) attn_bwd_kv_mp_kernel(AttnArgs g) {
   __shared__ __attribute__((aligned(16))) uint16_t Qp[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Op[NP][32][kKR];
   __shared__ __attribute__((aligned(16))) uint16_t Qt[NP][kHD][kVR];
   __shared__ __attribute__((aligned(16))) uint16_t Ot[NP][kHD][kVR];
   __shared__ float qm[32], qi[32], qd[32];
-  __shared__ __attribute__((aligned(16))) uint32_t kwd[4][32];   // per wave: the tile's 32 queries' words of its key tile
+  __shared__ __attribute__((aligned(16))) uint32_t kwd[W8 ? 8 : 4][32];   // per wave: the tile's 32 queries' words of its key tile
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c = lane & 31, hh = lane >> 5;
   const int nw = blockDim.x >> 6;
   int64_t bid = blockIdx.x;
@@ -1077,16 +1152,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) a
   };
   TileFetch<NP> fq, fo;
   float qm_n = 0.f, qi_n = 0.f, qd_n = 0.f;
+  const bool qside = threadIdx.x < 256;   // W8: this thread stages Q (else dctx)
+  const float* wbase = qside ? g.qkv : g.dctx;
+  const int64_t wld = qside ? g.ldq : g.ldd;
   if constexpr (PF) {
-    fq.fetch(g.qkv, g.ldq, row0, 0, L, head * kHD);
-    fo.fetch(g.dctx, g.ldd, row0, 0, L, head * kHD);
+    if constexpr (W8) {
+      fq.fetch(wbase, wld, row0, 0, L, head * kHD);
+    } else {
+      fq.fetch(g.qkv, g.ldq, row0, 0, L, head * kHD);
+      fo.fetch(g.dctx, g.ldd, row0, 0, L, head * kHD);
+    }
     if (threadIdx.x < 32) qstats(threadIdx.x, qm_n, qi_n, qd_n);
   }
   for (int qb = 0; qb < nqb; ++qb) {
     __syncthreads();
     if constexpr (PF) {
-      fq.store(Qp, Qt);
-      fo.store(Op, Ot);
+      if constexpr (W8) {
+        if (qside) fq.store(Qp, Qt);
+        else fq.store(Op, Ot);
+      } else {
+        fq.store(Qp, Qt);
+        fo.store(Op, Ot);
+      }
       if (threadIdx.x < 32) {
         qm[threadIdx.x] = qm_n;
         qi[threadIdx.x] = qi_n;
@@ -1094,8 +1181,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) a
       }
       if (kbits && lane < 32) kwd[wave][lane] = kw_n;
       if (qb + 1 < nqb) {
-        fq.fetch(g.qkv, g.ldq, row0, (qb + 1) * 32, L, head * kHD);
-        fo.fetch(g.dctx, g.ldd, row0, (qb + 1) * 32, L, head * kHD);
+        if constexpr (W8) {
+          fq.fetch(wbase, wld, row0, (qb + 1) * 32, L, head * kHD);
+        } else {
+          fq.fetch(g.qkv, g.ldq, row0, (qb + 1) * 32, L, head * kHD);
+          fo.fetch(g.dctx, g.ldd, row0, (qb + 1) * 32, L, head * kHD);
+        }
         if (threadIdx.x < 32) qstats((qb + 1) * 32 + threadIdx.x, qm_n, qi_n, qd_n);
         if (kbits && lane < 32) kw_n = kword((qb + 1) * 32 + lane);
       }
@@ -1551,21 +1642,37 @@ extern "C" int nr_bert_attn_bwd(const float* qkv, int64_t ldq, int64_t koff, int
   g.chunks = (L + 32 * nw - 1) / (32 * nw);
   const dim3 grid((unsigned)(nseq * heads * g.chunks)), block(64 * nw);
   const bool drop = p_drop > 0.f;
+  // the dK/dV pass of four-wave sequences with the MFMA arithmetic runs as eight-wave workgroups (W8)
+  const bool w8 = nw == 4 && prec != NR_GEMM_F32 && kNrAttnBwdW8;   // (the f32 kernels are 256-thread)
+  AttnArgs gkv = g;
+  gkv.chunks = w8 ? (L + 255) / 256 : g.chunks;
+  const dim3 gridkv((unsigned)(nseq * heads * gkv.chunks)), blockkv(w8 ? 512 : 64 * nw);
 #define NR_BWD(KV, Q)                                          \
   do {                                                         \
-    hipLaunchKernelGGL(KV, grid, block, 0, stream, g);         \
+    hipLaunchKernelGGL(KV, gridkv, blockkv, 0, stream, gkv);   \
     hipLaunchKernelGGL(Q, grid, block, 0, stream, g);          \
   } while (0)
   const bool kb = drop && g.keep != nullptr;
   if (prec == NR_GEMM_F32) {
     if (drop) NR_BWD(attn_bwd_kv_kernel<true>, attn_bwd_q_kernel<true>);
     else NR_BWD(attn_bwd_kv_kernel<false>, attn_bwd_q_kernel<false>);
-  } else if (kb && nw == 4) {   // the forward's keep bits instead of the per-element hash
+  } else if (kb && w8) {   // the forward's keep bits instead of the per-element hash
+    if (prec == NR_GEMM_BF16) NR_BWD((attn_bwd_kv_mp_kernel<1, true, true, true, true, true>), attn_bwd_q_ds_kernel<1>);
+    else NR_BWD((attn_bwd_kv_mp_kernel<3, true, true, true, true, true>), attn_bwd_q_ds_kernel<3>);
+  } else if (kb && nw == 4) {
     if (prec == NR_GEMM_BF16) NR_BWD((attn_bwd_kv_mp_kernel<1, true, true, true, true>), attn_bwd_q_ds_kernel<1>);
     else NR_BWD((attn_bwd_kv_mp_kernel<3, true, true, true, true>), attn_bwd_q_ds_kernel<3>);
   } else if (kb) {
     if (prec == NR_GEMM_BF16) NR_BWD((attn_bwd_kv_mp_kernel<1, true, false, true>), (attn_bwd_q_mp_kernel<1, true, false, true>));
     else NR_BWD((attn_bwd_kv_mp_kernel<3, true, false, true>), (attn_bwd_q_mp_kernel<3, true, false, true>));
+  } else if (w8) {
+    if (prec == NR_GEMM_BF16) {
+      if (drop) NR_BWD((attn_bwd_kv_mp_kernel<1, true, true, false, true, true>), attn_bwd_q_ds_kernel<1>);
+      else NR_BWD((attn_bwd_kv_mp_kernel<1, false, true, false, true, true>), attn_bwd_q_ds_kernel<1>);
+    } else {
+      if (drop) NR_BWD((attn_bwd_kv_mp_kernel<3, true, true, false, true, true>), attn_bwd_q_ds_kernel<3>);
+      else NR_BWD((attn_bwd_kv_mp_kernel<3, false, true, false, true, true>), attn_bwd_q_ds_kernel<3>);
+    }
   } else if (nw == 4) {
     if (prec == NR_GEMM_BF16) {
       if (drop) NR_BWD((attn_bwd_kv_mp_kernel<1, true, true, false, true>), attn_bwd_q_ds_kernel<1>);
